@@ -1,0 +1,129 @@
+"""ctypes mirror of include/fdbcs.h and the loader for the in-tree libraries.
+
+The product library must be the HIP build: there is no CPU fallback.  Loading
+fails loudly if ``libfdbcs.so`` is missing (run ``python -m
+foundationdb_amd.build`` or ``__graft_entry__.build()``).
+"""
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libfdbcs.so")
+WL_PATH = os.path.join(PKG, "libfdbcs_workload.so")
+
+CONFLICT, TOO_OLD, COMMITTED = 0, 1, 2
+
+OK = 0
+E_HIP, E_NOMEM, E_RANGE, E_STATE, E_ARG, E_KEY, E_NODEV, E_CAPACITY = -1, -2, -3, -4, -5, -6, -7, -8
+MAX_KEY = 30001
+
+
+class Range(C.Structure):
+    _fields_ = [("begin", C.c_void_p), ("begin_len", C.c_uint32), ("end", C.c_void_p), ("end_len", C.c_uint32)]
+
+
+class BatchView(C.Structure):
+    _fields_ = [
+        ("txn_count", C.c_int32),
+        ("read_count", C.c_int32),
+        ("write_count", C.c_int32),
+        ("reserved", C.c_int32),
+        ("snapshot", C.c_void_p),
+        ("read_off", C.c_void_p),
+        ("write_off", C.c_void_p),
+        ("key_off", C.c_void_p),
+        ("key_len", C.c_void_p),
+        ("key_bytes", C.c_void_p),
+        ("key_bytes_len", C.c_uint64),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("max_history", C.c_int64),
+        ("max_batch_keys", C.c_int64),
+        ("tail_arena_bytes", C.c_int64),
+    ]
+
+
+# (name, restype, argtypes) for every function declared in include/fdbcs.h
+FDBCS_FUNCS = [
+    ("fdbcs_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int64, C.POINTER(Config)]),
+    ("fdbcs_clear", C.c_int, [C.c_void_p, C.c_int64]),
+    ("fdbcs_set_version", C.c_int, [C.c_void_p, C.c_int64]),
+    ("fdbcs_destroy", None, [C.c_void_p]),
+    ("fdbcs_batch_begin", C.c_int, [C.c_void_p]),
+    ("fdbcs_batch_add", C.c_int, [C.c_void_p, C.c_int64, C.POINTER(Range), C.c_int32, C.POINTER(Range), C.c_int32]),
+    ("fdbcs_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_batch_txn_count", C.c_int32, [C.c_void_p]),
+    ("fdbcs_batch_detect_packed", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_detect_device", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p, C.c_int]),
+    ("fdbcs_history_size", C.c_int64, [C.c_void_p]),
+    ("fdbcs_header_version", C.c_int64, [C.c_void_p]),
+    ("fdbcs_oldest_version", C.c_int64, [C.c_void_p]),
+    ("fdbcs_dump_history", C.c_int64,
+     [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("fdbcs_load_history", C.c_int,
+     [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+      C.c_uint32]),
+    ("fdbcs_removal_key", C.c_int32, [C.c_void_p, C.c_void_p, C.c_int32]),
+    ("fdbcs_enable_stage_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("fdbcs_stage_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
+    ("fdbcs_stream", C.c_void_p, [C.c_void_p]),
+    ("fdbcs_strerror", C.c_char_p, [C.c_int]),
+    ("fdbcs_version", C.c_char_p, []),
+]
+
+WL_FUNCS = [
+    ("fdbwl_create", C.c_void_p, [C.c_int32, C.c_int32, C.c_int32]),
+    ("fdbwl_destroy", None, [C.c_void_p]),
+    ("fdbwl_generate", C.c_int, [C.c_void_p, C.c_int64, C.POINTER(BatchView), C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int64)]),
+]
+
+_lib = None
+_wl = None
+
+
+def _bind(lib, funcs):
+    for name, res, args in funcs:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def lib():
+    """The HIP product library.  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m foundationdb_amd.build`")
+        _lib = _bind(C.CDLL(LIB_PATH), FDBCS_FUNCS)
+    return _lib
+
+
+def workload_lib():
+    global _wl
+    if _wl is None:
+        if not os.path.exists(WL_PATH):
+            raise RuntimeError(f"{WL_PATH} is missing: build it with `python -m foundationdb_amd.build`")
+        _wl = _bind(C.CDLL(WL_PATH), WL_FUNCS)
+    return _wl
+
+
+class FdbcsError(RuntimeError):
+    """A nonzero fdbcs status: the reference's ASSERT -> internal_error()."""
+
+    def __init__(self, status, what=""):
+        msg = lib().fdbcs_strerror(status).decode()
+        super().__init__(f"{what}: fdbcs status {status} ({msg})" if what else f"fdbcs status {status} ({msg})")
+        self.status = status
+
+
+def check(status, what=""):
+    if status < 0:
+        raise FdbcsError(status, what)
+    return status

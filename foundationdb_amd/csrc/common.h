@@ -1,0 +1,137 @@
+// common.h -- shared device-side definitions for the MI355X conflict-set engine.
+//
+// Key encoding.  A key of length L is held as
+//   hi   = big-endian bytes [0, 8)   (zero padded)
+//   lo   = big-endian bytes [8, 16)  (zero padded)
+//   meta = (byte[16] << 24) | L      (byte[16] = 0 if L <= 16)
+//   tail = device pointer to bytes [17, L), 8-byte aligned and zero padded to
+//          a multiple of 8 -- only meaningful when L > 17.
+// (hi, lo, meta) compared as unsigned integers order any two keys exactly as
+// the reference's compare() (fdbserver/SkipList.cpp:113-120) unless both keys
+// are longer than 17 bytes and share their first 17 bytes; only then are the
+// tails consulted (8 bytes at a time, big-endian).  Point ranges [k, k\x00)
+// (fdbclient/FDBTypes.h:288-291) of 16-byte keys therefore never touch a tail.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdbcs_dev {
+
+constexpr int PAGE = 256;          // history page capacity (boundaries)
+constexpr int FILL = 192;          // target fill when a page is split / repacked
+constexpr uint32_t LEN_MASK = 0xFFFFFFu;
+
+struct Key {
+    uint64_t hi, lo;
+    uint32_t meta;
+    const uint8_t* tail;
+};
+
+__device__ __host__ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+__device__ __host__ inline uint32_t key_len(uint32_t meta) { return meta & LEN_MASK; }
+
+__device__ inline uint64_t load_be64(const uint8_t* p) {
+    uint64_t x = *reinterpret_cast<const uint64_t*>(p);
+    return __builtin_bswap64(x);
+}
+
+// Compare the tails (bytes 17..) of two keys that both have length > 17 and
+// identical first 17 bytes.  Tails are 8-byte aligned and zero padded.
+__device__ inline int tail_cmp(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
+    uint32_t m = (la < lb ? la : lb) - 17;
+    uint32_t words = (m + 7) >> 3;
+    for (uint32_t w = 0; w < words; w++) {
+        uint64_t a = load_be64(ta + 8 * w), b = load_be64(tb + 8 * w);
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+__device__ inline int kcmp(uint64_t ahi, uint64_t alo, uint32_t am, const uint8_t* at,
+                           uint64_t bhi, uint64_t blo, uint32_t bm, const uint8_t* bt) {
+    if (ahi != bhi) return ahi < bhi ? -1 : 1;
+    if (alo != blo) return alo < blo ? -1 : 1;
+    if (am == bm) {
+        if (key_len(am) <= 17) return 0;
+        return tail_cmp(at, key_len(am), bt, key_len(bm));
+    }
+    uint32_t ab = am >> 24, bb = bm >> 24;
+    if (ab != bb) return ab < bb ? -1 : 1;
+    uint32_t la = key_len(am), lb = key_len(bm);
+    if (la > 17 && lb > 17) return tail_cmp(at, la, bt, lb);
+    return la < lb ? -1 : 1;
+}
+
+__device__ inline int kcmp(const Key& a, const Key& b) {
+    return kcmp(a.hi, a.lo, a.meta, a.tail, b.hi, b.lo, b.meta, b.tail);
+}
+
+// Sort record: a key's fixed-width part plus the index of its range.
+struct SRec {
+    uint64_t hi, lo;
+    uint32_t meta, idx;
+};
+
+// ---- Structure-of-arrays views -------------------------------------------------
+
+struct KeyArrays {           // one key per slot
+    uint64_t* hi;
+    uint64_t* lo;
+    uint32_t* meta;
+    const uint8_t** tail;
+    __device__ Key get(int64_t i) const { return Key{hi[i], lo[i], meta[i], tail[i]}; }
+    __device__ void put(int64_t i, const Key& k) const {
+        hi[i] = k.hi; lo[i] = k.lo; meta[i] = k.meta; tail[i] = k.tail;
+    }
+};
+
+// The history: a pool of pages (PAGE slots each) plus a directory that lists
+// live pages in key order.  Page 0 of the directory may be empty only when it
+// is the only page (empty history).
+struct Pool {
+    uint64_t* hi;
+    uint64_t* lo;
+    uint32_t* meta;
+    int64_t* ver;
+    const uint8_t** tail;
+};
+
+struct Dir {
+    int32_t* page;      // pool page id
+    int32_t* cnt;       // boundaries in the page
+    int64_t* maxv;      // max version in the page
+    int64_t* start;     // global index of the page's first boundary; start[D] = H
+    uint64_t* fhi;      // first key of the page (copy, for the search)
+    uint64_t* flo;
+    uint32_t* fmeta;
+    const uint8_t** ftail;
+    int64_t* bmax;      // max of maxv over groups of 64 directory entries
+};
+
+// Device-resident scalars shared between the kernels of one batch.
+struct Scalars {
+    int32_t D;              // directory entries (current buffer)
+    int32_t D_next;         // directory entries being built
+    int32_t free_top;       // free page stack size
+    int32_t err;            // nonzero: abort history mutation
+    int32_t n_comb;         // combined write ranges
+    int32_t n_aff;          // affected pages
+    int32_t n_dep;          // dependent transactions (intra-batch)
+    int32_t edges_total;
+    int64_t H;              // boundaries
+    uint64_t tail_used;     // bytes used in the history tail arena
+    uint64_t btail_used;    // bytes used in the batch tail buffer
+    int64_t win_g0, win_g1; // compaction window [g0, g1) (global indices)
+    int32_t win_pA, win_pB; // first / last directory entry covering the window
+    int32_t win_newpages;   // pages produced by the repack
+    int32_t win_surv;       // survivors in the window pages
+    int32_t jac_iters;      // stats: Jacobi iterations in the decision
+    int32_t pad[3];
+};
+
+__device__ inline int64_t atomic_max_i64(int64_t* addr, int64_t v) {
+    return (int64_t)atomicMax((long long*)addr, (long long)v);
+}
+
+}  // namespace fdbcs_dev

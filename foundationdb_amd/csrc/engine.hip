@@ -1,0 +1,890 @@
+// engine.hip -- host orchestration and the C ABI (include/fdbcs.h).
+//
+// One fdbcs object = one ConflictSet (fdbserver/SkipList.cpp:926-954) whose
+// history lives in HBM.  ConflictBatch calls (ConflictSet.h:32-60) are staged
+// in host memory, shipped with one H2D copy, resolved by the kernel pipeline
+// below on the set's HIP stream, and the verdicts come back with one D2H copy.
+// Pipeline order follows ConflictBatch::detectConflicts (SkipList.cpp:
+// 1163-1208): read check -> intra-batch -> combine -> merge -> verdicts ->
+// compaction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "kernels.h"
+
+using namespace fdbcs_dev;
+
+namespace {
+
+static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+#define HIPOK(x)                                    \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) {                     \
+            last_hip_error() = e_;                  \
+            return FDBCS_E_HIP;                     \
+        }                                           \
+    } while (0)
+
+hipError_t& last_hip_error() {
+    static thread_local hipError_t e = hipSuccess;
+    return e;
+}
+
+template <typename T>
+int dalloc(T*& p, int64_t n) {
+    p = nullptr;
+    if (n <= 0) n = 1;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, (size_t)n * sizeof(T));
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        return FDBCS_E_NOMEM;
+    }
+    p = static_cast<T*>(q);
+    return FDBCS_OK;
+}
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) hipFree((void*)p);
+    p = nullptr;
+}
+
+// host-side key encoding identical to k_encode
+void encode_host(const uint8_t* p, uint32_t L, uint64_t& hi, uint64_t& lo, uint32_t& meta) {
+    hi = lo = 0;
+    uint32_t b16 = 0;
+    for (uint32_t i = 0; i < std::min<uint32_t>(L, 17); i++) {
+        uint64_t c = p[i];
+        if (i < 8) hi |= c << (56 - 8 * i);
+        else if (i < 16) lo |= c << (56 - 8 * (i - 8));
+        else b16 = (uint32_t)c;
+    }
+    meta = (b16 << 24) | L;
+}
+
+int keycmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+    uint32_t n = std::min(al, bl);
+    int c = n ? memcmp(a, b, n) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+}  // namespace
+
+struct fdbcs {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    HistBufs h{};
+    BatchBufs b{};
+    Scalars* sc = nullptr;       // device
+    Scalars* sc_host = nullptr;  // pinned mirror
+    int cur = 0;
+    int64_t v0 = 0;
+    int64_t oldest = 0;
+    // capacities of the per-batch buffers
+    int64_t capT = -1, capR = -1, capW = -1, capSlots = -1, capBtail = -1, capEdges = -1, capRowWords = -1;
+    int64_t capDirB = -1, capWinPages = -1;
+    // last known device state (valid after a synchronized batch)
+    int64_t known_D = 1, known_free = 0, known_H = 0;
+    uint64_t known_tail = 0;
+    int64_t pending_pages = 0;   // worst-case pages consumed by unsynchronized batches
+    uint64_t pending_tail = 0;
+    // host staging of ConflictBatch::addTransaction
+    bool in_batch = false;
+    std::vector<int64_t> snap;
+    std::vector<int32_t> roff{0}, woff{0};
+    std::vector<uint64_t> rkoff, wkoff;
+    std::vector<uint32_t> rklen, wklen;
+    std::vector<uint8_t> blob;
+    // pinned host staging + device input staging
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0;
+    uint8_t* din = nullptr;
+    size_t din_cap = 0;
+    uint8_t* vpin = nullptr;  // verdict pinned
+    size_t vpin_cap = 0;
+    // stage timing
+    bool timing = false;
+    hipEvent_t ev[8] = {};
+    double stage_us[7] = {0};
+    bool have_times = false;
+};
+
+namespace {
+
+int alloc_pool(fdbcs* cs, int32_t pages) {
+    HistBufs& h = cs->h;
+    int r;
+    h.cap_pages = pages;
+    const int64_t slots = (int64_t)pages * PAGE;
+    if ((r = dalloc(h.pool.hi, slots)) || (r = dalloc(h.pool.lo, slots)) || (r = dalloc(h.pool.meta, slots)) ||
+        (r = dalloc(h.pool.ver, slots)) || (r = dalloc(h.pool.tail, slots)) || (r = dalloc(h.free_stack, pages)))
+        return r;
+    h.cap_dir = pages + 1;
+    for (int d = 0; d < 2; d++) {
+        Dir& x = h.dir[d];
+        if ((r = dalloc(x.page, h.cap_dir)) || (r = dalloc(x.cnt, h.cap_dir)) || (r = dalloc(x.maxv, h.cap_dir)) ||
+            (r = dalloc(x.start, h.cap_dir + 1)) || (r = dalloc(x.fhi, h.cap_dir)) || (r = dalloc(x.flo, h.cap_dir)) ||
+            (r = dalloc(x.fmeta, h.cap_dir)) || (r = dalloc(x.ftail, h.cap_dir)) ||
+            (r = dalloc(x.bmax, h.cap_dir / 64 + 2)))
+            return r;
+    }
+    return FDBCS_OK;
+}
+
+void free_pool(HistBufs& h) {
+    dfree(h.pool.hi); dfree(h.pool.lo); dfree(h.pool.meta); dfree(h.pool.ver); dfree(h.pool.tail);
+    dfree(h.free_stack);
+    for (int d = 0; d < 2; d++) {
+        Dir& x = h.dir[d];
+        dfree(x.page); dfree(x.cnt); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
+        dfree(x.ftail); dfree(x.bmax);
+    }
+}
+
+int sync_state(fdbcs* cs) {
+    HIPOK(hipMemcpyAsync(cs->sc_host, cs->sc, sizeof(Scalars), hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    cs->known_D = cs->sc_host->D;
+    cs->known_free = cs->sc_host->free_top;
+    cs->known_H = cs->sc_host->H;
+    cs->known_tail = cs->sc_host->tail_used;
+    cs->pending_pages = 0;
+    cs->pending_tail = 0;
+    return FDBCS_OK;
+}
+
+// Grow the page pool (and directories) to at least `pages`, preserving content.
+int grow_pool(fdbcs* cs, int64_t pages) {
+    int r;
+    if ((r = sync_state(cs))) return r;
+    HistBufs old = cs->h;
+    int64_t np = std::max<int64_t>(pages, (int64_t)old.cap_pages * 2);
+    if (np > INT32_MAX / 2) return FDBCS_E_CAPACITY;
+    if ((r = alloc_pool(cs, (int32_t)np))) return r;
+    HistBufs& h = cs->h;
+    const size_t os = (size_t)old.cap_pages * PAGE;
+    hipStream_t s = cs->stream;
+    HIPOK(hipMemcpyAsync(h.pool.hi, old.pool.hi, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.lo, old.pool.lo, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.meta, old.pool.meta, os * 4, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.ver, old.pool.ver, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.tail, old.pool.tail, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.free_stack, old.free_stack, (size_t)old.cap_pages * 4, hipMemcpyDeviceToDevice, s));
+    const size_t od = (size_t)old.cap_dir;
+    for (int d = 0; d < 2; d++) {
+        HIPOK(hipMemcpyAsync(h.dir[d].page, old.dir[d].page, od * 4, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].cnt, old.dir[d].cnt, od * 4, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].maxv, old.dir[d].maxv, od * 8, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].start, old.dir[d].start, (od + 1) * 8, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].fhi, old.dir[d].fhi, od * 8, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].flo, old.dir[d].flo, od * 8, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].fmeta, old.dir[d].fmeta, od * 4, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].ftail, old.dir[d].ftail, od * 8, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].bmax, old.dir[d].bmax, (od / 64 + 2) * 8, hipMemcpyDeviceToDevice, s));
+    }
+    launch_push_free(h, (int32_t)cs->known_free, old.cap_pages, (int32_t)(np - old.cap_pages), s);
+    HIPOK(hipStreamSynchronize(s));
+    free_pool(old);
+    cs->known_free += np - old.cap_pages;
+    Scalars tmp = *cs->sc_host;
+    tmp.free_top = (int32_t)cs->known_free;
+    HIPOK(hipMemcpyAsync(&cs->sc->free_top, &tmp.free_top, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPOK(hipStreamSynchronize(s));
+    cs->capDirB = -1;  // per-batch arrays sized by cap_dir must be re-sized
+    return FDBCS_OK;
+}
+
+int grow_tail(fdbcs* cs, uint64_t need) {
+    int r;
+    if ((r = sync_state(cs))) return r;
+    HistBufs& h = cs->h;
+    uint64_t ncap = std::max<uint64_t>(need, h.tail_cap * 2);
+    uint8_t* na = nullptr;
+    if ((r = dalloc(na, (int64_t)ncap))) return r;
+    HIPOK(hipMemcpyAsync(na, h.tail_arena, cs->known_tail, hipMemcpyDeviceToDevice, cs->stream));
+    launch_relocate_tails(h, h.tail_arena, h.tail_cap, na, cs->stream);
+    HIPOK(hipStreamSynchronize(cs->stream));
+    dfree(h.tail_arena);
+    h.tail_arena = na;
+    h.tail_cap = ncap;
+    return FDBCS_OK;
+}
+
+void free_batch(BatchBufs& b) {
+    dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
+    dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
+    dfree(b.read_txn); dfree(b.write_txn);
+    dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
+    dfree(b.rec_r0); dfree(b.rec_r1); dfree(b.rec_w0); dfree(b.rec_w1);
+    dfree(b.pair_bits); dfree(b.edges);
+    dfree(b.cb.hi); dfree(b.cb.lo); dfree(b.cb.meta); dfree(b.cb.tail);
+    dfree(b.ce.hi); dfree(b.ce.lo); dfree(b.ce.meta); dfree(b.ce.tail);
+    dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
+    dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
+    dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
+    dfree(b.aff_free_off); dfree(b.aff_freed);
+    dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
+    dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
+    dfree(b.desc_fmeta); dfree(b.desc_ftail);
+    dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
+    dfree(b.scan_tmp);
+}
+
+int alloc_keys(KeyArrays& k, int64_t n) {
+    int r;
+    if ((r = dalloc(k.hi, n)) || (r = dalloc(k.lo, n)) || (r = dalloc(k.meta, n)) || (r = dalloc(k.tail, n)))
+        return r;
+    return FDBCS_OK;
+}
+void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.tail); }
+
+// Size the per-batch buffers (grow only).
+int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes) {
+    BatchBufs& b = cs->b;
+    int r;
+    hipStream_t s = cs->stream;
+    if (T > 65536) return FDBCS_E_CAPACITY;  // T x T pair matrix bound
+    if (!b.scan_tmp && (r = dalloc(b.scan_tmp, 1024))) return r;
+    if (T > cs->capT) {
+        int64_t n = std::max<int64_t>(T, 1024);
+        dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
+        dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
+        if ((r = dalloc(b.too_old, n)) || (r = dalloc(b.hist, n)) || (r = dalloc(b.committed, n)) ||
+            (r = dalloc(b.verdict, n)) || (r = dalloc(b.deg, n)) || (r = dalloc(b.off, n + 1)) ||
+            (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)))
+            return r;
+        // dedup matrix: rows of ceil(n/32) words, zero between batches
+        dfree(b.pair_bits);
+        b.row_words = (int32_t)((n + 31) / 32);
+        if ((r = dalloc(b.pair_bits, n * b.row_words))) return r;
+        HIPOK(hipMemsetAsync(b.pair_bits, 0, (size_t)n * b.row_words * 4, s));
+        dfree(b.edges);
+        b.edge_cap = std::max<int64_t>(1, n * (n - 1) / 2);
+        if ((r = dalloc(b.edges, b.edge_cap))) return r;
+        cs->capT = n;
+    }
+    if (R > cs->capR) {
+        int64_t n = std::max<int64_t>(R, 1024);
+        dfree(b.read_txn); dfree(b.rec_r0); dfree(b.rec_r1);
+        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.rec_r0, n)) || (r = dalloc(b.rec_r1, n))) return r;
+        cs->capR = n;
+    }
+    if (W > cs->capW) {
+        int64_t n = std::max<int64_t>(W, 1024);
+        dfree(b.write_txn); dfree(b.rec_w0); dfree(b.rec_w1);
+        free_keys(b.cb); free_keys(b.ce);
+        dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
+        dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
+        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, n)) || (r = dalloc(b.rec_w1, n)) ||
+            (r = alloc_keys(b.cb, n)) || (r = alloc_keys(b.ce, n)) || (r = dalloc(b.pb, n)) ||
+            (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
+            (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
+            (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||
+            (r = dalloc(b.ne_ins, 2 * n)))
+            return r;
+        cs->capW = n;
+    }
+    const int64_t slots = 2 * (R + W);
+    if (slots > cs->capSlots) {
+        int64_t n = std::max<int64_t>(slots, 4096);
+        free_keys(b.keys);
+        if ((r = alloc_keys(b.keys, n))) return r;
+        cs->capSlots = n;
+    }
+    const uint64_t btail_need = key_bytes + 8 * (uint64_t)slots + 64;
+    if ((int64_t)btail_need > cs->capBtail) {
+        uint64_t n = std::max<uint64_t>(btail_need, 1 << 16);
+        dfree(b.btail);
+        if ((r = dalloc(b.btail, (int64_t)n))) return r;
+        b.btail_cap = n;
+        cs->capBtail = (int64_t)n;
+    }
+    const int64_t win_pages = 3 * std::max<int64_t>(W, 1024) + 16;
+    if (win_pages > cs->capWinPages) {
+        dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
+        if ((r = dalloc(b.win_keep, win_pages * PAGE)) || (r = dalloc(b.win_cnt, win_pages)) ||
+            (r = dalloc(b.win_off, win_pages + 2)))
+            return r;
+        b.win_cap_pages = (int32_t)win_pages;
+        cs->capWinPages = win_pages;
+    }
+    const int64_t cd = cs->h.cap_dir;
+    if (cd > cs->capDirB) {
+        dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
+        dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
+        dfree(b.aff_free_off); dfree(b.aff_freed);
+        dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
+        dfree(b.desc_fmeta); dfree(b.desc_ftail);
+        const int64_t n = cd + 2;
+        if ((r = dalloc(b.aff_flag, n)) || (r = dalloc(b.aff_pos, n)) || (r = dalloc(b.aff_list, n)) ||
+            (r = dalloc(b.aff_jlo, n)) || (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) ||
+            (r = dalloc(b.aff_parts, n)) || (r = dalloc(b.aff_extra, n)) || (r = dalloc(b.aff_nn_off, n)) ||
+            (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
+            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_freed, n)) || (r = dalloc(b.desc_page, n)) ||
+            (r = dalloc(b.desc_cnt, n)) || (r = dalloc(b.desc_max, n)) || (r = dalloc(b.desc_fhi, n)) ||
+            (r = dalloc(b.desc_flo, n)) || (r = dalloc(b.desc_fmeta, n)) || (r = dalloc(b.desc_ftail, n)))
+            return r;
+        cs->capDirB = cd;
+    }
+    return FDBCS_OK;
+}
+
+// Make sure the pool and the tail arena can absorb one more batch of W writes
+// in the worst case.
+int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
+    int r;
+    const int64_t naff_max = std::min<int64_t>(cs->known_D + cs->pending_pages + 1, 2 * W + 2);
+    const int64_t need = 2 * naff_max + 2 * cdiv64(2 * W, FILL) + cdiv64(3 * W + 10 + 2 * PAGE, FILL) + 8;
+    if (cs->known_free - cs->pending_pages < need) {
+        if (cs->pending_pages && (r = sync_state(cs))) return r;
+        if (cs->known_free < need) {
+            const int64_t used = cs->h.cap_pages - cs->known_free;
+            if ((r = grow_pool(cs, used + 2 * need + 1024))) return r;
+        }
+    }
+    const uint64_t tneed = write_tail_bytes + 8 * 2 * (uint64_t)W + 64;
+    if (cs->known_tail + cs->pending_tail + tneed > cs->h.tail_cap) {
+        if (cs->pending_tail && (r = sync_state(cs))) return r;
+        if (cs->known_tail + tneed > cs->h.tail_cap) {
+            if ((r = grow_tail(cs, cs->known_tail + 2 * tneed + (1 << 20)))) return r;
+        }
+    }
+    cs->pending_pages += need;
+    cs->pending_tail += tneed;
+    return FDBCS_OK;
+}
+
+void record(fdbcs* cs, int i) {
+    if (cs->timing) hipEventRecord(cs->ev[i], cs->stream);
+}
+
+// The whole detectConflicts pipeline on a device-resident batch.
+int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
+              bool sync) {
+    int r;
+    const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
+    if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
+    if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
+    if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    BatchBufs& b = cs->b;
+    HistBufs& h = cs->h;
+    hipStream_t s = cs->stream;
+    Scalars* sc = cs->sc;
+    HIPOK(hipMemsetAsync(&sc->err, 0, sizeof(int32_t), s));
+    HIPOK(hipMemsetAsync(&sc->btail_used, 0, sizeof(uint64_t), s));
+    HIPOK(hipMemsetAsync(&sc->n_comb, 0, sizeof(int32_t), s));
+    record(cs, 0);
+    launch_prep(v, cs->oldest, b, sc, s);
+    launch_encode(v, b, sc, s);
+    record(cs, 1);
+    launch_read_check(v, b, h, cs->cur, sc, cs->v0, s);
+    record(cs, 2);
+    launch_sort_ranges(v, b, s);
+    launch_edges(v, b, sc, s);
+    launch_decide(v, b, sc, s);
+    record(cs, 3);
+    if (W > 0) launch_combine(v, b, sc, s);
+    record(cs, 4);
+    launch_merge(v, b, h, cs->cur, sc, now, cs->v0, s);
+    cs->cur ^= 1;
+    record(cs, 5);
+    const bool compact = new_oldest > cs->oldest;
+    if (compact) {
+        launch_compact(b, h, cs->cur, sc, new_oldest, s);
+        cs->cur ^= 1;
+    }
+    record(cs, 6);
+    if (T > 0 && dev_verdict && dev_verdict != b.verdict)
+        HIPOK(hipMemcpyAsync(dev_verdict, b.verdict, (size_t)T, hipMemcpyDeviceToDevice, s));
+    if (compact) cs->oldest = new_oldest;
+    if (sync) {
+        if ((r = sync_state(cs))) return r;
+        if (cs->timing) {
+            float ms;
+            const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
+            for (int i = 0; i < 7; i++) {
+                hipEventElapsedTime(&ms, cs->ev[map[i][0]], cs->ev[map[i][1]]);
+                cs->stage_us[i] = ms * 1000.0;
+            }
+            cs->have_times = true;
+        }
+        if (cs->sc_host->err) return cs->sc_host->err;
+    }
+    return FDBCS_OK;
+}
+
+int reset_history(fdbcs* cs, int64_t v) {
+    cs->v0 = v;
+    cs->cur = 0;
+    launch_reset_history(cs->h, cs->cur, cs->sc, cs->stream);
+    launch_dir_finish(cs->h, cs->cur, cs->sc, cs->b, cs->stream);
+    return sync_state(cs);
+}
+
+int ensure_pinned(uint8_t*& p, size_t& cap, size_t need) {
+    if (need <= cap) return FDBCS_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    size_t n = std::max(need, cap * 2);
+    hipError_t e = hipHostMalloc((void**)&p, n, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        cap = 0;
+        return FDBCS_E_NOMEM;
+    }
+    cap = n;
+    return FDBCS_OK;
+}
+
+// Lay a host batch view out in one pinned buffer, copy it to the device in one
+// transfer and return the device-side view.
+int stage_batch(fdbcs* cs, const fdbcs_batch_view& hv, fdbcs_batch_view& dv) {
+    const int64_t T = hv.txn_count, R = hv.read_count, W = hv.write_count, slots = 2 * (R + W);
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    const size_t o_snap = 0;
+    const size_t o_ro = al(o_snap + 8 * T);
+    const size_t o_wo = al(o_ro + 4 * (T + 1));
+    const size_t o_ko = al(o_wo + 4 * (T + 1));
+    const size_t o_kl = al(o_ko + 8 * slots);
+    const size_t o_kb = al(o_kl + 4 * slots);
+    const size_t total = al(o_kb + hv.key_bytes_len + 16);
+    int r;
+    if ((r = ensure_pinned(cs->pin, cs->pin_cap, total))) return r;
+    if (total > cs->din_cap) {
+        dfree(cs->din);
+        size_t n = std::max(total, cs->din_cap * 2);
+        if ((r = dalloc(cs->din, (int64_t)n))) return r;
+        cs->din_cap = n;
+    }
+    // the previous batch's H2D must be done before overwriting the pinned buffer
+    HIPOK(hipStreamSynchronize(cs->stream));
+    uint8_t* p = cs->pin;
+    if (T) memcpy(p + o_snap, hv.snapshot, 8 * T);
+    memcpy(p + o_ro, hv.read_off, 4 * (T + 1));
+    memcpy(p + o_wo, hv.write_off, 4 * (T + 1));
+    if (slots) {
+        memcpy(p + o_ko, hv.key_off, 8 * slots);
+        memcpy(p + o_kl, hv.key_len, 4 * slots);
+    }
+    if (hv.key_bytes_len) memcpy(p + o_kb, hv.key_bytes, hv.key_bytes_len);
+    HIPOK(hipMemcpyAsync(cs->din, p, total, hipMemcpyHostToDevice, cs->stream));
+    dv = hv;
+    dv.snapshot = (const int64_t*)(cs->din + o_snap);
+    dv.read_off = (const int32_t*)(cs->din + o_ro);
+    dv.write_off = (const int32_t*)(cs->din + o_wo);
+    dv.key_off = (const uint64_t*)(cs->din + o_ko);
+    dv.key_len = (const uint32_t*)(cs->din + o_kl);
+    dv.key_bytes = cs->din + o_kb;
+    return FDBCS_OK;
+}
+
+int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    int r;
+    if (hv.txn_count < 0 || hv.read_count < 0 || hv.write_count < 0) return FDBCS_E_ARG;
+    // preconditions checked on the host so that no device state changes on a bad batch
+    const int64_t nr = (int64_t)hv.read_count + hv.write_count;
+    for (int64_t i = 0; i < 2 * nr; i++)
+        if (hv.key_len[i] > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+    for (int64_t i = 0; i < nr; i++)
+        if (keycmp(hv.key_bytes + hv.key_off[2 * i], hv.key_len[2 * i], hv.key_bytes + hv.key_off[2 * i + 1],
+                   hv.key_len[2 * i + 1]) >= 0)
+            return FDBCS_E_RANGE;
+    fdbcs_batch_view dv;
+    if ((r = stage_batch(cs, hv, dv))) return r;
+    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
+    const int64_t T = hv.txn_count;
+    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
+    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
+    if ((r = sync_state(cs))) return r;
+    if (cs->sc_host->err) return cs->sc_host->err;
+    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    if (cs->timing) {
+        float ms;
+        const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
+        for (int i = 0; i < 7; i++) {
+            hipEventElapsedTime(&ms, cs->ev[map[i][0]], cs->ev[map[i][1]]);
+            cs->stage_us[i] = ms * 1000.0;
+        }
+        cs->have_times = true;
+    }
+    return FDBCS_OK;
+}
+
+}  // namespace
+
+// ============================================================== C ABI ====
+
+extern "C" {
+
+int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
+    if (!out) return FDBCS_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FDBCS_E_NODEV;
+    fdbcs* cs = new (std::nothrow) fdbcs();
+    if (!cs) return FDBCS_E_NOMEM;
+    int dev = cfg && cfg->device >= 0 ? cfg->device : -1;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    cs->device = dev;
+    int r = FDBCS_OK;
+    auto fail = [&](int code) {
+        fdbcs_destroy(cs);
+        return code;
+    };
+    if (hipSetDevice(dev) != hipSuccess) return fail(FDBCS_E_HIP);
+    if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) return fail(FDBCS_E_HIP);
+    if ((r = dalloc(cs->sc, 1))) return fail(r);
+    if (hipHostMalloc((void**)&cs->sc_host, sizeof(Scalars), hipHostMallocDefault) != hipSuccess)
+        return fail(FDBCS_E_NOMEM);
+    memset(cs->sc_host, 0, sizeof(Scalars));
+    if (hipMemset(cs->sc, 0, sizeof(Scalars)) != hipSuccess) return fail(FDBCS_E_HIP);
+    int64_t max_hist = cfg && cfg->max_history > 0 ? cfg->max_history : (1 << 20);
+    int64_t pages = std::max<int64_t>(1024, cdiv64(max_hist, FILL) * 2);
+    if ((r = alloc_pool(cs, (int32_t)pages))) return fail(r);
+    uint64_t tcap = cfg && cfg->tail_arena_bytes > 0 ? (uint64_t)cfg->tail_arena_bytes : (64ull << 20);
+    if ((r = dalloc(cs->h.tail_arena, (int64_t)tcap))) return fail(r);
+    cs->h.tail_cap = tcap;
+    if ((r = dalloc(cs->h.rk_hi, 1)) || (r = dalloc(cs->h.rk_lo, 1)) || (r = dalloc(cs->h.rk_meta, 1)) ||
+        (r = dalloc(cs->h.rk_tail, FDBCS_MAX_KEY + 16)))
+        return fail(r);
+    if (hipMemset(cs->h.rk_hi, 0, 8) || hipMemset(cs->h.rk_lo, 0, 8) || hipMemset(cs->h.rk_meta, 0, 4))
+        return fail(FDBCS_E_HIP);
+    for (int i = 0; i < 8; i++)
+        if (hipEventCreate(&cs->ev[i]) != hipSuccess) return fail(FDBCS_E_HIP);
+    if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
+    if ((r = reset_history(cs, v0))) return fail(r);
+    cs->oldest = 0;
+    *out = cs;
+    return FDBCS_OK;
+}
+
+int fdbcs_clear(fdbcs* cs, int64_t v) {
+    if (!cs) return FDBCS_E_ARG;
+    return reset_history(cs, v);  // oldestVersion and removalKey are kept (SkipList.cpp:957-959)
+}
+
+int fdbcs_set_version(fdbcs* cs, int64_t v) { return fdbcs_clear(cs, v); }
+
+void fdbcs_destroy(fdbcs* cs) {
+    if (!cs) return;
+    if (cs->stream) hipStreamSynchronize(cs->stream);
+    free_batch(cs->b);
+    free_pool(cs->h);
+    dfree(cs->h.tail_arena);
+    dfree(cs->h.rk_hi); dfree(cs->h.rk_lo); dfree(cs->h.rk_meta); dfree(cs->h.rk_tail);
+    dfree(cs->sc);
+    dfree(cs->din);
+    if (cs->sc_host) hipHostFree(cs->sc_host);
+    if (cs->pin) hipHostFree(cs->pin);
+    if (cs->vpin) hipHostFree(cs->vpin);
+    for (int i = 0; i < 8; i++)
+        if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
+    if (cs->stream) hipStreamDestroy(cs->stream);
+    delete cs;
+}
+
+int fdbcs_batch_begin(fdbcs* cs) {
+    if (!cs) return FDBCS_E_ARG;
+    cs->in_batch = true;
+    cs->snap.clear();
+    cs->roff.assign(1, 0);
+    cs->woff.assign(1, 0);
+    cs->rkoff.clear(); cs->rklen.clear(); cs->wkoff.clear(); cs->wklen.clear();
+    cs->blob.clear();
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
+                    const fdbcs_range* writes, int32_t nwrites) {
+    if (!cs) return FDBCS_E_ARG;
+    if (!cs->in_batch) return FDBCS_E_STATE;
+    if (nreads < 0 || nwrites < 0 || (nreads && !reads) || (nwrites && !writes)) return FDBCS_E_ARG;
+    for (int i = 0; i < nreads + nwrites; i++) {
+        const fdbcs_range& rg = i < nreads ? reads[i] : writes[i - nreads];
+        if (rg.begin_len > FDBCS_MAX_KEY || rg.end_len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+        if (keycmp(rg.begin, rg.begin_len, rg.end, rg.end_len) >= 0) return FDBCS_E_RANGE;
+    }
+    auto put = [&](const uint8_t* p, uint32_t n, std::vector<uint64_t>& off, std::vector<uint32_t>& len) {
+        off.push_back(cs->blob.size());
+        len.push_back(n);
+        if (n) cs->blob.insert(cs->blob.end(), p, p + n);
+    };
+    for (int i = 0; i < nreads; i++) {
+        put(reads[i].begin, reads[i].begin_len, cs->rkoff, cs->rklen);
+        put(reads[i].end, reads[i].end_len, cs->rkoff, cs->rklen);
+    }
+    for (int i = 0; i < nwrites; i++) {
+        put(writes[i].begin, writes[i].begin_len, cs->wkoff, cs->wklen);
+        put(writes[i].end, writes[i].end_len, cs->wkoff, cs->wklen);
+    }
+    cs->snap.push_back(read_snapshot);
+    cs->roff.push_back(cs->roff.back() + nreads);
+    cs->woff.push_back(cs->woff.back() + nwrites);
+    return FDBCS_OK;
+}
+
+int32_t fdbcs_batch_txn_count(const fdbcs* cs) { return cs ? (int32_t)cs->snap.size() : 0; }
+
+int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    if (!cs) return FDBCS_E_ARG;
+    if (!cs->in_batch) return FDBCS_E_STATE;
+    cs->in_batch = false;
+    const int32_t T = (int32_t)cs->snap.size();
+    if (T && !verdict) return FDBCS_E_ARG;
+    std::vector<uint64_t> koff(cs->rkoff);
+    koff.insert(koff.end(), cs->wkoff.begin(), cs->wkoff.end());
+    std::vector<uint32_t> klen(cs->rklen);
+    klen.insert(klen.end(), cs->wklen.begin(), cs->wklen.end());
+    fdbcs_batch_view hv{};
+    hv.txn_count = T;
+    hv.read_count = cs->roff.back();
+    hv.write_count = cs->woff.back();
+    hv.snapshot = cs->snap.data();
+    hv.read_off = cs->roff.data();
+    hv.write_off = cs->woff.data();
+    hv.key_off = koff.data();
+    hv.key_len = klen.data();
+    hv.key_bytes = cs->blob.data();
+    hv.key_bytes_len = cs->blob.size();
+    return detect_host_view(cs, hv, now, new_oldest, verdict);
+}
+
+int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest,
+                              uint8_t* verdict) {
+    if (!cs || !hb) return FDBCS_E_ARG;
+    if (hb->txn_count && !verdict) return FDBCS_E_ARG;
+    return detect_host_view(cs, *hb, now, new_oldest, verdict);
+}
+
+int fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest,
+                        uint8_t* dev_verdict, int sync) {
+    if (!cs || !db) return FDBCS_E_ARG;
+    return run_batch(cs, *db, now, new_oldest, dev_verdict, sync != 0);
+}
+
+int64_t fdbcs_history_size(fdbcs* cs) {
+    if (!cs) return FDBCS_E_ARG;
+    int r = sync_state(cs);
+    return r ? r : cs->known_H;
+}
+
+int64_t fdbcs_header_version(const fdbcs* cs) { return cs ? cs->v0 : 0; }
+int64_t fdbcs_oldest_version(const fdbcs* cs) { return cs ? cs->oldest : 0; }
+
+int64_t fdbcs_dump_history(fdbcs* cs, int64_t cap, int64_t* versions, uint32_t* key_len, uint64_t* key_off,
+                           uint8_t* key_bytes, uint64_t key_bytes_cap) {
+    if (!cs) return FDBCS_E_ARG;
+    int r;
+    if ((r = sync_state(cs))) return r;
+    const int64_t H = cs->known_H;
+    if (H > cap) return FDBCS_E_CAPACITY;
+    if (H == 0) return 0;
+    Pool out{};
+    if ((r = dalloc(out.hi, H)) || (r = dalloc(out.lo, H)) || (r = dalloc(out.meta, H)) || (r = dalloc(out.ver, H)) ||
+        (r = dalloc(out.tail, H))) {
+        dfree(out.hi); dfree(out.lo); dfree(out.meta); dfree(out.ver); dfree(out.tail);
+        return r;
+    }
+    launch_gather(cs->h, cs->cur, cs->sc, out, cs->stream);
+    std::vector<uint64_t> hi(H), lo(H), tail(H);
+    std::vector<uint32_t> meta(H);
+    std::vector<uint8_t> arena(cs->known_tail);
+    hipMemcpyAsync(hi.data(), out.hi, H * 8, hipMemcpyDeviceToHost, cs->stream);
+    hipMemcpyAsync(lo.data(), out.lo, H * 8, hipMemcpyDeviceToHost, cs->stream);
+    hipMemcpyAsync(meta.data(), out.meta, H * 4, hipMemcpyDeviceToHost, cs->stream);
+    hipMemcpyAsync(versions, out.ver, H * 8, hipMemcpyDeviceToHost, cs->stream);
+    hipMemcpyAsync(tail.data(), out.tail, H * 8, hipMemcpyDeviceToHost, cs->stream);
+    if (cs->known_tail)
+        hipMemcpyAsync(arena.data(), cs->h.tail_arena, cs->known_tail, hipMemcpyDeviceToHost, cs->stream);
+    hipError_t e = hipStreamSynchronize(cs->stream);
+    dfree(out.hi); dfree(out.lo); dfree(out.meta); dfree(out.ver); dfree(out.tail);
+    if (e != hipSuccess) return FDBCS_E_HIP;
+    uint64_t off = 0;
+    const uint64_t abase = (uint64_t)(uintptr_t)cs->h.tail_arena;
+    for (int64_t i = 0; i < H; i++) {
+        const uint32_t len = meta[i] & LEN_MASK;
+        if (off + len > key_bytes_cap) return FDBCS_E_CAPACITY;
+        uint8_t* d = key_bytes + off;
+        for (uint32_t k = 0; k < std::min<uint32_t>(len, 17); k++) {
+            if (k < 8) d[k] = (uint8_t)(hi[i] >> (56 - 8 * k));
+            else if (k < 16) d[k] = (uint8_t)(lo[i] >> (56 - 8 * (k - 8)));
+            else d[k] = (uint8_t)(meta[i] >> 24);
+        }
+        if (len > 17) {
+            const uint64_t t = tail[i] - abase;
+            if (t + (len - 17) > arena.size()) return FDBCS_E_STATE;
+            memcpy(d + 17, arena.data() + t, len - 17);
+        }
+        key_len[i] = len;
+        key_off[i] = off;
+        off += len;
+    }
+    return H;
+}
+
+int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint32_t* key_len,
+                       const uint64_t* key_off, const uint8_t* key_bytes, int64_t v0, int64_t oldest,
+                       const uint8_t* removal_key, uint32_t removal_key_len) {
+    if (!cs || n < 0) return FDBCS_E_ARG;
+    if (removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+    int r;
+    for (int64_t i = 0; i + 1 < n; i++)
+        if (keycmp(key_bytes + key_off[i], key_len[i], key_bytes + key_off[i + 1], key_len[i + 1]) >= 0)
+            return FDBCS_E_RANGE;
+    const int64_t np = std::max<int64_t>(1, cdiv64(n, FILL));
+    uint64_t tail_bytes = 0;
+    for (int64_t i = 0; i < n; i++)
+        if (key_len[i] > 17) tail_bytes += ((uint64_t)key_len[i] - 17 + 7) & ~7ull;
+    if ((r = sync_state(cs))) return r;
+    if (np + 64 > cs->h.cap_pages) {
+        if ((r = grow_pool(cs, 2 * np + 1024))) return r;
+    }
+    if (tail_bytes + 64 > cs->h.tail_cap) {
+        if ((r = grow_tail(cs, 2 * tail_bytes + (1 << 20)))) return r;
+    }
+    if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return r;
+    if ((r = reset_history(cs, v0))) return r;
+    HistBufs& h = cs->h;
+    const int64_t slots = np * PAGE;
+    std::vector<uint64_t> hi(slots, 0), lo(slots, 0), tail(slots, 0);
+    std::vector<uint32_t> meta(slots, 0);
+    std::vector<int64_t> ver(slots, 0);
+    std::vector<uint8_t> arena(tail_bytes + 8, 0);
+    std::vector<int32_t> dpage(np), dcnt(np);
+    std::vector<int64_t> dmax(np);
+    std::vector<uint64_t> dfhi(np), dflo(np), dftail(np);
+    std::vector<uint32_t> dfmeta(np);
+    const uint64_t abase = (uint64_t)(uintptr_t)h.tail_arena;
+    uint64_t toff = 0;
+    for (int64_t p = 0; p < np; p++) {
+        const int64_t a = n * p / np, e = n * (p + 1) / np;
+        dpage[p] = (int32_t)p;
+        dcnt[p] = (int32_t)(e - a);
+        int64_t mx = INT64_MIN;
+        for (int64_t i = a; i < e; i++) {
+            const int64_t sl = p * PAGE + (i - a);
+            encode_host(key_bytes + key_off[i], key_len[i], hi[sl], lo[sl], meta[sl]);
+            ver[sl] = versions[i];
+            mx = std::max(mx, versions[i]);
+            if (key_len[i] > 17) {
+                const uint32_t m = key_len[i] - 17;
+                memcpy(arena.data() + toff, key_bytes + key_off[i] + 17, m);
+                tail[sl] = abase + toff;
+                toff += (m + 7) & ~7u;
+            }
+        }
+        dmax[p] = mx;
+        const int64_t s0 = p * PAGE;
+        dfhi[p] = hi[s0]; dflo[p] = lo[s0]; dfmeta[p] = meta[s0]; dftail[p] = tail[s0];
+    }
+    hipStream_t s = cs->stream;
+    HIPOK(hipMemcpyAsync(h.pool.hi, hi.data(), slots * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.lo, lo.data(), slots * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.meta, meta.data(), slots * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.ver, ver.data(), slots * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.tail, tail.data(), slots * 8, hipMemcpyHostToDevice, s));
+    if (toff) HIPOK(hipMemcpyAsync(h.tail_arena, arena.data(), toff, hipMemcpyHostToDevice, s));
+    Dir& d = h.dir[cs->cur];
+    HIPOK(hipMemcpyAsync(d.page, dpage.data(), np * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.cnt, dcnt.data(), np * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.maxv, dmax.data(), np * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.fhi, dfhi.data(), np * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.flo, dflo.data(), np * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.fmeta, dfmeta.data(), np * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.ftail, dftail.data(), np * 8, hipMemcpyHostToDevice, s));
+    // free stack: pages [np, cap) ; scalars
+    HIPOK(hipStreamSynchronize(s));
+    Scalars tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    tmp.D = (int32_t)np;
+    tmp.free_top = 0;
+    tmp.tail_used = toff;
+    HIPOK(hipMemcpyAsync(cs->sc, &tmp, sizeof(Scalars), hipMemcpyHostToDevice, s));
+    launch_push_free(h, 0, (int32_t)np, (int32_t)(h.cap_pages - np), s);
+    HIPOK(hipStreamSynchronize(s));
+    tmp.free_top = (int32_t)(h.cap_pages - np);
+    HIPOK(hipMemcpyAsync(cs->sc, &tmp, sizeof(Scalars), hipMemcpyHostToDevice, s));
+    launch_dir_finish(h, cs->cur, cs->sc, cs->b, s);
+    // removal key
+    uint64_t rh, rl;
+    uint32_t rm;
+    encode_host(removal_key, removal_key_len, rh, rl, rm);
+    std::vector<uint8_t> rt(FDBCS_MAX_KEY + 16, 0);
+    if (removal_key_len > 17) memcpy(rt.data(), removal_key + 17, removal_key_len - 17);
+    HIPOK(hipMemcpyAsync(h.rk_hi, &rh, 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_lo, &rl, 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_meta, &rm, 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_tail, rt.data(), rt.size(), hipMemcpyHostToDevice, s));
+    cs->v0 = v0;
+    cs->oldest = oldest;
+    return sync_state(cs);
+}
+
+int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap) {
+    if (!cs) return FDBCS_E_ARG;
+    uint64_t hi = 0, lo = 0;
+    uint32_t meta = 0;
+    std::vector<uint8_t> t(FDBCS_MAX_KEY + 16);
+    hipStreamSynchronize(cs->stream);
+    hipMemcpy(&hi, cs->h.rk_hi, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(&lo, cs->h.rk_lo, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(&meta, cs->h.rk_meta, 4, hipMemcpyDeviceToHost);
+    const uint32_t len = meta & LEN_MASK;
+    if (len > 17) hipMemcpy(t.data(), cs->h.rk_tail, len - 17, hipMemcpyDeviceToHost);
+    std::vector<uint8_t> k(len);
+    for (uint32_t i = 0; i < len; i++) {
+        if (i < 8) k[i] = (uint8_t)(hi >> (56 - 8 * i));
+        else if (i < 16) k[i] = (uint8_t)(lo >> (56 - 8 * (i - 8)));
+        else if (i == 16) k[i] = (uint8_t)(meta >> 24);
+        else k[i] = t[i - 17];
+    }
+    if (buf && cap > 0) memcpy(buf, k.data(), std::min<int64_t>(cap, len));
+    return (int32_t)len;
+}
+
+int fdbcs_enable_stage_timing(fdbcs* cs, int on) {
+    if (!cs) return FDBCS_E_ARG;
+    cs->timing = on != 0;
+    return FDBCS_OK;
+}
+
+int fdbcs_stage_times(fdbcs* cs, double* out_us, int cap) {
+    if (!cs || !out_us) return FDBCS_E_ARG;
+    if (!cs->have_times) return 0;
+    int n = std::min(cap, 7);
+    for (int i = 0; i < n; i++) out_us[i] = cs->stage_us[i];
+    return n;
+}
+
+void* fdbcs_stream(fdbcs* cs) { return cs ? (void*)cs->stream : nullptr; }
+
+const char* fdbcs_strerror(int status) {
+    switch (status) {
+        case FDBCS_OK: return "ok";
+        case FDBCS_E_HIP: return hipGetErrorString(last_hip_error());
+        case FDBCS_E_NOMEM: return "out of memory";
+        case FDBCS_E_RANGE: return "conflict range with begin >= end";
+        case FDBCS_E_STATE: return "call out of order";
+        case FDBCS_E_ARG: return "bad argument";
+        case FDBCS_E_KEY: return "key longer than FDBCS_MAX_KEY";
+        case FDBCS_E_NODEV: return "no HIP device";
+        case FDBCS_E_CAPACITY: return "device capacity exceeded";
+        default: return "unknown status";
+    }
+}
+
+const char* fdbcs_version(void) { return "fdbcs gfx950 0.1.0"; }
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+// kernels.h -- launcher prototypes shared by the kernel TUs and the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "common.h"
+#include "../../include/fdbcs.h"
+
+namespace fdbcs_dev {
+
+// Per-batch device working set (sized by the engine before each batch).
+struct BatchBufs {
+    // transaction level [T]
+    uint8_t* too_old;
+    uint8_t* hist;
+    uint8_t* committed;
+    int32_t* deg;        // unique intra-batch sources per reader
+    int32_t* off;        // [T+1] exclusive scan of deg
+    int32_t* cur;        // fill cursors
+    int32_t* dep_list;   // dependents in index order
+    int32_t* dep_idx;    // t -> index in dep_list or -1
+    // range level
+    int32_t* read_txn;   // [R]
+    int32_t* write_txn;  // [W]
+    // encoded keys [2R+2W]
+    KeyArrays keys;
+    uint8_t* btail;      // tail bytes of batch keys (8-aligned)
+    uint64_t btail_cap;
+    // sort records
+    SRec* rec_r0; SRec* rec_r1;   // [R]
+    SRec* rec_w0; SRec* rec_w1;   // [W]
+    SRec* sr;            // sorted reads (one of rec_r0/1)
+    SRec* sw;            // sorted writes (one of rec_w0/1)
+    // intra-batch overlap dedup matrix and edges
+    uint32_t* pair_bits; // [T * row_words]
+    int32_t row_words;
+    int32_t* edges;      // [edge_cap]
+    int64_t edge_cap;
+    // combined write ranges [W]
+    KeyArrays cb, ce;
+    // insertion plan [W]
+    int32_t* pb; int32_t* ib; int32_t* pe; int32_t* ie;
+    uint8_t* need_e;
+    int64_t* vb;
+    // affected pages [dir cap]
+    int32_t* aff_flag;   // [cap_dir+1]
+    int32_t* aff_pos;    // [cap_dir+1] exclusive scan of aff_flag
+    int32_t* aff_list;
+    int32_t* aff_jlo; int32_t* aff_jhi;
+    int32_t* aff_nn;     // new entries landing
+    int32_t* aff_parts;  // output pages
+    int32_t* aff_extra;  // extra pages beyond the first
+    int32_t* aff_nn_off; int32_t* aff_parts_off; int32_t* aff_extra_off; int32_t* aff_free_off;
+    int32_t* aff_freed;  // 1 if the page disappears
+    // new-entry scratch [2W]
+    Pool ne;             // key + version of new entries in page order
+    int32_t* ne_ins;     // insertion index in the old page
+    // page descriptors produced by rebuilds [cap]
+    int32_t* desc_page; int32_t* desc_cnt; int64_t* desc_max;
+    uint64_t* desc_fhi; uint64_t* desc_flo; uint32_t* desc_fmeta; const uint8_t** desc_ftail;
+    // compaction window
+    uint8_t* win_keep;   // [window pages * PAGE]
+    int32_t* win_cnt;    // survivors per window page
+    int32_t* win_off;    // [win_cap_pages + 2]: offsets, then the window page count
+    int32_t win_cap_pages;
+    // scan scratch
+    int64_t* scan_tmp;   // [>= 1024]
+    // verdict
+    uint8_t* verdict;
+};
+
+struct HistBufs {
+    Pool pool;
+    int32_t cap_pages;
+    int32_t* free_stack;
+    Dir dir[2];
+    int32_t cap_dir;
+    uint8_t* tail_arena;
+    uint64_t tail_cap;
+    // removal key (device copy)
+    uint64_t* rk_hi; uint64_t* rk_lo; uint32_t* rk_meta; uint8_t* rk_tail;  // rk_tail: 30008 bytes
+};
+
+// ---- scans (scan.hip) ----
+// Exclusive scan of n (device-resident count *n_ptr, or n_host if n_ptr null)
+// int32 values; out[n] = total.  Optional *total_out.
+void scan_i32(const int32_t* in, int32_t* out, const int32_t* n_ptr, int32_t n_host, int32_t* total_out,
+              int64_t* tmp, hipStream_t s);
+void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, int32_t n_host, int64_t* total_out,
+                       int64_t* tmp, hipStream_t s);
+
+// ---- batch stages (kernels_batch.hip) ----
+void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_encode(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
+                       hipStream_t s);
+void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s);
+void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+
+// ---- history stages (kernels_hist.hip) ----
+void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
+                  int64_t v0, hipStream_t s);
+void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s);
+void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s);
+void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s);
+void launch_gather(HistBufs& h, int cur, Scalars* sc, Pool out, hipStream_t s);
+void launch_push_free(HistBufs& h, int32_t from_top, int32_t first_id, int32_t count, hipStream_t s);
+void launch_relocate_tails(HistBufs& h, const uint8_t* old_base, uint64_t old_cap, const uint8_t* new_base,
+                           hipStream_t s);
+
+}  // namespace fdbcs_dev

@@ -1,0 +1,262 @@
+// workload.cpp -- deterministic synthetic batch generators (see workload.h).
+#include "workload.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Rng {  // xoshiro256**
+    uint64_t s[4];
+    static uint64_t splitmix(uint64_t& x) {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    explicit Rng(uint64_t seed) {
+        for (auto& x : s) x = splitmix(seed);
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        const uint64_t r = rotl(s[1] * 5, 7) * 9;
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    uint64_t uniform(uint64_t n) { return n ? next() % n : 0; }           // [0, n)
+    int64_t range(int64_t a, int64_t b) { return a + (int64_t)uniform((uint64_t)(b - a + 1)); }  // [a, b]
+    double u01() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+inline void put_be64(uint8_t* p, uint64_t x) {
+    for (int i = 0; i < 8; i++) p[i] = (uint8_t)(x >> (56 - 8 * i));
+}
+inline void put_be32(uint8_t* p, uint32_t x) {
+    for (int i = 0; i < 4; i++) p[i] = (uint8_t)(x >> (24 - 8 * i));
+}
+
+struct Shape {
+    int reads, writes, stride;  // stride = bytes reserved per key slot
+};
+
+const int CHUNK = 1024;
+
+}  // namespace
+
+struct fdbwl {
+    int config = 2;
+    int T = 5000;
+    int threads = 1;
+    Shape shape{5, 2, 17};
+    std::vector<double> zipf_cdf;
+    // batch storage
+    std::vector<int64_t> snap;
+    std::vector<int32_t> roff, woff;
+    std::vector<uint64_t> koff;
+    std::vector<uint32_t> klen;
+    std::vector<uint8_t> bytes;
+};
+
+namespace {
+
+static const uint8_t kPath[56] = {
+    '/', 'a', 'p', 'p', '/', 't', 'e', 'n', 'a', 'n', 't', 's', '/', 'o', 'r', 'd', 'e', 'r', 's', '/',
+    'b', 'y', '-', 'c', 'u', 's', 't', 'o', 'm', 'e', 'r', '/', 'r', 'e', 'g', 'i', 'o', 'n', '/', 'e',
+    'u', '-', 'w', 'e', 's', 't', '/', 'i', 'n', 'd', 'e', 'x', '/', 'v', '1', '/'};
+
+// key slot s of the batch: bytes at s * stride
+struct Writer {
+    fdbwl* g;
+    uint8_t* key(int64_t slot) { return g->bytes.data() + slot * g->shape.stride; }
+    void set(int64_t slot, uint32_t len) {
+        g->koff[slot] = (uint64_t)slot * g->shape.stride;
+        g->klen[slot] = len;
+    }
+};
+
+// 16-byte big-endian integer helpers for short reads [k, k + d]
+void add128(uint8_t* k, uint64_t d) {
+    for (int i = 15; i >= 0 && d; i--) {
+        uint64_t x = (uint64_t)k[i] + (d & 0xFF);
+        k[i] = (uint8_t)x;
+        d = (d >> 8) + (x >> 8);
+    }
+}
+
+void gen_chunk(fdbwl* g, int64_t index, int c0, int c1) {
+    const int cfg = g->config;
+    Rng rng(0x5EED0000ull + (uint64_t)(cfg == 50 ? 5 : cfg) * 1000ull + (uint64_t)index * 0x100000001B3ull +
+            (uint64_t)(c0 / CHUNK) * 0x9E3779B97F4A7C15ull);
+    Writer w{g};
+    const int R = g->T * g->shape.reads;
+    const int64_t now = cfg == 1 ? index + 50 : (cfg == 50 ? 100000 * (index + 1) : 10000000 + index * 10000);
+    for (int t = c0; t < c1; t++) {
+        // snapshot
+        if (cfg == 1) g->snap[t] = index;
+        else if (cfg == 50) g->snap[t] = 0;
+        else if (rng.uniform(1000) == 0) g->snap[t] = now - 5000000 - 20000;
+        else g->snap[t] = now - rng.range(10000, 200000);
+        for (int k = 0; k < g->shape.reads + g->shape.writes; k++) {
+            const bool is_read = k < g->shape.reads;
+            const int64_t r = is_read ? (int64_t)t * g->shape.reads + k
+                                      : (int64_t)R + (int64_t)t * g->shape.writes + (k - g->shape.reads);
+            const int64_t sb = 2 * r, se = 2 * r + 1;
+            uint8_t* b = w.key(sb);
+            uint8_t* e = w.key(se);
+            if (cfg == 1) {
+                // skipListTest: setK(key), setK(key + 1 + U[0,10]) (SkipList.cpp:909-922, 1436-1447)
+                const uint32_t key = (uint32_t)rng.uniform(20000000);
+                const uint32_t key2 = key + 1 + (uint32_t)rng.uniform(11);
+                memset(b, '.', 12); put_be32(b + 12, key);
+                memset(e, '.', 12); put_be32(e + 12, key2);
+                w.set(sb, 16);
+                w.set(se, 16);
+                continue;
+            }
+            if (cfg == 4) {
+                const uint64_t tenant = rng.uniform(16);
+                put_be64(b, tenant);
+                memcpy(b + 8, kPath, 56);
+                if (is_read && k == g->shape.reads - 1) {
+                    // wide read over a log-uniform fraction of the tenant's space
+                    const double f = std::exp(std::log(1e-3) + rng.u01() * (std::log(1e-1) - std::log(1e-3)));
+                    const uint64_t x = rng.next();
+                    const double span = f * 18446744073709551616.0;
+                    uint64_t y = (double)(~x) < span ? ~0ull : x + (uint64_t)span;
+                    if (y == x) y = x + 1;
+                    put_be64(b + 64, x);
+                    memcpy(e, b, 64);
+                    put_be64(e + 64, y);
+                    w.set(sb, 72);
+                    w.set(se, 72);
+                    if (y < x || y == ~0ull) {  // span clipped at the top: end past every key of the tenant
+                        put_be64(e + 64, ~0ull);
+                        e[72] = 0xFF;
+                        w.set(se, 73);
+                    }
+                } else {
+                    const uint32_t n = (uint32_t)rng.range(4, 36);
+                    for (uint32_t i = 0; i < n; i++) b[64 + i] = (uint8_t)rng.next();
+                    memcpy(e, b, 64 + n);
+                    e[64 + n] = 0;
+                    w.set(sb, 64 + n);
+                    w.set(se, 65 + n);
+                }
+                continue;
+            }
+            // configs 2, 3, 5, 50: 16-byte keys
+            if (cfg == 3) {
+                const double u = rng.u01();
+                const auto& cdf = g->zipf_cdf;
+                const uint64_t rank = (uint64_t)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin());
+                put_be64(b, rank * 0x9E3779B97F4A7C15ull);
+                memcpy(b + 8, "zzzzzzzz", 8);
+            } else {
+                put_be64(b, rng.next());
+                put_be64(b + 8, rng.next());
+            }
+            memcpy(e, b, 16);
+            if (is_read && rng.uniform(5) == 0) {
+                add128(e, 1 + rng.uniform(16));
+                bool wrapped = memcmp(e, b, 16) <= 0;
+                if (!wrapped) {
+                    w.set(sb, 16);
+                    w.set(se, 16);
+                    continue;
+                }
+                memcpy(e, b, 16);
+            }
+            e[16] = 0;  // point range [k, k\0) (fdbclient/FDBTypes.h:288-291)
+            w.set(sb, 16);
+            w.set(se, 17);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+fdbwl* fdbwl_create(int32_t config, int32_t txns, int32_t threads) {
+    fdbwl* g = new fdbwl();
+    g->config = config;
+    switch (config) {
+        case 1: g->T = 2500; g->shape = {1, 1, 16}; break;
+        case 2: g->T = 5000; g->shape = {5, 2, 17}; break;
+        case 3: g->T = 5000; g->shape = {5, 2, 17}; break;
+        case 4: g->T = 5000; g->shape = {5, 2, 104}; break;
+        case 5: g->T = 1000000; g->shape = {5, 2, 17}; break;
+        case 50: g->T = 1000000; g->shape = {0, 1, 17}; break;
+        default: delete g; return nullptr;
+    }
+    if (txns > 0) g->T = txns;
+    if (config == 3) {
+        const int n = 1000000;
+        g->zipf_cdf.resize(n);
+        double s = 0;
+        for (int i = 0; i < n; i++) s += 1.0 / std::pow((double)(i + 1), 0.99);
+        double acc = 0;
+        for (int i = 0; i < n; i++) {
+            acc += 1.0 / std::pow((double)(i + 1), 0.99) / s;
+            g->zipf_cdf[i] = acc;
+        }
+        g->zipf_cdf[n - 1] = 1.0;
+    }
+    int hw = (int)std::thread::hardware_concurrency();
+    g->threads = threads > 0 ? threads : std::max(1, std::min(16, hw));
+    const int64_t T = g->T, R = T * g->shape.reads, W = T * g->shape.writes, slots = 2 * (R + W);
+    g->snap.resize(T);
+    g->roff.resize(T + 1);
+    g->woff.resize(T + 1);
+    for (int64_t t = 0; t <= T; t++) {
+        g->roff[t] = (int32_t)(t * g->shape.reads);
+        g->woff[t] = (int32_t)(t * g->shape.writes);
+    }
+    g->koff.resize(slots);
+    g->klen.resize(slots);
+    g->bytes.assign((size_t)slots * g->shape.stride, 0);
+    return g;
+}
+
+void fdbwl_destroy(fdbwl* g) { delete g; }
+
+int fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* v, int64_t* now, int64_t* new_oldest) {
+    if (!g || !v) return FDBCS_E_ARG;
+    const int T = g->T;
+    const int nchunks = (T + CHUNK - 1) / CHUNK;
+    const int nth = std::min(g->threads, nchunks);
+    if (nth <= 1) {
+        for (int c = 0; c < nchunks; c++) gen_chunk(g, index, c * CHUNK, std::min(T, (c + 1) * CHUNK));
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < nth; k++)
+            th.emplace_back([=]() {
+                for (int c = k; c < nchunks; c += nth) gen_chunk(g, index, c * CHUNK, std::min(T, (c + 1) * CHUNK));
+            });
+        for (auto& x : th) x.join();
+    }
+    const int cfg = g->config;
+    const int64_t nw = cfg == 1 ? index + 50 : (cfg == 50 ? 100000 * (index + 1) : 10000000 + index * 10000);
+    if (now) *now = nw;
+    if (new_oldest) *new_oldest = cfg == 1 ? index : (cfg == 50 ? 0 : nw - 5000000);
+    memset(v, 0, sizeof(*v));
+    v->txn_count = T;
+    v->read_count = T * g->shape.reads;
+    v->write_count = T * g->shape.writes;
+    v->snapshot = g->snap.data();
+    v->read_off = g->roff.data();
+    v->write_off = g->woff.data();
+    v->key_off = g->koff.data();
+    v->key_len = g->klen.data();
+    v->key_bytes = g->bytes.data();
+    v->key_bytes_len = g->bytes.size();
+    return FDBCS_OK;
+}
+
+}  // extern "C"

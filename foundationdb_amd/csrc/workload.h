@@ -1,0 +1,50 @@
+/*
+ * workload.h -- deterministic synthetic Resolver batches.
+ *
+ * Not part of the drop-in boundary: used by bench.py and the tests to produce
+ * the same batches on any host.  Batches come out in the fdbcs_batch_view
+ * layout of include/fdbcs.h.
+ *
+ * Configs (BASELINE.json "configs"):
+ *   1  skipListTest-shaped (fdbserver/SkipList.cpp:1412-1486): 2,500 txns,
+ *      1 read + 1 write, key = 12 x '.' + BE32(U[0, 2e7)), range [k, k+1+U[0,10]),
+ *      snapshot = i, now = i + 50, newOldest = i.
+ *   2  5,000 txns, 5 reads (80 % point [k, k\0), 20 % [k, k+U[1,16]] as a
+ *      128-bit big-endian integer) + 2 point writes, uniform 16-byte keys.
+ *   3  as 2 with key = BE64(r * 0x9E3779B97F4A7C15) || "zzzzzzzz",
+ *      r ~ Zipf(0.99) over 1e6 ranks.
+ *   4  68-100-byte keys BE64(tenant<16) || 56-byte path || U[4,36] random
+ *      bytes; 4 point reads + 1 wide read covering a log-uniform 1e-3..1e-1
+ *      fraction of the tenant's key space; 2 point writes.
+ *   5  as 2 with 1,000,000 txns (snapshots now - U[1e4, 2e5]).
+ *   50 config-5 preload: 1,000,000 blind point writes, now = 1e5 * (i + 1),
+ *      newOldest = 0.
+ * Versions (configs 2-5): now_i = 1e7 + i * 1e4, newOldest = now - 5e6
+ * (MAX_WRITE_TRANSACTION_LIFE_VERSIONS, fdbserver/Knobs.cpp:34), snapshot =
+ * now - U[1e4, 2e5]; 0.1 % of txns get now - 5e6 - 2e4 (tooOld next batch).
+ * RNG: xoshiro256** seeded by splitmix64(0x5EED0000 + config*1000 + i), one
+ * stream per 1,024-transaction chunk.
+ */
+#ifndef FDBCS_WORKLOAD_H
+#define FDBCS_WORKLOAD_H
+#include <stdint.h>
+#include "../../include/fdbcs.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fdbwl fdbwl;
+
+/* txns = 0 selects the config's default batch size. threads = 0: all cores. */
+fdbwl* fdbwl_create(int32_t config, int32_t txns, int32_t threads);
+void   fdbwl_destroy(fdbwl* g);
+
+/* Generates batch `index`.  *view points into generator-owned host memory that
+ * stays valid until the next call on g. */
+int    fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* view, int64_t* now, int64_t* new_oldest);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

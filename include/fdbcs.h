@@ -1,0 +1,200 @@
+/*
+ * fdbcs.h -- C ABI of the MI355X-native FoundationDB Resolver conflict set.
+ *
+ * This is the drop-in boundary for the Resolver's conflict-detection engine.
+ * In the reference that engine is fdbserver/SkipList.cpp behind
+ * fdbserver/ConflictSet.h; its only production caller is
+ * fdbserver/Resolver.actor.cpp:47,51,140-166.  Every entry point below says
+ * which reference interface it replaces.  The C++ drop-in TU
+ * (foundationdb_amd/shim/ConflictSetShim.cpp) maps ConflictSet.h onto these
+ * calls 1:1; see INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no C++ or torch types.
+ *   - Every function returning int returns 0 on success and a negative
+ *     FDBCS_E* code on failure (the reference ASSERTs -> internal_error,
+ *     flow/Error.h:86; the shim turns a nonzero status into that throw).
+ *   - Calls on one fdbcs are strictly serialized, as in the reference
+ *     (Resolver.actor.cpp:104-122: one network thread, batches in version
+ *     order).  Different fdbcs objects are independent.
+ *   - Keys are byte strings compared unsigned-lexicographically, a proper
+ *     prefix first (SkipList.cpp:113-120).  Every range must satisfy
+ *     begin < end (reference precondition); violating it
+ *     returns FDBCS_E_RANGE.
+ */
+#ifndef FDBCS_H
+#define FDBCS_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Verdict bytes: numeric values of ConflictBatch::TransactionCommitResult
+ * (ConflictSet.h:36-40).  The proxy takes the min across resolvers
+ * (MasterProxyServer.actor.cpp:566), so the order matters. */
+#define FDBCS_CONFLICT  0
+#define FDBCS_TOO_OLD   1
+#define FDBCS_COMMITTED 2
+
+/* Status codes. */
+#define FDBCS_OK          0
+#define FDBCS_E_HIP      -1   /* a HIP runtime call failed                    */
+#define FDBCS_E_NOMEM    -2   /* device or host allocation failed             */
+#define FDBCS_E_RANGE    -3   /* a range with begin >= end                     */
+#define FDBCS_E_STATE    -4   /* call out of order (e.g. add without begin)    */
+#define FDBCS_E_ARG      -5   /* bad argument (null pointer, negative count)   */
+#define FDBCS_E_KEY      -6   /* key longer than FDBCS_MAX_KEY                 */
+#define FDBCS_E_NODEV    -7   /* no HIP device / extension not usable          */
+#define FDBCS_E_CAPACITY -8   /* an internal device capacity was exceeded      */
+
+/* Longest key accepted: SYSTEM_KEY_SIZE_LIMIT (fdbclient/Knobs.cpp:58) plus
+ * one byte for keyAfter() (fdbclient/FDBTypes.h:269-279). */
+#define FDBCS_MAX_KEY 30001
+
+typedef struct fdbcs fdbcs;
+
+/* One conflict range [begin, end) -- KeyRangeRef (fdbclient/FDBTypes.h:161). */
+typedef struct fdbcs_range {
+    const uint8_t* begin;
+    uint32_t       begin_len;
+    const uint8_t* end;
+    uint32_t       end_len;
+} fdbcs_range;
+
+/*
+ * A whole batch in packed structure-of-arrays form.  All pointers are either
+ * host pointers (fdbcs_batch_detect_packed) or device pointers
+ * (fdbcs_detect_device).  Transaction t owns reads
+ * [read_off[t], read_off[t+1]) and writes [write_off[t], write_off[t+1]).
+ * Key slots: read r has begin slot 2r and end slot 2r+1; write w has begin
+ * slot 2R+2w and end slot 2R+2w+1 (R = read_count).  Slot s is the byte
+ * string key_bytes[key_off[s] .. key_off[s]+key_len[s]).
+ * Every transaction is listed, including ones that will turn out tooOld: the
+ * engine applies the tooOld rule itself (SkipList.cpp:985), so a staged batch
+ * does not depend on the conflict set's state.
+ */
+typedef struct fdbcs_batch_view {
+    int32_t         txn_count;      /* T */
+    int32_t         read_count;     /* R */
+    int32_t         write_count;    /* W */
+    int32_t         reserved;
+    const int64_t*  snapshot;       /* [T]   CommitTransactionRef::read_snapshot */
+    const int32_t*  read_off;       /* [T+1] */
+    const int32_t*  write_off;      /* [T+1] */
+    const uint64_t* key_off;        /* [2R+2W] */
+    const uint32_t* key_len;        /* [2R+2W] */
+    const uint8_t*  key_bytes;
+    uint64_t        key_bytes_len;
+} fdbcs_batch_view;
+
+/* Optional construction parameters (NULL = defaults). */
+typedef struct fdbcs_config {
+    int32_t  device;            /* HIP device ordinal, -1 = current            */
+    int32_t  reserved0;
+    int64_t  max_history;       /* boundaries to pre-size for (0 = default)    */
+    int64_t  max_batch_keys;    /* key slots per batch to pre-size (0 = grow)  */
+    int64_t  tail_arena_bytes;  /* device bytes for keys > 17 B (0 = default)  */
+} fdbcs_config;
+
+/* ---- ConflictSet lifecycle ------------------------------------------------ */
+
+/* newConflictSet() (ConflictSet.h:28, SkipList.cpp:956): empty history, every
+ * key at version v0 (the reference always uses 0), oldestVersion 0,
+ * removalKey "". */
+int  fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg);
+
+/* clearConflictSet(cs, v) (ConflictSet.h:29, SkipList.cpp:957-959): history
+ * reset to "every key at version v"; oldestVersion and removalKey are kept. */
+int  fdbcs_clear(fdbcs* cs, int64_t v);
+
+/* Alias named by the north star; identical to fdbcs_clear. */
+int  fdbcs_set_version(fdbcs* cs, int64_t v);
+
+/* destroyConflictSet() (ConflictSet.h:30, SkipList.cpp:960-962). */
+void fdbcs_destroy(fdbcs* cs);
+
+/* ---- ConflictBatch ----------------------------------------------------------- */
+
+/* ConflictBatch::ConflictBatch(cs) (ConflictSet.h:33, SkipList.cpp:964-967):
+ * starts an empty batch on cs. */
+int  fdbcs_batch_begin(fdbcs* cs);
+
+/* ConflictBatch::addTransaction(tr) (ConflictSet.h:42, SkipList.cpp:979-1008).
+ * Transaction index = call order within the batch.  Key bytes are copied
+ * into pinned staging memory immediately, so the caller's arena may be
+ * released after this returns (stricter than the reference's borrow). */
+int  fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot,
+                     const fdbcs_range* reads, int32_t nreads,
+                     const fdbcs_range* writes, int32_t nwrites);
+
+/* ConflictBatch::detectConflicts(now, newOldestVersion, nonConflicting,
+ * tooOld) (ConflictSet.h:43, SkipList.cpp:1163-1208), synchronous.
+ * verdict[t] receives FDBCS_CONFLICT / FDBCS_TOO_OLD / FDBCS_COMMITTED for
+ * each of the batch's T transactions (T = number of fdbcs_batch_add calls).
+ * Ends the batch. */
+int  fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verdict);
+
+/* Number of transactions added to the current batch. */
+int32_t fdbcs_batch_txn_count(const fdbcs* cs);
+
+/* Whole-batch variants of addTransaction x T + detectConflicts.
+ *   _packed: host-resident batch view; copied H2D through pinned staging.
+ *   _device: batch view whose arrays already live in device memory; verdict
+ *            is a device pointer of T bytes.  If sync != 0 the call returns
+ *            after the work completes, else it returns after enqueueing on the
+ *            conflict set's stream (the next call orders behind it). */
+int  fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* host_batch,
+                               int64_t now, int64_t new_oldest, uint8_t* verdict);
+int  fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* dev_batch,
+                         int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
+                         int sync);
+
+/* ---- Introspection (tests, bench, checkpoint) --------------------------------- */
+
+/* Number of boundaries in the history (skip-list nodes other than the header). */
+int64_t fdbcs_history_size(fdbcs* cs);
+/* Header version v0 and oldestVersion (ConflictSet::oldestVersion). */
+int64_t fdbcs_header_version(const fdbcs* cs);
+int64_t fdbcs_oldest_version(const fdbcs* cs);
+
+/* Copies the history in key order: versions[i], key_len[i], key_off[i] (into
+ * key_bytes).  Capacities are in elements / bytes; returns the number of
+ * boundaries written or a negative status (FDBCS_E_CAPACITY if too small). */
+int64_t fdbcs_dump_history(fdbcs* cs, int64_t cap, int64_t* versions, uint32_t* key_len,
+                           uint64_t* key_off, uint8_t* key_bytes, uint64_t key_bytes_cap);
+/* Replaces the history with the given sorted, distinct boundaries (v0, oldest
+ * and removalKey are set from the arguments).  For tests and warm starts. */
+int  fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint32_t* key_len,
+                        const uint64_t* key_off, const uint8_t* key_bytes,
+                        int64_t v0, int64_t oldest, const uint8_t* removal_key,
+                        uint32_t removal_key_len);
+/* ConflictSet::removalKey: copies up to cap bytes, returns the full length. */
+int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap);
+
+/* Per-stage device time of the last batch in microseconds, in the order of
+ * the reference's PerfDoubleCounters (SkipList.cpp:91-111): [0] encode/sort
+ * (D.Sort), [1] history read check (D.CheckRead), [2] intra-batch
+ * (D.CheckIntraBatch), [3] combine (D.Combine), [4] merge (D.MergeWrite),
+ * [5] compaction (D.RemoveBefore), [6] whole batch.  Only filled when stage
+ * timing is enabled. Returns the number of entries written. */
+int  fdbcs_enable_stage_timing(fdbcs* cs, int on);
+int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
+
+/* The HIP stream the conflict set enqueues on (as void*), for callers that
+ * want to time or order around it. */
+void* fdbcs_stream(fdbcs* cs);
+
+/* Human-readable message for a status code. */
+const char* fdbcs_strerror(int status);
+
+/* Library build identification (git-independent): "fdbcs gfx950 <version>". */
+const char* fdbcs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDBCS_H */

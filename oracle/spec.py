@@ -1,0 +1,168 @@
+"""Naive pure-Python restatement of the Resolver conflict-set semantics.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (``foundationdb_amd``)
+may import this module; only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg use ``oracle/``, and only as the checker.
+
+PARITY UNPINNED.  The reference engine (``fdbserver/SkipList.cpp``) cannot be
+built in this image: it includes ``flow/`` headers that need boost and
+actor-compiler output, neither of which exists here, and the task forbids
+writing stand-ins for them.  The reference ships no golden vectors for this
+path.  This file is therefore a restatement of the
+reference's behaviour read from its source, following SURVEY.md Appendix A
+(which the survey reports as differential-tested against the unmodified
+reference on 90,000 batches).  Every step cites the reference line it follows.
+
+Keys are ``bytes``; Python's ``bytes`` ordering (unsigned lexicographic, a
+proper prefix sorts first) is exactly the reference's ``compare()``
+(``fdbserver/SkipList.cpp:113-120``) and ``SkipList::less`` (``:379-391``).
+
+This version is O(T^2) per batch and is meant for small cases only; the C++
+restatement ``oracle/cpu_spec.cpp`` is the fast oracle and is itself checked
+against this file in ``tests/test_oracle.py``.
+"""
+from bisect import bisect_left
+
+CONFLICT, TOO_OLD, COMMITTED = 0, 1, 2  # ConflictSet.h:36-40 (enum order matters)
+
+
+class SpecConflictSet:
+    """``struct ConflictSet`` (SkipList.cpp:926-954).
+
+    History = step function key -> version held as a sorted list of
+    boundaries (``keys``/``vers``); ``v0`` is the header node's version
+    (SkipList.cpp:487-493), i.e. the version of every key below the first
+    boundary.
+    """
+
+    def __init__(self, v0=0):
+        # newConflictSet(): SkipList.cpp:956, ConflictSet ctor :927
+        self.v0 = v0
+        self.keys = []
+        self.vers = []
+        self.oldest = 0
+        self.removal_key = b""
+
+    def clear(self, v):
+        # clearConflictSet(): SkipList.cpp:957-959 -- oldest and removalKey kept
+        self.v0 = v
+        self.keys = []
+        self.vers = []
+
+    def value_before(self, k):
+        """Version of the last boundary < k, or the header version."""
+        i = bisect_left(self.keys, k)
+        return self.vers[i - 1] if i > 0 else self.v0
+
+    def history(self):
+        return list(zip(self.keys, self.vers))
+
+
+class SpecBatch:
+    """``ConflictBatch`` (ConflictSet.h:32-60, SkipList.cpp:964-1208)."""
+
+    def __init__(self, cs):
+        self.cs = cs
+        self.txns = []  # (too_old, reads, writes, snapshot)
+
+    def add_transaction(self, reads, writes, snapshot):
+        # ConflictBatch::addTransaction, SkipList.cpp:979-1008.  tooOld uses
+        # the oldestVersion of the *previous* batch and needs >= 1 read.
+        too_old = snapshot < self.cs.oldest and len(reads) > 0
+        for b, e in list(reads) + list(writes):
+            assert b < e, "empty range: reference precondition (SURVEY §0.6)"
+        if too_old:
+            self.txns.append((True, [], [], snapshot))
+        else:
+            self.txns.append((False, list(reads), list(writes), snapshot))
+
+    def detect_conflicts(self, now, new_oldest):
+        """Returns (verdict list, nonConflicting list, tooOld list)."""
+        cs = self.cs
+        T = len(self.txns)
+        # 1. checkReadConflictRanges (SkipList.cpp:1210-1233 -> CheckMax
+        #    :755-837): conflict iff max version over the boundaries in
+        #    [b, e), plus valueBefore(b) when b is not a boundary, > snapshot.
+        conflict = [False] * T
+        for t, (too_old, reads, _w, snap) in enumerate(self.txns):
+            for b, e in reads:
+                i = bisect_left(cs.keys, b)
+                if i < len(cs.keys) and cs.keys[i] == b:
+                    m = cs.vers[i]
+                else:
+                    m = cs.vers[i - 1] if i > 0 else cs.v0
+                j = bisect_left(cs.keys, e)
+                for x in range(i, j):
+                    m = max(m, cs.vers[x])
+                if m > snap:  # strict: SkipList.cpp:789,799,805,817
+                    conflict[t] = True
+        # 2. checkIntraBatchConflicts (SkipList.cpp:1133-1153): in index order,
+        #    a read conflicts with writes of earlier *committed* txns.
+        acc = []
+        for t, (too_old, reads, writes, _s) in enumerate(self.txns):
+            if conflict[t]:
+                continue
+            c = too_old or any(rb < we and wb < re_ for rb, re_ in reads for wb, we in acc)
+            conflict[t] = c
+            if not c:
+                acc.extend(writes)
+        # 3. combineWriteConflictRanges (SkipList.cpp:1320-1337): sweep with
+        #    END before BEGIN at equal keys (getCharacter tie digit :169-172),
+        #    so touching ranges stay separate.
+        pts = []
+        for t, (_o, _r, writes, _s) in enumerate(self.txns):
+            if conflict[t]:
+                continue
+            for b, e in writes:
+                pts.append((b, 1))
+                pts.append((e, 0))
+        pts.sort()
+        combined, active = [], 0
+        for k, is_begin in pts:
+            if is_begin:
+                active += 1
+                if active == 1:
+                    combined.append([k, None])
+            else:
+                active -= 1
+                if active == 0:
+                    combined[-1][1] = k
+        # 4. mergeWriteConflictRanges -> SkipList::addConflictRanges
+        #    (SkipList.cpp:511-522), processed last range first.
+        for b, e in reversed(combined):
+            j = bisect_left(cs.keys, e)
+            if not (j < len(cs.keys) and cs.keys[j] == e):
+                vb = cs.vers[j - 1] if j > 0 else cs.v0
+                cs.keys.insert(j, e)
+                cs.vers.insert(j, vb)
+            i = bisect_left(cs.keys, b)
+            j = bisect_left(cs.keys, e)
+            del cs.keys[i:j]
+            del cs.vers[i:j]
+            cs.keys.insert(i, b)
+            cs.vers.insert(i, now)
+        # 5. verdict emission (SkipList.cpp:1188-1196)
+        non_conflicting = [t for t in range(T) if not conflict[t]]
+        too_old_list = [t for t in range(T) if self.txns[t][0]]
+        verdict = [COMMITTED if not conflict[t] else (TOO_OLD if self.txns[t][0] else CONFLICT)
+                   for t in range(T)]
+        # 6. removeBefore window (SkipList.cpp:1198-1206, :665-702)
+        if new_oldest > cs.oldest:
+            cs.oldest = new_oldest
+            j = bisect_left(cs.keys, cs.removal_key)
+            budget = 3 * len(combined) + 10
+            prev_above = True
+            keep_k, keep_v = cs.keys[:j], cs.vers[:j]
+            while j < len(cs.keys) and budget > 0:
+                budget -= 1
+                above = cs.vers[j] >= cs.oldest
+                if above or prev_above:
+                    keep_k.append(cs.keys[j])
+                    keep_v.append(cs.vers[j])
+                prev_above = above
+                j += 1
+            cs.removal_key = cs.keys[j] if j < len(cs.keys) else b""
+            keep_k.extend(cs.keys[j:])
+            keep_v.extend(cs.vers[j:])
+            cs.keys, cs.vers = keep_k, keep_v
+        return verdict, non_conflicting, too_old_list

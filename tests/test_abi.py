@@ -1,0 +1,84 @@
+"""CPU: the C ABI library loads, exports every declared symbol, and fails loudly without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+from foundationdb_amd import _abi
+from foundationdb_amd.batch import PackedBatch
+from foundationdb_amd.workload import Workload
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fdb(?:cs|wl)_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared("fdbcs.h")
+    for n in ["fdbcs_create", "fdbcs_clear", "fdbcs_destroy", "fdbcs_batch_begin", "fdbcs_batch_add",
+              "fdbcs_batch_detect", "fdbcs_detect_device", "fdbcs_dump_history"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_abi.LIB_PATH)
+    for name in declared("fdbcs.h"):
+        assert hasattr(lib, name), name
+    bound = {n for n, _r, _a in _abi.FDBCS_FUNCS}
+    assert set(declared("fdbcs.h")) == bound
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_abi.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_strerror_without_gpu():
+    lib = _abi.lib()
+    assert lib.fdbcs_version().startswith(b"fdbcs gfx950")
+    assert lib.fdbcs_strerror(_abi.E_RANGE) == b"conflict range with begin >= end"
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure mode")
+def test_create_fails_loudly_without_gpu():
+    from foundationdb_amd import ConflictSet, FdbcsError
+    with pytest.raises(FdbcsError) as ei:
+        ConflictSet()
+    assert ei.value.status == _abi.E_NODEV
+
+
+def test_workload_deterministic_and_shaped():
+    for cfg, T, nr, nw in [(1, 2500, 1, 1), (2, 5000, 5, 2), (3, 5000, 5, 2), (4, 5000, 5, 2)]:
+        w1, w2 = Workload(cfg), Workload(cfg)
+        b1, now1, o1 = w1.batch(3)
+        b2, now2, o2 = w2.batch(3)
+        assert (now1, o1) == (now2, o2)
+        assert b1.T == T and b1.R == T * nr and b1.W == T * nw
+        for a in ["snapshot", "read_off", "write_off", "key_off", "key_len", "key_bytes"]:
+            assert np.array_equal(getattr(b1, a), getattr(b2, a)), (cfg, a)
+        b3, _, _ = w1.batch(4)
+        assert not np.array_equal(b1.key_bytes, b3.key_bytes)
+        # every range non-empty (reference precondition)
+        for r in range(0, min(b1.R + b1.W, 2000)):
+            assert b1.key(2 * r) < b1.key(2 * r + 1)
+
+
+def test_workload_versions_follow_survey():
+    _b, now, nold = Workload(2).batch(7)
+    assert now == 10_000_000 + 7 * 10_000 and nold == now - 5_000_000
+    _b, now, nold = Workload(1).batch(7)
+    assert (now, nold) == (57, 7)
+
+
+def test_packed_batch_roundtrip():
+    txns = [(5, [(b"a", b"b"), (b"", b"\x00")], [(b"x", b"y")]), (6, [], []), (7, [], [(b"k" * 40, b"l")])]
+    pb = PackedBatch.from_txns(txns)
+    assert pb.T == 3 and pb.R == 2 and pb.W == 2
+    assert pb.txns() == [(s, r, w) for s, r, w in txns]

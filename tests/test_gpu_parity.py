@@ -1,0 +1,185 @@
+"""GPU parity: the HIP engine vs the CPU oracle, bit-exact on verdicts and history.
+
+Every comparison checks the verdict bytes, the full post-batch boundary list
+(keys and versions), removalKey, oldestVersion and the header version
+(SURVEY.md §8c).  Oracle: oracle/cpu_spec.cpp (itself checked against the
+pure-Python spec and the golden fixtures in test_oracle.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from foundationdb_amd import ConflictBatch, ConflictSet, FdbcsError
+from foundationdb_amd import _abi
+from foundationdb_amd.batch import PackedBatch
+from foundationdb_amd.workload import Workload
+from gen import mixed_stream, tiny_stream
+from oracle import CpuSpec, SpecBatch, SpecConflictSet
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def same_history(g, c):
+    gv, gl, go, gk = g.dump_arrays()
+    cv, cl, co, ck = c.dump_arrays()
+    assert len(gv) == len(cv), (len(gv), len(cv))
+    if len(gv) == 0:
+        return
+    assert np.array_equal(gv, cv), "versions differ"
+    assert np.array_equal(gl, cl), "key lengths differ"
+    n = int(gl.astype(np.int64).sum())
+    assert np.array_equal(gk[:n], ck[:n]), "key bytes differ"
+
+
+def check_pair(g, c, batch, now, nold, history=True):
+    vg = g.detect_packed(batch, now, nold)
+    vc = c.detect_packed(batch, now, nold)
+    assert np.array_equal(vg, vc), (np.nonzero(vg != vc)[0][:10], vg[:20], vc[:20])
+    assert g.oldest_version == c.oldest_version
+    if history:
+        same_history(g, c)
+        assert g.removal_key() == c.removal_key()
+    return vg
+
+
+@pytest.fixture(scope="module")
+def cs(gpu):
+    g = ConflictSet()
+    yield g
+    g.close()
+
+
+def test_golden_fixtures(cs):
+    for name in ["tiny_alphabet", "long_keys", "clear_mid_stream", "appendix_c"]:
+        with open(os.path.join(GOLDEN, f"{name}.json")) as f:
+            streams = json.load(f)["streams"]
+        for stream in streams:
+            cs.clear(0)
+            cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+            for e in stream:
+                if "clear_before" in e:
+                    cs.clear(e["clear_before"])
+                txns = [(s, [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in r],
+                         [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in w]) for s, r, w in e["txns"]]
+                v = cs.detect_packed(PackedBatch.from_txns(txns), e["now"], e["new_oldest"])
+                assert list(v) == e["verdict"], name
+                assert [[k.hex(), ver] for k, ver in cs.history()] == e["history"], name
+                assert cs.removal_key().hex() == e["removal_key"], name
+                assert cs.oldest_version == e["oldest"]
+                assert cs.header_version == e["v0"]
+
+
+@pytest.mark.parametrize("maxlen", [3, 11, 40])
+def test_tiny_streams(cs, maxlen):
+    for seed in range(25):
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        for batch, now, nold in tiny_stream(seed * 13 + maxlen, n_batches=30, maxlen=maxlen):
+            check_pair(cs, c, batch, now, nold)
+
+
+def test_mixed_streams(cs):
+    for seed in range(4):
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        for batch, now, nold in mixed_stream(seed, n_batches=15, max_txns=600, keyspace=5000):
+            check_pair(cs, c, batch, now, nold)
+
+
+def test_per_transaction_api_appends(cs):
+    """ConflictBatch mirror: addTransaction x T + detectConflicts appends like the reference."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    spec = SpecConflictSet()
+    rounds = [
+        (10, 0, [([], [(b"a", b"b")], 0)]),
+        (20, 5, [([(b"a", b"b")], [], 1), ([(b"a", b"b")], [(b"a", b"c")], 10), ([], [(b"c", b"d")], 1),
+                 ([(b"b", b"bb")], [], 15)]),
+    ]
+    for now, nold, txns in rounds:
+        b = ConflictBatch(cs)
+        sb = SpecBatch(spec)
+        for r, w, s in txns:
+            b.add_transaction(r, w, s)
+            sb.add_transaction(r, w, s)
+        nc, to = [99], [98]
+        b.detect_conflicts(now, nold, nc, to)
+        v, snc, sto = sb.detect_conflicts(now, nold)
+        assert nc == [99] + snc and to == [98] + sto
+    assert cs.history() == spec.history()
+
+
+@pytest.mark.parametrize("cfg,T,nb", [(1, 2500, 20), (2, 800, 25), (3, 800, 25), (4, 400, 12)])
+def test_workload_configs_small(cs, cfg, T, nb):
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    wl = Workload(cfg, txns=T)
+    for i in range(nb):
+        batch, now, nold = wl.batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i % 5 == 4 or i == nb - 1))
+
+
+def test_config2_full_batches(cs):
+    """Config 2 at its real batch size (5,000 txns, 5R+2W) from an empty history."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    wl = Workload(2)
+    for i in range(30):
+        batch, now, nold = wl.batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i % 10 == 9))
+
+
+def test_steady_state_preloaded_history(cs):
+    """A multi-million-boundary history with old and new versions; compaction active."""
+    rng = np.random.default_rng(5)
+    n = 1_500_000
+    raw = np.unique(rng.integers(0, 2**63, size=n, dtype=np.int64))
+    keys = raw.astype(">u8").view(np.uint8).reshape(-1, 8)
+    blob = np.concatenate([keys, np.zeros((len(raw), 8), np.uint8)], axis=1).reshape(-1).copy()  # 16-byte keys
+    lens = np.full(len(raw), 16, np.uint32)
+    offs = (np.arange(len(raw), dtype=np.uint64) * 16)
+    vers = rng.integers(4_000_000, 10_000_000, size=len(raw)).astype(np.int64)
+    c = CpuSpec()
+    cs.load_history_arrays(len(raw), vers, lens, offs, blob, v0=0, oldest=4_000_000, removal_key=b"")
+    c.load_history_arrays(len(raw), vers, lens, offs, blob, v0=0, oldest=4_000_000, removal_key=b"")
+    same_history(cs, c)
+    wl = Workload(2)
+    for i in range(12):
+        batch, now, nold = wl.batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i in (0, 11)))
+
+
+def test_empty_and_degenerate_batches(cs):
+    cs.load_history([], [], v0=7, oldest=0, removal_key=b"")
+    c = CpuSpec(v0=7)
+    check_pair(cs, c, PackedBatch.from_txns([]), 10, 5)
+    check_pair(cs, c, PackedBatch.from_txns([(1, [], [])] * 5), 11, 6)
+    check_pair(cs, c, PackedBatch.from_txns([(1, [(b"a", b"b")], [])]), 12, 6)   # tooOld (oldest 6)
+    check_pair(cs, c, PackedBatch.from_txns([(1, [], [(b"", b"\xff")])]), 13, 6)  # blind write commits
+    check_pair(cs, c, PackedBatch.from_txns([(13, [(b"", b"\xff" * 30)], [(b"\x00", b"\x01")])]), 14, 7)
+
+
+def test_errors_leave_state_intact(cs):
+    cs.load_history([b"a", b"m"], [5, 6], v0=1, oldest=0, removal_key=b"")
+    before = cs.history()
+    with pytest.raises(FdbcsError) as ei:
+        cs.detect_packed(PackedBatch.from_txns([(1, [(b"b", b"b")], [])]), 10, 0)
+    assert ei.value.status == _abi.E_RANGE
+    with pytest.raises(FdbcsError) as ei:
+        cs.detect_packed(PackedBatch.from_txns([(1, [], [(b"z", b"a")])]), 10, 0)
+    assert ei.value.status == _abi.E_RANGE
+    with pytest.raises(FdbcsError) as ei:
+        cs.detect_packed(PackedBatch.from_txns([(1, [], [(b"a", b"b" * 30002)])]), 10, 0)
+    assert ei.value.status == _abi.E_KEY
+    assert cs.history() == before
+
+
+def test_load_dump_roundtrip(cs):
+    keys = [b"", b"\x00", b"a", b"a\x00", b"ab" * 20, b"b", b"\xff" * 18]
+    vers = [3, 1, 4, 1, 5, 9, 2]
+    cs.load_history(keys, vers, v0=11, oldest=2, removal_key=b"ab" * 20)
+    assert cs.history() == list(zip(keys, vers))
+    assert cs.removal_key() == b"ab" * 20
+    assert cs.header_version == 11 and cs.oldest_version == 2
