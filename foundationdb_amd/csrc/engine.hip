@@ -92,7 +92,7 @@ struct fdbcs {
     int64_t oldest = 0;
     // capacities of the per-batch buffers
     int64_t capT = -1, capR = -1, capW = -1, capSlots = -1, capBtail = -1, capEdges = -1, capRowWords = -1;
-    int64_t capDirB = -1, capWinPages = -1;
+    int64_t capDirB = -1, capWinPages = -1, capDesc = -1;
     // last known device state (valid after a synchronized batch)
     int64_t known_D = 1, known_free = 0, known_H = 0;
     uint64_t known_tail = 0;
@@ -226,13 +226,13 @@ void free_batch(BatchBufs& b) {
     dfree(b.read_txn); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_r1); dfree(b.rec_w0); dfree(b.rec_w1);
-    dfree(b.pair_bits); dfree(b.edges);
+    dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb.hi); dfree(b.cb.lo); dfree(b.cb.meta); dfree(b.cb.tail);
     dfree(b.ce.hi); dfree(b.ce.lo); dfree(b.ce.meta); dfree(b.ce.tail);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
     dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
-    dfree(b.aff_free_off); dfree(b.aff_freed);
+    dfree(b.aff_free_off); dfree(b.aff_freed); dfree(b.aff_delta); dfree(b.aff_delta_off);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
     dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
     dfree(b.desc_fmeta); dfree(b.desc_ftail);
@@ -268,9 +268,10 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         b.row_words = (int32_t)((n + 31) / 32);
         if ((r = dalloc(b.pair_bits, n * b.row_words))) return r;
         HIPOK(hipMemsetAsync(b.pair_bits, 0, (size_t)n * b.row_words * 4, s));
-        dfree(b.edges);
+        dfree(b.et); dfree(b.eu); dfree(b.csr);
         b.edge_cap = std::max<int64_t>(1, n * (n - 1) / 2);
-        if ((r = dalloc(b.edges, b.edge_cap))) return r;
+        if ((r = dalloc(b.et, b.edge_cap)) || (r = dalloc(b.eu, b.edge_cap)) || (r = dalloc(b.csr, b.edge_cap)))
+            return r;
         cs->capT = n;
     }
     if (R > cs->capR) {
@@ -285,7 +286,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         free_keys(b.cb); free_keys(b.ce);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, n)) || (r = dalloc(b.rec_w1, n)) ||
+        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.rec_w1, 2 * n)) ||
             (r = alloc_keys(b.cb, n)) || (r = alloc_keys(b.ce, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
@@ -322,19 +323,28 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (cd > cs->capDirB) {
         dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
         dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
-        dfree(b.aff_free_off); dfree(b.aff_freed);
-        dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
-        dfree(b.desc_fmeta); dfree(b.desc_ftail);
+        dfree(b.aff_free_off); dfree(b.aff_freed); dfree(b.aff_delta); dfree(b.aff_delta_off);
         const int64_t n = cd + 2;
         if ((r = dalloc(b.aff_flag, n)) || (r = dalloc(b.aff_pos, n)) || (r = dalloc(b.aff_list, n)) ||
             (r = dalloc(b.aff_jlo, n)) || (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) ||
             (r = dalloc(b.aff_parts, n)) || (r = dalloc(b.aff_extra, n)) || (r = dalloc(b.aff_nn_off, n)) ||
             (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
-            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_freed, n)) || (r = dalloc(b.desc_page, n)) ||
-            (r = dalloc(b.desc_cnt, n)) || (r = dalloc(b.desc_max, n)) || (r = dalloc(b.desc_fhi, n)) ||
-            (r = dalloc(b.desc_flo, n)) || (r = dalloc(b.desc_fmeta, n)) || (r = dalloc(b.desc_ftail, n)))
+            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_freed, n)) || (r = dalloc(b.aff_delta, n)) ||
+            (r = dalloc(b.aff_delta_off, n)))
             return r;
         cs->capDirB = cd;
+    }
+    // page descriptors: the merge makes at most cap_dir of them, the compaction
+    // window initialises 2 per window page
+    const int64_t nd = std::max<int64_t>(cd + 2, 2 * cs->capWinPages + 2);
+    if (nd > cs->capDesc) {
+        dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
+        dfree(b.desc_fmeta); dfree(b.desc_ftail);
+        if ((r = dalloc(b.desc_page, nd)) || (r = dalloc(b.desc_cnt, nd)) || (r = dalloc(b.desc_max, nd)) ||
+            (r = dalloc(b.desc_fhi, nd)) || (r = dalloc(b.desc_flo, nd)) || (r = dalloc(b.desc_fmeta, nd)) ||
+            (r = dalloc(b.desc_ftail, nd)))
+            return r;
+        cs->capDesc = nd;
     }
     return FDBCS_OK;
 }
@@ -391,9 +401,8 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     record(cs, 2);
     launch_sort_ranges(v, b, s);
     launch_edges(v, b, sc, s);
-    launch_decide(v, b, sc, s);
     record(cs, 3);
-    if (W > 0) launch_combine(v, b, sc, s);
+    launch_decide(v, b, sc, s);
     record(cs, 4);
     launch_merge(v, b, h, cs->cur, sc, now, cs->v0, s);
     cs->cur ^= 1;
@@ -545,6 +554,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     };
     if (hipSetDevice(dev) != hipSuccess) return fail(FDBCS_E_HIP);
     if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) return fail(FDBCS_E_HIP);
+    configure_batch_kernels();
     if ((r = dalloc(cs->sc, 1))) return fail(r);
     if (hipHostMalloc((void**)&cs->sc_host, sizeof(Scalars), hipHostMallocDefault) != hipSuccess)
         return fail(FDBCS_E_NOMEM);

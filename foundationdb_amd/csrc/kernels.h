@@ -25,14 +25,16 @@ struct BatchBufs {
     uint8_t* btail;      // tail bytes of batch keys (8-aligned)
     uint64_t btail_cap;
     // sort records
-    SRec* rec_r0; SRec* rec_r1;   // [R]
-    SRec* rec_w0; SRec* rec_w1;   // [W]
-    SRec* sr;            // sorted reads (one of rec_r0/1)
-    SRec* sw;            // sorted writes (one of rec_w0/1)
+    SRec* rec_r0; SRec* rec_r1;   // [R]   read begins
+    SRec* rec_w0; SRec* rec_w1;   // [2W]  write endpoints
+    SRec* sr;            // sorted read begins
+    SRec* sw;            // sorted write endpoints
     // intra-batch overlap dedup matrix and edges
     uint32_t* pair_bits; // [T * row_words]
     int32_t row_words;
-    int32_t* edges;      // [edge_cap]
+    int32_t* et;         // [edge_cap] reader of each unique overlap pair
+    int32_t* eu;         // [edge_cap] earlier writer
+    int32_t* csr;        // [edge_cap] sources bucketed by reader
     int64_t edge_cap;
     // combined write ranges [W]
     KeyArrays cb, ce;
@@ -50,6 +52,8 @@ struct BatchBufs {
     int32_t* aff_extra;  // extra pages beyond the first
     int32_t* aff_nn_off; int32_t* aff_parts_off; int32_t* aff_extra_off; int32_t* aff_free_off;
     int32_t* aff_freed;  // 1 if the page disappears
+    int32_t* aff_delta;  // output boundaries minus input boundaries
+    int32_t* aff_delta_off;
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order
     int32_t* ne_ins;     // insertion index in the old page
@@ -59,7 +63,7 @@ struct BatchBufs {
     // compaction window
     uint8_t* win_keep;   // [window pages * PAGE]
     int32_t* win_cnt;    // survivors per window page
-    int32_t* win_off;    // [win_cap_pages + 2]: offsets, then the window page count
+    int32_t* win_off;    // [win_cap_pages + 1]
     int32_t win_cap_pages;
     // scan scratch
     int64_t* scan_tmp;   // [>= 1024]
@@ -96,6 +100,7 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s);
 void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void configure_batch_kernels();
 
 // ---- history stages (kernels_hist.hip) ----
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,

@@ -19,16 +19,13 @@ namespace fdbcs_dev {
 __global__ __launch_bounds__(256) void k_prep(int T, const int64_t* __restrict__ snap, const int32_t* __restrict__ ro,
                                               const int32_t* __restrict__ wo, int64_t oldest,
                                               uint8_t* __restrict__ too_old, uint8_t* __restrict__ hist,
-                                              int32_t* __restrict__ read_txn, int32_t* __restrict__ write_txn,
-                                              int32_t* __restrict__ deg, int32_t* __restrict__ cur) {
+                                              int32_t* __restrict__ read_txn, int32_t* __restrict__ write_txn) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const int r0 = ro[t], r1 = ro[t + 1];
     // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
     too_old[t] = (snap[t] < oldest && r1 > r0) ? 1 : 0;
     hist[t] = 0;
-    deg[t] = 0;
-    cur[t] = 0;
     for (int r = r0; r < r1; r++) read_txn[r] = t;
     for (int w = wo[t], w1 = wo[t + 1]; w < w1; w++) write_txn[w] = t;
 }
@@ -37,7 +34,7 @@ void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalar
     (void)sc;
     if (v.txn_count == 0) return;
     hipLaunchKernelGGL(k_prep, dim3(cdiv(v.txn_count, 256)), dim3(256), 0, s, v.txn_count, v.snapshot, v.read_off,
-                       v.write_off, oldest, b.too_old, b.hist, b.read_txn, b.write_txn, b.deg, b.cur);
+                       v.write_off, oldest, b.too_old, b.hist, b.read_txn, b.write_txn);
 }
 
 // -------------------------------------------------------------- encode ----
@@ -160,251 +157,422 @@ void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int
 }
 
 // ---------------------------------------------------------------- sort ----
-// Merge sort of range begin keys: bitonic sort of 1024-record tiles in LDS,
-// then merge passes where every record finds its rank in the partner run by
-// binary search.  Ties between equal keys are irrelevant downstream (SURVEY.md
-// Appendix A, note on ties), so stability is not needed.
-static constexpr uint32_t INVALID = 0xFFFFFFFFu;
-static constexpr int SORT_TILE = 1024;
+// Two sorts per batch, in the same launches: the begin keys of all reads
+// (slots 2r) and all write endpoints (slots 2R+i, begins even, ends odd).
+// The order is total: key, then write END before write BEGIN at equal keys
+// (the reference's tie digit, SkipList.cpp:169-172, which makes touching
+// ranges stay separate in the combine), then slot.  A total order means no
+// ties, so every merge below is "count the partner elements that are less".
+//
+//   k_sort_tiles : one 1024-thread workgroup sorts a 4096-item tile in LDS:
+//                  4 items per lane sorted in registers, then 10 rank-merge
+//                  rounds (binary search in the partner run, scatter).
+//   k_sort_kmerge: each item finds its rank in every other tile of its job
+//                  (interleaved binary searches) and lands in place.
+//   k_merge_pass : pairwise fallback when a job has more than KMAX tiles.
+static constexpr int ST_THREADS = 1024;
+static constexpr int ST_ITEMS = 4;
+static constexpr int ST_TILE = ST_THREADS * ST_ITEMS;
+static constexpr int KMAX = 16;
 
-__device__ inline Key rec_key(const SRec& r, const uint8_t* const* tails, int64_t slot_base) {
-    return Key{r.hi, r.lo, r.meta, key_len(r.meta) > 17 ? tails[slot_base + 2 * (int64_t)r.idx] : nullptr};
+// key order with the tail fetched only when both keys are > 17 bytes and
+// share their first 17 bytes
+__device__ inline int rec_kcmp(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+    if (a.meta == b.meta && key_len(a.meta) <= 17) return 0;
+    if ((a.meta >> 24) != (b.meta >> 24)) return (a.meta >> 24) < (b.meta >> 24) ? -1 : 1;
+    const uint32_t la = key_len(a.meta), lb = key_len(b.meta);
+    if (la > 17 && lb > 17) return tail_cmp(tails[a.idx], la, tails[b.idx], lb);
+    return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 
-__device__ inline bool rec_less(const SRec& a, const SRec& b, const uint8_t* const* tails, int64_t slot_base) {
-    if (a.idx == INVALID) return false;
-    if (b.idx == INVALID) return true;
-    return kcmp(rec_key(a, tails, slot_base), rec_key(b, tails, slot_base)) < 0;
+__device__ inline bool rec_lt(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    const int c = rec_kcmp(a, b, tails);
+    if (c) return c < 0;
+    const uint32_t pa = a.idx & 1, pb = b.idx & 1;  // odd slot = range end: ends first
+    if (pa != pb) return pa > pb;
+    return a.idx < b.idx;
 }
 
-__global__ __launch_bounds__(256) void k_block_sort(int n, KeyArrays keys, int64_t slot_base, SRec* __restrict__ out) {
-    __shared__ SRec sm[SORT_TILE];
-    const int base = blockIdx.x * SORT_TILE;
-    for (int i = threadIdx.x; i < SORT_TILE; i += blockDim.x) {
-        const int g = base + i;
-        if (g < n) {
-            const int64_t slot = slot_base + 2 * (int64_t)g;
-            sm[i] = SRec{keys.hi[slot], keys.lo[slot], keys.meta[slot], (uint32_t)g};
-        } else {
-            sm[i] = SRec{~0ull, ~0ull, ~0u, INVALID};
+// key-only compare of a record against a key
+__device__ inline int rec_vs_key(const SRec& a, const Key& k, const uint8_t* const* tails) {
+    if (a.hi != k.hi) return a.hi < k.hi ? -1 : 1;
+    if (a.lo != k.lo) return a.lo < k.lo ? -1 : 1;
+    return kcmp(a.hi, a.lo, a.meta, key_len(a.meta) > 17 ? tails[a.idx] : nullptr, k.hi, k.lo, k.meta, k.tail);
+}
+
+struct SortJobs {
+    int32_t n[2];          // items per job
+    int32_t tiles[2];      // tiles per job
+    int64_t sbase[2];      // slot of item 0
+    int32_t sstride[2];    // slot step per item
+    SRec* tmp[2];          // tile-sorted output
+    SRec* out[2];          // final output
+};
+
+__device__ inline void cswap(SRec& a, SRec& b, bool va, bool vb, const uint8_t* const* tails) {
+    // invalid (beyond n) items sort last
+    const bool sw = (!va && vb) || (va && vb && rec_lt(b, a, tails));
+    if (sw) {
+        SRec t = a;
+        a = b;
+        b = t;
+    }
+}
+
+__global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays keys) {
+    extern __shared__ __attribute__((aligned(16))) SRec sm[];
+    const int job = blockIdx.x < J.tiles[0] ? 0 : 1;
+    const int tile = job ? blockIdx.x - J.tiles[0] : blockIdx.x;
+    const int n = J.n[job];
+    const int base = tile * ST_TILE;
+    const int nt = min(ST_TILE, n - base);
+    const uint8_t* const* tails = keys.tail;
+    const int tid = threadIdx.x;
+    SRec r[ST_ITEMS];
+    bool v[ST_ITEMS];
+#pragma unroll
+    for (int k = 0; k < ST_ITEMS; k++) {
+        const int p = tid * ST_ITEMS + k;
+        v[k] = p < nt;
+        if (v[k]) {
+            const int64_t slot = J.sbase[job] + (int64_t)(base + p) * J.sstride[job];
+            r[k] = SRec{keys.hi[slot], keys.lo[slot], keys.meta[slot], (uint32_t)slot};
         }
     }
+    const int nv = (int)v[0] + v[1] + v[2] + v[3];
+    cswap(r[0], r[1], v[0], v[1], tails);
+    cswap(r[2], r[3], v[2], v[3], tails);
+    cswap(r[0], r[2], v[0], v[2], tails);
+    cswap(r[1], r[3], v[1], v[3], tails);
+    cswap(r[1], r[2], v[1], v[2], tails);
+#pragma unroll
+    for (int k = 0; k < ST_ITEMS; k++)
+        if (k < nv) sm[tid * ST_ITEMS + k] = r[k];
     __syncthreads();
-    for (int k = 2; k <= SORT_TILE; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < SORT_TILE; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const SRec a = sm[i], c = sm[ixj];
-                    const bool up = (i & k) == 0;
-                    const bool sw = up ? rec_less(c, a, keys.tail, slot_base) : rec_less(a, c, keys.tail, slot_base);
-                    if (sw) {
-                        sm[i] = c;
-                        sm[ixj] = a;
-                    }
+    for (int w = ST_ITEMS; w < nt; w <<= 1) {
+        int np[ST_ITEMS];
+#pragma unroll
+        for (int k = 0; k < ST_ITEMS; k++) {
+            const int p = tid * ST_ITEMS + k;
+            np[k] = -1;
+            if (p < nt) {
+                r[k] = sm[p];
+                const int run = p / w;
+                const int ps = (run ^ 1) * w;
+                const int pe = min(ps + w, nt);
+                int lo = ps, hi = max(ps, pe);
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (rec_lt(sm[mid], r[k], tails)) lo = mid + 1;
+                    else hi = mid;
                 }
+                np[k] = (run & ~1) * w + (p - run * w) + (lo - ps);
             }
-            __syncthreads();
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ST_ITEMS; k++)
+            if (np[k] >= 0) sm[np[k]] = r[k];
+        __syncthreads();
+    }
+    SRec* out = J.tiles[job] == 1 ? J.out[job] : J.tmp[job];
+    for (int p = tid; p < nt; p += blockDim.x) out[base + p] = sm[p];
+}
+
+__global__ __launch_bounds__(256) void k_sort_kmerge(SortJobs J, const uint8_t* const* tails) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int job = g < J.n[0] ? 0 : 1;
+    const int i = job ? g - J.n[0] : g;
+    if (i >= J.n[job] || J.tiles[job] <= 1) return;
+    const SRec* in = J.tmp[job];
+    const int n = J.n[job], nt = J.tiles[job];
+    const SRec x = in[i];
+    const int mytile = i / ST_TILE;
+    int lo[KMAX], hi[KMAX];
+#pragma unroll
+    for (int t = 0; t < KMAX; t++) {
+        lo[t] = min(n, t * ST_TILE);
+        hi[t] = (t < nt && t != mytile) ? min(n, (t + 1) * ST_TILE) : lo[t];
+    }
+    bool active = true;
+    while (active) {
+        active = false;
+#pragma unroll
+        for (int t = 0; t < KMAX; t++) {
+            if (lo[t] < hi[t]) {
+                const int mid = (lo[t] + hi[t]) >> 1;
+                if (rec_lt(in[mid], x, tails)) lo[t] = mid + 1;
+                else hi[t] = mid;
+                active = true;
+            }
         }
     }
-    for (int i = threadIdx.x; i < SORT_TILE; i += blockDim.x) {
-        const int g = base + i;
-        if (g < n) out[g] = sm[i];
-    }
+    int pos = i - mytile * ST_TILE;
+#pragma unroll
+    for (int t = 0; t < KMAX; t++)
+        if (t < nt && t != mytile) pos += lo[t] - t * ST_TILE;
+    J.out[job][pos] = x;
 }
 
 __global__ __launch_bounds__(256) void k_merge_pass(int n, int width, const SRec* __restrict__ in,
-                                                    SRec* __restrict__ out, const uint8_t* const* tails,
-                                                    int64_t slot_base) {
+                                                    SRec* __restrict__ out, const uint8_t* const* tails) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int run = i / width;
     const int base = (run & ~1) * width;
-    const int a0 = base, a1 = min(n, base + width);
-    const int b0 = a1, b1 = min(n, base + 2 * width);
+    const int ps = (run ^ 1) * width;
+    const int pe = min(n, ps + width);
     const SRec x = in[i];
-    if (run & 1) {  // x in run B: count A records <= x
-        int lo = a0, hi = a1;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (!rec_less(x, in[mid], tails, slot_base)) lo = mid + 1;
-            else hi = mid;
-        }
-        out[base + (i - b0) + (lo - a0)] = x;
-    } else {        // x in run A: count B records < x
-        int lo = b0, hi = b1;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (rec_less(in[mid], x, tails, slot_base)) lo = mid + 1;
-            else hi = mid;
-        }
-        out[base + (i - a0) + (lo - b0)] = x;
+    int lo = min(ps, n), hi = max(lo, pe);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rec_lt(in[mid], x, tails)) lo = mid + 1;
+        else hi = mid;
     }
-}
-
-static SRec* sort_one(int n, KeyArrays keys, int64_t slot_base, SRec* buf0, SRec* buf1, hipStream_t s) {
-    if (n == 0) return buf0;
-    hipLaunchKernelGGL(k_block_sort, dim3(cdiv(n, SORT_TILE)), dim3(256), 0, s, n, keys, slot_base, buf0);
-    SRec* src = buf0;
-    SRec* dst = buf1;
-    for (int width = SORT_TILE; width < n; width <<= 1) {
-        hipLaunchKernelGGL(k_merge_pass, dim3(cdiv(n, 256)), dim3(256), 0, s, n, width, (const SRec*)src, dst,
-                           (const uint8_t* const*)keys.tail, slot_base);
-        std::swap(src, dst);
-    }
-    return src;
+    out[base + (i - run * width) + (lo - min(ps, n))] = x;
 }
 
 void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s) {
-    b.sr = sort_one(v.read_count, b.keys, 0, b.rec_r0, b.rec_r1, s);
-    b.sw = sort_one(v.write_count, b.keys, 2 * (int64_t)v.read_count, b.rec_w0, b.rec_w1, s);
+    const int R = v.read_count, W = v.write_count;
+    SortJobs J;
+    J.n[0] = R;
+    J.n[1] = 2 * W;
+    J.sbase[0] = 0;
+    J.sstride[0] = 2;
+    J.sbase[1] = 2 * (int64_t)R;
+    J.sstride[1] = 1;
+    J.tmp[0] = b.rec_r1;
+    J.out[0] = b.rec_r0;
+    J.tmp[1] = b.rec_w1;
+    J.out[1] = b.rec_w0;
+    for (int j = 0; j < 2; j++) J.tiles[j] = cdiv(J.n[j], ST_TILE);
+    b.sr = b.rec_r0;
+    b.sw = b.rec_w0;
+    const int blocks = J.tiles[0] + J.tiles[1];
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_sort_tiles, dim3(blocks), dim3(ST_THREADS), ST_TILE * sizeof(SRec), s, J, b.keys);
+    // jobs with 2..KMAX tiles: one k-way rank merge; more tiles: pairwise passes
+    SortJobs K = J;
+    bool any_k = false;
+    for (int j = 0; j < 2; j++) {
+        if (J.tiles[j] > KMAX) {
+            K.tiles[j] = 1;  // handled below; makes k_sort_kmerge skip this job
+            SRec* a = J.tmp[j];  // ping-pong; the result ends in `a`
+            SRec* c = J.out[j];
+            for (int w = ST_TILE; w < J.n[j]; w <<= 1) {
+                hipLaunchKernelGGL(k_merge_pass, dim3(cdiv(J.n[j], 256)), dim3(256), 0, s, J.n[j], w, (const SRec*)a,
+                                   c, (const uint8_t* const*)b.keys.tail);
+                std::swap(a, c);
+            }
+            if (j == 0) b.sr = a; else b.sw = a;
+        } else if (J.tiles[j] > 1) {
+            any_k = true;
+        }
+    }
+    if (any_k) {
+        const int n = K.n[0] + K.n[1];
+        hipLaunchKernelGGL(k_sort_kmerge, dim3(cdiv(n, 256)), dim3(256), 0, s, K, (const uint8_t* const*)b.keys.tail);
+    }
 }
 
 // --------------------------------------------------------------- edges ----
 // A read r of t and a write w of u overlap iff r.b < w.e && w.b < r.e.
 // Split on which begin comes first (keys only, no ranks):
-//   w.b >= r.b : w in  [lower_bound(W, r.b), lower_bound(W, r.e))  (by reader)
-//   w.b <  r.b : r in  [upper_bound(R, w.b), lower_bound(R, w.e))  (by writer)
+//   w.b >= r.b : the write begins among the sorted write endpoints with key in
+//                [r.b, r.e)                                       (by reader)
+//   w.b <  r.b : the read begins with key in (w.b, w.e)           (by writer)
 // Only pairs u < t where both are still undecided (not tooOld, no history
-// conflict) matter.  A T x T bit matrix dedups pairs: pass 0 sets bits and
-// counts unique sources per reader; pass 1 clears them and emits each pair
-// exactly once, leaving the matrix zero for the next batch.
-__device__ inline int lb_rec(const SRec* a, int n, const Key& k, const uint8_t* const* tails, int64_t slot_base) {
+// conflict) matter.  A T x T bit matrix dedups pairs; each new pair is
+// appended to (et, eu) through one global counter.  The decision kernel
+// clears the bits it consumes, leaving the matrix zero for the next batch.
+__device__ inline int lb_key(const SRec* a, int n, const Key& k, const uint8_t* const* tails) {
     int lo = 0, hi = n;
     while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (kcmp(rec_key(a[mid], tails, slot_base), k) < 0) lo = mid + 1;
+        const int mid = (lo + hi) >> 1;
+        if (rec_vs_key(a[mid], k, tails) < 0) lo = mid + 1;
         else hi = mid;
     }
     return lo;
 }
-__device__ inline int ub_rec(const SRec* a, int n, const Key& k, const uint8_t* const* tails, int64_t slot_base) {
+__device__ inline int ub_key(const SRec* a, int n, const Key& k, const uint8_t* const* tails) {
     int lo = 0, hi = n;
     while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (kcmp(rec_key(a[mid], tails, slot_base), k) <= 0) lo = mid + 1;
+        const int mid = (lo + hi) >> 1;
+        if (rec_vs_key(a[mid], k, tails) <= 0) lo = mid + 1;
         else hi = mid;
     }
     return lo;
 }
 
-template <int PASS>
-__device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, int32_t* deg, const int32_t* off,
-                                 int32_t* cur, int32_t* edges) {
+__device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, int32_t* et, int32_t* eu,
+                                 int64_t cap, Scalars* sc) {
     uint32_t* word = bits + (int64_t)t * row_words + (u >> 5);
     const uint32_t bit = 1u << (u & 31);
-    if (PASS == 0) {
-        const uint32_t old = atomicOr(word, bit);
-        if (!(old & bit)) atomicAdd(&deg[t], 1);
-    } else {
-        const uint32_t old = atomicAnd(word, ~bit);
-        if (old & bit) edges[off[t] + atomicAdd(&cur[t], 1)] = u;
+    const uint32_t old = atomicOr(word, bit);
+    if (!(old & bit)) {
+        const int idx = atomicAdd(&sc->edges_total, 1);
+        if (idx < cap) {
+            et[idx] = t;
+            eu[idx] = u;
+        }
     }
 }
 
-template <int PASS>
 __global__ __launch_bounds__(256) void k_edges(int R, int W, KeyArrays keys, const SRec* __restrict__ sr,
                                                const SRec* __restrict__ sw, const int32_t* __restrict__ read_txn,
                                                const int32_t* __restrict__ write_txn,
                                                const uint8_t* __restrict__ too_old, const uint8_t* __restrict__ hist,
-                                               uint32_t* bits, int row_words, int32_t* deg, const int32_t* off,
-                                               int32_t* cur, int32_t* edges) {
+                                               uint32_t* bits, int row_words, int32_t* et, int32_t* eu, int64_t cap,
+                                               Scalars* sc) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t wbase = 2 * (int64_t)R;
+    const uint8_t* const* tails = keys.tail;
     if (i < R) {
         const int t = read_txn[i];
         if (too_old[t] || hist[t]) return;
         const Key b = keys.get(2 * (int64_t)i), e = keys.get(2 * (int64_t)i + 1);
-        const int lo = lb_rec(sw, W, b, keys.tail, wbase);
-        const int hi = lb_rec(sw, W, e, keys.tail, wbase);
+        const int lo = lb_key(sw, 2 * W, b, tails);
+        const int hi = lb_key(sw, 2 * W, e, tails);
         for (int k = lo; k < hi; k++) {
-            const int u = write_txn[sw[k].idx];
-            if (u < t && !too_old[u] && !hist[u]) edge_pair<PASS>(t, u, bits, row_words, deg, off, cur, edges);
+            const uint32_t slot = sw[k].idx;
+            if (slot & 1) continue;  // a write end
+            const int u = write_txn[(slot - wbase) >> 1];
+            if (u < t && !too_old[u] && !hist[u]) edge_pair(t, u, bits, row_words, et, eu, cap, sc);
         }
     } else if (i < R + W) {
         const int w = i - R;
         const int u = write_txn[w];
         if (too_old[u] || hist[u]) return;
         const Key b = keys.get(wbase + 2 * (int64_t)w), e = keys.get(wbase + 2 * (int64_t)w + 1);
-        const int lo = ub_rec(sr, R, b, keys.tail, 0);
-        const int hi = lb_rec(sr, R, e, keys.tail, 0);
+        const int lo = ub_key(sr, R, b, tails);
+        const int hi = lb_key(sr, R, e, tails);
         for (int k = lo; k < hi; k++) {
-            const int t = read_txn[sr[k].idx];
-            if (t > u && !too_old[t] && !hist[t]) edge_pair<PASS>(t, u, bits, row_words, deg, off, cur, edges);
+            const int t = read_txn[sr[k].idx >> 1];
+            if (t > u && !too_old[t] && !hist[t]) edge_pair(t, u, bits, row_words, et, eu, cap, sc);
         }
     }
 }
 
 void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    const int R = v.read_count, W = v.write_count, T = v.txn_count;
-    const int n = R + W;
-    if (n > 0 && R > 0 && W > 0) {
-        hipLaunchKernelGGL(k_edges<0>, dim3(cdiv(n, 256)), dim3(256), 0, s, R, W, b.keys, (const SRec*)b.sr,
+    const int R = v.read_count, W = v.write_count;
+    if (R > 0 && W > 0)
+        hipLaunchKernelGGL(k_edges, dim3(cdiv(R + W, 256)), dim3(256), 0, s, R, W, b.keys, (const SRec*)b.sr,
                            (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old, b.hist, b.pair_bits, b.row_words,
-                           b.deg, b.off, b.cur, b.edges);
-    }
-    scan_i32(b.deg, b.off, nullptr, T, &sc->edges_total, b.scan_tmp, s);
-    if (n > 0 && R > 0 && W > 0) {
-        hipLaunchKernelGGL(k_edges<1>, dim3(cdiv(n, 256)), dim3(256), 0, s, R, W, b.keys, (const SRec*)b.sr,
-                           (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old, b.hist, b.pair_bits, b.row_words,
-                           b.deg, b.off, b.cur, b.edges);
-    }
+                           b.et, b.eu, b.edge_cap, sc);
 }
 
-// -------------------------------------------------------------- decide ----
-// The order-dependent decision of checkIntraBatchConflicts (SkipList.cpp:
-// 1133-1153): conflict[t] = tooOld[t] || hist[t] || some source u < t (an
-// earlier txn with a write overlapping a read of t) committed.  Txns without
-// sources are decided in parallel.  Dependents are walked in index order in
-// chunks of 64 by one wavefront: each lane folds in its sources from earlier
-// chunks (final), then the chunk's 64x64 lower-triangular dependency masks are
-// resolved by a Jacobi iteration on ballots, which reaches the unique
-// solution of the recurrence in at most depth+1 rounds.
-__global__ __launch_bounds__(1024) void k_decide(int T, const uint8_t* __restrict__ too_old,
-                                                 const uint8_t* __restrict__ hist, const int32_t* __restrict__ deg,
-                                                 const int32_t* __restrict__ off, const int32_t* __restrict__ edges,
-                                                 int32_t* __restrict__ dep_list, int32_t* __restrict__ dep_idx,
-                                                 uint8_t* __restrict__ committed, uint8_t* __restrict__ verdict,
-                                                 Scalars* sc) {
-    extern __shared__ uint32_t cbits[];
-    __shared__ int32_t tmp[1024 / 64 + 1];
+// ------------------------------------------------------ decide + combine ----
+// One workgroup.
+//
+// Decision (checkIntraBatchConflicts, SkipList.cpp:1133-1153):
+//   conflict[t] = tooOld[t] || hist[t] || some source u < t committed,
+// where the sources of t are the unique (t, u) edges.  Edges are bucketed by
+// reader into CSR in LDS.  Txns without sources are decided in parallel;
+// dependents are walked in index order in chunks of 64 by one wavefront:
+// each lane folds in its sources from earlier chunks (final), then the
+// chunk's 64x64 lower-triangular dependency masks are resolved by a Jacobi
+// iteration on ballots, which reaches the unique solution of the recurrence
+// in at most depth+1 rounds.
+//
+// Combine (combineWriteConflictRanges, SkipList.cpp:1320-1337): over the
+// sorted write endpoints (END before BEGIN at equal keys), a counter of open
+// committed writes; a combined range starts at a committed BEGIN seen with the
+// counter at 0 and ends at the committed END that brings it back to 0.  Two
+// workgroup scans: the counter, then the group index.
+struct DecideArgs {
+    int T, R, W;
+    const uint8_t* too_old;
+    const uint8_t* hist;
+    const int32_t* et;
+    const int32_t* eu;
+    uint32_t* bits;
+    int row_words;
+    int64_t edge_cap;
+    int32_t* g_deg;        // [T] global fallback storage (T > LDS_T)
+    int32_t* g_off;        // [T+1]
+    int32_t* g_idx;        // [T]
+    int32_t* csr;          // [E]
+    int32_t* dep_list;     // [T]
+    uint8_t* committed;
+    uint8_t* verdict;
+    const SRec* sw;        // sorted write endpoints [2W]
+    const int32_t* write_txn;
+    KeyArrays keys;
+    KeyArrays cb, ce;
+    Scalars* sc;
+};
+
+static constexpr int DC_THREADS = 1024;
+static constexpr int LDS_T = 8192;  // T up to which deg/off/idx live in LDS
+
+__global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ int32_t tmp[DC_THREADS / 64 + 1];
+    const int T = A.T;
+    const int tid = threadIdx.x, nthr = blockDim.x;
     const int nwords = (T + 31) >> 5;
-    for (int i = threadIdx.x; i < nwords; i += blockDim.x) cbits[i] = 0;
+    uint32_t* cbits = lds;
+    const bool small = T <= LDS_T;
+    int32_t* deg = small ? (int32_t*)(lds + nwords) : A.g_deg;
+    int32_t* off = small ? deg + T : A.g_off;
+    int32_t* didx = small ? off + T + 1 : A.g_idx;
+    Scalars* sc = A.sc;
+    const int E = (int)min((int64_t)sc->edges_total, A.edge_cap);
+
+    for (int i = tid; i < nwords; i += nthr) cbits[i] = 0;
+    for (int t = tid; t < T; t += nthr) deg[t] = 0;
     __syncthreads();
-    int ndep = 0;
-    for (int base = 0; base < T; base += blockDim.x) {
-        const int t = base + threadIdx.x;
+    for (int e = tid; e < E; e += nthr) atomicAdd(&deg[A.et[e]], 1);
+    __threadfence_block();
+    __syncthreads();
+    // CSR offsets, dependents list and the independent decisions
+    int ndep = 0, ebase = 0;
+    for (int base = 0; base < T; base += nthr) {
+        const int t = base + tid;
         const bool valid = t < T;
-        const bool und = valid && !too_old[t] && !hist[t];
-        const int d = valid ? deg[t] : 0;
+        const bool und = valid && !A.too_old[t] && !A.hist[t];
+        const int d = valid ? (small ? deg[t] : atomicAdd(&deg[t], 0)) : 0;
         const bool dep = und && d > 0;
         if (und && d == 0) atomicOr(&cbits[t >> 5], 1u << (t & 31));
         int tot;
         const int ex = block_excl_scan((int)dep, tmp, tot);
-        if (dep) {
-            dep_list[ndep + ex] = t;
-            dep_idx[t] = ndep + ex;
-        } else if (valid) {
-            dep_idx[t] = -1;
+        int etot;
+        const int eex = block_excl_scan(d, tmp, etot);
+        if (valid) {
+            off[t] = ebase + eex;
+            didx[t] = dep ? ndep + ex : -1;
         }
+        if (dep) A.dep_list[ndep + ex] = t;
         ndep += tot;
+        ebase += etot;
+    }
+    if (tid == 0) off[T] = ebase;
+    __threadfence_block();
+    __syncthreads();
+    for (int t = tid; t < T; t += nthr) deg[t] = 0;  // reused as fill cursors
+    __syncthreads();
+    for (int e = tid; e < E; e += nthr) {
+        const int t = A.et[e], u = A.eu[e];
+        A.csr[off[t] + atomicAdd(&deg[t], 1)] = u;
+        A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
     }
     __threadfence_block();
     __syncthreads();
     int iters = 0;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
+    if (tid < 64) {
+        const int lane = tid;
         for (int c0 = 0; c0 < ndep; c0 += 64) {
             const int k = c0 + lane;
             const bool valid = k < ndep;
-            const int t = valid ? dep_list[k] : 0;
+            const int t = valid ? A.dep_list[k] : 0;
             bool ext = false;
             uint64_t L = 0;
             if (valid) {
-                const int e0 = off[t], e1 = e0 + deg[t];
-                for (int e = e0; e < e1 && !ext; e++) {
-                    const int u = edges[e];
-                    const int di = dep_idx[u];
+                for (int e = off[t], e1 = off[t + 1]; e < e1 && !ext; e++) {
+                    const int u = A.csr[e];
+                    const int di = didx[u];
                     if (di >= c0) L |= 1ull << (di - c0);
                     else ext = (cbits[u >> 5] >> (u & 31)) & 1;
                 }
@@ -423,110 +591,90 @@ __global__ __launch_bounds__(1024) void k_decide(int T, const uint8_t* __restric
         }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    for (int t = tid; t < T; t += nthr) {
         const bool c = (cbits[t >> 5] >> (t & 31)) & 1;
-        committed[t] = c;
-        verdict[t] = c ? FDBCS_COMMITTED : (too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+        A.committed[t] = c;
+        A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
-    if (threadIdx.x == 0) {
+    // ---- combine ----
+    const int P = 2 * A.W;
+    const int64_t wbase = 2 * (int64_t)A.R;
+    const int per = (P + nthr - 1) / nthr;
+    const int p0 = min(P, tid * per), p1 = min(P, p0 + per);
+    auto delta_of = [&](int p, bool& is_begin, bool& com) -> int {
+        const uint32_t slot = A.sw[p].idx;
+        const int w = (int)((slot - wbase) >> 1);
+        const int u = A.write_txn[w];
+        com = (cbits[u >> 5] >> (u & 31)) & 1;
+        is_begin = !(slot & 1);
+        return com ? (is_begin ? 1 : -1) : 0;
+    };
+    int sum = 0;
+    for (int p = p0; p < p1; p++) {
+        bool ib, c;
+        sum += delta_of(p, ib, c);
+    }
+    int tot;
+    const int cnt0 = block_excl_scan(sum, tmp, tot);
+    int nstart = 0;
+    {
+        int cnt = cnt0;
+        for (int p = p0; p < p1; p++) {
+            bool ib, c;
+            const int d = delta_of(p, ib, c);
+            if (c && ib && cnt == 0) nstart++;
+            cnt += d;
+        }
+    }
+    int ngroups;
+    int g = block_excl_scan(nstart, tmp, ngroups);
+    {
+        int cnt = cnt0;
+        for (int p = p0; p < p1; p++) {
+            bool ib, c;
+            const int d = delta_of(p, ib, c);
+            if (c && ib && cnt == 0) {
+                A.cb.put(g, A.keys.get(A.sw[p].idx));
+                g++;
+            } else if (c && !ib && cnt == 1) {
+                A.ce.put(g - 1, A.keys.get(A.sw[p].idx));
+            }
+            cnt += d;
+        }
+    }
+    if (tid == 0) {
+        sc->n_comb = ngroups;
         sc->n_dep = ndep;
         sc->jac_iters = iters;
+        sc->edges_total = 0;  // next batch starts a new edge list
     }
 }
 
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
     const int T = v.txn_count;
-    if (T == 0) return;
-    const size_t lds = (size_t)((T + 31) / 32) * 4;
-    hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), lds, s, T, b.too_old, b.hist, b.deg, b.off, b.edges,
-                       b.dep_list, b.dep_idx, b.committed, b.verdict, sc);
-}
-
-// ------------------------------------------------------------- combine ----
-// Union of the committed writes (combineWriteConflictRanges, SkipList.cpp:
-// 1320-1337).  Over writes sorted by begin key, a group starts where the begin
-// is >= the running max of earlier committed ends (END sorts before BEGIN at
-// equal keys, so touching ranges stay separate); the group's range is
-// [first begin, max end).  Single workgroup: a 1024-wide Hillis-Steele
-// running max per chunk plus a carried max.
-static constexpr int COMBINE_THREADS = 512;
-
-struct MaxKey {
-    uint64_t hi, lo;
-    uint32_t meta;
-    uint32_t valid;
-    const uint8_t* tail;
-};
-
-__device__ inline MaxKey mk_max(const MaxKey& a, const MaxKey& b) {
-    if (!a.valid) return b;
-    if (!b.valid) return a;
-    return kcmp(a.hi, a.lo, a.meta, a.tail, b.hi, b.lo, b.meta, b.tail) >= 0 ? a : b;
-}
-
-__global__ __launch_bounds__(COMBINE_THREADS) void k_combine(int R, int W, KeyArrays keys, const SRec* __restrict__ sw,
-                                                  const int32_t* __restrict__ write_txn,
-                                                  const uint8_t* __restrict__ committed, KeyArrays cb, KeyArrays ce,
-                                                  Scalars* sc) {
-    __shared__ MaxKey buf[2][COMBINE_THREADS];
-    __shared__ int32_t tmp[COMBINE_THREADS / 64 + 1];
-    const int64_t wbase = 2 * (int64_t)R;
-    MaxKey carry{0, 0, 0, 0, nullptr};
-    int ngroups = 0;
-    for (int base = 0; base < W; base += COMBINE_THREADS) {
-        const int i = base + threadIdx.x;
-        const bool valid = i < W;
-        int w = 0;
-        bool c = false;
-        SRec rb{};
-        if (valid) {
-            rb = sw[i];
-            w = (int)rb.idx;
-            c = committed[write_txn[w]] != 0;
-        }
-        MaxKey e{0, 0, 0, 0, nullptr};
-        if (c) {
-            const int64_t slot = wbase + 2 * (int64_t)w + 1;
-            e = MaxKey{keys.hi[slot], keys.lo[slot], keys.meta[slot], 1u, keys.tail[slot]};
-        }
-        int cur = 0;
-        buf[cur][threadIdx.x] = e;
-        __syncthreads();
-        for (int d = 1; d < COMBINE_THREADS; d <<= 1) {
-            MaxKey x = buf[cur][threadIdx.x];
-            if (threadIdx.x >= (unsigned)d) x = mk_max(buf[cur][threadIdx.x - d], x);
-            buf[cur ^ 1][threadIdx.x] = x;
-            cur ^= 1;
-            __syncthreads();
-        }
-        MaxKey excl = threadIdx.x > 0 ? buf[cur][threadIdx.x - 1] : MaxKey{0, 0, 0, 0, nullptr};
-        excl = mk_max(carry, excl);
-        bool gs = false;
-        Key bk{};
-        if (c) {
-            bk = Key{rb.hi, rb.lo, rb.meta, key_len(rb.meta) > 17 ? keys.tail[wbase + 2 * (int64_t)w] : nullptr};
-            gs = !excl.valid || kcmp(bk.hi, bk.lo, bk.meta, bk.tail, excl.hi, excl.lo, excl.meta, excl.tail) >= 0;
-        }
-        int tot;
-        const int gex = block_excl_scan((int)gs, tmp, tot);
-        if (gs) {
-            const int g = ngroups + gex;
-            cb.put(g, bk);
-            if (g > 0) ce.put(g - 1, Key{excl.hi, excl.lo, excl.meta, excl.tail});
-        }
-        carry = mk_max(carry, buf[cur][COMBINE_THREADS - 1]);
-        ngroups += tot;
-        __syncthreads();
+    if (T == 0) {
+        hipMemsetAsync(&sc->n_comb, 0, sizeof(int32_t), s);
+        return;
     }
-    if (threadIdx.x == 0) {
-        if (ngroups > 0) ce.put(ngroups - 1, Key{carry.hi, carry.lo, carry.meta, carry.tail});
-        sc->n_comb = ngroups;
-    }
+    DecideArgs A;
+    A.T = T; A.R = v.read_count; A.W = v.write_count;
+    A.too_old = b.too_old; A.hist = b.hist; A.et = b.et; A.eu = b.eu; A.bits = b.pair_bits; A.row_words = b.row_words;
+    A.edge_cap = b.edge_cap;
+    A.g_deg = b.deg; A.g_off = b.off; A.g_idx = b.dep_idx; A.csr = b.csr; A.dep_list = b.dep_list;
+    A.committed = b.committed; A.verdict = b.verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
+    A.cb = b.cb; A.ce = b.ce; A.sc = sc;
+    const int nwords = (T + 31) / 32;
+    const size_t lds = (size_t)nwords * 4 + (T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0);
+    hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
 }
 
-void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    hipLaunchKernelGGL(k_combine, dim3(1), dim3(COMBINE_THREADS), 0, s, v.read_count, v.write_count, b.keys, (const SRec*)b.sw,
-                       b.write_txn, b.committed, b.cb, b.ce, sc);
-}
+void launch_combine(const fdbcs_batch_view&, BatchBufs&, Scalars*, hipStream_t) {}
 
+}  // namespace fdbcs_dev
+
+namespace fdbcs_dev {
+// Kernels use up to 160 KiB of dynamic LDS, which gfx950 grants without an
+// opt-in attribute; nothing to configure.  Clear any stale runtime error so it
+// is not reported by an unrelated later call.
+void configure_batch_kernels() { (void)hipGetLastError(); }
 }  // namespace fdbcs_dev

@@ -9,6 +9,11 @@
 // [b, e): e keeps its pre-batch value
 // valueBefore(e) unless e is already a boundary or the next range's begin;
 // every boundary in [b, e) is erased; b gets version `now`.
+//
+// Launches per batch: merge = bounds, aff_build, aff_plan, scan, page_merge,
+// dir_rebuild, bmax_commit; compaction = win_setup, win_keep, scan,
+// win_repack, win_dir, bmax_commit.  Directory `start[]` (global index of a
+// page's first boundary) is carried forward incrementally, never rescanned.
 #include <algorithm>
 #include "kernels.h"
 #include "devutil.h"
@@ -16,7 +21,8 @@
 
 namespace fdbcs_dev {
 
-static constexpr int GRID_PAGES = 2048;  // workgroups for per-page kernels (grid-stride)
+static constexpr int GRID_PAGES = 4096;  // workgroups for per-page kernels (grid-stride)
+static constexpr int MAXP = 64;          // output parts per page tracked in LDS
 
 // ------------------------------------------------ small single-block scan ----
 template <int NA>
@@ -26,36 +32,44 @@ struct ScanArgs {
 };
 
 // Exclusive scans of NA int32 arrays of the same device-resident length n;
-// out[k][n] receives the total.  One workgroup, contiguous segment per thread.
+// out[k][n] receives the total.  One workgroup, 4096-element tiles, 4
+// consecutive elements per lane.
 template <int NA>
 __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32_t* n_ptr) {
     __shared__ int32_t tmp[1024 / 64 + 1];
     const int n = *n_ptr;
-    const int per = (n + blockDim.x - 1) / blockDim.x;
-    const int beg = min(n, (int)threadIdx.x * per), end = min(n, beg + per);
 #pragma unroll
     for (int k = 0; k < NA; k++) {
-        int s = 0;
-        for (int i = beg; i < end; i++) s += a.in[k][i];
-        int tot;
-        int run = block_excl_scan(s, tmp, tot);
-        for (int i = beg; i < end; i++) {
-            const int x = a.in[k][i];
-            a.out[k][i] = run;
-            run += x;
+        int carry = 0;
+        for (int base = 0; base < n; base += 4096) {
+            const int i0 = base + threadIdx.x * 4;
+            int v[4];
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[j] = i0 + j < n ? a.in[k][i0 + j] : 0;
+                s += v[j];
+            }
+            int tot;
+            int run = carry + block_excl_scan(s, tmp, tot);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (i0 + j < n) a.out[k][i0 + j] = run;
+                run += v[j];
+            }
+            carry += tot;
         }
-        if (threadIdx.x == 0) a.out[k][n] = tot;
+        if (threadIdx.x == 0) a.out[k][n] = carry;
     }
 }
 
 // ------------------------------------------------------- insertion plan ----
 // Per combined range j: where b and e fall in the pre-batch history, whether
-// e needs a node, and the value it keeps.  Marks the pages [pb, pe] touched.
+// e needs a node, and the value it keeps.
 __global__ __launch_bounds__(256) void k_bounds(KeyArrays cb, KeyArrays ce, Pool pool, Dir dir, Scalars* sc,
                                                 int64_t v0, int32_t* __restrict__ pb_o, int32_t* __restrict__ ib_o,
                                                 int32_t* __restrict__ pe_o, int32_t* __restrict__ ie_o,
-                                                uint8_t* __restrict__ need_o, int64_t* __restrict__ vb_o,
-                                                int32_t* __restrict__ aff_flag) {
+                                                uint8_t* __restrict__ need_o, int64_t* __restrict__ vb_o) {
     if (sc->err) return;
     const int nC = sc->n_comb;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -81,60 +95,77 @@ __global__ __launch_bounds__(256) void k_bounds(KeyArrays cb, KeyArrays ce, Pool
     ie_o[j] = i_e;
     need_o[j] = (!found && !touch) ? 1 : 0;
     vb_o[j] = vb;
-    for (int p = p_b; p <= p_e; p++) aff_flag[p] = 1;
 }
 
-__global__ __launch_bounds__(256) void k_aff_scatter(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos,
-                                                     int32_t* __restrict__ list, const Scalars* sc) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < sc->D && flag[p]) list[pos[p]] = p;
+// The affected pages are the union of the intervals [pb_j, pe_j], which are
+// nondecreasing in j; range j contributes the pages after the previous
+// range's pe.  One workgroup: a scan over the contributions.  aff_jlo[a] = the
+// first range touching page a (the contributing one).
+__global__ __launch_bounds__(1024) void k_aff_build(const int32_t* __restrict__ pb, const int32_t* __restrict__ pe,
+                                                    Scalars* sc, int32_t* __restrict__ aff_list,
+                                                    int32_t* __restrict__ aff_jlo) {
+    __shared__ int32_t tmp[1024 / 64 + 1];
+    const int nC = sc->err ? 0 : sc->n_comb;
+    const int per = (nC + blockDim.x - 1) / blockDim.x;
+    const int j0 = min(nC, (int)threadIdx.x * per), j1 = min(nC, j0 + per);
+    int s = 0;
+    for (int j = j0; j < j1; j++) {
+        const int lo = max(pb[j], j > 0 ? pe[j - 1] + 1 : 0);
+        s += max(0, pe[j] - lo + 1);
+    }
+    int tot;
+    int pos = block_excl_scan(s, tmp, tot);
+    for (int j = j0; j < j1; j++) {
+        const int lo = max(pb[j], j > 0 ? pe[j - 1] + 1 : 0);
+        for (int p = lo; p <= pe[j]; p++) {
+            aff_list[pos] = p;
+            aff_jlo[pos] = j;
+            pos++;
+        }
+    }
+    if (threadIdx.x == 0) sc->n_aff = tot;
 }
 
-// Per affected page: the range of combined writes touching it, surviving old
+// One wavefront per affected page: the last range touching it, surviving old
 // entries, new entries landing in it, and how many output pages it becomes.
 __global__ __launch_bounds__(256) void k_aff_plan(Dir dir, const Scalars* sc, const int32_t* __restrict__ aff_list,
                                                   const int32_t* __restrict__ pb, const int32_t* __restrict__ ib,
                                                   const int32_t* __restrict__ pe, const int32_t* __restrict__ ie,
-                                                  const uint8_t* __restrict__ need_e, int32_t* __restrict__ jlo_o,
+                                                  const uint8_t* __restrict__ need_e, const int32_t* __restrict__ jlo_i,
                                                   int32_t* __restrict__ jhi_o, int32_t* __restrict__ nn_o,
                                                   int32_t* __restrict__ parts_o, int32_t* __restrict__ extra_o,
-                                                  int32_t* __restrict__ freed_o) {
-    __shared__ int32_t tmp[256 / 64 + 1];
+                                                  int32_t* __restrict__ freed_o, int32_t* __restrict__ delta_o) {
     const int naff = sc->err ? 0 : sc->n_aff, nC = sc->n_comb;
-    for (int a = blockIdx.x; a < naff; a += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const int wpb = blockDim.x >> 6;
+    for (int a = blockIdx.x * wpb + (threadIdx.x >> 6); a < naff; a += gridDim.x * wpb) {
         const int p = aff_list[a], cntp = dir.cnt[p];
-        int lo = 0, hi = nC;
+        const int jlo = jlo_i[a];
+        int lo = jlo, hi = nC;  // last j with pb[j] <= p
         while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (pe[mid] < p) lo = mid + 1; else hi = mid;
-        }
-        const int jlo = lo;
-        lo = 0; hi = nC;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
+            const int mid = (lo + hi) >> 1;
             if (pb[mid] <= p) lo = mid + 1; else hi = mid;
         }
         const int jhi = lo - 1;
         int erased = 0, nn = 0;
-        for (int j = jlo + threadIdx.x; j <= jhi; j += blockDim.x) {
+        for (int j = jlo + lane; j <= jhi; j += 64) {
             const int s = pb[j] < p ? 0 : ib[j];
             const int en = pe[j] > p ? cntp : ie[j];
             erased += max(0, en - s);
             nn += (pb[j] == p) + (pe[j] == p && need_e[j]);
         }
-        erased = block_reduce_sum(erased, tmp);
-        nn = block_reduce_sum(nn, tmp);
-        if (threadIdx.x == 0) {
+        erased = wave_reduce_sum(erased);
+        nn = wave_reduce_sum(nn);
+        if (lane == 0) {
             const int nout = cntp - erased + nn;
             const int parts = nout == 0 ? 0 : (nout <= PAGE ? 1 : cdiv(nout, FILL));
-            jlo_o[a] = jlo;
             jhi_o[a] = jhi;
             nn_o[a] = nn;
             parts_o[a] = parts;
             extra_o[a] = parts > 1 ? parts - 1 : 0;
             freed_o[a] = parts == 0;
+            delta_o[a] = nout - cntp;
         }
-        __syncthreads();
     }
 }
 
@@ -157,6 +188,16 @@ __device__ inline void copy_tail(const Key& k, uint8_t* arena, uint64_t cap, Sca
     *out = arena + o;
 }
 
+struct DescArrays {
+    int32_t* page;
+    int32_t* cnt;
+    int64_t* maxv;
+    uint64_t* fhi;
+    uint64_t* flo;
+    uint32_t* fmeta;
+    const uint8_t** ftail;
+};
+
 struct MergeArgs {
     Pool pool;
     Dir dir;
@@ -170,27 +211,33 @@ struct MergeArgs {
     KeyArrays cb, ce;
     Pool ne;
     int32_t* ne_ins;
-    int32_t* desc_page;
-    int32_t* desc_cnt;
-    int64_t* desc_max;
-    uint64_t* desc_fhi;
-    uint64_t* desc_flo;
-    uint32_t* desc_fmeta;
-    const uint8_t** desc_ftail;
+    DescArrays desc;
     uint8_t* arena;
     uint64_t arena_cap;
     int64_t now;
 };
 
+__device__ inline void put_entry(const Pool& pool, int64_t d, uint64_t hi, uint64_t lo, uint32_t meta, int64_t ver,
+                                 const uint8_t* tail) {
+    pool.hi[d] = hi; pool.lo[d] = lo; pool.meta[d] = meta; pool.ver[d] = ver; pool.tail[d] = tail;
+}
+
+__device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, uint64_t hi, uint64_t lo,
+                                uint32_t meta, const uint8_t* tail) {
+    D.page[x] = page; D.cnt[x] = cnt; D.fhi[x] = hi; D.flo[x] = lo; D.fmeta[x] = meta; D.ftail[x] = tail;
+}
+
 // One workgroup per affected page: load it into LDS, drop erased entries,
 // merge in the new boundaries, write 0..k output pages (the first in place,
-// the others from the free stack) and their directory descriptors.
+// the others from the free stack) and their directory descriptors.  Part
+// maxima come from LDS atomics as the entries are written.
 __global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
     __shared__ uint64_t o_hi[PAGE], o_lo[PAGE];
     __shared__ uint32_t o_meta[PAGE];
     __shared__ int64_t o_ver[PAGE];
     __shared__ const uint8_t* o_tail[PAGE];
     __shared__ int32_t kb[PAGE + 1];
+    __shared__ long long pmax[MAXP];
     __shared__ int32_t tmp[256 / 64 + 1];
     Scalars* sc = A.sc;
     if (sc->err) return;
@@ -211,17 +258,17 @@ __global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
             o_ver[tid] = A.pool.ver[pbase + tid];
             o_tail[tid] = A.pool.tail[pbase + tid];
         }
+        if (tid < MAXP) pmax[tid] = INT64_MIN;
         // erased iff inside [(pb_j, ib_j), (pe_j, ie_j)) for the last j starting at or before (p, tid)
         int keep = 0;
         if (tid < cntp) {
             int lo = jlo, hi = jhi + 1;
             while (lo < hi) {
-                int mid = (lo + hi) >> 1;
+                const int mid = (lo + hi) >> 1;
                 if (pos_le(A.pb[mid], A.ib[mid], p, tid)) lo = mid + 1; else hi = mid;
             }
             const int j = lo - 1;
-            const bool erased = j >= jlo && pos_lt(p, tid, A.pe[j], A.ie[j]);
-            keep = !erased;
+            keep = !(j >= jlo && pos_lt(p, tid, A.pe[j], A.ie[j]));
         }
         int kept;
         const int kex = block_excl_scan(keep, tmp, kept);
@@ -256,43 +303,48 @@ __global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
         const int nout = kept + nn;
         const int per = parts > 0 ? cdiv(nout, parts) : 1;
         const int xoff = A.extra_off[a];
+        const int doff = A.parts_off[a];
         auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
         if (tid < cntp && keep) {
             int lo = 0, hi = nn;
             while (lo < hi) {
-                int mid = (lo + hi) >> 1;
+                const int mid = (lo + hi) >> 1;
                 if (A.ne_ins[nn_off + mid] <= tid) lo = mid + 1; else hi = mid;
             }
             const int m = kb[tid] + lo;
-            const int q = m / per;
-            const int64_t d = (int64_t)dest(q) * PAGE + (m - q * per);
-            A.pool.hi[d] = o_hi[tid]; A.pool.lo[d] = o_lo[tid]; A.pool.meta[d] = o_meta[tid];
-            A.pool.ver[d] = o_ver[tid]; A.pool.tail[d] = o_tail[tid];
+            const int q = m / per, slot = m - q * per;
+            const int dp = dest(q);
+            put_entry(A.pool, (int64_t)dp * PAGE + slot, o_hi[tid], o_lo[tid], o_meta[tid], o_ver[tid], o_tail[tid]);
+            if (q < MAXP) atomicMax(&pmax[q], (long long)o_ver[tid]);
+            if (slot == 0)
+                put_desc(A.desc, doff + q, dp, min(per, nout - q * per), o_hi[tid], o_lo[tid], o_meta[tid], o_tail[tid]);
         }
         for (int k = tid; k < nn; k += blockDim.x) {
             const int s = nn_off + k;
             const int m = k + kb[A.ne_ins[s]];
-            const int q = m / per;
-            const int64_t d = (int64_t)dest(q) * PAGE + (m - q * per);
-            A.pool.hi[d] = A.ne.hi[s]; A.pool.lo[d] = A.ne.lo[s]; A.pool.meta[d] = A.ne.meta[s];
-            A.pool.ver[d] = A.ne.ver[s]; A.pool.tail[d] = A.ne.tail[s];
+            const int q = m / per, slot = m - q * per;
+            const int dp = dest(q);
+            const uint64_t hi = A.ne.hi[s], lo = A.ne.lo[s];
+            const uint32_t meta = A.ne.meta[s];
+            const int64_t ver = A.ne.ver[s];
+            const uint8_t* tail = A.ne.tail[s];
+            put_entry(A.pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
+            if (q < MAXP) atomicMax(&pmax[q], (long long)ver);
+            if (slot == 0) put_desc(A.desc, doff + q, dp, min(per, nout - q * per), hi, lo, meta, tail);
         }
         __threadfence_block();
         __syncthreads();
-        const int doff = A.parts_off[a];
         for (int q = tid; q < parts; q += blockDim.x) {
-            const int c = min(per, nout - q * per);
-            const int pgq = dest(q);
-            const int64_t bq = (int64_t)pgq * PAGE;
-            int64_t mx = INT64_MIN;
-            for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
-            A.desc_page[doff + q] = pgq;
-            A.desc_cnt[doff + q] = c;
-            A.desc_max[doff + q] = mx;
-            A.desc_fhi[doff + q] = A.pool.hi[bq];
-            A.desc_flo[doff + q] = A.pool.lo[bq];
-            A.desc_fmeta[doff + q] = A.pool.meta[bq];
-            A.desc_ftail[doff + q] = A.pool.tail[bq];
+            int64_t mx;
+            if (q < MAXP) {
+                mx = pmax[q];
+            } else {  // very large outputs (e.g. a first batch into an empty history)
+                const int64_t bq = (int64_t)dest(q) * PAGE;
+                const int c = min(per, nout - q * per);
+                mx = INT64_MIN;
+                for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
+            }
+            A.desc.maxv[doff + q] = mx;
         }
         __syncthreads();
     }
@@ -303,76 +355,93 @@ __device__ inline void dir_copy(const Dir& s, int x, const Dir& d, int y) {
     d.fhi[y] = s.fhi[x]; d.flo[y] = s.flo[x]; d.fmeta[y] = s.fmeta[x]; d.ftail[y] = s.ftail[x];
 }
 
-struct DescArrays {
-    const int32_t* page;
-    const int32_t* cnt;
-    const int64_t* maxv;
-    const uint64_t* fhi;
-    const uint64_t* flo;
-    const uint32_t* fmeta;
-    const uint8_t* const* ftail;
-};
-
 __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y) {
     d.page[y] = s.page[x]; d.cnt[y] = s.cnt[x]; d.maxv[y] = s.maxv[x];
     d.fhi[y] = s.fhi[x]; d.flo[y] = s.flo[x]; d.fmeta[y] = s.fmeta[x]; d.ftail[y] = s.ftail[x];
 }
 
+struct RebuildArgs {
+    Dir src, dst;
+    Scalars* sc;
+    DescArrays desc;
+    const int32_t *aff_list, *parts, *parts_off, *freed, *free_off, *extra_off, *delta_off;
+    int32_t* free_stack;
+};
+
 // Directory after the merge: unaffected entries move by the number of extra
 // pages inserted before them; affected entries are replaced by their parts.
-__global__ __launch_bounds__(256) void k_dir_rebuild(Dir src, Dir dst, const Scalars* sc, DescArrays desc,
-                                                     const int32_t* __restrict__ aff_list,
-                                                     const int32_t* __restrict__ parts,
-                                                     const int32_t* __restrict__ parts_off,
-                                                     const int32_t* __restrict__ freed,
-                                                     const int32_t* __restrict__ free_off,
-                                                     const int32_t* __restrict__ extra_off, int32_t* free_stack) {
+// start[] moves by the boundary-count change of the affected pages before.
+__global__ __launch_bounds__(256) void k_dir_rebuild(RebuildArgs A) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const Scalars* sc = A.sc;
     const int D = sc->D;
-    if (x >= D) return;
     const int naff = sc->err ? 0 : sc->n_aff;
+    const int Dn = naff ? D - naff + A.parts_off[naff] : D;
+    if (x == 0) {
+        A.sc->D_next = Dn;
+        A.sc->free_next = naff ? sc->free_top - A.extra_off[naff] + A.free_off[naff] : sc->free_top;
+        A.dst.start[Dn] = A.src.start[D] + (naff ? A.delta_off[naff] : 0);
+    }
+    if (x >= D) return;
     if (naff == 0) {
-        dir_copy(src, x, dst, x);
+        dir_copy(A.src, x, A.dst, x);
+        A.dst.start[x] = A.src.start[x];
         return;
     }
     int lo = 0, hi = naff;
     while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (aff_list[mid] < x) lo = mid + 1; else hi = mid;
+        const int mid = (lo + hi) >> 1;
+        if (A.aff_list[mid] < x) lo = mid + 1; else hi = mid;
     }
     const int na = lo;
-    const int base = x - na + parts_off[na];
-    if (na < naff && aff_list[na] == x) {
-        const int np = parts[na], off = parts_off[na];
-        for (int q = 0; q < np; q++) desc_copy(desc, off + q, dst, base + q);
-        if (freed[na]) free_stack[sc->free_top - extra_off[naff] + free_off[na]] = src.page[x];
+    const int base = x - na + A.parts_off[na];
+    const int64_t st = A.src.start[x] + A.delta_off[na];
+    if (na < naff && A.aff_list[na] == x) {
+        const int np = A.parts[na], off = A.parts_off[na];
+        int64_t s = st;
+        for (int q = 0; q < np; q++) {
+            desc_copy(A.desc, off + q, A.dst, base + q);
+            A.dst.start[base + q] = s;
+            s += A.desc.cnt[off + q];
+        }
+        if (A.freed[na]) A.free_stack[sc->free_top - A.extra_off[naff] + A.free_off[na]] = A.src.page[x];
     } else {
-        dir_copy(src, x, dst, base);
+        dir_copy(A.src, x, A.dst, base);
+        A.dst.start[base] = st;
     }
 }
 
-__global__ void k_dir_commit(Scalars* sc, const int32_t* parts_off, const int32_t* extra_off,
-                             const int32_t* free_off) {
-    const int naff = sc->err ? 0 : sc->n_aff;
-    if (naff > 0) {
-        sc->D = sc->D - naff + parts_off[naff];
-        sc->free_top = sc->free_top - extra_off[naff] + free_off[naff];
+// Per-64-entry maxima of the new directory (one wavefront per group), then
+// commit the directory size, free-stack top and history size.
+__global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc) {
+    const int Dn = sc->D_next;
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (g * 64 < Dn) {
+        const int x = g * 64 + lane;
+        int64_t m = x < Dn ? d.maxv[x] : INT64_MIN;
+        m = wave_reduce_max(m);
+        if (lane == 0) d.bmax[g] = m;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sc->D = Dn;
+        sc->free_top = sc->free_next;
+        sc->H = d.start[Dn];
     }
 }
 
-__global__ __launch_bounds__(256) void k_bmax(Dir d, const Scalars* sc) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int D = sc->D;
-    if (g * 64 >= D) return;
-    int64_t m = INT64_MIN;
-    for (int x = g * 64; x < min(D, g * 64 + 64); x++) m = max(m, d.maxv[x]);
-    d.bmax[g] = m;
+static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
+    const int groups = cdiv(h.cap_dir, 64);
+    hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc);
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
+    // full recompute of start[] (used after reset / load)
     Dir& d = h.dir[cur];
     scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
-    hipLaunchKernelGGL(k_bmax, dim3(cdiv(cdiv(h.cap_dir, 64), 256)), dim3(256), 0, s, d, sc);
+    hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    launch_bmax_commit(h, cur, sc, s);
 }
 
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
@@ -380,38 +449,41 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     const int W = v.write_count;
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
-    hipMemsetAsync(&sc->n_aff, 0, sizeof(int32_t), s);
     if (W > 0) {
-        hipMemsetAsync(b.aff_flag, 0, sizeof(int32_t) * (size_t)(h.cap_dir + 1), s);
         hipLaunchKernelGGL(k_bounds, dim3(cdiv(W, 256)), dim3(256), 0, s, b.cb, b.ce, h.pool, src, sc, v0, b.pb,
-                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.aff_flag);
-        scan_i32(b.aff_flag, b.aff_pos, &sc->D, 0, &sc->n_aff, b.scan_tmp, s);
-        hipLaunchKernelGGL(k_aff_scatter, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, b.aff_flag, b.aff_pos,
-                           b.aff_list, sc);
-        hipLaunchKernelGGL(k_aff_plan, dim3(GRID_PAGES), dim3(256), 0, s, src, sc, b.aff_list, b.pb, b.ib, b.pe,
-                           b.ie, b.need_e, b.aff_jlo, b.aff_jhi, b.aff_nn, b.aff_parts, b.aff_extra, b.aff_freed);
-        ScanArgs<4> sa;
+                           b.ib, b.pe, b.ie, b.need_e, b.vb);
+    }
+    hipLaunchKernelGGL(k_aff_build, dim3(1), dim3(1024), 0, s, b.pb, b.pe, sc, b.aff_list, b.aff_jlo);
+    if (W > 0) {
+        const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
+        hipLaunchKernelGGL(k_aff_plan, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, 4)))), dim3(256), 0, s,
+                           src, sc, b.aff_list, b.pb, b.ib, b.pe, b.ie, b.need_e, b.aff_jlo, b.aff_jhi, b.aff_nn,
+                           b.aff_parts, b.aff_extra, b.aff_freed, b.aff_delta);
+        ScanArgs<5> sa;
         sa.in[0] = b.aff_nn; sa.out[0] = b.aff_nn_off;
         sa.in[1] = b.aff_parts; sa.out[1] = b.aff_parts_off;
         sa.in[2] = b.aff_extra; sa.out[2] = b.aff_extra_off;
         sa.in[3] = b.aff_freed; sa.out[3] = b.aff_free_off;
-        hipLaunchKernelGGL(k_scan_small<4>, dim3(1), dim3(1024), 0, s, sa, &sc->n_aff);
+        sa.in[4] = b.aff_delta; sa.out[4] = b.aff_delta_off;
+        hipLaunchKernelGGL(k_scan_small<5>, dim3(1), dim3(1024), 0, s, sa, &sc->n_aff);
         MergeArgs A;
         A.pool = h.pool; A.dir = src; A.sc = sc; A.free_stack = h.free_stack; A.aff_list = b.aff_list;
         A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
         A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off;
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
         A.cb = b.cb; A.ce = b.ce; A.ne = b.ne; A.ne_ins = b.ne_ins;
-        A.desc_page = b.desc_page; A.desc_cnt = b.desc_cnt; A.desc_max = b.desc_max; A.desc_fhi = b.desc_fhi;
-        A.desc_flo = b.desc_flo; A.desc_fmeta = b.desc_fmeta; A.desc_ftail = b.desc_ftail;
+        A.desc = DescArrays{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
-        hipLaunchKernelGGL(k_page_merge, dim3(GRID_PAGES), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, max_aff))), dim3(256), 0, s, A);
     }
-    DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
-    hipLaunchKernelGGL(k_dir_rebuild, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, src, dst, sc, da, b.aff_list,
-                       b.aff_parts, b.aff_parts_off, b.aff_freed, b.aff_free_off, b.aff_extra_off, h.free_stack);
-    hipLaunchKernelGGL(k_dir_commit, dim3(1), dim3(1), 0, s, sc, b.aff_parts_off, b.aff_extra_off, b.aff_free_off);
-    launch_dir_finish(h, cur ^ 1, sc, b, s);
+    RebuildArgs R;
+    R.src = src; R.dst = dst; R.sc = sc;
+    R.desc = DescArrays{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
+    R.aff_list = b.aff_list; R.parts = b.aff_parts; R.parts_off = b.aff_parts_off; R.freed = b.aff_freed;
+    R.free_off = b.aff_free_off; R.extra_off = b.aff_extra_off; R.delta_off = b.aff_delta_off;
+    R.free_stack = h.free_stack;
+    hipLaunchKernelGGL(k_dir_rebuild, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, R);
+    launch_bmax_commit(h, cur ^ 1, sc, s);
 }
 
 // ------------------------------------------------------------ compaction ----
@@ -422,77 +494,115 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
 // its version and the version of node g-1 (original values) are < oldest.
 // removalKey becomes the key at g1, or "" at the end.  Survivors of the pages
 // covering the window are repacked into fresh pages at FILL density.
-struct WinState {
-    int64_t g0, g1;
-    int32_t pA, pB, np;
-};
+//
+// k_win_setup runs its searches with a whole wavefront: a 64-ary search over
+// the directory (64 first keys compared per step), then over the page.
+__device__ inline int wave_dir_search(const Dir& dir, int D, const Key& k) {
+    // last j in [0, D) with j == 0 or first(j) <= k
+    const int lane = threadIdx.x & 63;
+    int lo = 1, hi = D;  // answer-1 in [lo-1, hi-1]; find first j in [lo, hi) with first(j) > k
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) / 64;
+        const int j = lo + lane * step;
+        const bool le = j < hi && kcmp(dir_first(dir, j), k) <= 0;
+        const uint64_t m = __ballot(le);
+        const int cnt = __popcll(m);  // lanes 0..cnt-1 are <= k (monotone)
+        if (cnt == 0) { hi = lo; break; }
+        const int nlo = lo + (cnt - 1) * step + 1;
+        const int nhi = min(hi, lo + cnt * step);
+        lo = nlo;
+        hi = nhi;
+        if (cnt == 64) hi = min(hi, D);
+    }
+    const int j = lo + lane;
+    const bool le = j < hi && kcmp(dir_first(dir, j), k) <= 0;
+    return lo - 1 + __popcll(__ballot(le));
+}
 
-__global__ __launch_bounds__(256) void k_win_setup(Pool pool, Dir dir, Scalars* sc, uint64_t* rk_hi, uint64_t* rk_lo,
-                                                   uint32_t* rk_meta, uint8_t* rk_tail, int32_t* win_np) {
-    __shared__ Key nk;
-    __shared__ int has_key;
-    if (threadIdx.x == 0) {
-        const int D = sc->D;
-        const int64_t H = dir.start[D];
-        int64_t g0 = 0, g1 = 0;
-        int pA = 1, pB = 0;
-        has_key = 0;
-        if (!sc->err) {
-            const Key rk{rk_hi[0], rk_lo[0], rk_meta[0], rk_tail};
-            const int p0 = dir_search(dir, D, rk, 1);
-            const int i0 = page_lb(pool, dir.page[p0], 0, dir.cnt[p0], rk);
-            g0 = dir.start[p0] + i0;
-            if (g0 < H) {
-                const int64_t budget = 3 * (int64_t)sc->n_comb + 10;
-                g1 = min(H, g0 + budget);
-                pA = i0 < dir.cnt[p0] ? p0 : p0 + 1;
-                int lo = 0, hi = D;  // last q with start[q] <= g1 - 1
-                while (lo < hi) {
-                    int mid = (lo + hi) >> 1;
-                    if (dir.start[mid] <= g1 - 1) lo = mid + 1; else hi = mid;
-                }
-                pB = lo - 1;
-                if (g1 < H) {
-                    lo = 0; hi = D;
-                    while (lo < hi) {
-                        int mid = (lo + hi) >> 1;
-                        if (dir.start[mid] <= g1) lo = mid + 1; else hi = mid;
-                    }
-                    const int q1 = lo - 1;
-                    nk = pool_key(pool, (int64_t)dir.page[q1] * PAGE + (g1 - dir.start[q1]));
-                    has_key = 1;
-                }
-            } else {
-                g0 = g1 = H;
+__device__ inline int wave_page_lb(const Pool& pool, int page, int cnt, const Key& k) {
+    // first i with key(i) >= k: count of keys < k over up to 256 entries
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)page * PAGE;
+    int c = 0;
+    for (int i = lane; i < cnt; i += 64) c += kcmp(pool_key(pool, b + i), k) < 0;
+    return wave_reduce_sum(c);
+}
+
+__device__ inline int wave_start_search(const int64_t* start, int D, int64_t g) {
+    // last q in [0, D) with start[q] <= g
+    const int lane = threadIdx.x & 63;
+    int lo = 0, hi = D;  // find first q in [lo, hi) with start[q] > g
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) / 64;
+        const int q = lo + lane * step;
+        const bool le = q < hi && start[q] <= g;
+        const int cnt = __popcll(__ballot(le));
+        if (cnt == 0) { hi = lo; break; }
+        const int nlo = lo + (cnt - 1) * step + 1;
+        hi = min(hi, lo + cnt * step);
+        lo = nlo;
+    }
+    const int q = lo + lane;
+    return lo - 1 + __popcll(__ballot(q < hi && start[q] <= g));
+}
+
+__global__ __launch_bounds__(64) void k_win_setup(Pool pool, Dir dir, Scalars* sc, uint64_t* rk_hi, uint64_t* rk_lo,
+                                                  uint32_t* rk_meta, uint8_t* rk_tail) {
+    const int lane = threadIdx.x;
+    const int D = sc->D;
+    const int64_t H = dir.start[D];
+    int64_t g0 = 0, g1 = 0;
+    int pA = 1, pB = 0;
+    bool has_key = false;
+    Key nk{0, 0, 0, nullptr};
+    if (!sc->err) {
+        const Key rk{rk_hi[0], rk_lo[0], rk_meta[0], rk_tail};
+        const int p0 = wave_dir_search(dir, D, rk);
+        const int i0 = wave_page_lb(pool, dir.page[p0], dir.cnt[p0], rk);
+        g0 = dir.start[p0] + i0;
+        if (g0 < H) {
+            const int64_t budget = 3 * (int64_t)sc->n_comb + 10;
+            g1 = min(H, g0 + budget);
+            pA = i0 < dir.cnt[p0] ? p0 : p0 + 1;
+            pB = wave_start_search(dir.start, D, g1 - 1);
+            if (g1 < H) {
+                const int q1 = wave_start_search(dir.start, D, g1);
+                nk = pool_key(pool, (int64_t)dir.page[q1] * PAGE + (g1 - dir.start[q1]));
+                has_key = true;
             }
+        } else {
+            g0 = g1 = H;
         }
+    }
+    if (lane == 0) {
         sc->win_g0 = g0;
         sc->win_g1 = g1;
         sc->win_pA = pA;
         sc->win_pB = pB;
-        *win_np = pB - pA + 1 > 0 ? pB - pA + 1 : 0;
+        sc->win_np = pB - pA + 1 > 0 ? pB - pA + 1 : 0;
+        if (!sc->err) {
+            rk_hi[0] = has_key ? nk.hi : 0;
+            rk_lo[0] = has_key ? nk.lo : 0;
+            rk_meta[0] = has_key ? nk.meta : 0;
+        }
     }
-    __syncthreads();
-    if (sc->err) return;
-    if (threadIdx.x == 0) {
-        rk_hi[0] = has_key ? nk.hi : 0;
-        rk_lo[0] = has_key ? nk.lo : 0;
-        rk_meta[0] = has_key ? nk.meta : 0;
-    }
-    if (has_key && key_len(nk.meta) > 17) {
+    if (!sc->err && has_key && key_len(nk.meta) > 17) {
         const uint32_t words = (key_len(nk.meta) - 17 + 7) / 8;
         const uint64_t* s = reinterpret_cast<const uint64_t*>(nk.tail);
         uint64_t* d = reinterpret_cast<uint64_t*>(rk_tail);
-        for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) d[w] = s[w];
+        for (uint32_t w = lane; w < words; w += 64) d[w] = s[w];
     }
 }
 
 __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scalars* sc, int64_t oldest,
-                                                  uint8_t* __restrict__ keep_o, int32_t* __restrict__ cnt_o) {
+                                                  uint8_t* __restrict__ keep_o, int32_t* __restrict__ cnt_o,
+                                                  int64_t* __restrict__ part_max) {
     __shared__ int32_t tmp[256 / 64 + 1];
     const int64_t g0 = sc->win_g0, g1 = sc->win_g1;
-    const int pA = sc->win_pA, pB = sc->win_pB;
-    for (int w = blockIdx.x; w <= pB - pA; w += gridDim.x) {
+    const int pA = sc->win_pA, np = sc->win_np;
+    for (int w = blockIdx.x; w < np; w += gridDim.x) {
+        // the repack makes at most ceil(np * PAGE / FILL) <= 2 * np pages
+        if (threadIdx.x < 2) part_max[2 * w + threadIdx.x] = INT64_MIN;
         const int q = pA + w;
         const int pg = dir.page[q], c = dir.cnt[q];
         const int64_t st = dir.start[q];
@@ -514,11 +624,12 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
     }
 }
 
+// survivors -> fresh pages at FILL density, with their descriptors
 __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Scalars* sc,
                                                     const uint8_t* __restrict__ keep, const int32_t* __restrict__ off,
-                                                    const int32_t* win_np, const int32_t* __restrict__ free_stack) {
+                                                    const int32_t* __restrict__ free_stack, DescArrays desc) {
     __shared__ int32_t tmp[256 / 64 + 1];
-    const int np = *win_np;
+    const int np = sc->win_np;
     const int pA = sc->win_pA;
     const int top0 = sc->free_top;
     const int S = off[np];
@@ -533,85 +644,70 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Sc
         const int ex = block_excl_scan(kp, tmp, tot);
         if (kp) {
             const int m = off[w] + ex;
-            const int part = m / per;
-            const int64_t d = (int64_t)free_stack[top0 - 1 - part] * PAGE + (m - part * per);
+            const int part = m / per, slot = m - part * per;
+            const int dp = free_stack[top0 - 1 - part];
             const int64_t sidx = (int64_t)pg * PAGE + i;
-            pool.hi[d] = pool.hi[sidx]; pool.lo[d] = pool.lo[sidx]; pool.meta[d] = pool.meta[sidx];
-            pool.ver[d] = pool.ver[sidx]; pool.tail[d] = pool.tail[sidx];
+            const uint64_t hi = pool.hi[sidx], lo = pool.lo[sidx];
+            const uint32_t meta = pool.meta[sidx];
+            const int64_t ver = pool.ver[sidx];
+            const uint8_t* tail = pool.tail[sidx];
+            put_entry(pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
+            atomicMax((long long*)&desc.maxv[part], (long long)ver);
+            if (slot == 0) put_desc(desc, part, dp, min(per, S - part * per), hi, lo, meta, tail);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_win_desc(Pool pool, const int32_t* __restrict__ off, const int32_t* win_np,
-                                                  const Scalars* sc, const int32_t* __restrict__ free_stack,
-                                                  int32_t* desc_page, int32_t* desc_cnt, int64_t* desc_max,
-                                                  uint64_t* desc_fhi, uint64_t* desc_flo, uint32_t* desc_fmeta,
-                                                  const uint8_t** desc_ftail) {
-    const int np = *win_np;
+__global__ __launch_bounds__(256) void k_win_dir(Dir src, Dir dst, Scalars* sc, DescArrays desc,
+                                                 const int32_t* __restrict__ off, int32_t* free_stack) {
+    const int np = sc->win_np;
     const int S = off[np];
     const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int per = k > 0 ? cdiv(S, k) : 1;
-    const int top0 = sc->free_top;
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= k) return;
-    const int c = min(per, S - q * per);
-    const int pg = free_stack[top0 - 1 - q];
-    const int64_t b = (int64_t)pg * PAGE;
-    int64_t mx = INT64_MIN;
-    for (int i = 0; i < c; i++) mx = max(mx, pool.ver[b + i]);
-    desc_page[q] = pg; desc_cnt[q] = c; desc_max[q] = mx;
-    desc_fhi[q] = pool.hi[b]; desc_flo[q] = pool.lo[b]; desc_fmeta[q] = pool.meta[b]; desc_ftail[q] = pool.tail[b];
-}
-
-__global__ __launch_bounds__(256) void k_win_dir(Dir src, Dir dst, const Scalars* sc, DescArrays desc,
-                                                 const int32_t* __restrict__ off, const int32_t* win_np,
-                                                 int32_t* free_stack) {
-    const int np = *win_np;
-    const int S = off[np];
-    const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int D = sc->D, pA = sc->win_pA;
     const int Dn = D - np + k;
+    const int64_t removed = np ? (src.start[pA + np] - src.start[pA]) - S : 0;
     const int y = blockIdx.x * blockDim.x + threadIdx.x;
+    if (y == 0) {
+        sc->D_next = Dn;
+        sc->free_next = sc->free_top - k + np;
+        dst.start[Dn] = src.start[D] - removed;
+        sc->win_newpages = k;
+        sc->win_surv = S;
+    }
     if (y < Dn) {
-        if (np == 0 || y < pA) dir_copy(src, y, dst, y);
-        else if (y < pA + k) desc_copy(desc, y - pA, dst, y);
-        else dir_copy(src, y - k + np, dst, y);
+        if (np == 0 || y < pA) {
+            dir_copy(src, y, dst, y);
+            dst.start[y] = src.start[y];
+        } else if (y < pA + k) {
+            desc_copy(desc, y - pA, dst, y);
+            dst.start[y] = src.start[pA] + (int64_t)(y - pA) * per;
+        } else {
+            dir_copy(src, y - k + np, dst, y);
+            dst.start[y] = src.start[y - k + np] - removed;
+        }
     }
     if (y < np) free_stack[sc->free_top - k + y] = src.page[pA + y];
-}
-
-__global__ void k_win_commit(Scalars* sc, const int32_t* off, const int32_t* win_np) {
-    const int np = *win_np;
-    const int S = off[np];
-    const int k = S > 0 ? cdiv(S, FILL) : 0;
-    sc->D = sc->D - np + k;
-    sc->free_top = sc->free_top - k + np;
-    sc->win_newpages = k;
-    sc->win_surv = S;
 }
 
 void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s) {
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
-    int32_t* win_np = b.win_off + b.win_cap_pages + 1;  // scalar slot after the offsets
-    hipLaunchKernelGGL(k_win_setup, dim3(1), dim3(256), 0, s, h.pool, src, sc, h.rk_hi, h.rk_lo, h.rk_meta,
-                       h.rk_tail, win_np);
-    hipLaunchKernelGGL(k_win_keep, dim3(GRID_PAGES), dim3(256), 0, s, h.pool, src, sc, oldest, b.win_keep,
-                       b.win_cnt);
+    const int win_cap = b.win_cap_pages;
+    hipLaunchKernelGGL(k_win_setup, dim3(1), dim3(64), 0, s, h.pool, src, sc, h.rk_hi, h.rk_lo, h.rk_meta,
+                       h.rk_tail);
+    hipLaunchKernelGGL(k_win_keep, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc, oldest,
+                       b.win_keep, b.win_cnt, b.desc_max);
     ScanArgs<1> sa;
     sa.in[0] = b.win_cnt;
     sa.out[0] = b.win_off;
-    hipLaunchKernelGGL(k_scan_small<1>, dim3(1), dim3(1024), 0, s, sa, win_np);
-    hipLaunchKernelGGL(k_win_repack, dim3(GRID_PAGES), dim3(256), 0, s, h.pool, src, sc, b.win_keep, b.win_off,
-                       win_np, h.free_stack);
-    hipLaunchKernelGGL(k_win_desc, dim3(cdiv(b.win_cap_pages, 256)), dim3(256), 0, s, h.pool, b.win_off, win_np, sc,
-                       h.free_stack, b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta,
-                       b.desc_ftail);
+    hipLaunchKernelGGL(k_scan_small<1>, dim3(1), dim3(1024), 0, s, sa, &sc->win_np);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
-    hipLaunchKernelGGL(k_win_dir, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, src, dst, sc, da, b.win_off, win_np,
+    hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
+                       b.win_keep, b.win_off, h.free_stack, da);
+    hipLaunchKernelGGL(k_win_dir, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, src, dst, sc, da, b.win_off,
                        h.free_stack);
-    hipLaunchKernelGGL(k_win_commit, dim3(1), dim3(1), 0, s, sc, b.win_off, win_np);
-    launch_dir_finish(h, cur ^ 1, sc, b, s);
+    launch_bmax_commit(h, cur ^ 1, sc, s);
 }
 
 // ------------------------------------------------------------------ reset ----
