@@ -164,13 +164,14 @@ void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int
 // ranges stay separate in the combine), then slot.  A total order means no
 // ties, so every merge below is "count the partner elements that are less".
 //
-//   k_sort_tiles : one 1024-thread workgroup sorts a 4096-item tile in LDS:
-//                  4 items per lane sorted in registers, then 10 rank-merge
-//                  rounds (binary search in the partner run, scatter).
+//   k_sort_tiles : one 512-thread workgroup sorts a 2048-item tile in LDS:
+//                  4 items per lane sorted in registers, then 9 rank-merge
+//                  rounds (the lane's 4 binary searches in the partner run
+//                  run interleaved, then scatter).
 //   k_sort_kmerge: each item finds its rank in every other tile of its job
 //                  (interleaved binary searches) and lands in place.
 //   k_merge_pass : pairwise fallback when a job has more than KMAX tiles.
-static constexpr int ST_THREADS = 1024;
+static constexpr int ST_THREADS = 512;
 static constexpr int ST_ITEMS = 4;
 static constexpr int ST_TILE = ST_THREADS * ST_ITEMS;
 static constexpr int KMAX = 16;
@@ -252,29 +253,43 @@ __global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays
         if (k < nv) sm[tid * ST_ITEMS + k] = r[k];
     __syncthreads();
     for (int w = ST_ITEMS; w < nt; w <<= 1) {
-        int np[ST_ITEMS];
+        int np[ST_ITEMS], lo[ST_ITEMS], len[ST_ITEMS], ps[ST_ITEMS];
 #pragma unroll
         for (int k = 0; k < ST_ITEMS; k++) {
             const int p = tid * ST_ITEMS + k;
             np[k] = -1;
+            len[k] = 0;
             if (p < nt) {
                 r[k] = sm[p];
                 const int run = p / w;
-                const int ps = (run ^ 1) * w;
-                const int pe = min(ps + w, nt);
-                int lo = ps, hi = max(ps, pe);
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (rec_lt(sm[mid], r[k], tails)) lo = mid + 1;
-                    else hi = mid;
+                ps[k] = (run ^ 1) * w;
+                lo[k] = ps[k];
+                len[k] = max(0, min(ps[k] + w, nt) - ps[k]);
+                np[k] = (run & ~1) * w + (p - run * w);
+            }
+        }
+        // branch-light lower bounds, the four searches interleaved
+        bool more = true;
+        while (more) {
+            more = false;
+#pragma unroll
+            for (int k = 0; k < ST_ITEMS; k++) {
+                if (len[k] > 0) {
+                    const int half = len[k] >> 1;
+                    if (rec_lt(sm[lo[k] + half], r[k], tails)) {
+                        lo[k] += half + 1;
+                        len[k] -= half + 1;
+                    } else {
+                        len[k] = half;
+                    }
+                    more = true;
                 }
-                np[k] = (run & ~1) * w + (p - run * w) + (lo - ps);
             }
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ST_ITEMS; k++)
-            if (np[k] >= 0) sm[np[k]] = r[k];
+            if (np[k] >= 0) sm[np[k] + (lo[k] - ps[k])] = r[k];
         __syncthreads();
     }
     SRec* out = J.tiles[job] == 1 ? J.out[job] : J.tmp[job];
@@ -502,6 +517,7 @@ struct DecideArgs {
     KeyArrays keys;
     KeyArrays cb, ce;
     Scalars* sc;
+    int combine_in_lds;
 };
 
 static constexpr int DC_THREADS = 1024;
@@ -597,50 +613,52 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
     // ---- combine ----
+    // Stage the sorted endpoints' slots and a committed flag per write in LDS
+    // (aliasing the decision's arrays) so the serial chunk loop below runs on
+    // LDS only; fall back to global reads when they do not fit.
     const int P = 2 * A.W;
     const int64_t wbase = 2 * (int64_t)A.R;
-    const int per = (P + nthr - 1) / nthr;
-    const int p0 = min(P, tid * per), p1 = min(P, p0 + per);
-    auto delta_of = [&](int p, bool& is_begin, bool& com) -> int {
-        const uint32_t slot = A.sw[p].idx;
-        const int w = (int)((slot - wbase) >> 1);
-        const int u = A.write_txn[w];
-        com = (cbits[u >> 5] >> (u & 31)) & 1;
-        is_begin = !(slot & 1);
-        return com ? (is_begin ? 1 : -1) : 0;
-    };
-    int sum = 0;
-    for (int p = p0; p < p1; p++) {
-        bool ib, c;
-        sum += delta_of(p, ib, c);
-    }
-    int tot;
-    const int cnt0 = block_excl_scan(sum, tmp, tot);
-    int nstart = 0;
-    {
-        int cnt = cnt0;
-        for (int p = p0; p < p1; p++) {
-            bool ib, c;
-            const int d = delta_of(p, ib, c);
-            if (c && ib && cnt == 0) nstart++;
-            cnt += d;
+    __syncthreads();
+    uint32_t* s_slot = A.combine_in_lds ? lds + nwords : nullptr;
+    uint8_t* s_cw = A.combine_in_lds ? (uint8_t*)(s_slot + P) : nullptr;
+    if (A.combine_in_lds) {
+#pragma unroll 4
+        for (int w = tid; w < A.W; w += nthr) {
+            const int u = A.write_txn[w];
+            s_cw[w] = (cbits[u >> 5] >> (u & 31)) & 1;
         }
+#pragma unroll 4
+        for (int p = tid; p < P; p += nthr) s_slot[p] = A.sw[p].idx;
+        __syncthreads();
     }
-    int ngroups;
-    int g = block_excl_scan(nstart, tmp, ngroups);
-    {
-        int cnt = cnt0;
-        for (int p = p0; p < p1; p++) {
-            bool ib, c;
-            const int d = delta_of(p, ib, c);
-            if (c && ib && cnt == 0) {
-                A.cb.put(g, A.keys.get(A.sw[p].idx));
-                g++;
-            } else if (c && !ib && cnt == 1) {
-                A.ce.put(g - 1, A.keys.get(A.sw[p].idx));
+    int carry_cnt = 0, ngroups = 0;
+    for (int base = 0; base < P; base += nthr) {
+        const int p = base + tid;
+        const bool valid = p < P;
+        uint32_t slot = 0;
+        bool c = false;
+        if (valid) {
+            slot = A.combine_in_lds ? s_slot[p] : A.sw[p].idx;
+            const int w = (int)((slot - wbase) >> 1);
+            if (A.combine_in_lds) {
+                c = s_cw[w];
+            } else {
+                const int u = A.write_txn[w];
+                c = (cbits[u >> 5] >> (u & 31)) & 1;
             }
-            cnt += d;
         }
+        const bool is_begin = !(slot & 1);
+        const int d = c ? (is_begin ? 1 : -1) : 0;
+        int tot;
+        const int cnt = carry_cnt + block_excl_scan(d, tmp, tot);
+        const bool st = c && is_begin && cnt == 0;   // counter 0 -> 1: a combined range opens
+        const bool en = c && !is_begin && cnt == 1;  // counter 1 -> 0: it closes
+        int gtot;
+        const int g = ngroups + block_excl_scan((int)st, tmp, gtot);
+        if (st) A.cb.put(g, A.keys.get(slot));
+        if (en) A.ce.put(g - 1, A.keys.get(slot));
+        carry_cnt += tot;
+        ngroups += gtot;
     }
     if (tid == 0) {
         sc->n_comb = ngroups;
@@ -664,7 +682,10 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStre
     A.committed = b.committed; A.verdict = b.verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
     A.cb = b.cb; A.ce = b.ce; A.sc = sc;
     const int nwords = (T + 31) / 32;
-    const size_t lds = (size_t)nwords * 4 + (T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0);
+    const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
+    const size_t comb = (size_t)2 * v.write_count * 4 + v.write_count + 16;
+    A.combine_in_lds = (size_t)nwords * 4 + comb <= 150 * 1024;
+    const size_t lds = (size_t)nwords * 4 + std::max(dec, A.combine_in_lds ? comb : 0);
     hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
 }
 

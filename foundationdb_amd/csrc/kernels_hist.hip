@@ -32,35 +32,58 @@ struct ScanArgs {
 };
 
 // Exclusive scans of NA int32 arrays of the same device-resident length n;
-// out[k][n] receives the total.  One workgroup, 4096-element tiles, 4
-// consecutive elements per lane.
+// out[k][n] receives the total.  One workgroup; each 4096-element tile of all
+// NA arrays is staged in LDS with coalesced loads (all in flight together),
+// scanned there (4 consecutive elements per lane), and written back coalesced.
 template <int NA>
 __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32_t* n_ptr) {
+    __shared__ int32_t tile[NA][4096];
     __shared__ int32_t tmp[1024 / 64 + 1];
     const int n = *n_ptr;
+    const int tid = threadIdx.x;
+    int carry[NA];
 #pragma unroll
-    for (int k = 0; k < NA; k++) {
-        int carry = 0;
-        for (int base = 0; base < n; base += 4096) {
-            const int i0 = base + threadIdx.x * 4;
+    for (int k = 0; k < NA; k++) carry[k] = 0;
+    for (int base = 0; base < n; base += 4096) {
+#pragma unroll
+        for (int k = 0; k < NA; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int i = base + j * 1024 + tid;
+                tile[k][j * 1024 + tid] = i < n ? a.in[k][i] : 0;
+            }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
             int v[4];
             int s = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                v[j] = i0 + j < n ? a.in[k][i0 + j] : 0;
+                v[j] = tile[k][tid * 4 + j];
                 s += v[j];
             }
             int tot;
-            int run = carry + block_excl_scan(s, tmp, tot);
+            int run = carry[k] + block_excl_scan(s, tmp, tot);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (i0 + j < n) a.out[k][i0 + j] = run;
+                tile[k][tid * 4 + j] = run;
                 run += v[j];
             }
-            carry += tot;
+            carry[k] += tot;
         }
-        if (threadIdx.x == 0) a.out[k][n] = carry;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NA; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int i = base + j * 1024 + tid;
+                if (i < n) a.out[k][i] = tile[k][j * 1024 + tid];
+            }
+        __syncthreads();
     }
+    if (tid == 0)
+#pragma unroll
+        for (int k = 0; k < NA; k++) a.out[k][n] = carry[k];
 }
 
 // ------------------------------------------------------- insertion plan ----
@@ -104,26 +127,47 @@ __global__ __launch_bounds__(256) void k_bounds(KeyArrays cb, KeyArrays ce, Pool
 __global__ __launch_bounds__(1024) void k_aff_build(const int32_t* __restrict__ pb, const int32_t* __restrict__ pe,
                                                     Scalars* sc, int32_t* __restrict__ aff_list,
                                                     int32_t* __restrict__ aff_jlo) {
+    __shared__ int32_t s_pb[4096], s_pe[4097];
     __shared__ int32_t tmp[1024 / 64 + 1];
     const int nC = sc->err ? 0 : sc->n_comb;
-    const int per = (nC + blockDim.x - 1) / blockDim.x;
-    const int j0 = min(nC, (int)threadIdx.x * per), j1 = min(nC, j0 + per);
-    int s = 0;
-    for (int j = j0; j < j1; j++) {
-        const int lo = max(pb[j], j > 0 ? pe[j - 1] + 1 : 0);
-        s += max(0, pe[j] - lo + 1);
-    }
-    int tot;
-    int pos = block_excl_scan(s, tmp, tot);
-    for (int j = j0; j < j1; j++) {
-        const int lo = max(pb[j], j > 0 ? pe[j - 1] + 1 : 0);
-        for (int p = lo; p <= pe[j]; p++) {
-            aff_list[pos] = p;
-            aff_jlo[pos] = j;
-            pos++;
+    const int tid = threadIdx.x;
+    int carry = 0;
+    for (int base = 0; base < nC; base += 4096) {
+        const int n = min(4096, nC - base);
+        // s_pe[0] = pe of the range before the tile (or -1)
+        if (tid == 0) s_pe[0] = base > 0 ? pe[base - 1] : -1;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = j * 1024 + tid;
+            if (i < n) {
+                s_pb[i] = pb[base + i];
+                s_pe[i + 1] = pe[base + i];
+            }
         }
+        __syncthreads();
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = tid * 4 + j;
+            if (i < n) s += max(0, s_pe[i + 1] - max(s_pb[i], s_pe[i] + 1) + 1);
+        }
+        int tot;
+        int pos = carry + block_excl_scan(s, tmp, tot);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = tid * 4 + j;
+            if (i < n) {
+                for (int p = max(s_pb[i], s_pe[i] + 1); p <= s_pe[i + 1]; p++) {
+                    aff_list[pos] = p;
+                    aff_jlo[pos] = base + i;
+                    pos++;
+                }
+            }
+        }
+        carry += tot;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) sc->n_aff = tot;
+    if (tid == 0) sc->n_aff = carry;
 }
 
 // One wavefront per affected page: the last range touching it, surviving old
@@ -231,122 +275,171 @@ __device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, u
 // merge in the new boundaries, write 0..k output pages (the first in place,
 // the others from the free stack) and their directory descriptors.  Part
 // maxima come from LDS atomics as the entries are written.
+//
+// Fast path (<= JCAP combined ranges touch the page -- the common case): the
+// ranges' insertion plan and the page's new entries are staged in LDS, so a
+// page costs ~3 dependent global round trips.  Otherwise the new entries go
+// through the global scratch list (A.ne) and the plan is read from global.
+static constexpr int JCAP = 64;
+
+struct MergeShared {
+    uint64_t o_hi[PAGE], o_lo[PAGE];
+    int64_t o_ver[PAGE];
+    const uint8_t* o_tail[PAGE];
+    uint32_t o_meta[PAGE];
+    int32_t kb[PAGE + 1];
+    long long pmax[MAXP];
+    int32_t tmp[256 / 64 + 1];
+    int32_t j_pb[JCAP], j_ib[JCAP], j_pe[JCAP], j_ie[JCAP];
+    int64_t j_vb[JCAP];
+    uint8_t j_need[JCAP];
+    uint64_t n_hi[2 * JCAP], n_lo[2 * JCAP];
+    int64_t n_ver[2 * JCAP];
+    const uint8_t* n_tail[2 * JCAP];
+    uint32_t n_meta[2 * JCAP];
+    int32_t n_ins[2 * JCAP];
+};
+
+template <bool FAST>
+__device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) {
+    Scalars* sc = A.sc;
+    const int tid = threadIdx.x;
+    const int p = A.aff_list[a];
+    const int pg = A.dir.page[p], cntp = A.dir.cnt[p];
+    const int jlo = A.jlo[a], jhi = A.jhi[a];
+    const int nj = jhi - jlo + 1;
+    const int nn = A.nn[a], nn_off = A.nn_off[a];
+    const int parts = A.parts[a];
+    const int xoff = A.extra_off[a];
+    const int doff = A.parts_off[a];
+    const int64_t pbase = (int64_t)pg * PAGE;
+    if (tid < cntp) {
+        S.o_hi[tid] = A.pool.hi[pbase + tid];
+        S.o_lo[tid] = A.pool.lo[pbase + tid];
+        S.o_meta[tid] = A.pool.meta[pbase + tid];
+        S.o_ver[tid] = A.pool.ver[pbase + tid];
+        S.o_tail[tid] = A.pool.tail[pbase + tid];
+    }
+    if (tid < MAXP) S.pmax[tid] = INT64_MIN;
+    if (FAST && tid < nj) {
+        const int j = jlo + tid;
+        S.j_pb[tid] = A.pb[j];
+        S.j_ib[tid] = A.ib[j];
+        S.j_pe[tid] = A.pe[j];
+        S.j_ie[tid] = A.ie[j];
+        S.j_need[tid] = A.need_e[j];
+        S.j_vb[tid] = A.vb[j];
+    }
+    if (FAST) __syncthreads();
+    auto PB = [&](int j) { return FAST ? S.j_pb[j - jlo] : A.pb[j]; };
+    auto IB = [&](int j) { return FAST ? S.j_ib[j - jlo] : A.ib[j]; };
+    auto PE = [&](int j) { return FAST ? S.j_pe[j - jlo] : A.pe[j]; };
+    auto IE = [&](int j) { return FAST ? S.j_ie[j - jlo] : A.ie[j]; };
+    auto NEED = [&](int j) { return FAST ? S.j_need[j - jlo] : A.need_e[j]; };
+    auto VB = [&](int j) { return FAST ? S.j_vb[j - jlo] : A.vb[j]; };
+    // erased iff inside [(pb_j, ib_j), (pe_j, ie_j)) for the last j starting at or before (p, tid)
+    int keep = 0;
+    if (tid < cntp) {
+        int lo = jlo, hi = jhi + 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pos_le(PB(mid), IB(mid), p, tid)) lo = mid + 1; else hi = mid;
+        }
+        const int j = lo - 1;
+        keep = !(j >= jlo && pos_lt(p, tid, PE(j), IE(j)));
+    }
+    int kept;
+    const int kex = block_excl_scan(keep, S.tmp, kept);
+    if (tid < cntp) S.kb[tid] = kex;
+    if (tid == 0) S.kb[cntp] = kept;
+    // new entries landing here, in key order: b_j (version now), then e_j
+    uint64_t* NHI = FAST ? S.n_hi : A.ne.hi + nn_off;
+    uint64_t* NLO = FAST ? S.n_lo : A.ne.lo + nn_off;
+    uint32_t* NMETA = FAST ? S.n_meta : A.ne.meta + nn_off;
+    int64_t* NVER = FAST ? S.n_ver : A.ne.ver + nn_off;
+    const uint8_t** NTAIL = FAST ? S.n_tail : A.ne.tail + nn_off;
+    int32_t* NINS = FAST ? S.n_ins : A.ne_ins + nn_off;
+    int local = 0;
+    for (int jb = jlo; jb <= jhi; jb += blockDim.x) {
+        const int j = jb + tid;
+        const bool eb = j <= jhi && PB(j) == p;
+        const bool ee = j <= jhi && PE(j) == p && NEED(j);
+        int t2;
+        int k = local + block_excl_scan((int)eb + (int)ee, S.tmp, t2);
+        if (eb) {
+            const Key kk = A.cb.get(j);
+            NHI[k] = kk.hi; NLO[k] = kk.lo; NMETA[k] = kk.meta; NVER[k] = A.now;
+            copy_tail(kk, A.arena, A.arena_cap, sc, &NTAIL[k]);
+            NINS[k] = IB(j);
+            k++;
+        }
+        if (ee) {
+            const Key kk = A.ce.get(j);
+            NHI[k] = kk.hi; NLO[k] = kk.lo; NMETA[k] = kk.meta; NVER[k] = VB(j);
+            copy_tail(kk, A.arena, A.arena_cap, sc, &NTAIL[k]);
+            NINS[k] = IE(j);
+        }
+        local += t2;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const int nout = kept + nn;
+    const int per = parts > 0 ? cdiv(nout, parts) : 1;
+    auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
+    if (tid < cntp && keep) {
+        int lo = 0, hi = nn;  // new entries that go before old entry tid
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (NINS[mid] <= tid) lo = mid + 1; else hi = mid;
+        }
+        const int m = S.kb[tid] + lo;
+        const int q = m / per, slot = m - q * per;
+        const int dp = dest(q);
+        put_entry(A.pool, (int64_t)dp * PAGE + slot, S.o_hi[tid], S.o_lo[tid], S.o_meta[tid], S.o_ver[tid],
+                  S.o_tail[tid]);
+        if (q < MAXP) atomicMax(&S.pmax[q], (long long)S.o_ver[tid]);
+        if (slot == 0)
+            put_desc(A.desc, doff + q, dp, min(per, nout - q * per), S.o_hi[tid], S.o_lo[tid], S.o_meta[tid],
+                     S.o_tail[tid]);
+    }
+    for (int k = tid; k < nn; k += blockDim.x) {
+        const int m = k + S.kb[NINS[k]];
+        const int q = m / per, slot = m - q * per;
+        const int dp = dest(q);
+        const uint64_t hi = NHI[k], lo = NLO[k];
+        const uint32_t meta = NMETA[k];
+        const int64_t ver = NVER[k];
+        const uint8_t* tail = NTAIL[k];
+        put_entry(A.pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
+        if (q < MAXP) atomicMax(&S.pmax[q], (long long)ver);
+        if (slot == 0) put_desc(A.desc, doff + q, dp, min(per, nout - q * per), hi, lo, meta, tail);
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int q = tid; q < parts; q += blockDim.x) {
+        int64_t mx;
+        if (q < MAXP) {
+            mx = S.pmax[q];
+        } else {  // very large outputs (e.g. a first batch into an empty history)
+            const int64_t bq = (int64_t)dest(q) * PAGE;
+            const int c = min(per, nout - q * per);
+            mx = INT64_MIN;
+            for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
+        }
+        A.desc.maxv[doff + q] = mx;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
-    __shared__ uint64_t o_hi[PAGE], o_lo[PAGE];
-    __shared__ uint32_t o_meta[PAGE];
-    __shared__ int64_t o_ver[PAGE];
-    __shared__ const uint8_t* o_tail[PAGE];
-    __shared__ int32_t kb[PAGE + 1];
-    __shared__ long long pmax[MAXP];
-    __shared__ int32_t tmp[256 / 64 + 1];
+    __shared__ MergeShared S;
     Scalars* sc = A.sc;
     if (sc->err) return;
     const int naff = sc->n_aff;
     const int top0 = sc->free_top;
-    const int tid = threadIdx.x;
     for (int a = blockIdx.x; a < naff; a += gridDim.x) {
-        const int p = A.aff_list[a];
-        const int pg = A.dir.page[p], cntp = A.dir.cnt[p];
-        const int jlo = A.jlo[a], jhi = A.jhi[a];
-        const int nn = A.nn[a], nn_off = A.nn_off[a];
-        const int parts = A.parts[a];
-        const int64_t pbase = (int64_t)pg * PAGE;
-        if (tid < cntp) {
-            o_hi[tid] = A.pool.hi[pbase + tid];
-            o_lo[tid] = A.pool.lo[pbase + tid];
-            o_meta[tid] = A.pool.meta[pbase + tid];
-            o_ver[tid] = A.pool.ver[pbase + tid];
-            o_tail[tid] = A.pool.tail[pbase + tid];
-        }
-        if (tid < MAXP) pmax[tid] = INT64_MIN;
-        // erased iff inside [(pb_j, ib_j), (pe_j, ie_j)) for the last j starting at or before (p, tid)
-        int keep = 0;
-        if (tid < cntp) {
-            int lo = jlo, hi = jhi + 1;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (pos_le(A.pb[mid], A.ib[mid], p, tid)) lo = mid + 1; else hi = mid;
-            }
-            const int j = lo - 1;
-            keep = !(j >= jlo && pos_lt(p, tid, A.pe[j], A.ie[j]));
-        }
-        int kept;
-        const int kex = block_excl_scan(keep, tmp, kept);
-        if (tid < cntp) kb[tid] = kex;
-        if (tid == 0) kb[cntp] = kept;
-        // new entries landing here, in key order: b_j (version now), then e_j
-        int local = 0;
-        for (int jb = jlo; jb <= jhi; jb += blockDim.x) {
-            const int j = jb + tid;
-            const bool eb = j <= jhi && A.pb[j] == p;
-            const bool ee = j <= jhi && A.pe[j] == p && A.need_e[j];
-            int t2;
-            const int ex = block_excl_scan((int)eb + (int)ee, tmp, t2);
-            int k = nn_off + local + ex;
-            if (eb) {
-                const Key kk = A.cb.get(j);
-                A.ne.hi[k] = kk.hi; A.ne.lo[k] = kk.lo; A.ne.meta[k] = kk.meta; A.ne.ver[k] = A.now;
-                copy_tail(kk, A.arena, A.arena_cap, sc, &A.ne.tail[k]);
-                A.ne_ins[k] = A.ib[j];
-                k++;
-            }
-            if (ee) {
-                const Key kk = A.ce.get(j);
-                A.ne.hi[k] = kk.hi; A.ne.lo[k] = kk.lo; A.ne.meta[k] = kk.meta; A.ne.ver[k] = A.vb[j];
-                copy_tail(kk, A.arena, A.arena_cap, sc, &A.ne.tail[k]);
-                A.ne_ins[k] = A.ie[j];
-            }
-            local += t2;
-        }
-        __threadfence_block();
-        __syncthreads();
-        const int nout = kept + nn;
-        const int per = parts > 0 ? cdiv(nout, parts) : 1;
-        const int xoff = A.extra_off[a];
-        const int doff = A.parts_off[a];
-        auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
-        if (tid < cntp && keep) {
-            int lo = 0, hi = nn;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (A.ne_ins[nn_off + mid] <= tid) lo = mid + 1; else hi = mid;
-            }
-            const int m = kb[tid] + lo;
-            const int q = m / per, slot = m - q * per;
-            const int dp = dest(q);
-            put_entry(A.pool, (int64_t)dp * PAGE + slot, o_hi[tid], o_lo[tid], o_meta[tid], o_ver[tid], o_tail[tid]);
-            if (q < MAXP) atomicMax(&pmax[q], (long long)o_ver[tid]);
-            if (slot == 0)
-                put_desc(A.desc, doff + q, dp, min(per, nout - q * per), o_hi[tid], o_lo[tid], o_meta[tid], o_tail[tid]);
-        }
-        for (int k = tid; k < nn; k += blockDim.x) {
-            const int s = nn_off + k;
-            const int m = k + kb[A.ne_ins[s]];
-            const int q = m / per, slot = m - q * per;
-            const int dp = dest(q);
-            const uint64_t hi = A.ne.hi[s], lo = A.ne.lo[s];
-            const uint32_t meta = A.ne.meta[s];
-            const int64_t ver = A.ne.ver[s];
-            const uint8_t* tail = A.ne.tail[s];
-            put_entry(A.pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
-            if (q < MAXP) atomicMax(&pmax[q], (long long)ver);
-            if (slot == 0) put_desc(A.desc, doff + q, dp, min(per, nout - q * per), hi, lo, meta, tail);
-        }
-        __threadfence_block();
-        __syncthreads();
-        for (int q = tid; q < parts; q += blockDim.x) {
-            int64_t mx;
-            if (q < MAXP) {
-                mx = pmax[q];
-            } else {  // very large outputs (e.g. a first batch into an empty history)
-                const int64_t bq = (int64_t)dest(q) * PAGE;
-                const int c = min(per, nout - q * per);
-                mx = INT64_MIN;
-                for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
-            }
-            A.desc.maxv[doff + q] = mx;
-        }
-        __syncthreads();
+        if (A.jhi[a] - A.jlo[a] + 1 <= JCAP) merge_page<true>(A, S, a, top0);
+        else merge_page<false>(A, S, a, top0);
     }
 }
 
@@ -624,11 +717,14 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
     }
 }
 
-// survivors -> fresh pages at FILL density, with their descriptors
+// survivors -> fresh pages at FILL density, with their descriptors; each
+// workgroup's survivors span at most 3 parts, reduced in LDS before one
+// global atomic per part
 __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Scalars* sc,
                                                     const uint8_t* __restrict__ keep, const int32_t* __restrict__ off,
                                                     const int32_t* __restrict__ free_stack, DescArrays desc) {
     __shared__ int32_t tmp[256 / 64 + 1];
+    __shared__ long long lmax[4];
     const int np = sc->win_np;
     const int pA = sc->win_pA;
     const int top0 = sc->free_top;
@@ -639,9 +735,11 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Sc
         const int q = pA + w;
         const int pg = dir.page[q], c = dir.cnt[q];
         const int i = threadIdx.x;
+        if (i < 4) lmax[i] = INT64_MIN;
         const int kp = i < c ? keep[(int64_t)w * PAGE + i] : 0;
         int tot;
         const int ex = block_excl_scan(kp, tmp, tot);
+        const int part0 = off[w] / per;
         if (kp) {
             const int m = off[w] + ex;
             const int part = m / per, slot = m - part * per;
@@ -652,9 +750,12 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Sc
             const int64_t ver = pool.ver[sidx];
             const uint8_t* tail = pool.tail[sidx];
             put_entry(pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
-            atomicMax((long long*)&desc.maxv[part], (long long)ver);
+            atomicMax(&lmax[min(3, part - part0)], (long long)ver);
             if (slot == 0) put_desc(desc, part, dp, min(per, S - part * per), hi, lo, meta, tail);
         }
+        __syncthreads();
+        if (i < 4 && lmax[i] != INT64_MIN) atomicMax((long long*)&desc.maxv[part0 + i], lmax[i]);
+        __syncthreads();
     }
 }
 
