@@ -67,11 +67,30 @@ __device__ inline int kcmp(const Key& a, const Key& b) {
     return kcmp(a.hi, a.lo, a.meta, a.tail, b.hi, b.lo, b.meta, b.tail);
 }
 
-// Sort record: a key's fixed-width part plus the index of its range.
-struct SRec {
+__device__ __noinline__ bool key_lt_tail(const Key& a, const Key& b) {
+    return tail_cmp(a.tail, key_len(a.meta), b.tail, key_len(b.meta)) < 0;
+}
+
+// a < b, branch-free unless both keys are > 17 bytes and equal on 17 bytes
+__device__ inline bool key_lt(const Key& a, const Key& b) {
+    const bool heq = a.hi == b.hi, leq = a.lo == b.lo;
+    const bool tail_case = heq & leq & ((a.meta >> 24) == (b.meta >> 24)) & (key_len(a.meta) > 17) &
+                           (key_len(b.meta) > 17);
+    if (__builtin_expect(tail_case, 0)) return key_lt_tail(a, b);
+    return (a.hi < b.hi) | (heq & ((a.lo < b.lo) | (leq & (a.meta < b.meta))));
+}
+
+__device__ inline bool key_le(const Key& a, const Key& b) { return !key_lt(b, a); }
+
+// Sort record: a key's fixed-width part plus its key slot (32 B so that LDS
+// copies are two ds_read_b128).
+struct __attribute__((aligned(16))) SRec {
     uint64_t hi, lo;
     uint32_t meta, idx;
+    uint64_t pad;
 };
+
+
 
 // ---- Structure-of-arrays views -------------------------------------------------
 
@@ -84,6 +103,14 @@ struct KeyArrays {           // one key per slot
     __device__ void put(int64_t i, const Key& k) const {
         hi[i] = k.hi; lo[i] = k.lo; meta[i] = k.meta; tail[i] = k.tail;
     }
+};
+
+// Key slots addressed through an index (combined write ranges point at the
+// batch's key slots instead of copying keys).
+struct IndirectKeys {
+    KeyArrays k;
+    const int32_t* slot;
+    __device__ Key get(int64_t j) const { return k.get(slot[j]); }
 };
 
 // The history: a pool of pages (PAGE slots each) plus a directory that lists

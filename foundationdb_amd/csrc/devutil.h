@@ -42,14 +42,11 @@ __device__ inline T block_excl_scan(T v, T* tmp, T& total) {
     T x = wave_incl_scan(v);
     if (lane == 63) tmp[wid] = x;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        T s = 0;
-        for (int w = 0; w < nw; w++) {
-            T t = tmp[w];
-            tmp[w] = s;
-            s += t;
-        }
-        tmp[nw] = s;
+    if (wid == 0) {  // scan of the wave totals by one wavefront
+        const T y = lane < nw ? tmp[lane] : T(0);
+        const T z = wave_incl_scan(y);
+        if (lane < nw) tmp[lane] = z - y;
+        if (lane == nw - 1) tmp[nw] = z;
     }
     __syncthreads();
     T r = x - v + tmp[wid];

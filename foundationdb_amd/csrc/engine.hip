@@ -227,8 +227,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_r1); dfree(b.rec_w0); dfree(b.rec_w1);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
-    dfree(b.cb.hi); dfree(b.cb.lo); dfree(b.cb.meta); dfree(b.cb.tail);
-    dfree(b.ce.hi); dfree(b.ce.lo); dfree(b.ce.meta); dfree(b.ce.tail);
+    dfree(b.cb_slot); dfree(b.ce_slot);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
     dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
@@ -283,11 +282,11 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (W > cs->capW) {
         int64_t n = std::max<int64_t>(W, 1024);
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.rec_w1);
-        free_keys(b.cb); free_keys(b.ce);
+        dfree(b.cb_slot); dfree(b.ce_slot);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.rec_w1, 2 * n)) ||
-            (r = alloc_keys(b.cb, n)) || (r = alloc_keys(b.ce, n)) || (r = dalloc(b.pb, n)) ||
+            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
             (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||

@@ -22,7 +22,7 @@ __device__ inline int dir_search(const Dir& d, int D, const Key& k, int lo0 = 1)
     int lo = lo0, hi = D;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (kcmp(dir_first(d, mid), k) <= 0) lo = mid + 1;
+        if (key_le(dir_first(d, mid), k)) lo = mid + 1;
         else hi = mid;
     }
     return lo - 1;
@@ -34,7 +34,7 @@ __device__ inline int page_lb(const Pool& p, int page, int lo, int cnt, const Ke
     int hi = cnt;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (kcmp(pool_key(p, base + mid), k) < 0) lo = mid + 1;
+        if (key_lt(pool_key(p, base + mid), k)) lo = mid + 1;
         else hi = mid;
     }
     return lo;

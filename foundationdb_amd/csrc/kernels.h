@@ -36,8 +36,9 @@ struct BatchBufs {
     int32_t* eu;         // [edge_cap] earlier writer
     int32_t* csr;        // [edge_cap] sources bucketed by reader
     int64_t edge_cap;
-    // combined write ranges [W]
-    KeyArrays cb, ce;
+    // combined write ranges [W], as key slots of their begin / end
+    int32_t* cb_slot;
+    int32_t* ce_slot;
     // insertion plan [W]
     int32_t* pb; int32_t* ib; int32_t* pe; int32_t* ie;
     uint8_t* need_e;

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_read_check(int R, KeyArrays keys, const
     }
     if (!conflict) {
         int pe = pb;
-        if (pb + 1 < D && kcmp(dir_first(dir, pb + 1), e) <= 0) pe = dir_search(dir, D, e, pb + 1);
+        if (pb + 1 < D && key_le(dir_first(dir, pb + 1), e)) pe = dir_search(dir, D, e, pb + 1);
         if (pe == pb) {
             const int ie = page_lb(pool, pgb, ib, cb, e);
             for (int i = ib; i < ie && !conflict; i++) conflict = pool.ver[baseb + i] > s;
@@ -176,31 +176,42 @@ static constexpr int ST_ITEMS = 4;
 static constexpr int ST_TILE = ST_THREADS * ST_ITEMS;
 static constexpr int KMAX = 16;
 
-// key order with the tail fetched only when both keys are > 17 bytes and
-// share their first 17 bytes
-__device__ inline int rec_kcmp(const SRec& a, const SRec& b, const uint8_t* const* tails) {
-    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
-    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
-    if (a.meta == b.meta && key_len(a.meta) <= 17) return 0;
-    if ((a.meta >> 24) != (b.meta >> 24)) return (a.meta >> 24) < (b.meta >> 24) ? -1 : 1;
-    const uint32_t la = key_len(a.meta), lb = key_len(b.meta);
-    if (la > 17 && lb > 17) return tail_cmp(tails[a.idx], la, tails[b.idx], lb);
-    return la < lb ? -1 : (la > lb ? 1 : 0);
+// Total order on sort records: key, then END (odd slot) before BEGIN, then
+// slot.  Branch-free on the fixed-width part; the tails are consulted only
+// when both keys are > 17 bytes and equal on 17 bytes.  (hi, lo, meta) as
+// integers is the key order otherwise: meta = byte16 << 24 | len.
+__device__ __noinline__ bool rec_lt_tail(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    const int c = tail_cmp(tails[a.idx], key_len(a.meta), tails[b.idx], key_len(b.meta));
+    if (c) return c < 0;
+    const uint32_t pa = a.idx & 1, pb = b.idx & 1;
+    return pa != pb ? pa > pb : a.idx < b.idx;
 }
 
 __device__ inline bool rec_lt(const SRec& a, const SRec& b, const uint8_t* const* tails) {
-    const int c = rec_kcmp(a, b, tails);
-    if (c) return c < 0;
-    const uint32_t pa = a.idx & 1, pb = b.idx & 1;  // odd slot = range end: ends first
-    if (pa != pb) return pa > pb;
-    return a.idx < b.idx;
+    const bool heq = a.hi == b.hi, leq = a.lo == b.lo;
+    const bool tail_case = heq & leq & ((a.meta >> 24) == (b.meta >> 24)) & (key_len(a.meta) > 17) &
+                           (key_len(b.meta) > 17);
+    if (__builtin_expect(tail_case, 0)) return rec_lt_tail(a, b, tails);
+    const uint32_t pa = a.idx & 1, pb = b.idx & 1;
+    const bool tlt = (pa > pb) | ((pa == pb) & (a.idx < b.idx));
+    const bool mlt = (a.meta < b.meta) | ((a.meta == b.meta) & tlt);
+    const bool llt = (a.lo < b.lo) | (leq & mlt);
+    return (a.hi < b.hi) | (heq & llt);
 }
 
-// key-only compare of a record against a key
+// key-only three-way compare of a record against a key
+__device__ __noinline__ int rec_vs_key_tail(const SRec& a, const Key& k, const uint8_t* const* tails) {
+    return tail_cmp(tails[a.idx], key_len(a.meta), k.tail, key_len(k.meta));
+}
+
 __device__ inline int rec_vs_key(const SRec& a, const Key& k, const uint8_t* const* tails) {
-    if (a.hi != k.hi) return a.hi < k.hi ? -1 : 1;
-    if (a.lo != k.lo) return a.lo < k.lo ? -1 : 1;
-    return kcmp(a.hi, a.lo, a.meta, key_len(a.meta) > 17 ? tails[a.idx] : nullptr, k.hi, k.lo, k.meta, k.tail);
+    const bool heq = a.hi == k.hi, leq = a.lo == k.lo;
+    const bool tail_case = heq & leq & ((a.meta >> 24) == (k.meta >> 24)) & (key_len(a.meta) > 17) &
+                           (key_len(k.meta) > 17);
+    if (__builtin_expect(tail_case, 0)) return rec_vs_key_tail(a, k, tails);
+    const bool lt = (a.hi < k.hi) | (heq & ((a.lo < k.lo) | (leq & (a.meta < k.meta))));
+    const bool eq = heq & leq & (a.meta == k.meta);
+    return lt ? -1 : (eq ? 0 : 1);
 }
 
 struct SortJobs {
@@ -515,7 +526,8 @@ struct DecideArgs {
     const SRec* sw;        // sorted write endpoints [2W]
     const int32_t* write_txn;
     KeyArrays keys;
-    KeyArrays cb, ce;
+    int32_t* cb_slot;      // combined range begins / ends, as key slots
+    int32_t* ce_slot;
     Scalars* sc;
     int combine_in_lds;
 };
@@ -632,31 +644,49 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
         __syncthreads();
     }
     int carry_cnt = 0, ngroups = 0;
-    for (int base = 0; base < P; base += nthr) {
-        const int p = base + tid;
-        const bool valid = p < P;
-        uint32_t slot = 0;
-        bool c = false;
-        if (valid) {
-            slot = A.combine_in_lds ? s_slot[p] : A.sw[p].idx;
-            const int w = (int)((slot - wbase) >> 1);
-            if (A.combine_in_lds) {
-                c = s_cw[w];
-            } else {
-                const int u = A.write_txn[w];
-                c = (cbits[u >> 5] >> (u & 31)) & 1;
+    for (int base = 0; base < P; base += 4 * nthr) {
+        // 4 consecutive endpoints per lane
+        uint32_t slot[4];
+        int d[4];
+        bool beg[4], com[4];
+        int dsum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = base + 4 * tid + k;
+            slot[k] = 0;
+            com[k] = false;
+            if (p < P) {
+                slot[k] = A.combine_in_lds ? s_slot[p] : A.sw[p].idx;
+                const int w = (int)((slot[k] - wbase) >> 1);
+                if (A.combine_in_lds) {
+                    com[k] = s_cw[w];
+                } else {
+                    const int u = A.write_txn[w];
+                    com[k] = (cbits[u >> 5] >> (u & 31)) & 1;
+                }
             }
+            beg[k] = !(slot[k] & 1);
+            d[k] = com[k] ? (beg[k] ? 1 : -1) : 0;
+            dsum += d[k];
         }
-        const bool is_begin = !(slot & 1);
-        const int d = c ? (is_begin ? 1 : -1) : 0;
         int tot;
-        const int cnt = carry_cnt + block_excl_scan(d, tmp, tot);
-        const bool st = c && is_begin && cnt == 0;   // counter 0 -> 1: a combined range opens
-        const bool en = c && !is_begin && cnt == 1;  // counter 1 -> 0: it closes
+        int cnt = carry_cnt + block_excl_scan(dsum, tmp, tot);
+        bool st[4], en[4];
+        int ns = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            st[k] = com[k] && beg[k] && cnt == 0;   // counter 0 -> 1: a combined range opens
+            en[k] = com[k] && !beg[k] && cnt == 1;  // counter 1 -> 0: it closes
+            ns += st[k];
+            cnt += d[k];
+        }
         int gtot;
-        const int g = ngroups + block_excl_scan((int)st, tmp, gtot);
-        if (st) A.cb.put(g, A.keys.get(slot));
-        if (en) A.ce.put(g - 1, A.keys.get(slot));
+        int g = ngroups + block_excl_scan(ns, tmp, gtot);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (st[k]) A.cb_slot[g++] = (int32_t)slot[k];
+            if (en[k]) A.ce_slot[g - 1] = (int32_t)slot[k];
+        }
         carry_cnt += tot;
         ngroups += gtot;
     }
@@ -680,7 +710,7 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStre
     A.edge_cap = b.edge_cap;
     A.g_deg = b.deg; A.g_off = b.off; A.g_idx = b.dep_idx; A.csr = b.csr; A.dep_list = b.dep_list;
     A.committed = b.committed; A.verdict = b.verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
-    A.cb = b.cb; A.ce = b.ce; A.sc = sc;
+    A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
     const int nwords = (T + 31) / 32;
     const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
     const size_t comb = (size_t)2 * v.write_count * 4 + v.write_count + 16;

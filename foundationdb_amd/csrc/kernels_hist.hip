@@ -89,7 +89,7 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 // ------------------------------------------------------- insertion plan ----
 // Per combined range j: where b and e fall in the pre-batch history, whether
 // e needs a node, and the value it keeps.
-__global__ __launch_bounds__(256) void k_bounds(KeyArrays cb, KeyArrays ce, Pool pool, Dir dir, Scalars* sc,
+__global__ __launch_bounds__(256) void k_bounds(IndirectKeys cb, IndirectKeys ce, Pool pool, Dir dir, Scalars* sc,
                                                 int64_t v0, int32_t* __restrict__ pb_o, int32_t* __restrict__ ib_o,
                                                 int32_t* __restrict__ pe_o, int32_t* __restrict__ ie_o,
                                                 uint8_t* __restrict__ need_o, int64_t* __restrict__ vb_o) {
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void k_bounds(KeyArrays cb, KeyArrays ce, Pool
     const int c_b = dir.cnt[p_b], g_b = dir.page[p_b];
     const int i_b = page_lb(pool, g_b, 0, c_b, b);
     int p_e = p_b;
-    if (p_b + 1 < D && kcmp(dir_first(dir, p_b + 1), e) <= 0) p_e = dir_search(dir, D, e, p_b + 1);
+    if (p_b + 1 < D && key_le(dir_first(dir, p_b + 1), e)) p_e = dir_search(dir, D, e, p_b + 1);
     const int c_e = dir.cnt[p_e], g_e = dir.page[p_e];
     const int i_e = page_lb(pool, g_e, p_e == p_b ? i_b : 0, c_e, e);
     const bool found = i_e < c_e && kcmp(pool_key(pool, (int64_t)g_e * PAGE + i_e), e) == 0;
@@ -252,7 +252,7 @@ struct MergeArgs {
     const int32_t *pb, *ib, *pe, *ie;
     const uint8_t* need_e;
     const int64_t* vb;
-    KeyArrays cb, ce;
+    IndirectKeys cb, ce;
     Pool ne;
     int32_t* ne_ins;
     DescArrays desc;
@@ -543,7 +543,8 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
     if (W > 0) {
-        hipLaunchKernelGGL(k_bounds, dim3(cdiv(W, 256)), dim3(256), 0, s, b.cb, b.ce, h.pool, src, sc, v0, b.pb,
+        const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
+        hipLaunchKernelGGL(k_bounds, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
                            b.ib, b.pe, b.ie, b.need_e, b.vb);
     }
     hipLaunchKernelGGL(k_aff_build, dim3(1), dim3(1024), 0, s, b.pb, b.pe, sc, b.aff_list, b.aff_jlo);
@@ -564,7 +565,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
         A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off;
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
-        A.cb = b.cb; A.ce = b.ce; A.ne = b.ne; A.ne_ins = b.ne_ins;
+        A.cb = IndirectKeys{b.keys, b.cb_slot}; A.ce = IndirectKeys{b.keys, b.ce_slot}; A.ne = b.ne; A.ne_ins = b.ne_ins;
         A.desc = DescArrays{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
         hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, max_aff))), dim3(256), 0, s, A);
