@@ -16,13 +16,15 @@ __device__ inline Key pool_key(const Pool& p, int64_t slot) {
     return Key{p.hi[slot], p.lo[slot], p.meta[slot], p.tail[slot]};
 }
 
+// (Global-memory searches use the early-exit kcmp: with random keys the
+// first word decides, so one 8-byte load per step.)
 // Last directory entry j in [lo0-1, D) such that j == lo0-1 or first(j) <= k.
 // With lo0 = 1 this is "the page a key k belongs to".
 __device__ inline int dir_search(const Dir& d, int D, const Key& k, int lo0 = 1) {
     int lo = lo0, hi = D;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (key_le(dir_first(d, mid), k)) lo = mid + 1;
+        if (kcmp(dir_first(d, mid), k) <= 0) lo = mid + 1;
         else hi = mid;
     }
     return lo - 1;
@@ -34,7 +36,7 @@ __device__ inline int page_lb(const Pool& p, int page, int lo, int cnt, const Ke
     int hi = cnt;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (key_lt(pool_key(p, base + mid), k)) lo = mid + 1;
+        if (kcmp(pool_key(p, base + mid), k) < 0) lo = mid + 1;
         else hi = mid;
     }
     return lo;

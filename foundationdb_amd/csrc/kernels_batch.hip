@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_read_check(int R, KeyArrays keys, const
     }
     if (!conflict) {
         int pe = pb;
-        if (pb + 1 < D && key_le(dir_first(dir, pb + 1), e)) pe = dir_search(dir, D, e, pb + 1);
+        if (pb + 1 < D && kcmp(dir_first(dir, pb + 1), e) <= 0) pe = dir_search(dir, D, e, pb + 1);
         if (pe == pb) {
             const int ie = page_lb(pool, pgb, ib, cb, e);
             for (int i = ib; i < ie && !conflict; i++) conflict = pool.ver[baseb + i] > s;
@@ -164,10 +164,10 @@ void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int
 // ranges stay separate in the combine), then slot.  A total order means no
 // ties, so every merge below is "count the partner elements that are less".
 //
-//   k_sort_tiles : one 512-thread workgroup sorts a 2048-item tile in LDS:
-//                  4 items per lane sorted in registers, then 9 rank-merge
-//                  rounds (the lane's 4 binary searches in the partner run
-//                  run interleaved, then scatter).
+//   k_sort_tiles : one 512-thread workgroup sorts a 2048-item tile in LDS
+//                  by 11 rank-merge rounds (each item binary-searches its
+//                  rank in the partner run; a lane's 4 searches run in
+//                  lockstep), then scatter.
 //   k_sort_kmerge: each item finds its rank in every other tile of its job
 //                  (interleaved binary searches) and lands in place.
 //   k_merge_pass : pairwise fallback when a job has more than KMAX tiles.
@@ -223,18 +223,15 @@ struct SortJobs {
     SRec* out[2];          // final output
 };
 
-__device__ inline void cswap(SRec& a, SRec& b, bool va, bool vb, const uint8_t* const* tails) {
-    // invalid (beyond n) items sort last
-    const bool sw = (!va && vb) || (va && vb && rec_lt(b, a, tails));
-    if (sw) {
-        SRec t = a;
-        a = b;
-        b = t;
-    }
-}
-
+// Tile sort.  LDS holds the tile as three arrays (hi, lo, meta<<32|slot) and
+// lane t handles positions t, t+512, t+1024, t+1536 (striped), so the
+// neighbouring lanes' records are neighbouring 8-byte words: conflict-free
+// ds_read_b64.  Rank-merge rounds start from runs of one record.
 __global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays keys) {
-    extern __shared__ __attribute__((aligned(16))) SRec sm[];
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
+    uint64_t* s_hi = lds64;
+    uint64_t* s_lo = lds64 + ST_TILE;
+    uint64_t* s_mi = lds64 + 2 * ST_TILE;
     const int job = blockIdx.x < J.tiles[0] ? 0 : 1;
     const int tile = job ? blockIdx.x - J.tiles[0] : blockIdx.x;
     const int n = J.n[job];
@@ -242,36 +239,30 @@ __global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays
     const int nt = min(ST_TILE, n - base);
     const uint8_t* const* tails = keys.tail;
     const int tid = threadIdx.x;
-    SRec r[ST_ITEMS];
-    bool v[ST_ITEMS];
 #pragma unroll
     for (int k = 0; k < ST_ITEMS; k++) {
-        const int p = tid * ST_ITEMS + k;
-        v[k] = p < nt;
-        if (v[k]) {
+        const int p = k * ST_THREADS + tid;
+        if (p < nt) {
             const int64_t slot = J.sbase[job] + (int64_t)(base + p) * J.sstride[job];
-            r[k] = SRec{keys.hi[slot], keys.lo[slot], keys.meta[slot], (uint32_t)slot};
+            s_hi[p] = keys.hi[slot];
+            s_lo[p] = keys.lo[slot];
+            s_mi[p] = ((uint64_t)keys.meta[slot] << 32) | (uint32_t)slot;
         }
     }
-    const int nv = (int)v[0] + v[1] + v[2] + v[3];
-    cswap(r[0], r[1], v[0], v[1], tails);
-    cswap(r[2], r[3], v[2], v[3], tails);
-    cswap(r[0], r[2], v[0], v[2], tails);
-    cswap(r[1], r[3], v[1], v[3], tails);
-    cswap(r[1], r[2], v[1], v[2], tails);
-#pragma unroll
-    for (int k = 0; k < ST_ITEMS; k++)
-        if (k < nv) sm[tid * ST_ITEMS + k] = r[k];
     __syncthreads();
-    for (int w = ST_ITEMS; w < nt; w <<= 1) {
+    for (int w = 1; w < nt; w <<= 1) {
+        SRec r[ST_ITEMS];
         int np[ST_ITEMS], lo[ST_ITEMS], len[ST_ITEMS], ps[ST_ITEMS];
 #pragma unroll
         for (int k = 0; k < ST_ITEMS; k++) {
-            const int p = tid * ST_ITEMS + k;
+            const int p = k * ST_THREADS + tid;
             np[k] = -1;
             len[k] = 0;
+            lo[k] = 0;
+            ps[k] = 0;
             if (p < nt) {
-                r[k] = sm[p];
+                const uint64_t mi = s_mi[p];
+                r[k] = SRec{s_hi[p], s_lo[p], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
                 const int run = p / w;
                 ps[k] = (run ^ 1) * w;
                 lo[k] = ps[k];
@@ -279,32 +270,45 @@ __global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays
                 np[k] = (run & ~1) * w + (p - run * w);
             }
         }
-        // branch-light lower bounds, the four searches interleaved
-        bool more = true;
-        while (more) {
-            more = false;
+        // lower bounds, the four searches in lockstep: all probes are loaded
+        // first (unconditionally, so the LDS reads overlap), then compared
+        for (int step = 0; step < 16; step++) {
+            const bool more = (len[0] | len[1] | len[2] | len[3]) > 0;
+            if (!__any(more)) break;
+            SRec m[ST_ITEMS];
+            int half[ST_ITEMS];
 #pragma unroll
             for (int k = 0; k < ST_ITEMS; k++) {
-                if (len[k] > 0) {
-                    const int half = len[k] >> 1;
-                    if (rec_lt(sm[lo[k] + half], r[k], tails)) {
-                        lo[k] += half + 1;
-                        len[k] -= half + 1;
-                    } else {
-                        len[k] = half;
-                    }
-                    more = true;
-                }
+                half[k] = len[k] >> 1;
+                const int q = min(lo[k] + half[k], ST_TILE - 1);
+                const uint64_t mi = s_mi[q];
+                m[k] = SRec{s_hi[q], s_lo[q], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < ST_ITEMS; k++) {
+                const bool lt = rec_lt(m[k], r[k], tails);
+                const bool act = len[k] > 0;
+                lo[k] = (act && lt) ? lo[k] + half[k] + 1 : lo[k];
+                len[k] = act ? (lt ? len[k] - half[k] - 1 : half[k]) : 0;
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < ST_ITEMS; k++)
-            if (np[k] >= 0) sm[np[k] + (lo[k] - ps[k])] = r[k];
+        for (int k = 0; k < ST_ITEMS; k++) {
+            if (np[k] >= 0) {
+                const int d = np[k] + (lo[k] - ps[k]);
+                s_hi[d] = r[k].hi;
+                s_lo[d] = r[k].lo;
+                s_mi[d] = ((uint64_t)r[k].meta << 32) | r[k].idx;
+            }
+        }
         __syncthreads();
     }
     SRec* out = J.tiles[job] == 1 ? J.out[job] : J.tmp[job];
-    for (int p = tid; p < nt; p += blockDim.x) out[base + p] = sm[p];
+    for (int p = tid; p < nt; p += blockDim.x) {
+        const uint64_t mi = s_mi[p];
+        out[base + p] = SRec{s_hi[p], s_lo[p], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
+    }
 }
 
 __global__ __launch_bounds__(256) void k_sort_kmerge(SortJobs J, const uint8_t* const* tails) {
@@ -322,16 +326,25 @@ __global__ __launch_bounds__(256) void k_sort_kmerge(SortJobs J, const uint8_t* 
         lo[t] = min(n, t * ST_TILE);
         hi[t] = (t < nt && t != mytile) ? min(n, (t + 1) * ST_TILE) : lo[t];
     }
-    bool active = true;
-    while (active) {
-        active = false;
+    // probes read only the 8-byte hi word; the whole record only on a tie
+    for (int step = 0; step < 24; step++) {
+        bool active = false;
+#pragma unroll
+        for (int t = 0; t < KMAX; t++) active |= lo[t] < hi[t];
+        if (!active) break;
+        uint64_t mh[KMAX];
+        int mid[KMAX];
+#pragma unroll
+        for (int t = 0; t < KMAX; t++) {
+            mid[t] = (lo[t] + hi[t]) >> 1;
+            mh[t] = in[min(mid[t], n - 1)].hi;
+        }
 #pragma unroll
         for (int t = 0; t < KMAX; t++) {
             if (lo[t] < hi[t]) {
-                const int mid = (lo[t] + hi[t]) >> 1;
-                if (rec_lt(in[mid], x, tails)) lo[t] = mid + 1;
-                else hi[t] = mid;
-                active = true;
+                const bool lt = mh[t] != x.hi ? mh[t] < x.hi : rec_lt(in[mid[t]], x, tails);
+                if (lt) lo[t] = mid[t] + 1;
+                else hi[t] = mid[t];
             }
         }
     }
@@ -378,7 +391,7 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s) 
     b.sw = b.rec_w0;
     const int blocks = J.tiles[0] + J.tiles[1];
     if (blocks == 0) return;
-    hipLaunchKernelGGL(k_sort_tiles, dim3(blocks), dim3(ST_THREADS), ST_TILE * sizeof(SRec), s, J, b.keys);
+    hipLaunchKernelGGL(k_sort_tiles, dim3(blocks), dim3(ST_THREADS), ST_TILE * 3 * sizeof(uint64_t), s, J, b.keys);
     // jobs with 2..KMAX tiles: one k-way rank merge; more tiles: pairwise passes
     SortJobs K = J;
     bool any_k = false;

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void k_bounds(IndirectKeys cb, IndirectKeys ce
     const int c_b = dir.cnt[p_b], g_b = dir.page[p_b];
     const int i_b = page_lb(pool, g_b, 0, c_b, b);
     int p_e = p_b;
-    if (p_b + 1 < D && key_le(dir_first(dir, p_b + 1), e)) p_e = dir_search(dir, D, e, p_b + 1);
+    if (p_b + 1 < D && kcmp(dir_first(dir, p_b + 1), e) <= 0) p_e = dir_search(dir, D, e, p_b + 1);
     const int c_e = dir.cnt[p_e], g_e = dir.page[p_e];
     const int i_e = page_lb(pool, g_e, p_e == p_b ? i_b : 0, c_e, e);
     const bool found = i_e < c_e && kcmp(pool_key(pool, (int64_t)g_e * PAGE + i_e), e) == 0;
