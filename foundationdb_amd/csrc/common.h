@@ -157,6 +157,7 @@ struct Scalars {
     int32_t free_next;      // free_top after the rebuild in flight
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)
+    int32_t ss_resample;    // a sort bucket overflowed: recompute the splitter quantiles
 };
 
 __device__ inline int64_t atomic_max_i64(int64_t* addr, int64_t v) {

@@ -92,7 +92,7 @@ struct fdbcs {
     int64_t oldest = 0;
     // capacities of the per-batch buffers
     int64_t capT = -1, capR = -1, capW = -1, capSlots = -1, capBtail = -1, capEdges = -1, capRowWords = -1;
-    int64_t capDirB = -1, capWinPages = -1, capDesc = -1;
+    int64_t capDirB = -1, capWinPages = -1, capDesc = -1, capSortRec = -1;
     // last known device state (valid after a synchronized batch)
     int64_t known_D = 1, known_free = 0, known_H = 0;
     uint64_t known_tail = 0;
@@ -117,6 +117,7 @@ struct fdbcs {
     hipEvent_t ev[8] = {};
     double stage_us[7] = {0};
     bool have_times = false;
+    bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
 };
 
 namespace {
@@ -158,6 +159,7 @@ int sync_state(fdbcs* cs) {
     cs->known_free = cs->sc_host->free_top;
     cs->known_H = cs->sc_host->H;
     cs->known_tail = cs->sc_host->tail_used;
+    if (cs->sc_host->ss_resample) cs->have_quantiles = false;
     cs->pending_pages = 0;
     cs->pending_tail = 0;
     return FDBCS_OK;
@@ -225,7 +227,8 @@ void free_batch(BatchBufs& b) {
     dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
     dfree(b.read_txn); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
-    dfree(b.rec_r0); dfree(b.rec_r1); dfree(b.rec_w0); dfree(b.rec_w1);
+    dfree(b.rec_r0); dfree(b.rec_w0);
+    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_bkt); dfree(b.ss_tmp);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb_slot); dfree(b.ce_slot);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
@@ -275,17 +278,17 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     if (R > cs->capR) {
         int64_t n = std::max<int64_t>(R, 1024);
-        dfree(b.read_txn); dfree(b.rec_r0); dfree(b.rec_r1);
-        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.rec_r0, n)) || (r = dalloc(b.rec_r1, n))) return r;
+        dfree(b.read_txn); dfree(b.rec_r0);
+        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.rec_r0, n))) return r;
         cs->capR = n;
     }
     if (W > cs->capW) {
         int64_t n = std::max<int64_t>(W, 1024);
-        dfree(b.write_txn); dfree(b.rec_w0); dfree(b.rec_w1);
+        dfree(b.write_txn); dfree(b.rec_w0);
         dfree(b.cb_slot); dfree(b.ce_slot);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.rec_w1, 2 * n)) ||
+        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, 2 * n)) ||
             (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
@@ -293,6 +296,20 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.ne_ins, 2 * n)))
             return r;
         cs->capW = n;
+    }
+    if (!b.ss_cnt && ((r = dalloc(b.ss_cnt, 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)))) return r;
+    if (R + 2 * W > cs->capSortRec) {
+        const int64_t n = std::max<int64_t>(R + 2 * W, 4096);
+        dfree(b.ss_bkt);
+        if ((r = dalloc(b.ss_bkt, n))) return r;
+        cs->capSortRec = n;
+    }
+    const int64_t stage = sort_staging_records((int)R, (int)W);
+    if (stage > b.ss_tmp_cap) {
+        const int64_t n = std::max<int64_t>(stage, 1 << 16);
+        dfree(b.ss_tmp);
+        if ((r = dalloc(b.ss_tmp, n))) return r;
+        b.ss_tmp_cap = n;
     }
     const int64_t slots = 2 * (R + W);
     if (slots > cs->capSlots) {
@@ -389,19 +406,17 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     HistBufs& h = cs->h;
     hipStream_t s = cs->stream;
     Scalars* sc = cs->sc;
-    HIPOK(hipMemsetAsync(&sc->err, 0, sizeof(int32_t), s));
-    HIPOK(hipMemsetAsync(&sc->btail_used, 0, sizeof(uint64_t), s));
-    HIPOK(hipMemsetAsync(&sc->n_comb, 0, sizeof(int32_t), s));
     record(cs, 0);
     launch_prep(v, cs->oldest, b, sc, s);
     launch_encode(v, b, sc, s);
     record(cs, 1);
     launch_read_check(v, b, h, cs->cur, sc, cs->v0, s);
     record(cs, 2);
-    launch_sort_ranges(v, b, s);
+    launch_sort_ranges(v, b, sc, !cs->have_quantiles, s);
+    cs->have_quantiles = true;
     launch_edges(v, b, sc, s);
     record(cs, 3);
-    launch_decide(v, b, sc, s);
+    launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s);
     record(cs, 4);
     launch_merge(v, b, h, cs->cur, sc, now, cs->v0, s);
     cs->cur ^= 1;
@@ -412,8 +427,6 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
         cs->cur ^= 1;
     }
     record(cs, 6);
-    if (T > 0 && dev_verdict && dev_verdict != b.verdict)
-        HIPOK(hipMemcpyAsync(dev_verdict, b.verdict, (size_t)T, hipMemcpyDeviceToDevice, s));
     if (compact) cs->oldest = new_oldest;
     if (sync) {
         if ((r = sync_state(cs))) return r;

@@ -25,10 +25,16 @@ struct BatchBufs {
     uint8_t* btail;      // tail bytes of batch keys (8-aligned)
     uint64_t btail_cap;
     // sort records
-    SRec* rec_r0; SRec* rec_r1;   // [R]   read begins
-    SRec* rec_w0; SRec* rec_w1;   // [2W]  write endpoints
+    SRec* rec_r0;        // [R]   read begins, sorted
+    SRec* rec_w0;        // [2W]  write endpoints, sorted
     SRec* sr;            // sorted read begins
     SRec* sw;            // sorted write endpoints
+    // sample sort scratch
+    int32_t* ss_cnt;     // [2 * 1024] bucket counts (k_prep zeroes them)
+    SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
+    int32_t* ss_bkt;     // [R + 2W] bucket of each record
+    SRec* ss_tmp;        // bucket staging rows
+    int64_t ss_tmp_cap;
     // intra-batch overlap dedup matrix and edges
     uint32_t* pair_bits; // [T * row_words]
     int32_t row_words;
@@ -97,9 +103,10 @@ void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalar
 void launch_encode(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                        hipStream_t s);
-void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s);
+void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, hipStream_t s);
+int64_t sort_staging_records(int R, int W);
 void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void configure_batch_kernels();
 

@@ -8,6 +8,7 @@
 //   decide      ordered commit decision                  checkIntraBatchConflicts :1133-1153
 //   combine     union of committed writes                combineWriteConflictRanges :1320-1337
 #include <algorithm>
+#include <cstdlib>
 #include "kernels.h"
 #include "devutil.h"
 #include "hist_search.h"
@@ -19,8 +20,16 @@ namespace fdbcs_dev {
 __global__ __launch_bounds__(256) void k_prep(int T, const int64_t* __restrict__ snap, const int32_t* __restrict__ ro,
                                               const int32_t* __restrict__ wo, int64_t oldest,
                                               uint8_t* __restrict__ too_old, uint8_t* __restrict__ hist,
-                                              int32_t* __restrict__ read_txn, int32_t* __restrict__ write_txn) {
+                                              int32_t* __restrict__ read_txn, int32_t* __restrict__ write_txn,
+                                              Scalars* sc, int32_t* __restrict__ ss_cnt) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < 2 * 1024; k += blockDim.x) ss_cnt[k] = 0;  // sample-sort bucket counters
+    if (t == 0) {  // per-batch scalars (first kernel of the batch)
+        sc->err = 0;
+        sc->btail_used = 0;
+        sc->n_comb = 0;
+    }
     if (t >= T) return;
     const int r0 = ro[t], r1 = ro[t + 1];
     // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
@@ -31,10 +40,8 @@ __global__ __launch_bounds__(256) void k_prep(int T, const int64_t* __restrict__
 }
 
 void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    (void)sc;
-    if (v.txn_count == 0) return;
-    hipLaunchKernelGGL(k_prep, dim3(cdiv(v.txn_count, 256)), dim3(256), 0, s, v.txn_count, v.snapshot, v.read_off,
-                       v.write_off, oldest, b.too_old, b.hist, b.read_txn, b.write_txn);
+    hipLaunchKernelGGL(k_prep, dim3(std::max(1, cdiv(v.txn_count, 256))), dim3(256), 0, s, v.txn_count, v.snapshot,
+                       v.read_off, v.write_off, oldest, b.too_old, b.hist, b.read_txn, b.write_txn, sc, b.ss_cnt);
 }
 
 // -------------------------------------------------------------- encode ----
@@ -162,19 +169,30 @@ void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int
 // The order is total: key, then write END before write BEGIN at equal keys
 // (the reference's tie digit, SkipList.cpp:169-172, which makes touching
 // ranges stay separate in the combine), then slot.  A total order means no
-// ties, so every merge below is "count the partner elements that are less".
+// ties, so a record's output position is simply its rank.
 //
-//   k_sort_tiles : one 512-thread workgroup sorts a 2048-item tile in LDS
-//                  by 11 rank-merge rounds (each item binary-searches its
-//                  rank in the partner run; a lane's 4 searches run in
-//                  lockstep), then scatter.
-//   k_sort_kmerge: each item finds its rank in every other tile of its job
-//                  (interleaved binary searches) and lands in place.
-//   k_merge_pass : pairwise fallback when a job has more than KMAX tiles.
-static constexpr int ST_THREADS = 512;
-static constexpr int ST_ITEMS = 4;
-static constexpr int ST_TILE = ST_THREADS * ST_ITEMS;
-static constexpr int KMAX = 16;
+// Sample sort (replaces the reference's MSD radix sort, sortPoints
+// SkipList.cpp:227-279):
+//   k_ss_scatter: splitters = every (1024/nb)-th of the 1024 quantile records
+//                 kept from the previous batch's sorted output (LDS); lane per
+//                 record: binary search -> bucket, atomicAdd -> slot in the
+//                 bucket's staging row.
+//   k_ss_bucket : one wavefront per bucket (~24 records): offset = sum of the
+//                 earlier buckets' counts, bitonic sort of <= 128 records held
+//                 two per lane in registers (partners exchanged by shuffles --
+//                 no LDS, no barriers), write out[offset ...] and the
+//                 quantiles the next batch splits by.
+//   k_ss_sample : only when no quantiles exist yet (first batch, after an
+//                 unbalanced batch): one workgroup per job bitonic-sorts 1024
+//                 strided samples in LDS and keeps them as the quantiles.
+// Splitters from an earlier batch are valid for any input (they only decide
+// balance); a bucket above 128 records is sorted in LDS by its wavefront and
+// flags a re-sample, above SS_ROW it is ranked from global memory.  Ties are
+// broken by slot, so duplicated keys (Zipf hot keys) spread over buckets.
+static constexpr int SS_MAXB = 1024;     // buckets per job (power of two)
+static constexpr int SS_Q = 1024;        // quantile records kept per job
+static constexpr int SS_WAVE = 128;      // bucket size sorted in registers
+static constexpr int SS_ROW = 512;       // staging row per bucket (LDS path)
 
 // Total order on sort records: key, then END (odd slot) before BEGIN, then
 // slot.  Branch-free on the fixed-width part; the tails are consulted only
@@ -215,165 +233,237 @@ __device__ inline int rec_vs_key(const SRec& a, const Key& k, const uint8_t* con
 }
 
 struct SortJobs {
-    int32_t n[2];          // items per job
-    int32_t tiles[2];      // tiles per job
-    int64_t sbase[2];      // slot of item 0
-    int32_t sstride[2];    // slot step per item
-    SRec* tmp[2];          // tile-sorted output
-    SRec* out[2];          // final output
+    int32_t n[2];          // records per job
+    int32_t nb[2];         // buckets per job (power of two, <= SS_MAXB)
+    int32_t blocks0;       // scatter blocks of job 0
+    int64_t sbase[2];      // slot of record 0
+    int32_t sstride[2];    // slot step per record
+    SRec* out[2];          // sorted output
+    SRec* quant;           // [2][SS_Q] quantiles (persist across batches)
+    int32_t* cnt;          // [2][SS_MAXB]
+    int32_t* bkt;          // [n0 + n1] bucket of each record
+    SRec* tmp;             // [2][SS_MAXB][SS_ROW] staging rows
+    Scalars* sc;
 };
 
-// Tile sort.  LDS holds the tile as three arrays (hi, lo, meta<<32|slot) and
-// lane t handles positions t, t+512, t+1024, t+1536 (striped), so the
-// neighbouring lanes' records are neighbouring 8-byte words: conflict-free
-// ds_read_b64.  Rank-merge rounds start from runs of one record.
-__global__ __launch_bounds__(ST_THREADS) void k_sort_tiles(SortJobs J, KeyArrays keys) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
-    uint64_t* s_hi = lds64;
-    uint64_t* s_lo = lds64 + ST_TILE;
-    uint64_t* s_mi = lds64 + 2 * ST_TILE;
-    const int job = blockIdx.x < J.tiles[0] ? 0 : 1;
-    const int tile = job ? blockIdx.x - J.tiles[0] : blockIdx.x;
-    const int n = J.n[job];
-    const int base = tile * ST_TILE;
-    const int nt = min(ST_TILE, n - base);
-    const uint8_t* const* tails = keys.tail;
-    const int tid = threadIdx.x;
+__device__ inline SRec load_rec(const KeyArrays& keys, int64_t slot) {
+    return SRec{keys.hi[slot], keys.lo[slot], keys.meta[slot], (uint32_t)slot, 0};
+}
+
+// LDS record image: three 8-byte arrays; idx == REC_INF marks +infinity
+// (padding), which compares above everything without touching a tail.
+struct LdsRecs {
+    uint64_t* hi;
+    uint64_t* lo;
+    uint64_t* mi;  // meta << 32 | idx
+    __device__ SRec get(int i) const {
+        const uint64_t m = mi[i];
+        return SRec{hi[i], lo[i], (uint32_t)(m >> 32), (uint32_t)m, 0};
+    }
+    __device__ void put(int i, const SRec& r) const {
+        hi[i] = r.hi;
+        lo[i] = r.lo;
+        mi[i] = ((uint64_t)r.meta << 32) | r.idx;
+    }
+};
+constexpr uint32_t REC_INF = 0xFFFFFFFFu;
+__device__ inline SRec rec_inf() { return SRec{~0ull, ~0ull, ~0u, REC_INF, 0}; }
+
+__device__ inline bool rec_lt_inf(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    if (b.idx == REC_INF) return a.idx != REC_INF;
+    if (a.idx == REC_INF) return false;
+    return rec_lt(a, b, tails);
+}
+
+// Ascending bitonic sort of P (power of two) records in LDS; every thread of
+// the workgroup calls it.
+__device__ void lds_bitonic(const LdsRecs& L, int P, const uint8_t* const* tails) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
+                const int a = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                const int b = a | j;
+                const SRec x = L.get(a), y = L.get(b);
+                const bool up = (a & k) == 0;
+                const bool sw = up ? rec_lt_inf(y, x, tails) : rec_lt_inf(x, y, tails);
+                if (sw) {
+                    L.put(a, y);
+                    L.put(b, x);
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ inline SRec shfl_xor_rec(const SRec& r, int m) {
+    return SRec{__shfl_xor(r.hi, m, 64), __shfl_xor(r.lo, m, 64), (uint32_t)__shfl_xor((int)r.meta, m, 64),
+                (uint32_t)__shfl_xor((int)r.idx, m, 64), 0};
+}
+
+// Ascending bitonic sort of P <= 128 records held by one wavefront, element
+// e = 2*lane + q in r[q].  Partners at distance j >= 2 live in lane ^ (j/2).
+__device__ void wave_bitonic(SRec r[2], int P, const uint8_t* const* tails) {
+    const int lane = threadIdx.x & 63;
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j == 1) {
+                const bool up = ((2 * lane) & k) == 0;
+                const bool sw = up ? rec_lt_inf(r[1], r[0], tails) : rec_lt_inf(r[0], r[1], tails);
+                if (sw) {
+                    const SRec t = r[0];
+                    r[0] = r[1];
+                    r[1] = t;
+                }
+            } else {
 #pragma unroll
-    for (int k = 0; k < ST_ITEMS; k++) {
-        const int p = k * ST_THREADS + tid;
-        if (p < nt) {
-            const int64_t slot = J.sbase[job] + (int64_t)(base + p) * J.sstride[job];
-            s_hi[p] = keys.hi[slot];
-            s_lo[p] = keys.lo[slot];
-            s_mi[p] = ((uint64_t)keys.meta[slot] << 32) | (uint32_t)slot;
+                for (int q = 0; q < 2; q++) {
+                    const int e = 2 * lane + q;
+                    const SRec o = shfl_xor_rec(r[q], j >> 1);
+                    const bool up = (e & k) == 0, lower = (e & j) == 0;
+                    const bool take = (lower == up) ? rec_lt_inf(o, r[q], tails) : rec_lt_inf(r[q], o, tails);
+                    if (take) r[q] = o;
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys) {
+    __shared__ uint64_t s_hi[SS_Q], s_lo[SS_Q], s_mi[SS_Q];
+    const int job = blockIdx.x;
+    const int n = J.n[job];
+    if (blockIdx.x == 0 && threadIdx.x == 0) J.sc->ss_resample = 0;
+    if (n == 0) return;
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    const int ns = min(n, SS_Q);
+    for (int k = threadIdx.x; k < SS_Q; k += blockDim.x) {
+        if (k < ns) {
+            const int64_t r = ((int64_t)k * n + n / (2 * ns)) / ns;
+            L.put(k, load_rec(keys, J.sbase[job] + r * J.sstride[job]));
+        } else {
+            L.put(k, rec_inf());
         }
     }
     __syncthreads();
-    for (int w = 1; w < nt; w <<= 1) {
-        SRec r[ST_ITEMS];
-        int np[ST_ITEMS], lo[ST_ITEMS], len[ST_ITEMS], ps[ST_ITEMS];
-#pragma unroll
-        for (int k = 0; k < ST_ITEMS; k++) {
-            const int p = k * ST_THREADS + tid;
-            np[k] = -1;
-            len[k] = 0;
-            lo[k] = 0;
-            ps[k] = 0;
-            if (p < nt) {
-                const uint64_t mi = s_mi[p];
-                r[k] = SRec{s_hi[p], s_lo[p], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
-                const int run = p / w;
-                ps[k] = (run ^ 1) * w;
-                lo[k] = ps[k];
-                len[k] = max(0, min(ps[k] + w, nt) - ps[k]);
-                np[k] = (run & ~1) * w + (p - run * w);
-            }
-        }
-        // lower bounds, the four searches in lockstep: all probes are loaded
-        // first (unconditionally, so the LDS reads overlap), then compared
-        for (int step = 0; step < 16; step++) {
-            const bool more = (len[0] | len[1] | len[2] | len[3]) > 0;
-            if (!__any(more)) break;
-            SRec m[ST_ITEMS];
-            int half[ST_ITEMS];
-#pragma unroll
-            for (int k = 0; k < ST_ITEMS; k++) {
-                half[k] = len[k] >> 1;
-                const int q = min(lo[k] + half[k], ST_TILE - 1);
-                const uint64_t mi = s_mi[q];
-                m[k] = SRec{s_hi[q], s_lo[q], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
-            }
-#pragma unroll
-            for (int k = 0; k < ST_ITEMS; k++) {
-                const bool lt = rec_lt(m[k], r[k], tails);
-                const bool act = len[k] > 0;
-                lo[k] = (act && lt) ? lo[k] + half[k] + 1 : lo[k];
-                len[k] = act ? (lt ? len[k] - half[k] - 1 : half[k]) : 0;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < ST_ITEMS; k++) {
-            if (np[k] >= 0) {
-                const int d = np[k] + (lo[k] - ps[k]);
-                s_hi[d] = r[k].hi;
-                s_lo[d] = r[k].lo;
-                s_mi[d] = ((uint64_t)r[k].meta << 32) | r[k].idx;
-            }
-        }
-        __syncthreads();
-    }
-    SRec* out = J.tiles[job] == 1 ? J.out[job] : J.tmp[job];
-    for (int p = tid; p < nt; p += blockDim.x) {
-        const uint64_t mi = s_mi[p];
-        out[base + p] = SRec{s_hi[p], s_lo[p], (uint32_t)(mi >> 32), (uint32_t)mi, 0};
-    }
+    lds_bitonic(L, SS_Q, keys.tail);
+    for (int q = threadIdx.x; q < SS_Q; q += blockDim.x)
+        J.quant[job * SS_Q + q] = L.get((int)((int64_t)q * ns / SS_Q));
 }
 
-__global__ __launch_bounds__(256) void k_sort_kmerge(SortJobs J, const uint8_t* const* tails) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int job = g < J.n[0] ? 0 : 1;
-    const int i = job ? g - J.n[0] : g;
-    if (i >= J.n[job] || J.tiles[job] <= 1) return;
-    const SRec* in = J.tmp[job];
-    const int n = J.n[job], nt = J.tiles[job];
-    const SRec x = in[i];
-    const int mytile = i / ST_TILE;
-    int lo[KMAX], hi[KMAX];
-#pragma unroll
-    for (int t = 0; t < KMAX; t++) {
-        lo[t] = min(n, t * ST_TILE);
-        hi[t] = (t < nt && t != mytile) ? min(n, (t + 1) * ST_TILE) : lo[t];
-    }
-    // probes read only the 8-byte hi word; the whole record only on a tie
-    for (int step = 0; step < 24; step++) {
-        bool active = false;
-#pragma unroll
-        for (int t = 0; t < KMAX; t++) active |= lo[t] < hi[t];
-        if (!active) break;
-        uint64_t mh[KMAX];
-        int mid[KMAX];
-#pragma unroll
-        for (int t = 0; t < KMAX; t++) {
-            mid[t] = (lo[t] + hi[t]) >> 1;
-            mh[t] = in[min(mid[t], n - 1)].hi;
-        }
-#pragma unroll
-        for (int t = 0; t < KMAX; t++) {
-            if (lo[t] < hi[t]) {
-                const bool lt = mh[t] != x.hi ? mh[t] < x.hi : rec_lt(in[mid[t]], x, tails);
-                if (lt) lo[t] = mid[t] + 1;
-                else hi[t] = mid[t];
-            }
-        }
-    }
-    int pos = i - mytile * ST_TILE;
-#pragma unroll
-    for (int t = 0; t < KMAX; t++)
-        if (t < nt && t != mytile) pos += lo[t] - t * ST_TILE;
-    J.out[job][pos] = x;
-}
-
-__global__ __launch_bounds__(256) void k_merge_pass(int n, int width, const SRec* __restrict__ in,
-                                                    SRec* __restrict__ out, const uint8_t* const* tails) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) {
+    __shared__ uint64_t s_hi[SS_MAXB], s_lo[SS_MAXB], s_mi[SS_MAXB];
+    const int job = blockIdx.x < J.blocks0 ? 0 : 1;
+    const int i = (job ? blockIdx.x - J.blocks0 : blockIdx.x) * blockDim.x + threadIdx.x;
+    const int n = J.n[job], nb = J.nb[job];
+    const uint8_t* const* tails = keys.tail;
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    const int step = SS_Q / nb;
+    for (int s = threadIdx.x; s < nb - 1; s += blockDim.x) L.put(s, J.quant[job * SS_Q + (s + 1) * step]);
+    __syncthreads();
     if (i >= n) return;
-    const int run = i / width;
-    const int base = (run & ~1) * width;
-    const int ps = (run ^ 1) * width;
-    const int pe = min(n, ps + width);
-    const SRec x = in[i];
-    int lo = min(ps, n), hi = max(lo, pe);
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (rec_lt(in[mid], x, tails)) lo = mid + 1;
-        else hi = mid;
+    const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
+    // bucket = number of splitters <= x (splitters nondecreasing)
+    int lo = 0, len = nb - 1;
+    while (len > 0) {
+        const int half = len >> 1;
+        if (!rec_lt(x, L.get(lo + half), tails)) {
+            lo += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
     }
-    out[base + (i - run * width) + (lo - min(ps, n))] = x;
+    const int b = lo;
+    const int slot = atomicAdd(&J.cnt[job * SS_MAXB + b], 1);
+    J.bkt[(job ? J.n[0] : 0) + i] = b;
+    if (slot < SS_ROW) J.tmp[((int64_t)job * SS_MAXB + b) * SS_ROW + slot] = x;
 }
 
-void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s) {
+// quantile q of the sorted output sits at position floor(q * n / SS_Q)
+__device__ inline void emit_quantiles(const SortJobs& J, int job, int64_t pos, const SRec& x) {
+    const int64_t n = J.n[job];
+    for (int64_t q = (pos * SS_Q + n - 1) / n; q < SS_Q && (q * n) / SS_Q == pos; q++)
+        J.quant[job * SS_Q + q] = x;
+}
+
+__global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
+    __shared__ uint64_t s_hi[SS_ROW], s_lo[SS_ROW], s_mi[SS_ROW];
+    const int job = blockIdx.x < J.nb[0] ? 0 : 1;
+    const int b = job ? blockIdx.x - J.nb[0] : blockIdx.x;
+    const int lane = threadIdx.x;
+    const int32_t* cnt = J.cnt + job * SS_MAXB;
+    const uint8_t* const* tails = keys.tail;
+    int part = 0;
+    for (int k = lane; k < b; k += 64) part += cnt[k];
+    const int offset = wave_reduce_sum(part);
+    const int c = cnt[b];
+    if (c == 0) return;
+    SRec* out = J.out[job] + offset;
+    const SRec* row = J.tmp + ((int64_t)job * SS_MAXB + b) * SS_ROW;
+    if (c <= SS_WAVE) {
+        int P = 2;
+        while (P < c) P <<= 1;
+        SRec r[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) r[q] = 2 * lane + q < c ? row[2 * lane + q] : rec_inf();
+        wave_bitonic(r, P, tails);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int e = 2 * lane + q;
+            if (e < c) {
+                out[e] = r[q];
+                emit_quantiles(J, job, (int64_t)offset + e, r[q]);
+            }
+        }
+        return;
+    }
+    if (lane == 0) J.sc->ss_resample = 1;  // unbalanced: sample afresh next batch
+    if (c <= SS_ROW) {
+        int P = 1;
+        while (P < c) P <<= 1;
+        const LdsRecs L{s_hi, s_lo, s_mi};
+        for (int k = lane; k < P; k += 64) L.put(k, k < c ? row[k] : rec_inf());
+        __syncthreads();
+        lds_bitonic(L, P, tails);
+        for (int k = lane; k < c; k += 64) {
+            const SRec x = L.get(k);
+            out[k] = x;
+            emit_quantiles(J, job, (int64_t)offset + k, x);
+        }
+        return;
+    }
+    // overflow: members are found through the per-record bucket ids
+    const int n = J.n[job];
+    const int32_t* bkt = J.bkt + (job ? J.n[0] : 0);
+    for (int i = lane; i < n; i += 64) {
+        if (bkt[i] != b) continue;
+        const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
+        int rank = 0;
+        for (int j = 0; j < n; j++) {
+            if (bkt[j] != b) continue;
+            rank += rec_lt(load_rec(keys, J.sbase[job] + (int64_t)j * J.sstride[job]), x, tails);
+        }
+        out[rank] = x;
+        emit_quantiles(J, job, (int64_t)offset + rank, x);
+    }
+}
+
+static int ss_buckets(int n) {
+    // FDBCS_TEST_SORT_BUCKETS forces few buckets so tests reach the LDS and
+    // global-memory bucket paths
+    const char* force = getenv("FDBCS_TEST_SORT_BUCKETS");
+    if (n <= 0) return 0;
+    if (force && atoi(force) > 0) return std::min(atoi(force), SS_MAXB);
+    int want = (n + 23) / 24, nb = 1;
+    while (nb < want && nb < SS_MAXB) nb <<= 1;
+    return nb;
+}
+
+// Staging records the sort needs (engine sizes b.ss_tmp).
+int64_t sort_staging_records(int, int) { return 2 * (int64_t)SS_MAXB * SS_ROW; }
+
+void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
     SortJobs J;
     J.n[0] = R;
@@ -382,38 +472,21 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, hipStream_t s) 
     J.sstride[0] = 2;
     J.sbase[1] = 2 * (int64_t)R;
     J.sstride[1] = 1;
-    J.tmp[0] = b.rec_r1;
     J.out[0] = b.rec_r0;
-    J.tmp[1] = b.rec_w1;
     J.out[1] = b.rec_w0;
-    for (int j = 0; j < 2; j++) J.tiles[j] = cdiv(J.n[j], ST_TILE);
+    J.quant = b.ss_q;
+    J.cnt = b.ss_cnt;
+    J.bkt = b.ss_bkt;
+    J.tmp = b.ss_tmp;
+    J.sc = sc;
+    for (int j = 0; j < 2; j++) J.nb[j] = ss_buckets(J.n[j]);
+    J.blocks0 = cdiv(J.n[0], 256);
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
-    const int blocks = J.tiles[0] + J.tiles[1];
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_sort_tiles, dim3(blocks), dim3(ST_THREADS), ST_TILE * 3 * sizeof(uint64_t), s, J, b.keys);
-    // jobs with 2..KMAX tiles: one k-way rank merge; more tiles: pairwise passes
-    SortJobs K = J;
-    bool any_k = false;
-    for (int j = 0; j < 2; j++) {
-        if (J.tiles[j] > KMAX) {
-            K.tiles[j] = 1;  // handled below; makes k_sort_kmerge skip this job
-            SRec* a = J.tmp[j];  // ping-pong; the result ends in `a`
-            SRec* c = J.out[j];
-            for (int w = ST_TILE; w < J.n[j]; w <<= 1) {
-                hipLaunchKernelGGL(k_merge_pass, dim3(cdiv(J.n[j], 256)), dim3(256), 0, s, J.n[j], w, (const SRec*)a,
-                                   c, (const uint8_t* const*)b.keys.tail);
-                std::swap(a, c);
-            }
-            if (j == 0) b.sr = a; else b.sw = a;
-        } else if (J.tiles[j] > 1) {
-            any_k = true;
-        }
-    }
-    if (any_k) {
-        const int n = K.n[0] + K.n[1];
-        hipLaunchKernelGGL(k_sort_kmerge, dim3(cdiv(n, 256)), dim3(256), 0, s, K, (const uint8_t* const*)b.keys.tail);
-    }
+    if (J.n[0] + J.n[1] == 0) return;
+    if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys);
+    hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
+    hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
 }
 
 // --------------------------------------------------------------- edges ----
@@ -711,18 +784,15 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
     }
 }
 
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
+void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s) {
     const int T = v.txn_count;
-    if (T == 0) {
-        hipMemsetAsync(&sc->n_comb, 0, sizeof(int32_t), s);
-        return;
-    }
+    if (T == 0) return;  // n_comb was zeroed by k_prep
     DecideArgs A;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
     A.too_old = b.too_old; A.hist = b.hist; A.et = b.et; A.eu = b.eu; A.bits = b.pair_bits; A.row_words = b.row_words;
     A.edge_cap = b.edge_cap;
     A.g_deg = b.deg; A.g_off = b.off; A.g_idx = b.dep_idx; A.csr = b.csr; A.dep_list = b.dep_list;
-    A.committed = b.committed; A.verdict = b.verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
+    A.committed = b.committed; A.verdict = verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
     A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
     const int nwords = (T + 31) / 32;
     const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;

@@ -16,11 +16,10 @@ def main():
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-    if len(starts) < last + 1:
-        last = len(starts) - 1
-    first = starts[-last - 1] if last < len(starts) else starts[0]
-    sel = rows[first:starts[-1]]  # whole batches only
-    nb = last
+    last = min(last, len(starts))
+    first = starts[-last]
+    sel = rows[first:starts[-1]]  # whole batches only (the last one is partial)
+    nb = last - 1
     tot = defaultdict(float)
     cnt = defaultdict(int)
     for r in sel:

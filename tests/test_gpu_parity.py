@@ -121,6 +121,23 @@ def test_workload_configs_small(cs, cfg, T, nb):
         check_pair(cs, c, batch, now, nold, history=(i % 5 == 4 or i == nb - 1))
 
 
+@pytest.mark.parametrize("buckets", ["1", "2", "8"])
+def test_sort_bucket_paths(cs, buckets):
+    """Few sample-sort buckets push them past the register path (128 records)
+    onto the LDS path (<= 512) and the global-memory ranking path; results
+    must not change.  Also exercises the re-sample after an unbalanced batch."""
+    os.environ["FDBCS_TEST_SORT_BUCKETS"] = buckets
+    try:
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        wl = Workload(3, txns=300)
+        for i in range(4):
+            b, now, nold = wl.batch(i)
+            check_pair(cs, c, b, now, nold)
+    finally:
+        del os.environ["FDBCS_TEST_SORT_BUCKETS"]
+
+
 def test_config2_full_batches(cs):
     """Config 2 at its real batch size (5,000 txns, 5R+2W) from an empty history."""
     cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
