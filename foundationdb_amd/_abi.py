@@ -72,6 +72,7 @@ FDBCS_FUNCS = [
     ("fdbcs_enable_stage_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("fdbcs_stage_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
     ("fdbcs_stream", C.c_void_p, [C.c_void_p]),
+    ("fdbcs_debug_phases", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
 ]

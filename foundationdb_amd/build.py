@@ -20,6 +20,8 @@ ARCH = os.environ.get("FDBCS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value"]
+if os.environ.get("FDBCS_PHASES"):  # profiling build: kernels record phase timestamps
+    HIP_FLAGS.append("-DFDBCS_PHASES")
 
 LIB = os.path.join(PKG, "libfdbcs.so")
 WL_LIB = os.path.join(PKG, "libfdbcs_workload.so")

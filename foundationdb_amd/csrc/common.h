@@ -158,7 +158,22 @@ struct Scalars {
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)
     int32_t ss_resample;    // a sort bucket overflowed: recompute the splitter quantiles
+    int32_t extra_total;    // free pages the merge takes (parts beyond each page's first)
+    int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
+
+// Intra-kernel phase timestamps for profiling builds (-DFDBCS_PHASES): block 0
+// thread 0 records the 100 MHz wall clock into Scalars::ph[i].
+#ifdef FDBCS_PHASES
+#define PHASE(sc, i)                                                                           \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x == 0) (sc)->ph[(i)] = (int64_t)wall_clock64();     \
+    } while (0)
+#else
+#define PHASE(sc, i) \
+    do {             \
+    } while (0)
+#endif
 
 __device__ inline int64_t atomic_max_i64(int64_t* addr, int64_t v) {
     return (int64_t)atomicMax((long long*)addr, (long long)v);

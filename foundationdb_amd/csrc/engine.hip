@@ -222,19 +222,25 @@ int grow_tail(fdbcs* cs, uint64_t need) {
     return FDBCS_OK;
 }
 
+void free_plan(BatchBufs& b) {
+    dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff);
+    dfree(b.blk_agg); dfree(b.blk_diff);
+    dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn); dfree(b.aff_parts);
+    dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off); dfree(b.aff_free_off); dfree(b.aff_start);
+    dfree(b.freed_list);
+}
+
 void free_batch(BatchBufs& b) {
     dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
     dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
     dfree(b.read_txn); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
-    dfree(b.rec_r0); dfree(b.rec_w0);
+    dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_bkt); dfree(b.ss_tmp);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb_slot); dfree(b.ce_slot);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
-    dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
-    dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
-    dfree(b.aff_free_off); dfree(b.aff_freed); dfree(b.aff_delta); dfree(b.aff_delta_off);
+    free_plan(b);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
     dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
     dfree(b.desc_fmeta); dfree(b.desc_ftail);
@@ -261,7 +267,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         int64_t n = std::max<int64_t>(T, 1024);
         dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
         dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
-        if ((r = dalloc(b.too_old, n)) || (r = dalloc(b.hist, n)) || (r = dalloc(b.committed, n)) ||
+        // +64: k_decide_combine reads these byte arrays as 4-byte words
+        if ((r = dalloc(b.too_old, n + 64)) || (r = dalloc(b.hist, n + 64)) || (r = dalloc(b.committed, n)) ||
             (r = dalloc(b.verdict, n)) || (r = dalloc(b.deg, n)) || (r = dalloc(b.off, n + 1)) ||
             (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)))
             return r;
@@ -284,11 +291,12 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     if (W > cs->capW) {
         int64_t n = std::max<int64_t>(W, 1024);
-        dfree(b.write_txn); dfree(b.rec_w0);
+        dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
         dfree(b.cb_slot); dfree(b.ce_slot);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-        if ((r = dalloc(b.write_txn, n)) || (r = dalloc(b.rec_w0, 2 * n)) ||
+        if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_combine
+             (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
             (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
@@ -337,17 +345,21 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     const int64_t cd = cs->h.cap_dir;
     if (cd > cs->capDirB) {
-        dfree(b.aff_flag); dfree(b.aff_pos); dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn);
-        dfree(b.aff_parts); dfree(b.aff_extra); dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off);
-        dfree(b.aff_free_off); dfree(b.aff_freed); dfree(b.aff_delta); dfree(b.aff_delta_off);
+        free_plan(b);
         const int64_t n = cd + 2;
-        if ((r = dalloc(b.aff_flag, n)) || (r = dalloc(b.aff_pos, n)) || (r = dalloc(b.aff_list, n)) ||
-            (r = dalloc(b.aff_jlo, n)) || (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) ||
-            (r = dalloc(b.aff_parts, n)) || (r = dalloc(b.aff_extra, n)) || (r = dalloc(b.aff_nn_off, n)) ||
-            (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
-            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_freed, n)) || (r = dalloc(b.aff_delta, n)) ||
-            (r = dalloc(b.aff_delta_off, n)))
+        const int64_t nblk = plan_blocks((int)cd) + 1;
+        if ((r = dalloc(b.acc.er, n)) || (r = dalloc(b.acc.nn, n)) || (r = dalloc(b.acc.jlo, n)) ||
+            (r = dalloc(b.acc.jhi, n)) || (r = dalloc(b.acc.diff, n)) || (r = dalloc(b.blk_agg, 6 * nblk)) ||
+            (r = dalloc(b.blk_diff, nblk)) || (r = dalloc(b.aff_list, n)) || (r = dalloc(b.aff_jlo, n)) ||
+            (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) || (r = dalloc(b.aff_parts, n)) ||
+            (r = dalloc(b.aff_nn_off, n)) || (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
+            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)))
             return r;
+        HIPOK(hipMemsetAsync(b.acc.er, 0, n * 4, s));
+        HIPOK(hipMemsetAsync(b.acc.nn, 0, n * 4, s));
+        HIPOK(hipMemsetAsync(b.acc.diff, 0, n * 4, s));
+        HIPOK(hipMemsetAsync(b.acc.jlo, 0x7F, n * 4, s));  // "no range yet" (> any range index)
+        HIPOK(hipMemsetAsync(b.acc.jhi, 0xFF, n * 4, s));  // -1
         cs->capDirB = cd;
     }
     // page descriptors: the merge makes at most cap_dir of them, the compaction
@@ -888,6 +900,18 @@ int fdbcs_stage_times(fdbcs* cs, double* out_us, int cap) {
     int n = std::min(cap, 7);
     for (int i = 0; i < n; i++) out_us[i] = cs->stage_us[i];
     return n;
+}
+
+int fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap) {
+#ifdef FDBCS_PHASES
+    if (!cs || !out) return FDBCS_E_ARG;
+    const int n = std::min(cap, 32);
+    for (int i = 0; i < n; i++) out[i] = cs->sc_host->ph[i];
+    return n;
+#else
+    (void)cs; (void)out; (void)cap;
+    return 0;
+#endif
 }
 
 void* fdbcs_stream(fdbcs* cs) { return cs ? (void*)cs->stream : nullptr; }

@@ -6,6 +6,15 @@
 
 namespace fdbcs_dev {
 
+// Merge-plan accumulators, indexed by directory entry.
+struct PageAcc {
+    int32_t* er;    // old boundaries erased
+    int32_t* nn;    // new boundaries landing
+    int32_t* jlo;   // first combined range touching the page
+    int32_t* jhi;   // last one
+    int32_t* diff;  // +1 / -1 marks of pages wholly inside a range
+};
+
 // Per-batch device working set (sized by the engine before each batch).
 struct BatchBufs {
     // transaction level [T]
@@ -29,6 +38,7 @@ struct BatchBufs {
     SRec* rec_w0;        // [2W]  write endpoints, sorted
     SRec* sr;            // sorted read begins
     SRec* sw;            // sorted write endpoints
+    uint32_t* sw_slot;   // [2W]  their slots (compact copy for the combine)
     // sample sort scratch
     int32_t* ss_cnt;     // [2 * 1024] bucket counts (k_prep zeroes them)
     SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
@@ -49,18 +59,19 @@ struct BatchBufs {
     int32_t* pb; int32_t* ib; int32_t* pe; int32_t* ie;
     uint8_t* need_e;
     int64_t* vb;
-    // affected pages [dir cap]
-    int32_t* aff_flag;   // [cap_dir+1]
-    int32_t* aff_pos;    // [cap_dir+1] exclusive scan of aff_flag
-    int32_t* aff_list;
-    int32_t* aff_jlo; int32_t* aff_jhi;
+    // per-directory-entry accumulators of the merge plan [cap_dir + 2]; zero
+    // (jlo INT32_MAX, jhi -1) between batches -- k_plan_scan resets them
+    PageAcc acc;
+    int64_t* blk_agg;    // [plan blocks * 6] per-block plan aggregates (2 start states x 3 packed words)
+    int32_t* blk_diff;   // [plan blocks]
+    // affected pages, compacted [cap_dir + 2]
+    int32_t* aff_list;   // directory entry
+    int32_t* aff_jlo; int32_t* aff_jhi;  // combined ranges touching it
     int32_t* aff_nn;     // new entries landing
     int32_t* aff_parts;  // output pages
-    int32_t* aff_extra;  // extra pages beyond the first
     int32_t* aff_nn_off; int32_t* aff_parts_off; int32_t* aff_extra_off; int32_t* aff_free_off;
-    int32_t* aff_freed;  // 1 if the page disappears
-    int32_t* aff_delta;  // output boundaries minus input boundaries
-    int32_t* aff_delta_off;
+    int64_t* aff_start;  // start[] of its first output page
+    int32_t* freed_list; // pages the merge frees, pushed after its pops
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order
     int32_t* ne_ins;     // insertion index in the old page
@@ -111,6 +122,7 @@ void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStr
 void configure_batch_kernels();
 
 // ---- history stages (kernels_hist.hip) ----
+int plan_blocks(int cap_dir);
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
                   int64_t v0, hipStream_t s);
 void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s);

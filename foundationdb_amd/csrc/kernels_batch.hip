@@ -239,6 +239,7 @@ struct SortJobs {
     int64_t sbase[2];      // slot of record 0
     int32_t sstride[2];    // slot step per record
     SRec* out[2];          // sorted output
+    uint32_t* out_slot;    // [n1] slots of job 1's sorted records (compact copy)
     SRec* quant;           // [2][SS_Q] quantiles (persist across batches)
     int32_t* cnt;          // [2][SS_MAXB]
     int32_t* bkt;          // [n0 + n1] bucket of each record
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
             const int e = 2 * lane + q;
             if (e < c) {
                 out[e] = r[q];
+                if (job) J.out_slot[offset + e] = r[q].idx;
                 emit_quantiles(J, job, (int64_t)offset + e, r[q]);
             }
         }
@@ -429,6 +431,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
         for (int k = lane; k < c; k += 64) {
             const SRec x = L.get(k);
             out[k] = x;
+            if (job) J.out_slot[offset + k] = x.idx;
             emit_quantiles(J, job, (int64_t)offset + k, x);
         }
         return;
@@ -445,6 +448,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
             rank += rec_lt(load_rec(keys, J.sbase[job] + (int64_t)j * J.sstride[job]), x, tails);
         }
         out[rank] = x;
+        if (job) J.out_slot[offset + rank] = x.idx;
         emit_quantiles(J, job, (int64_t)offset + rank, x);
     }
 }
@@ -474,6 +478,7 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     J.sstride[1] = 1;
     J.out[0] = b.rec_r0;
     J.out[1] = b.rec_w0;
+    J.out_slot = b.sw_slot;
     J.quant = b.ss_q;
     J.cnt = b.ss_cnt;
     J.bkt = b.ss_bkt;
@@ -576,12 +581,14 @@ void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStrea
 }
 
 // ------------------------------------------------------ decide + combine ----
-// One workgroup.
+// One workgroup; every thread owns a contiguous chunk of transactions (and
+// later of sorted endpoints), so each phase issues its global loads together
+// and needs a single workgroup scan.
 //
 // Decision (checkIntraBatchConflicts, SkipList.cpp:1133-1153):
 //   conflict[t] = tooOld[t] || hist[t] || some source u < t committed,
 // where the sources of t are the unique (t, u) edges.  Edges are bucketed by
-// reader into CSR in LDS.  Txns without sources are decided in parallel;
+// reader into CSR.  Txns without sources are decided in parallel;
 // dependents are walked in index order in chunks of 64 by one wavefront:
 // each lane folds in its sources from earlier chunks (final), then the
 // chunk's 64x64 lower-triangular dependency masks are resolved by a Jacobi
@@ -591,8 +598,7 @@ void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStrea
 // Combine (combineWriteConflictRanges, SkipList.cpp:1320-1337): over the
 // sorted write endpoints (END before BEGIN at equal keys), a counter of open
 // committed writes; a combined range starts at a committed BEGIN seen with the
-// counter at 0 and ends at the committed END that brings it back to 0.  Two
-// workgroup scans: the counter, then the group index.
+// counter at 0 and ends at the committed END that brings it back to 0.
 struct DecideArgs {
     int T, R, W;
     const uint8_t* too_old;
@@ -609,71 +615,86 @@ struct DecideArgs {
     int32_t* dep_list;     // [T]
     uint8_t* committed;
     uint8_t* verdict;
-    const SRec* sw;        // sorted write endpoints [2W]
+    const uint32_t* sw_slot;  // slots of the sorted write endpoints [2W]
     const int32_t* write_txn;
-    KeyArrays keys;
     int32_t* cb_slot;      // combined range begins / ends, as key slots
     int32_t* ce_slot;
     Scalars* sc;
-    int combine_in_lds;
 };
 
 static constexpr int DC_THREADS = 1024;
 static constexpr int LDS_T = 8192;  // T up to which deg/off/idx live in LDS
+static constexpr int CPMAX = 32;    // sorted endpoints per thread kept in registers
 
 __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ int32_t tmp[DC_THREADS / 64 + 1];
-    const int T = A.T;
+    __shared__ int64_t red64[DC_THREADS / 64 + 1];
+    __shared__ int32_t red32[DC_THREADS / 64 + 1];
+    const int T = A.T, W = A.W, P = 2 * A.W;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const int nwords = (T + 31) >> 5;
-    uint32_t* cbits = lds;
+    const int nwords = (T + 31) >> 5, wwords = (W + 31) >> 5;
+    uint32_t* cbits = lds;            // committed, per txn
+    uint32_t* cwb = lds + nwords;     // committed, per write
+    uint32_t* rest = cwb + wwords;
     const bool small = T <= LDS_T;
-    int32_t* deg = small ? (int32_t*)(lds + nwords) : A.g_deg;
+    int32_t* deg = small ? (int32_t*)rest : A.g_deg;
     int32_t* off = small ? deg + T : A.g_off;
     int32_t* didx = small ? off + T + 1 : A.g_idx;
     Scalars* sc = A.sc;
     const int E = (int)min((int64_t)sc->edges_total, A.edge_cap);
+    PHASE(sc, 0);
 
     for (int i = tid; i < nwords; i += nthr) cbits[i] = 0;
     for (int t = tid; t < T; t += nthr) deg[t] = 0;
     __syncthreads();
     for (int e = tid; e < E; e += nthr) atomicAdd(&deg[A.et[e]], 1);
-    __threadfence_block();
     __syncthreads();
-    // CSR offsets, dependents list and the independent decisions
-    int ndep = 0, ebase = 0;
-    for (int base = 0; base < T; base += nthr) {
-        const int t = base + tid;
-        const bool valid = t < T;
-        const bool und = valid && !A.too_old[t] && !A.hist[t];
-        const int d = valid ? (small ? deg[t] : atomicAdd(&deg[t], 0)) : 0;
-        const bool dep = und && d > 0;
-        if (und && d == 0) atomicOr(&cbits[t >> 5], 1u << (t & 31));
-        int tot;
-        const int ex = block_excl_scan((int)dep, tmp, tot);
-        int etot;
-        const int eex = block_excl_scan(d, tmp, etot);
-        if (valid) {
-            off[t] = ebase + eex;
-            didx[t] = dep ? ndep + ex : -1;
-        }
-        if (dep) A.dep_list[ndep + ex] = t;
-        ndep += tot;
-        ebase += etot;
+    PHASE(sc, 1);
+
+    // ---- per-thread chunk of transactions: [t0, t1), CH a multiple of 4 ----
+    const int CH = (((T + nthr - 1) / nthr) + 3) & ~3;
+    const int t0 = min(T, tid * CH), t1 = min(T, t0 + CH);
+    uint64_t und = 0;  // bit k: txn t0+k undecided (not tooOld, no history conflict)
+    for (int t = t0; t < t1; t += 4) {
+        const uint32_t to = *reinterpret_cast<const uint32_t*>(A.too_old + t);
+        const uint32_t hs = *reinterpret_cast<const uint32_t*>(A.hist + t);
+        const uint32_t bad = to | hs;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (t + k < t1 && !((bad >> (8 * k)) & 0xFF)) und |= 1ull << (t + k - t0);
     }
-    if (tid == 0) off[T] = ebase;
-    __threadfence_block();
+    int ndep_l = 0, e_l = 0;
+    for (int t = t0; t < t1; t++) {
+        const int d = deg[t];
+        const bool u = (und >> (t - t0)) & 1;
+        ndep_l += u && d > 0;
+        e_l += d;
+        if (u && d == 0) atomicOr(&cbits[t >> 5], 1u << (t & 31));
+    }
+    int64_t tot64;
+    const int64_t ex64 = block_excl_scan(((int64_t)ndep_l << 32) | (uint32_t)e_l, red64, tot64);
+    int nd = (int)(ex64 >> 32), eo = (int)(uint32_t)ex64;
+    const int ndep = (int)(tot64 >> 32);
+    PHASE(sc, 2);
+    for (int t = t0; t < t1; t++) {
+        const int d = deg[t];
+        const bool dep = ((und >> (t - t0)) & 1) && d > 0;
+        off[t] = eo;
+        didx[t] = dep ? nd : -1;
+        if (dep) A.dep_list[nd++] = t;
+        eo += d;
+        deg[t] = 0;  // reused as fill cursors
+    }
+    if (tid == nthr - 1) off[T] = (int)(uint32_t)tot64;
     __syncthreads();
-    for (int t = tid; t < T; t += nthr) deg[t] = 0;  // reused as fill cursors
-    __syncthreads();
+    PHASE(sc, 3);
     for (int e = tid; e < E; e += nthr) {
         const int t = A.et[e], u = A.eu[e];
         A.csr[off[t] + atomicAdd(&deg[t], 1)] = u;
         A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
     }
-    __threadfence_block();
     __syncthreads();
+    PHASE(sc, 4);
     int iters = 0;
     if (tid < 64) {
         const int lane = tid;
@@ -705,79 +726,101 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
         }
     }
     __syncthreads();
-    for (int t = tid; t < T; t += nthr) {
+    PHASE(sc, 5);
+    for (int t = t0; t < t1; t++) {
         const bool c = (cbits[t >> 5] >> (t & 31)) & 1;
         A.committed[t] = c;
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
     // ---- combine ----
-    // Stage the sorted endpoints' slots and a committed flag per write in LDS
-    // (aliasing the decision's arrays) so the serial chunk loop below runs on
-    // LDS only; fall back to global reads when they do not fit.
-    const int P = 2 * A.W;
-    const int64_t wbase = 2 * (int64_t)A.R;
-    __syncthreads();
-    uint32_t* s_slot = A.combine_in_lds ? lds + nwords : nullptr;
-    uint8_t* s_cw = A.combine_in_lds ? (uint8_t*)(s_slot + P) : nullptr;
-    if (A.combine_in_lds) {
-#pragma unroll 4
-        for (int w = tid; w < A.W; w += nthr) {
-            const int u = A.write_txn[w];
-            s_cw[w] = (cbits[u >> 5] >> (u & 31)) & 1;
+    // committed flag per write, 32 writes per thread-word
+    for (int i = tid; i < wwords; i += nthr) {
+        // write_txn is padded to a multiple of 32 entries: eight 16-byte loads
+        const int4* src = reinterpret_cast<const int4*>(A.write_txn + 32 * i);
+        int4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = src[k];
+        uint32_t m = 0;
+        const int w0 = 32 * i;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int us[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int u = us[q];
+                if (w0 + 4 * k + q < W) m |= ((cbits[u >> 5] >> (u & 31)) & 1u) << (4 * k + q);
+            }
         }
-#pragma unroll 4
-        for (int p = tid; p < P; p += nthr) s_slot[p] = A.sw[p].idx;
-        __syncthreads();
+        cwb[i] = m;
     }
-    int carry_cnt = 0, ngroups = 0;
-    for (int base = 0; base < P; base += 4 * nthr) {
-        // 4 consecutive endpoints per lane
-        uint32_t slot[4];
-        int d[4];
-        bool beg[4], com[4];
+    __syncthreads();
+    PHASE(sc, 6);
+    const int64_t wbase = 2 * (int64_t)A.R;
+    const int CP = (P + nthr - 1) / nthr;
+    const int p0 = min(P, tid * CP), p1 = min(P, p0 + CP);
+    int gtot;
+    if (CP <= CPMAX) {
+        // this thread's endpoints live in registers for all three passes
+        uint32_t slot[CPMAX];
+        int8_t d[CPMAX];
+#pragma unroll
+        for (int k = 0; k < CPMAX; k++) slot[k] = p0 + k < p1 ? A.sw_slot[p0 + k] : 0;
         int dsum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int p = base + 4 * tid + k;
-            slot[k] = 0;
-            com[k] = false;
-            if (p < P) {
-                slot[k] = A.combine_in_lds ? s_slot[p] : A.sw[p].idx;
-                const int w = (int)((slot[k] - wbase) >> 1);
-                if (A.combine_in_lds) {
-                    com[k] = s_cw[w];
-                } else {
-                    const int u = A.write_txn[w];
-                    com[k] = (cbits[u >> 5] >> (u & 31)) & 1;
-                }
-            }
-            beg[k] = !(slot[k] & 1);
-            d[k] = com[k] ? (beg[k] ? 1 : -1) : 0;
+        for (int k = 0; k < CPMAX; k++) {
+            const int w = (int)((slot[k] - wbase) >> 1);
+            const bool com = p0 + k < p1 && ((cwb[w >> 5] >> (w & 31)) & 1);
+            d[k] = com ? ((slot[k] & 1) ? -1 : 1) : 0;
             dsum += d[k];
         }
-        int tot;
-        int cnt = carry_cnt + block_excl_scan(dsum, tmp, tot);
-        bool st[4], en[4];
-        int ns = 0;
+        PHASE(sc, 7);
+        int dtot;
+        const int cnt0 = block_excl_scan(dsum, red32, dtot);
+        int ns = 0, c2 = cnt0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            st[k] = com[k] && beg[k] && cnt == 0;   // counter 0 -> 1: a combined range opens
-            en[k] = com[k] && !beg[k] && cnt == 1;  // counter 1 -> 0: it closes
-            ns += st[k];
-            cnt += d[k];
+        for (int k = 0; k < CPMAX; k++) {
+            ns += d[k] == 1 && c2 == 0;  // counter 0 -> 1: a combined range opens
+            c2 += d[k];
         }
-        int gtot;
-        int g = ngroups + block_excl_scan(ns, tmp, gtot);
+        PHASE(sc, 8);
+        int g = block_excl_scan(ns, red32, gtot);
+        c2 = cnt0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (st[k]) A.cb_slot[g++] = (int32_t)slot[k];
-            if (en[k]) A.ce_slot[g - 1] = (int32_t)slot[k];
+        for (int k = 0; k < CPMAX; k++) {
+            if (d[k] == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot[k];
+            if (d[k] == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // counter 1 -> 0: it closes
+            c2 += d[k];
         }
-        carry_cnt += tot;
-        ngroups += gtot;
+    } else {
+        auto dval = [&](int p, uint32_t& slot) -> int {
+            slot = A.sw_slot[p];
+            const int w = (int)((slot - wbase) >> 1);
+            if (!((cwb[w >> 5] >> (w & 31)) & 1)) return 0;
+            return (slot & 1) ? -1 : 1;
+        };
+        int dsum = 0;
+        uint32_t slot;
+        for (int p = p0; p < p1; p++) dsum += dval(p, slot);
+        int dtot;
+        const int cnt0 = block_excl_scan(dsum, red32, dtot);
+        int ns = 0, c2 = cnt0;
+        for (int p = p0; p < p1; p++) {
+            const int dd = dval(p, slot);
+            ns += dd == 1 && c2 == 0;
+            c2 += dd;
+        }
+        int g = block_excl_scan(ns, red32, gtot);
+        c2 = cnt0;
+        for (int p = p0; p < p1; p++) {
+            const int dd = dval(p, slot);
+            if (dd == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot;
+            if (dd == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot;
+            c2 += dd;
+        }
     }
+    PHASE(sc, 9);
     if (tid == 0) {
-        sc->n_comb = ngroups;
+        sc->n_comb = gtot;
         sc->n_dep = ndep;
         sc->jac_iters = iters;
         sc->edges_total = 0;  // next batch starts a new edge list
@@ -792,13 +835,11 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     A.too_old = b.too_old; A.hist = b.hist; A.et = b.et; A.eu = b.eu; A.bits = b.pair_bits; A.row_words = b.row_words;
     A.edge_cap = b.edge_cap;
     A.g_deg = b.deg; A.g_off = b.off; A.g_idx = b.dep_idx; A.csr = b.csr; A.dep_list = b.dep_list;
-    A.committed = b.committed; A.verdict = verdict; A.sw = b.sw; A.write_txn = b.write_txn; A.keys = b.keys;
+    A.committed = b.committed; A.verdict = verdict; A.sw_slot = b.sw_slot; A.write_txn = b.write_txn;
     A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
-    const int nwords = (T + 31) / 32;
+    const size_t head = ((size_t)(T + 31) / 32 + (size_t)(v.write_count + 31) / 32) * 4;
     const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
-    const size_t comb = (size_t)2 * v.write_count * 4 + v.write_count + 16;
-    A.combine_in_lds = (size_t)nwords * 4 + comb <= 150 * 1024;
-    const size_t lds = (size_t)nwords * 4 + std::max(dec, A.combine_in_lds ? comb : 0);
+    const size_t lds = head + dec;
     hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
 }
 

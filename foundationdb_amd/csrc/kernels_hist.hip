@@ -87,12 +87,17 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 }
 
 // ------------------------------------------------------- insertion plan ----
-// Per combined range j: where b and e fall in the pre-batch history, whether
-// e needs a node, and the value it keeps.
-__global__ __launch_bounds__(256) void k_bounds(IndirectKeys cb, IndirectKeys ce, Pool pool, Dir dir, Scalars* sc,
-                                                int64_t v0, int32_t* __restrict__ pb_o, int32_t* __restrict__ ib_o,
-                                                int32_t* __restrict__ pe_o, int32_t* __restrict__ ie_o,
-                                                uint8_t* __restrict__ need_o, int64_t* __restrict__ vb_o) {
+// K1 k_plan_ranges, one lane per combined range j: where b and e fall in the
+// pre-batch history, whether e needs a node and the value it keeps, and the
+// range's contribution to the pages it touches, accumulated per directory
+// entry: erased old entries, new entries, first/last range touching the page.
+// Pages strictly inside [pb, pe] are wholly erased; they are marked in a
+// difference array (+1 at pb+1, -1 at pe) and resolved by the scan.
+__global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, Pool pool, Dir dir,
+                                                     Scalars* sc, int64_t v0, int32_t* __restrict__ pb_o,
+                                                     int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
+                                                     int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
+                                                     int64_t* __restrict__ vb_o, PageAcc acc) {
     if (sc->err) return;
     const int nC = sc->n_comb;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -112,104 +117,273 @@ __global__ __launch_bounds__(256) void k_bounds(IndirectKeys cb, IndirectKeys ce
     else if (p_e > 0) vb = pool.ver[(int64_t)dir.page[p_e - 1] * PAGE + dir.cnt[p_e - 1] - 1];
     else vb = v0;
     const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
+    const int need = (!found && !touch) ? 1 : 0;
     pb_o[j] = p_b;
     ib_o[j] = i_b;
     pe_o[j] = p_e;
     ie_o[j] = i_e;
-    need_o[j] = (!found && !touch) ? 1 : 0;
+    need_o[j] = (uint8_t)need;
     vb_o[j] = vb;
-}
-
-// The affected pages are the union of the intervals [pb_j, pe_j], which are
-// nondecreasing in j; range j contributes the pages after the previous
-// range's pe.  One workgroup: a scan over the contributions.  aff_jlo[a] = the
-// first range touching page a (the contributing one).
-__global__ __launch_bounds__(1024) void k_aff_build(const int32_t* __restrict__ pb, const int32_t* __restrict__ pe,
-                                                    Scalars* sc, int32_t* __restrict__ aff_list,
-                                                    int32_t* __restrict__ aff_jlo) {
-    __shared__ int32_t s_pb[4096], s_pe[4097];
-    __shared__ int32_t tmp[1024 / 64 + 1];
-    const int nC = sc->err ? 0 : sc->n_comb;
-    const int tid = threadIdx.x;
-    int carry = 0;
-    for (int base = 0; base < nC; base += 4096) {
-        const int n = min(4096, nC - base);
-        // s_pe[0] = pe of the range before the tile (or -1)
-        if (tid == 0) s_pe[0] = base > 0 ? pe[base - 1] : -1;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int i = j * 1024 + tid;
-            if (i < n) {
-                s_pb[i] = pb[base + i];
-                s_pe[i + 1] = pe[base + i];
-            }
+    if (p_b == p_e) {
+        atomicAdd(&acc.er[p_b], max(0, i_e - i_b));
+        atomicAdd(&acc.nn[p_b], 1 + need);
+        atomicMin(&acc.jlo[p_b], j);
+        atomicMax(&acc.jhi[p_b], j);
+    } else {
+        atomicAdd(&acc.er[p_b], c_b - i_b);
+        atomicAdd(&acc.nn[p_b], 1);
+        atomicMin(&acc.jlo[p_b], j);
+        atomicMax(&acc.jhi[p_b], j);
+        atomicAdd(&acc.er[p_e], i_e);
+        if (need) atomicAdd(&acc.nn[p_e], 1);
+        atomicMin(&acc.jlo[p_e], j);
+        atomicMax(&acc.jhi[p_e], j);
+        if (p_e > p_b + 1) {
+            atomicAdd(&acc.diff[p_b + 1], 1);
+            atomicAdd(&acc.diff[p_e], -1);
         }
-        __syncthreads();
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int i = tid * 4 + j;
-            if (i < n) s += max(0, s_pe[i + 1] - max(s_pb[i], s_pe[i] + 1) + 1);
-        }
-        int tot;
-        int pos = carry + block_excl_scan(s, tmp, tot);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int i = tid * 4 + j;
-            if (i < n) {
-                for (int p = max(s_pb[i], s_pe[i] + 1); p <= s_pe[i + 1]; p++) {
-                    aff_list[pos] = p;
-                    aff_jlo[pos] = base + i;
-                    pos++;
-                }
-            }
-        }
-        carry += tot;
-        __syncthreads();
     }
-    if (tid == 0) sc->n_aff = carry;
 }
 
-// One wavefront per affected page: the last range touching it, surviving old
-// entries, new entries landing in it, and how many output pages it becomes.
-__global__ __launch_bounds__(256) void k_aff_plan(Dir dir, const Scalars* sc, const int32_t* __restrict__ aff_list,
-                                                  const int32_t* __restrict__ pb, const int32_t* __restrict__ ib,
-                                                  const int32_t* __restrict__ pe, const int32_t* __restrict__ ie,
-                                                  const uint8_t* __restrict__ need_e, const int32_t* __restrict__ jlo_i,
-                                                  int32_t* __restrict__ jhi_o, int32_t* __restrict__ nn_o,
-                                                  int32_t* __restrict__ parts_o, int32_t* __restrict__ extra_o,
-                                                  int32_t* __restrict__ freed_o, int32_t* __restrict__ delta_o) {
-    const int naff = sc->err ? 0 : sc->n_aff, nC = sc->n_comb;
+// K2: the directory after the merge.  Per directory entry x: affected?
+// (touched by a range, or wholly inside one), boundaries out, output pages
+// (parts), pages taken from / returned to the free stack, boundary delta, new
+// entries.  Exclusive scans over x give every entry its new directory
+// position, start[] shift and free-stack slots.  Two launches: K2a reduces
+// each 1024-entry block for both possible "inside a wide range" states at the
+// block start (the state is the prefix of the difference array, 0 or 1, as
+// combined ranges are disjoint); K2b resolves every block's prefix from its
+// predecessors' aggregates, scans, writes the unaffected directory entries
+// at their new positions and the affected pages' merge plan, and resets the
+// accumulators for the next batch.
+static constexpr int PS_THREADS = 256;
+static constexpr int PS_ITEMS = 4;
+static constexpr int PS_BLOCK = PS_THREADS * PS_ITEMS;
+
+struct PlanItem {
+    bool affected;
+    int32_t nout, parts, nn, jlo, jhi;
+};
+
+__device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, bool covered) {
+    PlanItem it;
+    const int cnt = dir.cnt[x];
+    it.jlo = acc.jlo[x];
+    it.jhi = acc.jhi[x];
+    it.nn = 0;
+    if (covered) {
+        it.affected = true;
+        it.nout = 0;
+    } else if (it.jhi >= 0) {
+        it.affected = true;
+        it.nn = acc.nn[x];
+        it.nout = cnt - acc.er[x] + it.nn;
+    } else {
+        it.affected = false;
+        it.nout = cnt;
+    }
+    it.parts = !it.affected ? 1 : (it.nout == 0 ? 0 : (it.nout <= PAGE ? 1 : cdiv(it.nout, FILL)));
+    return it;
+}
+
+// packed scan words: (parts << 32 | affected), (freed << 32 | extra), (delta << 32 | nn)
+__device__ inline void pack_item(const PlanItem& it, int cnt, int64_t w[3]) {
+    const int64_t extra = it.affected && it.parts > 1 ? it.parts - 1 : 0;
+    const int64_t freed = it.affected && it.parts == 0;
+    w[0] = ((int64_t)it.parts << 32) | (int64_t)it.affected;
+    w[1] = (freed << 32) | extra;
+    w[2] = (int64_t)((uint64_t)(uint32_t)(it.nout - cnt) << 32) | (int64_t)it.nn;
+}
+
+template <int N>
+__device__ inline void block_reduce_n(int64_t (&v)[N], int64_t (*red)[N]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int k = 0; k < N; k++) v[k] = wave_reduce_sum(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < N; k++) red[wid][k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        int64_t t = 0;
+        for (int w = 0; w < nw; w++) t += red[w][k];
+        v[k] = t;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(PS_THREADS) void k_plan_aggr(Dir dir, const Scalars* sc, PageAcc acc,
+                                                          int64_t* __restrict__ blk_agg,
+                                                          int32_t* __restrict__ blk_diff) {
+    __shared__ int32_t red32[PS_THREADS / 64 + 1];
+    __shared__ int64_t red[PS_THREADS / 64][7];
+    const int D = sc->D;
+    const int base = blockIdx.x * PS_BLOCK;
+    if (base >= D) return;
+    const int x0 = base + threadIdx.x * PS_ITEMS;
+    int dl[PS_ITEMS], dsum = 0;
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        dl[k] = x0 + k < D ? acc.diff[x0 + k] : 0;
+        dsum += dl[k];
+    }
+    int dtot;
+    int cov = block_excl_scan(dsum, red32, dtot);  // local prefix, excluding this thread's items
+    int64_t v[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        cov += dl[k];
+        const int x = x0 + k;
+        if (x < D) {
+            const int cnt = dir.cnt[x];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {  // s = state at the block start
+                const PlanItem it = plan_item(acc, dir, x, s + cov > 0);
+                int64_t w[3];
+                pack_item(it, cnt, w);
+                v[3 * s + 0] += w[0];
+                v[3 * s + 1] += w[1];
+                v[3 * s + 2] += w[2];
+            }
+        }
+    }
+    block_reduce_n<7>(v, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) blk_agg[(int64_t)blockIdx.x * 6 + k] = v[k];
+        blk_diff[blockIdx.x] = dtot;
+    }
+}
+
+struct PlanArgs {
+    Dir src, dst;
+    Scalars* sc;
+    PageAcc acc;
+    const int64_t* blk_agg;
+    const int32_t* blk_diff;
+    int32_t *aff_list, *aff_jlo, *aff_jhi, *aff_nn, *aff_parts, *aff_nn_off, *aff_parts_off, *aff_extra_off,
+        *aff_free_off;
+    int64_t* aff_start;
+};
+
+__global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
+    __shared__ int32_t red32[PS_THREADS / 64 + 1];
+    __shared__ int64_t red64[PS_THREADS / 64 + 1];
+    __shared__ int64_t s_pre[4];  // block prefix: 3 packed words + start state
+    Scalars* sc = A.sc;
+    const int D = sc->D;
+    const int base = blockIdx.x * PS_BLOCK;
+    if (base >= D) return;
     const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    for (int a = blockIdx.x * wpb + (threadIdx.x >> 6); a < naff; a += gridDim.x * wpb) {
-        const int p = aff_list[a], cntp = dir.cnt[p];
-        const int jlo = jlo_i[a];
-        int lo = jlo, hi = nC;  // last j with pb[j] <= p
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pb[mid] <= p) lo = mid + 1; else hi = mid;
+    // ---- this block's prefix from its predecessors (wave 0) ----
+    if (threadIdx.x < 64) {
+        int64_t p0 = 0, p1 = 0, p2 = 0;
+        int carry = 0;
+        for (int k0 = 0; k0 < (int)blockIdx.x; k0 += 64) {
+            const int k = k0 + lane;
+            const bool ok = k < (int)blockIdx.x;
+            const int d = ok ? A.blk_diff[k] : 0;
+            const int st = carry + wave_incl_scan(d) - d;  // state at block k's start
+            if (ok) {
+                const int64_t* g = A.blk_agg + (int64_t)k * 6 + 3 * (st > 0);
+                p0 += g[0];
+                p1 += g[1];
+                p2 += g[2];
+            }
+            carry += wave_reduce_sum(d);
         }
-        const int jhi = lo - 1;
-        int erased = 0, nn = 0;
-        for (int j = jlo + lane; j <= jhi; j += 64) {
-            const int s = pb[j] < p ? 0 : ib[j];
-            const int en = pe[j] > p ? cntp : ie[j];
-            erased += max(0, en - s);
-            nn += (pb[j] == p) + (pe[j] == p && need_e[j]);
-        }
-        erased = wave_reduce_sum(erased);
-        nn = wave_reduce_sum(nn);
+        p0 = wave_reduce_sum(p0);
+        p1 = wave_reduce_sum(p1);
+        p2 = wave_reduce_sum(p2);
         if (lane == 0) {
-            const int nout = cntp - erased + nn;
-            const int parts = nout == 0 ? 0 : (nout <= PAGE ? 1 : cdiv(nout, FILL));
-            jhi_o[a] = jhi;
-            nn_o[a] = nn;
-            parts_o[a] = parts;
-            extra_o[a] = parts > 1 ? parts - 1 : 0;
-            freed_o[a] = parts == 0;
-            delta_o[a] = nout - cntp;
+            s_pre[0] = p0;
+            s_pre[1] = p1;
+            s_pre[2] = p2;
+            s_pre[3] = carry;
         }
+    }
+    __syncthreads();
+    const int x0 = base + threadIdx.x * PS_ITEMS;
+    int dl[PS_ITEMS], dsum = 0;
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        dl[k] = x0 + k < D ? A.acc.diff[x0 + k] : 0;
+        dsum += dl[k];
+    }
+    int dtot;
+    int cov = (int)s_pre[3] + block_excl_scan(dsum, red32, dtot);
+    PlanItem it[PS_ITEMS];
+    int cnt[PS_ITEMS];
+    int64_t w[PS_ITEMS][3], tsum[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        cov += dl[k];
+        const int x = x0 + k;
+        cnt[k] = 0;
+        it[k] = PlanItem{false, 0, 0, 0, 0, -1};
+        w[k][0] = w[k][1] = w[k][2] = 0;
+        if (x < D) {
+            cnt[k] = A.src.cnt[x];
+            it[k] = plan_item(A.acc, A.src, x, cov > 0);
+            pack_item(it[k], cnt[k], w[k]);
+        }
+        tsum[0] += w[k][0];
+        tsum[1] += w[k][1];
+        tsum[2] += w[k][2];
+    }
+    int64_t tot[3], ex[3];
+#pragma unroll
+    for (int f = 0; f < 3; f++) ex[f] = s_pre[f] + block_excl_scan(tsum[f], red64, tot[f]);
+    const int64_t top0 = sc->free_top;
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        const int x = x0 + k;
+        if (x < D) {
+            const int pos = (int)(ex[0] >> 32);
+            const int64_t st = A.src.start[x] + (int64_t)(int32_t)(uint32_t)((uint64_t)ex[2] >> 32);
+            if (it[k].affected) {
+                const int a = (int)(uint32_t)ex[0];
+                A.aff_list[a] = x;
+                A.aff_jlo[a] = it[k].jlo;
+                A.aff_jhi[a] = it[k].jhi;
+                A.aff_nn[a] = it[k].nn;
+                A.aff_parts[a] = it[k].parts;
+                A.aff_nn_off[a] = (int)(uint32_t)ex[2];
+                A.aff_parts_off[a] = pos;
+                A.aff_extra_off[a] = (int)(uint32_t)ex[1];
+                A.aff_free_off[a] = (int)(ex[1] >> 32);
+                A.aff_start[a] = st;
+            } else {
+                A.dst.page[pos] = A.src.page[x];
+                A.dst.cnt[pos] = cnt[k];
+                A.dst.maxv[pos] = A.src.maxv[x];
+                A.dst.fhi[pos] = A.src.fhi[x];
+                A.dst.flo[pos] = A.src.flo[x];
+                A.dst.fmeta[pos] = A.src.fmeta[x];
+                A.dst.ftail[pos] = A.src.ftail[x];
+                A.dst.start[pos] = st;
+            }
+            // reset the accumulators for the next batch
+            A.acc.er[x] = 0;
+            A.acc.nn[x] = 0;
+            A.acc.jlo[x] = INT32_MAX;
+            A.acc.jhi[x] = -1;
+            A.acc.diff[x] = 0;
+#pragma unroll
+            for (int f = 0; f < 3; f++) ex[f] += w[k][f];
+        }
+    }
+    if (blockIdx.x == (D - 1) / PS_BLOCK && threadIdx.x == 0) {
+        // totals: the last block's inclusive sums
+        const int64_t t0 = s_pre[0] + tot[0], t1 = s_pre[1] + tot[1], t2 = s_pre[2] + tot[2];
+        const int Dn = (int)(t0 >> 32);
+        const int extra = (int)(uint32_t)t1, freed = (int)(t1 >> 32);
+        sc->n_aff = (int)(uint32_t)t0;
+        sc->D_next = Dn;
+        sc->extra_total = extra;
+        sc->free_next = (int)(top0 - extra + freed);
+        A.dst.start[Dn] = A.src.start[D] + (int64_t)(int32_t)(uint32_t)((uint64_t)t2 >> 32);
     }
 }
 
@@ -244,18 +418,20 @@ struct DescArrays {
 
 struct MergeArgs {
     Pool pool;
-    Dir dir;
+    Dir dir;   // pre-batch directory
+    Dir dst;   // directory being built (affected pages' parts are written here)
     Scalars* sc;
     const int32_t* free_stack;
+    int32_t* freed_list;
     const int32_t* aff_list;
-    const int32_t *jlo, *jhi, *nn, *nn_off, *parts, *parts_off, *extra_off;
+    const int32_t *jlo, *jhi, *nn, *nn_off, *parts, *parts_off, *extra_off, *free_off;
+    const int64_t* aff_start;
     const int32_t *pb, *ib, *pe, *ie;
     const uint8_t* need_e;
     const int64_t* vb;
     IndirectKeys cb, ce;
     Pool ne;
     int32_t* ne_ins;
-    DescArrays desc;
     uint8_t* arena;
     uint64_t arena_cap;
     int64_t now;
@@ -271,10 +447,11 @@ __device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, u
     D.page[x] = page; D.cnt[x] = cnt; D.fhi[x] = hi; D.flo[x] = lo; D.fmeta[x] = meta; D.ftail[x] = tail;
 }
 
-// One workgroup per affected page: load it into LDS, drop erased entries,
+// K3: one workgroup per affected page: load it into LDS, drop erased entries,
 // merge in the new boundaries, write 0..k output pages (the first in place,
-// the others from the free stack) and their directory descriptors.  Part
-// maxima come from LDS atomics as the entries are written.
+// the others from the free stack) and their directory entries at the
+// positions K2 assigned.  Part maxima come from LDS atomics as the entries
+// are written.  A page that disappears goes back on the free stack.
 //
 // Fast path (<= JCAP combined ranges touch the page -- the common case): the
 // ranges' insertion plan and the page's new entries are staged in LDS, so a
@@ -301,15 +478,19 @@ struct MergeShared {
 };
 
 template <bool FAST>
-__device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) {
+__device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0, int extra_total) {
     Scalars* sc = A.sc;
     const int tid = threadIdx.x;
     const int p = A.aff_list[a];
     const int pg = A.dir.page[p], cntp = A.dir.cnt[p];
+    const int parts = A.parts[a];
+    if (parts == 0) {  // wholly erased: returns to the free stack in k_bmax_commit (after all pops)
+        if (tid == 0) A.freed_list[A.free_off[a]] = pg;
+        return;
+    }
     const int jlo = A.jlo[a], jhi = A.jhi[a];
     const int nj = jhi - jlo + 1;
     const int nn = A.nn[a], nn_off = A.nn_off[a];
-    const int parts = A.parts[a];
     const int xoff = A.extra_off[a];
     const int doff = A.parts_off[a];
     const int64_t pbase = (int64_t)pg * PAGE;
@@ -384,8 +565,15 @@ __device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) 
     __threadfence_block();
     __syncthreads();
     const int nout = kept + nn;
-    const int per = parts > 0 ? cdiv(nout, parts) : 1;
+    const int per = cdiv(nout, parts);
     auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
+    const Dir& D = A.dst;
+    auto put_dir = [&](int q, int dp, uint64_t hi, uint64_t lo, uint32_t meta, const uint8_t* tail) {
+        const int y = doff + q;
+        D.page[y] = dp; D.cnt[y] = min(per, nout - q * per);
+        D.fhi[y] = hi; D.flo[y] = lo; D.fmeta[y] = meta; D.ftail[y] = tail;
+        D.start[y] = A.aff_start[a] + (int64_t)q * per;
+    };
     if (tid < cntp && keep) {
         int lo = 0, hi = nn;  // new entries that go before old entry tid
         while (lo < hi) {
@@ -398,9 +586,7 @@ __device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) 
         put_entry(A.pool, (int64_t)dp * PAGE + slot, S.o_hi[tid], S.o_lo[tid], S.o_meta[tid], S.o_ver[tid],
                   S.o_tail[tid]);
         if (q < MAXP) atomicMax(&S.pmax[q], (long long)S.o_ver[tid]);
-        if (slot == 0)
-            put_desc(A.desc, doff + q, dp, min(per, nout - q * per), S.o_hi[tid], S.o_lo[tid], S.o_meta[tid],
-                     S.o_tail[tid]);
+        if (slot == 0) put_dir(q, dp, S.o_hi[tid], S.o_lo[tid], S.o_meta[tid], S.o_tail[tid]);
     }
     for (int k = tid; k < nn; k += blockDim.x) {
         const int m = k + S.kb[NINS[k]];
@@ -412,7 +598,7 @@ __device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) 
         const uint8_t* tail = NTAIL[k];
         put_entry(A.pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
         if (q < MAXP) atomicMax(&S.pmax[q], (long long)ver);
-        if (slot == 0) put_desc(A.desc, doff + q, dp, min(per, nout - q * per), hi, lo, meta, tail);
+        if (slot == 0) put_dir(q, dp, hi, lo, meta, tail);
     }
     __threadfence_block();
     __syncthreads();
@@ -426,7 +612,7 @@ __device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0) 
             mx = INT64_MIN;
             for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
         }
-        A.desc.maxv[doff + q] = mx;
+        D.maxv[doff + q] = mx;
     }
     __syncthreads();
 }
@@ -437,9 +623,10 @@ __global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
     if (sc->err) return;
     const int naff = sc->n_aff;
     const int top0 = sc->free_top;
+    const int extra_total = sc->extra_total;
     for (int a = blockIdx.x; a < naff; a += gridDim.x) {
-        if (A.jhi[a] - A.jlo[a] + 1 <= JCAP) merge_page<true>(A, S, a, top0);
-        else merge_page<false>(A, S, a, top0);
+        if (A.jhi[a] - A.jlo[a] + 1 <= JCAP) merge_page<true>(A, S, a, top0, extra_total);
+        else merge_page<false>(A, S, a, top0, extra_total);
     }
 }
 
@@ -453,61 +640,18 @@ __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y
     d.fhi[y] = s.fhi[x]; d.flo[y] = s.flo[x]; d.fmeta[y] = s.fmeta[x]; d.ftail[y] = s.ftail[x];
 }
 
-struct RebuildArgs {
-    Dir src, dst;
-    Scalars* sc;
-    DescArrays desc;
-    const int32_t *aff_list, *parts, *parts_off, *freed, *free_off, *extra_off, *delta_off;
-    int32_t* free_stack;
-};
-
-// Directory after the merge: unaffected entries move by the number of extra
-// pages inserted before them; affected entries are replaced by their parts.
-// start[] moves by the boundary-count change of the affected pages before.
-__global__ __launch_bounds__(256) void k_dir_rebuild(RebuildArgs A) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const Scalars* sc = A.sc;
-    const int D = sc->D;
-    const int naff = sc->err ? 0 : sc->n_aff;
-    const int Dn = naff ? D - naff + A.parts_off[naff] : D;
-    if (x == 0) {
-        A.sc->D_next = Dn;
-        A.sc->free_next = naff ? sc->free_top - A.extra_off[naff] + A.free_off[naff] : sc->free_top;
-        A.dst.start[Dn] = A.src.start[D] + (naff ? A.delta_off[naff] : 0);
-    }
-    if (x >= D) return;
-    if (naff == 0) {
-        dir_copy(A.src, x, A.dst, x);
-        A.dst.start[x] = A.src.start[x];
-        return;
-    }
-    int lo = 0, hi = naff;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (A.aff_list[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    const int na = lo;
-    const int base = x - na + A.parts_off[na];
-    const int64_t st = A.src.start[x] + A.delta_off[na];
-    if (na < naff && A.aff_list[na] == x) {
-        const int np = A.parts[na], off = A.parts_off[na];
-        int64_t s = st;
-        for (int q = 0; q < np; q++) {
-            desc_copy(A.desc, off + q, A.dst, base + q);
-            A.dst.start[base + q] = s;
-            s += A.desc.cnt[off + q];
-        }
-        if (A.freed[na]) A.free_stack[sc->free_top - A.extra_off[naff] + A.free_off[na]] = A.src.page[x];
-    } else {
-        dir_copy(A.src, x, A.dst, base);
-        A.dst.start[base] = st;
-    }
-}
-
-// Per-64-entry maxima of the new directory (one wavefront per group), then
+// Per-64-entry maxima of the new directory (one wavefront per group), pages
+// the merge freed back onto the free stack (above the ones it took), then
 // commit the directory size, free-stack top and history size.
-__global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc) {
+__global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
+                                                     int32_t* free_stack) {
     const int Dn = sc->D_next;
+    if (freed_list) {
+        const int base = sc->free_top - sc->extra_total;
+        const int nf = sc->free_next - base;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x)
+            free_stack[base + i] = freed_list[i];
+    }
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (g * 64 < Dn) {
@@ -523,9 +667,11 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc) {
     }
 }
 
-static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
+static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s,
+                               const int32_t* freed_list = nullptr) {
     const int groups = cdiv(h.cap_dir, 64);
-    hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc);
+    hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
+                       h.free_stack);
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
@@ -537,6 +683,8 @@ void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStrea
     launch_bmax_commit(h, cur, sc, s);
 }
 
+int plan_blocks(int cap_dir) { return cdiv(cap_dir, PS_BLOCK); }
+
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
                   int64_t v0, hipStream_t s) {
     const int W = v.write_count;
@@ -544,40 +692,32 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     Dir& dst = h.dir[cur ^ 1];
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
-        hipLaunchKernelGGL(k_bounds, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
-                           b.ib, b.pe, b.ie, b.need_e, b.vb);
+        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
+                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc);
     }
-    hipLaunchKernelGGL(k_aff_build, dim3(1), dim3(1024), 0, s, b.pb, b.pe, sc, b.aff_list, b.aff_jlo);
+    const int nblk = plan_blocks(h.cap_dir);
+    hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
+                       b.blk_diff);
+    PlanArgs P;
+    P.src = src; P.dst = dst; P.sc = sc; P.acc = b.acc; P.blk_agg = b.blk_agg; P.blk_diff = b.blk_diff;
+    P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
+    P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
+    P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
+    hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
     if (W > 0) {
         const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
-        hipLaunchKernelGGL(k_aff_plan, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, 4)))), dim3(256), 0, s,
-                           src, sc, b.aff_list, b.pb, b.ib, b.pe, b.ie, b.need_e, b.aff_jlo, b.aff_jhi, b.aff_nn,
-                           b.aff_parts, b.aff_extra, b.aff_freed, b.aff_delta);
-        ScanArgs<5> sa;
-        sa.in[0] = b.aff_nn; sa.out[0] = b.aff_nn_off;
-        sa.in[1] = b.aff_parts; sa.out[1] = b.aff_parts_off;
-        sa.in[2] = b.aff_extra; sa.out[2] = b.aff_extra_off;
-        sa.in[3] = b.aff_freed; sa.out[3] = b.aff_free_off;
-        sa.in[4] = b.aff_delta; sa.out[4] = b.aff_delta_off;
-        hipLaunchKernelGGL(k_scan_small<5>, dim3(1), dim3(1024), 0, s, sa, &sc->n_aff);
         MergeArgs A;
-        A.pool = h.pool; A.dir = src; A.sc = sc; A.free_stack = h.free_stack; A.aff_list = b.aff_list;
+        A.pool = h.pool; A.dir = src; A.dst = dst; A.sc = sc; A.free_stack = h.free_stack; A.freed_list = b.freed_list;
+        A.aff_list = b.aff_list;
         A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
-        A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off;
+        A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off; A.free_off = b.aff_free_off;
+        A.aff_start = b.aff_start;
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
         A.cb = IndirectKeys{b.keys, b.cb_slot}; A.ce = IndirectKeys{b.keys, b.ce_slot}; A.ne = b.ne; A.ne_ins = b.ne_ins;
-        A.desc = DescArrays{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
         hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, max_aff))), dim3(256), 0, s, A);
     }
-    RebuildArgs R;
-    R.src = src; R.dst = dst; R.sc = sc;
-    R.desc = DescArrays{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
-    R.aff_list = b.aff_list; R.parts = b.aff_parts; R.parts_off = b.aff_parts_off; R.freed = b.aff_freed;
-    R.free_off = b.aff_free_off; R.extra_off = b.aff_extra_off; R.delta_off = b.aff_delta_off;
-    R.free_stack = h.free_stack;
-    hipLaunchKernelGGL(k_dir_rebuild, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, R);
-    launch_bmax_commit(h, cur ^ 1, sc, s);
+    launch_bmax_commit(h, cur ^ 1, sc, s, b.freed_list);
 }
 
 // ------------------------------------------------------------ compaction ----

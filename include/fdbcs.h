@@ -183,6 +183,11 @@ int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap);
 int  fdbcs_enable_stage_timing(fdbcs* cs, int on);
 int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
 
+/* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the
+ * kernels recorded at their phase boundaries during the last synchronized
+ * batch.  Returns the number of entries written (0 in normal builds). */
+int  fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap);
+
 /* The HIP stream the conflict set enqueues on (as void*), for callers that
  * want to time or order around it. */
 void* fdbcs_stream(fdbcs* cs);
