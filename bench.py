@@ -1,21 +1,32 @@
 """Resolver conflict-detection benchmark (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (N > 1)
 
 A step = one ConflictBatch (addTransaction x T + detectConflicts) over one
 synthetic batch already staged in HBM; detectConflicts is synchronous, as the
 Resolver needs the verdicts before replying (Resolver.actor.cpp:139-166).
-Workload (BASELINE.json configs[1]): config 2 = 5,000 txns per
-batch, 5 reads + 2 point writes per txn, uniform 16-byte keys, 5M-version MVCC
-window; W warmup batches grow the history to steady state (~19 M boundaries
-after ~2,500 batches), then K measured batches.
 
-Prints ONE JSON line (rank 0).  `value` = resolved txns/s over the timed
-region (max over ranks), `p99_batch_ms` = p99 per-batch detectConflicts
-latency.  `roofline` is for the dominant kernel;
-`cpu_baseline` times the CPU oracle (oracle/cpu_spec.cpp, 1 core) on the
-same measured batches starting from the GPU's own steady-state history, and
-cross-checks its verdicts against the GPU's.
+N = 1: BASELINE.json configs[1] = SURVEY.md §8d config 2: 5,000-txn batches,
+5 reads (80 % point, 20 % short) + 2 point writes per txn, uniform 16-byte
+keys, 5M-version MVCC window; W warmup batches grow the history to steady
+state (~19 M boundaries after ~2,500 batches), then K measured batches.
+
+N > 1: FoundationDB's multi-resolver scale-out: GPU g is the
+resolver for the g-th equal slice of the key space; one global batch of
+5,000 x N transactions is split by the proxy rule (fdbcs_split_batch,
+MasterProxyServer.actor.cpp:267-307), every GPU resolves its sub-batch, and
+the proxy's min-combine (:558-569) is a scatter + RCCL MIN all-reduce of the
+verdict bytes inside the timed step.  Per-GPU work stays ~fixed: weak scaling.
+
+Prints ONE JSON line (rank 0).  `value` = resolved txns/s (whole node, max
+time over ranks), `p99_batch_ms` = p99 per-batch latency.  `roofline`: the
+pipeline of one detectConflicts (all its kernels, bracketed by HIP events on
+the conflict set's stream) against the HBM peak, with SURVEY.md §8d's
+algorithmic bytes per batch; `dominant_stage` gives the longest stage with its
+own byte model.  `cpu_baseline` times the CPU oracle
+(oracle/cpu_spec.cpp, 1 core) on the same measured batches starting from the
+GPU's own steady-state history, and cross-checks its verdicts.
 """
 import argparse
 import ctypes as C
@@ -29,7 +40,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STAGES = ["encode", "read_check", "sort_edges", "decide_combine", "merge", "compaction"]
+E_HIST = 28.0  # SURVEY.md §8d bytes per boundary (16-B prefix + 8-B version + 4-B meta)
 
 
 def parse():
@@ -38,36 +51,79 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=2500)
     p.add_argument("--config", type=int, default=2)
+    p.add_argument("--txns", type=int, default=5000, help="transactions per batch per GPU")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--stage-timing", type=int, default=1)
+    p.add_argument("--stage-batches", type=int, default=50, help="extra instrumented batches after the timed region")
     return p.parse_args()
 
 
-def stage_batches(wl, first, k, torch, dev):
-    """Generate batches [first, first+k) and copy them into device memory."""
+def to_device(v, torch, dev):
+    """Copy a host fdbcs_batch_view into device tensors; returns (device view, keepalive)."""
     from foundationdb_amd._abi import BatchView
-    staged = []
-    for i in range(first, first + k):
-        v, now, nold = wl.view(i)
-        T, R, W = v.txn_count, v.read_count, v.write_count
-        slots = 2 * (R + W)
+    T, R, W = v.txn_count, v.read_count, v.write_count
+    slots = 2 * (R + W)
 
-        def to_dev(ptr, ctype, n, dtype):
-            a = np.ctypeslib.as_array((ctype * max(n, 1)).from_address(ptr))[:n].astype(dtype, copy=True)
-            return torch.from_numpy(a).to(dev)
+    def arr(ptr, ctype, n, dtype):
+        if n == 0:
+            return torch.zeros(1, dtype=torch.uint8, device=dev)
+        a = np.ctypeslib.as_array((ctype * n).from_address(ptr)).astype(dtype, copy=True)
+        return torch.from_numpy(a).to(dev)
 
-        bufs = [to_dev(v.snapshot, C.c_int64, T, np.int64), to_dev(v.read_off, C.c_int32, T + 1, np.int32),
-                to_dev(v.write_off, C.c_int32, T + 1, np.int32), to_dev(v.key_off, C.c_uint64, slots, np.int64),
-                to_dev(v.key_len, C.c_uint32, slots, np.int32),
-                to_dev(v.key_bytes, C.c_uint8, int(v.key_bytes_len), np.uint8)]
-        dv = BatchView()
-        dv.txn_count, dv.read_count, dv.write_count = T, R, W
-        dv.snapshot, dv.read_off, dv.write_off = bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr()
-        dv.key_off, dv.key_len, dv.key_bytes = bufs[3].data_ptr(), bufs[4].data_ptr(), bufs[5].data_ptr()
-        dv.key_bytes_len = int(v.key_bytes_len)
-        staged.append((dv, now, nold, bufs, int(v.key_bytes_len)))
-    return staged
+    bufs = [arr(v.snapshot, C.c_int64, T, np.int64), arr(v.read_off, C.c_int32, T + 1, np.int32),
+            arr(v.write_off, C.c_int32, T + 1, np.int32), arr(v.key_off, C.c_uint64, slots, np.int64),
+            arr(v.key_len, C.c_uint32, slots, np.int32), arr(v.key_bytes, C.c_uint8, int(v.key_bytes_len), np.uint8)]
+    dv = BatchView()
+    dv.txn_count, dv.read_count, dv.write_count = T, R, W
+    dv.snapshot, dv.read_off, dv.write_off = bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr()
+    dv.key_off, dv.key_len, dv.key_bytes = bufs[3].data_ptr(), bufs[4].data_ptr(), bufs[5].data_ptr()
+    dv.key_bytes_len = int(v.key_bytes_len)
+    return dv, bufs
+
+
+class Source:
+    """Batches for this rank: the whole batch (N = 1) or this resolver's share."""
+
+    def __init__(self, cfg, txns, world, rank):
+        from foundationdb_amd.workload import Workload
+        self.world, self.rank = world, rank
+        self.wl = Workload(cfg, txns=txns * world)
+        self.kr = None
+        if world > 1:
+            from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
+            self.kr = KeyRangeResolvers(uniform_bounds(world))
+
+    def host(self, i):
+        """(host view, now, new_oldest, T_global, txn_index or None, keepalive)."""
+        if self.kr is None:
+            v, now, nold = self.wl.view(i)
+            return v, now, nold, v.txn_count, None, None
+        batch, now, nold = self.wl.batch(i)
+        sub, idx = self.kr.split(batch, self.rank)
+        return sub.view(), now, nold, batch.T, idx, (sub, batch)
+
+
+def pipeline_bytes(key_bytes, T, h_pre, h_post):
+    """SURVEY.md §8d algorithmic bytes per batch: inputs + 8 T snapshots + T
+    verdicts + E (H_pre + H_post) (history read once, written once)."""
+    return key_bytes + 9.0 * T + E_HIST * (h_pre + h_post)
+
+
+def stage_bytes(name, st, key_bytes):
+    """Bytes each stage must move in this design."""
+    T, R, W = st["txns"], st["reads"], st["writes"]
+    fill = st["history"] / max(1, st["dir_entries"])
+    if name == "merge":  # rewrite the touched pages + the directory
+        return 2 * st["pages_merged"] * fill * 36.0 + 2 * st["dir_entries"] * 52.0 + st["combined"] * 64.0
+    if name == "compaction":
+        return st["window_pages"] * fill * 36.0 + st["window_survivors"] * 36.0 + 2 * st["dir_entries"] * 52.0
+    if name == "read_check":
+        return R * (2 * 24.0 + 4 + 8 + 2 * 36.0) + T
+    if name == "sort_edges":
+        return (R + 2 * W) * (24.0 + 4 * 32.0) + (R + W) * 48.0
+    if name == "decide_combine":
+        return T * 8.0 + 2 * W * (4.0 + 8.0)
+    return key_bytes + 2 * (R + W) * 24.0  # encode
 
 
 def main():
@@ -77,24 +133,29 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL over xGMI; FDBCS_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs
+        backend = os.environ.get("FDBCS_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from foundationdb_amd import ConflictSet
-    from foundationdb_amd.workload import Workload
+    from foundationdb_amd.resolvers import scatter_verdicts
 
     cfg = args.config
-    wl = Workload(cfg)
+    src = Source(cfg, args.txns, world, rank)
     cs = ConflictSet(device=local, max_history=30_000_000)
 
     # ---- warmup: grow the history to steady state (untimed) ----------------
     t_w = time.time()
     verdict_host = None
     for i in range(args.warmup):
-        v, now, nold = wl.view(i)
+        v, now, nold, _T, _idx, _keep = src.host(i)
         verdict_host = cs.detect_view(v, now, nold, verdict_host)
         if rank == 0 and (i + 1) % 500 == 0:
             print(f"# warmup {i + 1}/{args.warmup} H={cs.history_size()} {time.time() - t_w:.1f}s",
@@ -106,25 +167,36 @@ def main():
     if not args.no_cpu and rank == 0 and world == 1:
         snap = cs.dump_arrays() + (cs.header_version, cs.oldest_version, cs.removal_key())
 
-    # ---- stage K measured batches in HBM --------------------------------------
-    staged = stage_batches(wl, args.warmup, args.steps, torch, dev)
-    T = staged[0][0].txn_count
-    verdicts = torch.zeros((args.steps, max(T, 1)), dtype=torch.uint8, device=dev)
-    cs.enable_stage_timing(bool(args.stage_timing))
+    # ---- stage the K measured batches (+ instrumented ones) in HBM -------------
+    n_stage = args.steps + args.stage_batches
+    staged = []
+    for i in range(args.warmup, args.warmup + n_stage):
+        v, now, nold, Tg, idx, keep = src.host(i)
+        dv, bufs = to_device(v, torch, dev)
+        didx = torch.from_numpy(idx).to(dev) if idx is not None else None
+        staged.append((dv, now, nold, Tg, didx, bufs, int(v.key_bytes_len)))
+        del keep
+    Tg = staged[0][3]
+    Tmax = max(max(s[0].txn_count for s in staged), 1)
+    sub_verdicts = torch.zeros((args.steps, Tmax), dtype=torch.uint8, device=dev)
+    global_verdicts = torch.full((args.steps, max(Tg, 1)), 2, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
 
-    # ---- timed region -----------------------------------------------------------
+    # ---- timed region: K steps -------------------------------------------------
     lat = []
-    stages = []
     t0 = time.perf_counter()
-    for k, (dv, now, nold, _bufs, _nb) in enumerate(staged):
+    for k in range(args.steps):
+        dv, now, nold, _Tg, didx, _b, _nb = staged[k]
         ts = time.perf_counter()
-        cs.detect_device(dv, now, nold, verdicts[k].data_ptr(), sync=True)
+        cs.detect_device(dv, now, nold, sub_verdicts[k].data_ptr(), sync=True)
+        if world > 1:  # proxy combine: scatter this resolver's verdicts, MIN over resolvers
+            scatter_verdicts(None, sub_verdicts[k].data_ptr(), didx.data_ptr(), dv.txn_count,
+                             global_verdicts[k].data_ptr())
+            dist.all_reduce(global_verdicts[k], op=dist.ReduceOp.MIN)
+            torch.cuda.current_stream().synchronize()
         lat.append(time.perf_counter() - ts)
-        if args.stage_timing:
-            stages.append(cs.stage_times())
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -133,55 +205,83 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
     H_post = cs.history_size()
-    total_txns = T * args.steps * world
+    total_txns = Tg * args.steps
     value = total_txns / elapsed
     lat_ms = np.array(lat) * 1e3
 
-    # ---- roofline (dominant stage) ----------------------------------------------
+    # ---- instrumented pass: per-stage HIP-event times on the engine's stream ---
     roofline = None
-    if stages:
-        st = np.array(stages)  # [K, 7] us: sort/encode, read, intra, combine, merge, compact, total
-        names = ["encode", "read_check", "intra_batch", "combine", "merge", "compaction"]
-        mean = st.mean(axis=0)
+    if args.stage_batches > 0:
+        cs.enable_stage_timing(True)
+        st_us, stats, hp = [], [], []
+        scratch = torch.zeros(Tmax, dtype=torch.uint8, device=dev)
+        for k in range(args.steps, n_stage):
+            dv, now, nold, _Tg, _didx, _b, nbytes = staged[k]
+            h0 = cs.history_size()
+            cs.detect_device(dv, now, nold, scratch.data_ptr(), sync=True)
+            st_us.append(cs.stage_times())
+            stats.append(cs.batch_stats())
+            hp.append((h0, cs.history_size(), nbytes, dv.txn_count))
+        cs.enable_stage_timing(False)
+        mean = np.array(st_us).mean(axis=0)  # [6 stages..., whole batch] us
+        batch_us = float(mean[6])
+        algo = float(np.mean([pipeline_bytes(nb, T, a, b) for a, b, nb, T in hp]))
         dom = int(np.argmax(mean[:6]))
-        key_bytes = float(np.mean([s[4] for s in staged]))
-        # SURVEY.md §8d algorithmic bytes per batch: inputs + verdicts + 28 B x (H_pre + H_post)
-        algo_batch = key_bytes + 9.0 * T + 28.0 * (H_pre + H_post) / 1.0
+        dom_bytes = float(np.mean([stage_bytes(STAGES[dom], s, nb) for s, (_a, _b, nb, _T) in zip(stats, hp)]))
+        achieved = algo / (batch_us * 1e-6) / 1e9
         roofline = {
             "bound": "hbm",
-            "kernel": names[dom],
-            "stage_us": {n: round(float(mean[i]), 2) for i, n in enumerate(names)},
-            "batch_us": round(float(mean[6]), 2),
-            "achieved": round(algo_batch / (mean[6] * 1e-6) / 1e9, 1),
+            "kernel": "detectConflicts pipeline (one batch, all stages; SURVEY §8d bytes)",
+            "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
+            "algo_bytes_per_batch": round(algo),
+            "batch_us": round(batch_us, 2),
+            "stage_us": {n: round(float(mean[i]), 2) for i, n in enumerate(STAGES)},
+            "dominant_stage": {
+                "name": STAGES[dom],
+                "us": round(float(mean[dom]), 2),
+                "bytes": round(dom_bytes),
+                "achieved": round(dom_bytes / (mean[dom] * 1e-6) / 1e9, 1),
+                "frac": round(dom_bytes / (mean[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "measured_over": f"{args.stage_batches} batches after the timed region (HIP events per stage)",
         }
-        roofline["frac"] = round(roofline["achieved"] / HBM_PEAK_GBS, 4)
+        prof = os.path.join(ROOT, "profiles", f"pmc_traffic_config{cfg}.json")
+        if os.path.exists(prof):  # per-batch HBM bytes from separate rocprofv3 --pmc passes
+            with open(prof) as f:
+                pm = json.load(f)
+            roofline["traffic"] = pm.get("bytes_per_batch")
+            roofline["traffic_source"] = pm.get("source")
 
     # ---- CPU baseline (oracle, 1 core) on the same batches, same start state -----
     cpu = None
     if snap is not None:
         from oracle import CpuSpec
-        from foundationdb_amd.workload import Workload as W2
         vers, lens, offs, kb, v0, oldest, rk = snap
         c = CpuSpec()
         c.load_history_arrays(len(vers), vers, lens, offs, kb, v0=v0, oldest=oldest, removal_key=rk)
-        wl2 = W2(cfg)
         n, mism, tc = 0, 0, 0.0
-        gv = verdicts.cpu().numpy()
+        gv = sub_verdicts.cpu().numpy()
         while n < args.steps and tc < args.cpu_seconds:
-            b, now, nold = wl2.batch(args.warmup + n)
+            b, now, nold = src.wl.batch(args.warmup + n)
             ts = time.perf_counter()
             vc = c.detect_packed(b, now, nold)
             tc += time.perf_counter() - ts
-            mism += int((vc != gv[n][:T]).sum())
+            mism += int((vc != gv[n][:b.T]).sum())
             n += 1
-        cpu = {"value": round(n * T / tc, 1), "unit": "txn/s", "cores": 1, "kind": "port",
-               "sample": f"config {cfg}: batches {args.warmup}..{args.warmup + n - 1} ({n} x {T} txns) from the "
+        cpu = {"value": round(n * Tg / tc, 1), "unit": "txn/s", "cores": 1, "kind": "port",
+               "sample": f"config {cfg}: batches {args.warmup}..{args.warmup + n - 1} ({n} x {Tg} txns) from the "
                          f"GPU's steady-state history (H={H_pre}); verdict mismatches vs GPU: {mism}"}
 
     if rank == 0:
+        if world > 1:
+            workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
+                        f"5M-version window; {world} key-range resolvers (proxy split + RCCL MIN combine)")
+        else:
+            workload = f"config{cfg}: {Tg}-txn batches, 5R+2W, uniform 16-byte keys, 5M-version window"
         out = {
             "metric": "resolved txns/sec (whole node) at 5k-txn batches; p99 detectConflicts latency",
             "value": round(value, 1),
@@ -197,8 +297,7 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (deterministic generator, SURVEY.md §8d)",
-            "config": {"workload": f"config{cfg}: {T}-txn batches, 5R+2W, uniform 16-byte keys, 5M-version window",
-                       "txns_per_batch": T, "history_pre": H_pre, "history_post": H_post,
+            "config": {"workload": workload, "txns_per_batch": Tg, "history_pre": H_pre, "history_post": H_post,
                        "parallelism": f"keyrange{world}" if world > 1 else "single"},
             "roofline": roofline,
             "cpu_baseline": cpu,

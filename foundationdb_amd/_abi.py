@@ -72,7 +72,13 @@ FDBCS_FUNCS = [
     ("fdbcs_enable_stage_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("fdbcs_stage_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
     ("fdbcs_stream", C.c_void_p, [C.c_void_p]),
+    ("fdbcs_batch_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_debug_phases", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
+    ("fdbcs_split_batch", C.c_int,
+     [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(BatchView), C.c_void_p,
+      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fdbcs_key_owner", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("fdbcs_scatter_verdicts", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
 ]

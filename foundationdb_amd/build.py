@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("FDBCS_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip"]
+HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip", "resolvers.hip"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value"]
 if os.environ.get("FDBCS_PHASES"):  # profiling build: kernels record phase timestamps
     HIP_FLAGS.append("-DFDBCS_PHASES")

@@ -130,6 +130,15 @@ class ConflictSet:
         return list(out[:n])
 
     # --- whole-batch entry points -------------------------------------------------
+    STAT_NAMES = ("txns", "reads", "writes", "combined", "pages_merged", "dir_entries", "history", "window_pages",
+                  "window_survivors", "dependents", "decision_rounds")
+
+    def batch_stats(self):
+        """Shape and outcome of the last synchronized batch (fdbcs_batch_stats)."""
+        out = (C.c_int64 * len(self.STAT_NAMES))()
+        n = check(self._lib.fdbcs_batch_stats(self.handle, out, len(self.STAT_NAMES)))
+        return dict(zip(self.STAT_NAMES, [int(x) for x in out[:n]]))
+
     def detect_packed(self, batch: PackedBatch, now, new_oldest):
         """addTransaction x T + detectConflicts for a packed host batch; returns the verdict bytes."""
         out = np.zeros(max(batch.T, 1), np.uint8)
@@ -140,7 +149,7 @@ class ConflictSet:
     def detect_view(self, host_view, now, new_oldest, out=None):
         """detectConflicts on a raw host fdbcs_batch_view (e.g. generator memory)."""
         T = host_view.txn_count
-        if out is None:
+        if out is None or out.size < max(T, 1):
             out = np.zeros(max(T, 1), np.uint8)
         check(self._lib.fdbcs_batch_detect_packed(self.handle, C.byref(host_view), now, new_oldest,
                                                   out.ctypes.data), "detectConflicts")

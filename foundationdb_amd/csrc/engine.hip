@@ -118,6 +118,7 @@ struct fdbcs {
     double stage_us[7] = {0};
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
+    int64_t last_T = 0, last_R = 0, last_W = 0;  // shape of the last batch (stats)
 };
 
 namespace {
@@ -414,6 +415,9 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
     if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    cs->last_T = T;
+    cs->last_R = R;
+    cs->last_W = W;
     BatchBufs& b = cs->b;
     HistBufs& h = cs->h;
     hipStream_t s = cs->stream;
@@ -899,6 +903,16 @@ int fdbcs_stage_times(fdbcs* cs, double* out_us, int cap) {
     if (!cs->have_times) return 0;
     int n = std::min(cap, 7);
     for (int i = 0; i < n; i++) out_us[i] = cs->stage_us[i];
+    return n;
+}
+
+int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
+    if (!cs || !out) return FDBCS_E_ARG;
+    const Scalars& h = *cs->sc_host;
+    const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
+                                    h.win_surv, h.n_dep, h.jac_iters};
+    const int n = std::min(cap, (int)FDBCS_STATS);
+    for (int i = 0; i < n; i++) out[i] = v[i];
     return n;
 }
 

@@ -152,6 +152,36 @@ int  fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* dev_batch,
                          int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
                          int sync);
 
+/* ---- Key-range resolvers: the proxy side of multi-resolver scale-out ------------ */
+
+/* ResolutionRequestBuilder::addTransaction (MasterProxyServer.actor.cpp:267-307)
+ * for a static key -> resolver map of nres resolvers: resolver g owns keys in
+ * [bound[g-1], bound[g]) with bound[-1] = "" and bound[nres-1] = +infinity;
+ * the nres-1 bounds (strictly ascending) are bound_bytes[bound_off[i] ..
+ * + bound_len[i]).  Writes into *out the sub-batch resolver `resolver`
+ * receives: every transaction with at least one read or write range
+ * intersecting its keys, in batch order, carrying all such ranges unclipped
+ * and its read_snapshot; txn_index[i] = the sub-batch transaction's index in
+ * the input.  The output arrays are caller-provided with the input's sizes
+ * (T, T+1, T+1, 2R+2W, 2R+2W, T); out->key_bytes aliases in->key_bytes.
+ * Host memory only. */
+int  fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
+                       const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
+                       fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
+                       uint64_t* key_off, uint32_t* key_len, int32_t* txn_index);
+
+/* The resolver owning key (keyResolvers lookup), or a negative status. */
+int32_t fdbcs_key_owner(int32_t nres, const uint8_t* bound_bytes, const uint64_t* bound_off,
+                        const uint32_t* bound_len, const uint8_t* key, uint32_t key_len);
+
+/* The proxy's verdict combine (MasterProxyServer.actor.cpp:558-569), one
+ * resolver's share: dev_global[dev_index[i]] = dev_sub[i] for i < n, on cs's
+ * stream (NULL cs: the null stream).  dev_global starts as T bytes of
+ * FDBCS_COMMITTED; the element-wise MIN over all resolvers' arrays (an RCCL
+ * MIN all-reduce when the resolvers are GPUs) is the combined verdict. */
+int  fdbcs_scatter_verdicts(fdbcs* cs, const uint8_t* dev_sub, const int32_t* dev_index, int32_t n,
+                            uint8_t* dev_global);
+
 /* ---- Introspection (tests, bench, checkpoint) --------------------------------- */
 
 /* Number of boundaries in the history (skip-list nodes other than the header). */
@@ -182,6 +212,14 @@ int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap);
  * timing is enabled. Returns the number of entries written. */
 int  fdbcs_enable_stage_timing(fdbcs* cs, int on);
 int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
+
+/* Shape and outcome of the last synchronized batch (bench byte models):
+ * [0] T  [1] R  [2] W  [3] combined write ranges  [4] history pages the merge
+ * rewrote  [5] directory entries  [6] history boundaries  [7] compaction
+ * window pages  [8] boundaries surviving in them  [9] transactions with
+ * intra-batch sources  [10] decision rounds.  Returns the count written. */
+#define FDBCS_STATS 11
+int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
 
 /* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the
  * kernels recorded at their phase boundaries during the last synchronized

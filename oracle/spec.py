@@ -166,3 +166,43 @@ class SpecBatch:
             keep_v.extend(cs.vers[j:])
             cs.keys, cs.vers = keep_k, keep_v
         return verdict, non_conflicting, too_old_list
+
+
+# ---------------------------------------------------------------------------
+# Multi-resolver scale-out (the proxy side), for a static key -> resolver map.
+
+
+def proxy_split(txns, bounds, g):
+    """Sub-batch resolver g receives: ResolutionRequestBuilder::addTransaction
+    (fdbserver/MasterProxyServer.actor.cpp:267-307).  Resolver g owns
+    [bounds[g-1], bounds[g]) (bounds[-1] = "", bounds[len] = +inf).  A read
+    or write range goes, unclipped, to every resolver whose keys it intersects
+    (keyResolvers.intersectingRanges, :283, :295); a transaction reaches a
+    resolver only through getOutTransaction (:256-265), i.e. only if one of
+    its ranges does, and keeps its read_snapshot and batch order.
+    txns: [(snapshot, reads, writes)]; returns (sub_txns, txn_index)."""
+    lo = bounds[g - 1] if g > 0 else b""
+    hi = bounds[g] if g < len(bounds) else None
+
+    def hits(b, e):
+        return lo < e and (hi is None or b < hi)
+
+    sub, idx = [], []
+    for t, (snap, reads, writes) in enumerate(txns):
+        rs = [r for r in reads if hits(*r)]
+        ws = [w for w in writes if hits(*w)]
+        if rs or ws:
+            sub.append((snap, rs, ws))
+            idx.append(t)
+    return sub, idx
+
+
+def proxy_combine(T, parts):
+    """The proxy's conservative combine (MasterProxyServer.actor.cpp:558-569):
+    committed[t] = min over the resolvers that received t of their verdict,
+    TransactionCommitted if none did.  parts: [(sub_verdicts, txn_index)]."""
+    out = [COMMITTED] * T
+    for verdicts, idx in parts:
+        for v, t in zip(verdicts, idx):
+            out[t] = min(out[t], v)
+    return out

@@ -138,6 +138,43 @@ def test_sort_bucket_paths(cs, buckets):
         del os.environ["FDBCS_TEST_SORT_BUCKETS"]
 
 
+def test_key_range_resolvers_on_gpu(gpu):
+    """Three key-range resolvers (three conflict sets on one GPU) fed by the
+    native proxy split; the GPU verdict scatter + MIN combine and every
+    resolver's history must equal three oracle resolvers'."""
+    import torch
+    from foundationdb_amd.resolvers import KeyRangeResolvers, combine, scatter_verdicts, uniform_bounds
+
+    kr = KeyRangeResolvers(uniform_bounds(3))
+    gres = [ConflictSet() for _ in range(3)]
+    cres = [CpuSpec() for _ in range(3)]
+    wl = Workload(2, txns=1500)
+    try:
+        for i in range(8):
+            batch, now, nold = wl.batch(i)
+            full = torch.full((batch.T,), 2, dtype=torch.uint8, device="cuda")
+            parts = []
+            for g in range(3):
+                sub, idx = kr.split(batch, g)
+                vg = gres[g].detect_packed(sub, now, nold)
+                vc = cres[g].detect_packed(sub, now, nold)
+                assert np.array_equal(vg, vc), (i, g)
+                part = torch.full((batch.T,), 2, dtype=torch.uint8, device="cuda")
+                dv = torch.from_numpy(vg.copy()).cuda()
+                di = torch.from_numpy(idx).cuda()
+                torch.cuda.synchronize()
+                scatter_verdicts(None, dv.data_ptr(), di.data_ptr(), len(idx), part.data_ptr())
+                full = torch.minimum(full, part)
+                parts.append((vc, idx))
+            torch.cuda.synchronize()
+            assert np.array_equal(full.cpu().numpy(), combine(batch.T, parts))
+        for g in range(3):
+            same_history(gres[g], cres[g])
+    finally:
+        for x in gres:
+            x.close()
+
+
 def test_config2_full_batches(cs):
     """Config 2 at its real batch size (5,000 txns, 5R+2W) from an empty history."""
     cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
