@@ -84,10 +84,36 @@ def build_oracle(verbose=False):
     return ORACLE_LIB
 
 
+SHIM = os.path.join(PKG, "shim", "ConflictSetShim.cpp")
+SHIM_CHECK = os.path.join(ROOT, "tests", "shim", "shim_smoke")
+REF_HEADER_DIR = os.environ.get("FDBCS_REFERENCE", "/root/reference")
+
+
+def build_shim_check(verbose=False):
+    """Compile the ConflictSet.h drop-in TU against the reference's own
+    fdbserver/ConflictSet.h (present only in the build container) and link it
+    with libfdbcs.so into tests/shim/shim_smoke, which the GPU tests run.
+    Skipped (returns None) where the reference tree is absent."""
+    hdr = os.path.join(REF_HEADER_DIR, "fdbserver", "ConflictSet.h")
+    if not os.path.exists(hdr):
+        return None
+    main = os.path.join(ROOT, "tests", "shim", "shim_main.cpp")
+    stub = os.path.join(ROOT, "tests", "shim", "stub")
+    deps = [SHIM, main, os.path.join(stub, "fdbclient", "CommitTransaction.h"), LIB,
+            os.path.join(ROOT, "include", "fdbcs.h")]
+    if _stale(SHIM_CHECK, deps):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-iquote", stub, "-iquote", REF_HEADER_DIR, "-I",
+              os.path.join(ROOT, "include"), SHIM, main, "-L", PKG, "-lfdbcs",
+              "-Wl,-rpath,$ORIGIN/../../foundationdb_amd", "-o", SHIM_CHECK], verbose)
+    return SHIM_CHECK
+
+
 def build_all(verbose=False):
     with ThreadPoolExecutor(3) as ex:
         fs = [ex.submit(build_hip, verbose), ex.submit(build_workload, verbose), ex.submit(build_oracle, verbose)]
-        return [f.result() for f in fs]
+        out = [f.result() for f in fs]
+    out.append(build_shim_check(verbose))
+    return out
 
 
 if __name__ == "__main__":

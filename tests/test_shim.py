@@ -1,0 +1,76 @@
+"""The ConflictSet.h drop-in TU (foundationdb_amd/shim/ConflictSetShim.cpp).
+
+CPU: it compiles against the reference's own fdbserver/ConflictSet.h and links
+with libfdbcs.so (build container only: the reference tree is not on the GPU
+box).  GPU: the linked driver runs batches through ConflictBatch exactly as
+Resolver.actor.cpp:140-153 does, and nonConflicting / tooOld must equal the
+oracle's."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from foundationdb_amd import build as B
+from foundationdb_amd.workload import Workload
+from gen import mixed_stream, tiny_stream
+from oracle import CpuSpec
+
+HAVE_REF = os.path.exists(os.path.join(B.REF_HEADER_DIR, "fdbserver", "ConflictSet.h"))
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference tree absent (GPU box)")
+def test_shim_compiles_against_reference_header():
+    path = B.build_shim_check()
+    assert path and os.path.exists(path)
+
+
+def write_batches(path, batches):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<i", len(batches)))
+        for batch, now, nold in batches:
+            txns = batch.txns()
+            f.write(struct.pack("<qqi", now, nold, len(txns)))
+            for snap, reads, writes in txns:
+                f.write(struct.pack("<qii", snap, len(reads), len(writes)))
+                for b, e in reads + writes:
+                    f.write(struct.pack("<I", len(b)) + b + struct.pack("<I", len(e)) + e)
+
+
+def read_results(path, n):
+    out = []
+    with open(path, "rb") as f:
+        for _ in range(n):
+            (k,) = struct.unpack("<i", f.read(4))
+            nc = list(struct.unpack(f"<{k}i", f.read(4 * k)))
+            (m,) = struct.unpack("<i", f.read(4))
+            to = list(struct.unpack(f"<{m}i", f.read(4 * m)))
+            out.append((nc, to))
+    return out
+
+
+@pytest.mark.gpu
+def test_shim_resolver_call_sequence(gpu, tmp_path):
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built (needs the reference header at build time)")
+    batches = list(tiny_stream(11, n_batches=20, max_txns=40)) + list(mixed_stream(12, n_batches=6))
+    wl = Workload(2, txns=600)
+    batches += [wl.batch(i) for i in range(4)]
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    write_batches(fin, batches)
+    subprocess.run([B.SHIM_CHECK, str(fin), str(fout)], check=True, timeout=120)
+    got = read_results(fout, len(batches))
+    c = CpuSpec()
+    for (batch, now, nold), (nc, to) in zip(batches, got):
+        v = c.detect_packed(batch, now, nold)
+        assert nc == list(np.nonzero(v == 2)[0])
+        assert to == list(np.nonzero(v == 1)[0])
+
+
+@pytest.mark.gpu
+def test_shim_skiplisttest_entry(gpu):
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    r = subprocess.run([B.SHIM_CHECK, "skiplisttest"], capture_output=True, text=True, timeout=120, check=True)
+    assert "fdbcs skipListTest" in r.stdout
