@@ -119,6 +119,7 @@ struct fdbcs {
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
     int64_t last_T = 0, last_R = 0, last_W = 0;  // shape of the last batch (stats)
+    int64_t sorts = 0;                           // sorts launched (sort-counter parity)
 };
 
 namespace {
@@ -306,7 +307,11 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             return r;
         cs->capW = n;
     }
-    if (!b.ss_cnt && ((r = dalloc(b.ss_cnt, 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)))) return r;
+    if (!b.ss_cnt) {
+        if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024))) return r;
+        HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 2 * 1024 * sizeof(int32_t), s));
+        HIPOK(hipMemsetAsync(b.ss_q, 0, 2 * 1024 * sizeof(SRec), s));  // equal records: valid (sorted) splitters
+    }
     if (R + 2 * W > cs->capSortRec) {
         const int64_t n = std::max<int64_t>(R + 2 * W, 4096);
         dfree(b.ss_bkt);
@@ -423,21 +428,22 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     hipStream_t s = cs->stream;
     Scalars* sc = cs->sc;
     record(cs, 0);
-    launch_prep(v, cs->oldest, b, sc, s);
-    launch_encode(v, b, sc, s);
+    launch_ingest(v, cs->oldest, b, sc, s);
     record(cs, 1);
     launch_read_check(v, b, h, cs->cur, sc, cs->v0, s);
     record(cs, 2);
-    launch_sort_ranges(v, b, sc, !cs->have_quantiles, s);
-    cs->have_quantiles = true;
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), s)) {
+        cs->sorts++;
+        cs->have_quantiles = true;
+    }
     launch_edges(v, b, sc, s);
     record(cs, 3);
     launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s);
     record(cs, 4);
-    launch_merge(v, b, h, cs->cur, sc, now, cs->v0, s);
+    const bool compact = new_oldest > cs->oldest;
+    launch_merge(v, b, h, cs->cur, sc, now, cs->v0, !compact, s);
     cs->cur ^= 1;
     record(cs, 5);
-    const bool compact = new_oldest > cs->oldest;
     if (compact) {
         launch_compact(b, h, cs->cur, sc, new_oldest, s);
         cs->cur ^= 1;
@@ -455,7 +461,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
             }
             cs->have_times = true;
         }
-        if (cs->sc_host->err) return cs->sc_host->err;
+        if (cs->sc_host->last_err) return cs->sc_host->last_err;
     }
     return FDBCS_OK;
 }
@@ -543,7 +549,7 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
     if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
     if ((r = sync_state(cs))) return r;
-    if (cs->sc_host->err) return cs->sc_host->err;
+    if (cs->sc_host->last_err) return cs->sc_host->last_err;
     if (T) memcpy(verdict, cs->vpin, (size_t)T);
     if (cs->timing) {
         float ms;

@@ -40,7 +40,7 @@ struct BatchBufs {
     SRec* sw;            // sorted write endpoints
     uint32_t* sw_slot;   // [2W]  their slots (compact copy for the combine)
     // sample sort scratch
-    int32_t* ss_cnt;     // [2 * 1024] bucket counts (k_prep zeroes them)
+    int32_t* ss_cnt;     // [2 parities][2 * 1024] bucket counts; a batch zeroes the next batch's
     SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
     int32_t* ss_bkt;     // [R + 2W] bucket of each record
     SRec* ss_tmp;        // bucket staging rows
@@ -110,11 +110,11 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
                        int64_t* tmp, hipStream_t s);
 
 // ---- batch stages (kernels_batch.hip) ----
-void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s);
-void launch_encode(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s);
 void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                        hipStream_t s);
-void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, hipStream_t s);
+bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
+                        hipStream_t s);
 int64_t sort_staging_records(int R, int W);
 void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
@@ -124,7 +124,7 @@ void configure_batch_kernels();
 // ---- history stages (kernels_hist.hip) ----
 int plan_blocks(int cap_dir);
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
-                  int64_t v0, hipStream_t s);
+                  int64_t v0, bool end_of_batch, hipStream_t s);
 void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s);
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s);
 void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s);

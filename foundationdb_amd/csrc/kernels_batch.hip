@@ -16,43 +16,16 @@
 namespace fdbcs_dev {
 
 
-// ---------------------------------------------------------------- prep ----
-__global__ __launch_bounds__(256) void k_prep(int T, const int64_t* __restrict__ snap, const int32_t* __restrict__ ro,
-                                              const int32_t* __restrict__ wo, int64_t oldest,
-                                              uint8_t* __restrict__ too_old, uint8_t* __restrict__ hist,
-                                              int32_t* __restrict__ read_txn, int32_t* __restrict__ write_txn,
-                                              Scalars* sc, int32_t* __restrict__ ss_cnt) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0)
-        for (int k = threadIdx.x; k < 2 * 1024; k += blockDim.x) ss_cnt[k] = 0;  // sample-sort bucket counters
-    if (t == 0) {  // per-batch scalars (first kernel of the batch)
-        sc->err = 0;
-        sc->btail_used = 0;
-        sc->n_comb = 0;
-    }
-    if (t >= T) return;
-    const int r0 = ro[t], r1 = ro[t + 1];
-    // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
-    too_old[t] = (snap[t] < oldest && r1 > r0) ? 1 : 0;
-    hist[t] = 0;
-    for (int r = r0; r < r1; r++) read_txn[r] = t;
-    for (int w = wo[t], w1 = wo[t + 1]; w < w1; w++) write_txn[w] = t;
-}
-
-void launch_prep(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    hipLaunchKernelGGL(k_prep, dim3(std::max(1, cdiv(v.txn_count, 256))), dim3(256), 0, s, v.txn_count, v.snapshot,
-                       v.read_off, v.write_off, oldest, b.too_old, b.hist, b.read_txn, b.write_txn, sc, b.ss_cnt);
-}
-
-// -------------------------------------------------------------- encode ----
-__global__ __launch_bounds__(256) void k_encode(int64_t nslots, const uint64_t* __restrict__ koff,
-                                                const uint32_t* __restrict__ klen, const uint8_t* __restrict__ bytes,
-                                                KeyArrays out, uint8_t* __restrict__ btail, uint64_t btail_cap,
-                                                Scalars* sc) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nslots) return;
-    const uint8_t* p = bytes + koff[s];
-    uint32_t L = klen[s];
+// -------------------------------------------------------------- ingest ----
+// One launch, two kinds of blocks:
+//   prep   (lane per txn):   addTransaction's tooOld rule (SkipList.cpp:979-1008)
+//                            and the range -> txn maps;
+//   encode (lane per range): both endpoints -> (hi, lo, meta, tail) records
+//                            (replaces KeyInfo/getCharacter, :134-177) and the
+//                            begin < end precondition.
+// The per-batch scalars the encoder allocates from (err, btail_used) were
+// reset by the previous batch's last kernel (k_bmax_commit, end of batch).
+__device__ inline Key encode_key(const uint8_t* p, uint32_t L, uint8_t* btail, uint64_t btail_cap, Scalars* sc) {
     if (L > FDBCS_MAX_KEY) {
         atomicCAS(&sc->err, 0, FDBCS_E_KEY);
         L = FDBCS_MAX_KEY;
@@ -78,25 +51,60 @@ __global__ __launch_bounds__(256) void k_encode(int64_t nslots, const uint64_t* 
             tail = d;
         }
     }
-    out.hi[s] = hi;
-    out.lo[s] = lo;
-    out.meta[s] = (b16 << 24) | L;
-    out.tail[s] = tail;
+    return Key{hi, lo, (b16 << 24) | L, tail};
 }
 
-// every range must be non-empty: reference precondition
-__global__ __launch_bounds__(256) void k_validate(int64_t nranges, KeyArrays k, Scalars* sc) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nranges) return;
-    if (kcmp(k.get(2 * i), k.get(2 * i + 1)) >= 0) atomicCAS(&sc->err, 0, FDBCS_E_RANGE);
+struct IngestArgs {
+    int T, R, W, prep_blocks;
+    const int64_t* snap;
+    const int32_t* ro;
+    const int32_t* wo;
+    const uint64_t* koff;
+    const uint32_t* klen;
+    const uint8_t* bytes;
+    int64_t oldest;
+    uint8_t* too_old;
+    uint8_t* hist;
+    int32_t* read_txn;
+    int32_t* write_txn;
+    KeyArrays keys;
+    uint8_t* btail;
+    uint64_t btail_cap;
+    Scalars* sc;
+};
+
+__global__ __launch_bounds__(256) void k_ingest(IngestArgs A) {
+    if ((int)blockIdx.x < A.prep_blocks) {
+        const int t = blockIdx.x * blockDim.x + threadIdx.x;
+        if (t == 0) A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+        if (t >= A.T) return;
+        const int r0 = A.ro[t], r1 = A.ro[t + 1];
+        // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
+        A.too_old[t] = (A.snap[t] < A.oldest && r1 > r0) ? 1 : 0;
+        A.hist[t] = 0;
+        for (int r = r0; r < r1; r++) A.read_txn[r] = t;
+        for (int w = A.wo[t], w1 = A.wo[t + 1]; w < w1; w++) A.write_txn[w] = t;
+        return;
+    }
+    const int64_t i = (int64_t)(blockIdx.x - A.prep_blocks) * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)A.R + A.W) return;
+    const Key b = encode_key(A.bytes + A.koff[2 * i], A.klen[2 * i], A.btail, A.btail_cap, A.sc);
+    const Key e = encode_key(A.bytes + A.koff[2 * i + 1], A.klen[2 * i + 1], A.btail, A.btail_cap, A.sc);
+    A.keys.put(2 * i, b);
+    A.keys.put(2 * i + 1, e);
+    if (kcmp(b, e) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
 }
 
-void launch_encode(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    const int64_t nr = (int64_t)v.read_count + v.write_count;
-    if (nr == 0) return;
-    hipLaunchKernelGGL(k_encode, dim3(cdiv(2 * nr, 256)), dim3(256), 0, s, 2 * nr, v.key_off, v.key_len, v.key_bytes,
-                       b.keys, b.btail, b.btail_cap, sc);
-    hipLaunchKernelGGL(k_validate, dim3(cdiv(nr, 256)), dim3(256), 0, s, nr, b.keys, sc);
+void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s) {
+    IngestArgs A;
+    A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
+    A.prep_blocks = std::max(1, cdiv(v.txn_count, 256));
+    A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
+    A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
+    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.write_txn = b.write_txn;
+    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc;
+    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
+    hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(256), 0, s, A);
 }
 
 // ---------------------------------------------------------- read check ----
@@ -241,7 +249,8 @@ struct SortJobs {
     SRec* out[2];          // sorted output
     uint32_t* out_slot;    // [n1] slots of job 1's sorted records (compact copy)
     SRec* quant;           // [2][SS_Q] quantiles (persist across batches)
-    int32_t* cnt;          // [2][SS_MAXB]
+    int32_t* cnt;          // [2][SS_MAXB] this batch's bucket counts
+    int32_t* cnt_next;     // [2][SS_MAXB] the next batch's (zeroed here)
     int32_t* bkt;          // [n0 + n1] bucket of each record
     SRec* tmp;             // [2][SS_MAXB][SS_ROW] staging rows
     Scalars* sc;
@@ -395,6 +404,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
     const int lane = threadIdx.x;
     const int32_t* cnt = J.cnt + job * SS_MAXB;
     const uint8_t* const* tails = keys.tail;
+    for (int k = blockIdx.x * 64 + lane; k < 2 * SS_MAXB; k += gridDim.x * 64) J.cnt_next[k] = 0;
     int part = 0;
     for (int k = lane; k < b; k += 64) part += cnt[k];
     const int offset = wave_reduce_sum(part);
@@ -467,7 +477,8 @@ static int ss_buckets(int n) {
 // Staging records the sort needs (engine sizes b.ss_tmp).
 int64_t sort_staging_records(int, int) { return 2 * (int64_t)SS_MAXB * SS_ROW; }
 
-void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, hipStream_t s) {
+bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
+                        hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
     SortJobs J;
     J.n[0] = R;
@@ -480,7 +491,8 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     J.out[1] = b.rec_w0;
     J.out_slot = b.sw_slot;
     J.quant = b.ss_q;
-    J.cnt = b.ss_cnt;
+    J.cnt = b.ss_cnt + parity * 2 * SS_MAXB;
+    J.cnt_next = b.ss_cnt + (parity ^ 1) * 2 * SS_MAXB;
     J.bkt = b.ss_bkt;
     J.tmp = b.ss_tmp;
     J.sc = sc;
@@ -488,10 +500,11 @@ void launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     J.blocks0 = cdiv(J.n[0], 256);
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
-    if (J.n[0] + J.n[1] == 0) return;
+    if (J.n[0] + J.n[1] == 0) return false;
     if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys);
     hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
     hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
+    return true;  // the counters of the other parity are zero now
 }
 
 // --------------------------------------------------------------- edges ----

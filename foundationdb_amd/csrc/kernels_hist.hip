@@ -644,7 +644,7 @@ __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y
 // the merge freed back onto the free stack (above the ones it took), then
 // commit the directory size, free-stack top and history size.
 __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
-                                                     int32_t* free_stack) {
+                                                     int32_t* free_stack, int end_of_batch) {
     const int Dn = sc->D_next;
     if (freed_list) {
         const int base = sc->free_top - sc->extra_total;
@@ -664,14 +664,19 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         sc->D = Dn;
         sc->free_top = sc->free_next;
         sc->H = d.start[Dn];
+        if (end_of_batch) {  // the next batch's encoder allocates from these
+            sc->last_err = sc->err;
+            sc->err = 0;
+            sc->btail_used = 0;
+        }
     }
 }
 
-static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s,
+static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s, bool end_of_batch,
                                const int32_t* freed_list = nullptr) {
     const int groups = cdiv(h.cap_dir, 64);
     hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
-                       h.free_stack);
+                       h.free_stack, (int)end_of_batch);
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
@@ -680,13 +685,13 @@ void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStrea
     scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
     hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
     hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
-    launch_bmax_commit(h, cur, sc, s);
+    launch_bmax_commit(h, cur, sc, s, true);
 }
 
 int plan_blocks(int cap_dir) { return cdiv(cap_dir, PS_BLOCK); }
 
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
-                  int64_t v0, hipStream_t s) {
+                  int64_t v0, bool end_of_batch, hipStream_t s) {
     const int W = v.write_count;
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
@@ -717,7 +722,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
         hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, max_aff))), dim3(256), 0, s, A);
     }
-    launch_bmax_commit(h, cur ^ 1, sc, s, b.freed_list);
+    launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
 }
 
 // ------------------------------------------------------------ compaction ----
@@ -949,7 +954,7 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        b.win_keep, b.win_off, h.free_stack, da);
     hipLaunchKernelGGL(k_win_dir, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, src, dst, sc, da, b.win_off,
                        h.free_stack);
-    launch_bmax_commit(h, cur ^ 1, sc, s);
+    launch_bmax_commit(h, cur ^ 1, sc, s, true);
 }
 
 // ------------------------------------------------------------------ reset ----
