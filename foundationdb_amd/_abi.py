@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libfdbcs.so")
+LIB_PATH = os.environ.get("FDBCS_LIB_PATH", os.path.join(PKG, "libfdbcs.so"))  # override: experiments only
 WL_PATH = os.path.join(PKG, "libfdbcs_workload.so")
 
 CONFLICT, TOO_OLD, COMMITTED = 0, 1, 2

@@ -64,6 +64,12 @@ __device__ inline T wave_reduce_sum(T x) {
 }
 
 template <typename T>
+__device__ inline T wave_reduce_min(T x) {
+    const T highest = std::numeric_limits<T>::max();
+    return wave_read_lane(wave_incl_scan_op(x, highest, [](T a, T b) { return a < b ? a : b; }), 63);
+}
+
+template <typename T>
 __device__ inline T wave_reduce_max(T x) {
     const T lowest = std::numeric_limits<T>::lowest();
     return wave_read_lane(wave_incl_scan_op(x, lowest, [](T a, T b) { return a > b ? a : b; }), 63);

@@ -224,12 +224,20 @@ int grow_tail(fdbcs* cs, uint64_t need) {
     return FDBCS_OK;
 }
 
+int alloc_keys(KeyArrays& k, int64_t n) {
+    int r;
+    if ((r = dalloc(k.hi, n)) || (r = dalloc(k.lo, n)) || (r = dalloc(k.meta, n)) || (r = dalloc(k.tail, n)))
+        return r;
+    return FDBCS_OK;
+}
+void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.tail); }
+
 void free_plan(BatchBufs& b) {
     dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff);
     dfree(b.blk_agg); dfree(b.blk_diff);
     dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn); dfree(b.aff_parts);
     dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off); dfree(b.aff_free_off); dfree(b.aff_start);
-    dfree(b.freed_list);
+    dfree(b.freed_list); dfree(b.aff_page); dfree(b.aff_cnt);
 }
 
 void free_batch(BatchBufs& b) {
@@ -240,7 +248,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_bkt); dfree(b.ss_tmp);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
-    dfree(b.cb_slot); dfree(b.ce_slot);
+    dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     free_plan(b);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
@@ -250,13 +258,6 @@ void free_batch(BatchBufs& b) {
     dfree(b.scan_tmp);
 }
 
-int alloc_keys(KeyArrays& k, int64_t n) {
-    int r;
-    if ((r = dalloc(k.hi, n)) || (r = dalloc(k.lo, n)) || (r = dalloc(k.meta, n)) || (r = dalloc(k.tail, n)))
-        return r;
-    return FDBCS_OK;
-}
-void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.tail); }
 
 // Size the per-batch buffers (grow only).
 int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes) {
@@ -294,12 +295,13 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (W > cs->capW) {
         int64_t n = std::max<int64_t>(W, 1024);
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
-        dfree(b.cb_slot); dfree(b.ce_slot);
+        dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_combine
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
-            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.pb, n)) ||
+            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = alloc_keys(b.rkb, n)) ||
+            (r = alloc_keys(b.rke, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
             (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||
@@ -359,7 +361,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.blk_diff, nblk)) || (r = dalloc(b.aff_list, n)) || (r = dalloc(b.aff_jlo, n)) ||
             (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) || (r = dalloc(b.aff_parts, n)) ||
             (r = dalloc(b.aff_nn_off, n)) || (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
-            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)))
+            (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)) ||
+            (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)))
             return r;
         HIPOK(hipMemsetAsync(b.acc.er, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.nn, 0, n * 4, s));

@@ -55,6 +55,7 @@ struct BatchBufs {
     // combined write ranges [W], as key slots of their begin / end
     int32_t* cb_slot;
     int32_t* ce_slot;
+    KeyArrays rkb, rke;  // [W] their keys, compact (written by k_plan_ranges)
     // insertion plan [W]
     int32_t* pb; int32_t* ib; int32_t* pe; int32_t* ie;
     uint8_t* need_e;
@@ -71,6 +72,8 @@ struct BatchBufs {
     int32_t* aff_parts;  // output pages
     int32_t* aff_nn_off; int32_t* aff_parts_off; int32_t* aff_extra_off; int32_t* aff_free_off;
     int64_t* aff_start;  // start[] of its first output page
+    int32_t* aff_page;   // its pool page and boundary count
+    int32_t* aff_cnt;
     int32_t* freed_list; // pages the merge frees, pushed after its pops
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order

@@ -405,8 +405,18 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
     const int32_t* cnt = J.cnt + job * SS_MAXB;
     const uint8_t* const* tails = keys.tail;
     for (int k = blockIdx.x * 64 + lane; k < 2 * SS_MAXB; k += gridDim.x * 64) J.cnt_next[k] = 0;
+    // offset = counts of the earlier buckets: lane L sums counts [16L, 16L+16)
+    // below b with four independent 16-byte loads (one round trip)
     int part = 0;
-    for (int k = lane; k < b; k += 64) part += cnt[k];
+    {
+        const int4* c4 = reinterpret_cast<const int4*>(cnt) + 4 * lane;
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int4 x = c4[v];
+            const int k0 = 16 * lane + 4 * v;
+            part += (k0 < b ? x.x : 0) + (k0 + 1 < b ? x.y : 0) + (k0 + 2 < b ? x.z : 0) + (k0 + 3 < b ? x.w : 0);
+        }
+    }
     const int offset = wave_reduce_sum(part);
     const int c = cnt[b];
     if (c == 0) return;

@@ -97,13 +97,16 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
                                                      Scalars* sc, int64_t v0, int32_t* __restrict__ pb_o,
                                                      int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
                                                      int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
-                                                     int64_t* __restrict__ vb_o, PageAcc acc) {
+                                                     int64_t* __restrict__ vb_o, PageAcc acc, KeyArrays rb,
+                                                     KeyArrays re) {
     if (sc->err) return;
     const int nC = sc->n_comb;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nC) return;
     const int D = sc->D;
     const Key b = cb.get(j), e = ce.get(j);
+    rb.put(j, b);  // compact copies for the page merge
+    re.put(j, e);
     const int p_b = dir_search(dir, D, b, 1);
     const int c_b = dir.cnt[p_b], g_b = dir.page[p_b];
     const int i_b = page_lb(pool, g_b, 0, c_b, b);
@@ -187,6 +190,8 @@ __device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, 
 }
 
 // packed scan words: (parts << 32 | affected), (freed << 32 | extra), (delta << 32 | nn)
+// An affected page keeps its pool page for its first part; further parts come
+// from the free stack ("extra"); a page that disappears goes back ("freed").
 __device__ inline void pack_item(const PlanItem& it, int cnt, int64_t w[3]) {
     const int64_t extra = it.affected && it.parts > 1 ? it.parts - 1 : 0;
     const int64_t freed = it.affected && it.parts == 0;
@@ -263,7 +268,7 @@ struct PlanArgs {
     const int64_t* blk_agg;
     const int32_t* blk_diff;
     int32_t *aff_list, *aff_jlo, *aff_jhi, *aff_nn, *aff_parts, *aff_nn_off, *aff_parts_off, *aff_extra_off,
-        *aff_free_off;
+        *aff_free_off, *aff_page, *aff_cnt;
     int64_t* aff_start;
 };
 
@@ -345,6 +350,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
             if (it[k].affected) {
                 const int a = (int)(uint32_t)ex[0];
                 A.aff_list[a] = x;
+                A.aff_page[a] = A.src.page[x];
+                A.aff_cnt[a] = cnt[k];
                 A.aff_jlo[a] = it[k].jlo;
                 A.aff_jhi[a] = it[k].jhi;
                 A.aff_nn[a] = it[k].nn;
@@ -424,12 +431,13 @@ struct MergeArgs {
     const int32_t* free_stack;
     int32_t* freed_list;
     const int32_t* aff_list;
+    const int32_t *aff_page, *aff_cnt;
     const int32_t *jlo, *jhi, *nn, *nn_off, *parts, *parts_off, *extra_off, *free_off;
     const int64_t* aff_start;
     const int32_t *pb, *ib, *pe, *ie;
     const uint8_t* need_e;
     const int64_t* vb;
-    IndirectKeys cb, ce;
+    KeyArrays rb, re;  // keys of each combined range's begin / end (compact, from K1)
     Pool ne;
     int32_t* ne_ins;
     uint8_t* arena;
@@ -447,162 +455,231 @@ __device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, u
     D.page[x] = page; D.cnt[x] = cnt; D.fhi[x] = hi; D.flo[x] = lo; D.fmeta[x] = meta; D.ftail[x] = tail;
 }
 
-// K3: one workgroup per affected page: load it into LDS, drop erased entries,
-// merge in the new boundaries, write 0..k output pages (the first in place,
-// the others from the free stack) and their directory entries at the
-// positions K2 assigned.  Part maxima come from LDS atomics as the entries
-// are written.  A page that disappears goes back on the free stack.
-//
-// Fast path (<= JCAP combined ranges touch the page -- the common case): the
-// ranges' insertion plan and the page's new entries are staged in LDS, so a
-// page costs ~3 dependent global round trips.  Otherwise the new entries go
-// through the global scratch list (A.ne) and the plan is read from global.
-static constexpr int JCAP = 64;
+// K3: one wavefront per affected page (four pages per workgroup, no
+// workgroup barriers), four consecutive old slots per lane.
+//   1. plan lanes (one per combined range touching the page) mark the slots
+//      their range erases (+1 / -1 in a difference array) and count the new
+//      boundaries inserted before each old slot (b_j at ib_j, e_j at ie_j);
+//   2. slot lanes prefix-scan both: an old slot survives if no range covers
+//      it, and lands at (kept before it) + (new entries at or before it);
+//   3. every lane writes its surviving old entries, every plan lane its new
+//      ones at (new entries before it) + (kept before its slot).
+// Output pages: the first in place (the lane's old slots are loaded before any
+// write), the others from the free stack; a page that disappears goes back on
+// it (k_bmax_commit pushes it after every pop).  Directory entries go to the
+// positions K2 assigned.  Old slots before the first changed one keep their
+// slot when the page stays one page, so they are not rewritten.
+static constexpr int MW_WAVES = 4;  // pages in flight per workgroup
 
-struct MergeShared {
-    uint64_t o_hi[PAGE], o_lo[PAGE];
-    int64_t o_ver[PAGE];
-    const uint8_t* o_tail[PAGE];
-    uint32_t o_meta[PAGE];
-    int32_t kb[PAGE + 1];
+struct WaveMerge {
+    int32_t er[PAGE + 1];   // erase marks (difference array), then kept-before per slot
+    int32_t ins[PAGE + 1];  // new boundaries inserted before each old slot
     long long pmax[MAXP];
-    int32_t tmp[256 / 64 + 1];
-    int32_t j_pb[JCAP], j_ib[JCAP], j_pe[JCAP], j_ie[JCAP];
-    int64_t j_vb[JCAP];
-    uint8_t j_need[JCAP];
-    uint64_t n_hi[2 * JCAP], n_lo[2 * JCAP];
-    int64_t n_ver[2 * JCAP];
-    const uint8_t* n_tail[2 * JCAP];
-    uint32_t n_meta[2 * JCAP];
-    int32_t n_ins[2 * JCAP];
+    // first key of each output part (its directory entry), written by whichever lane lands it
+    uint64_t f_hi[MAXP], f_lo[MAXP];
+    const uint8_t* f_tail[MAXP];
+    uint32_t f_meta[MAXP];
+    int32_t f_dp[MAXP];
 };
 
-template <bool FAST>
-__device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0, int extra_total) {
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline int lane_read(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+// A part's first entry: its directory entry is stashed in LDS (written after
+// the merge by one lane per part); parts beyond MAXP write it directly.
+__device__ inline void part_first_direct(const Dir& D, const MergeArgs& A, int a, int y, int q, int per,
+                                               int nout, int dp, uint64_t h, uint64_t l, uint32_t mt,
+                                               const uint8_t* tl) {
+    D.page[y] = dp; D.cnt[y] = min(per, nout - q * per);
+    D.fhi[y] = h; D.flo[y] = l; D.fmeta[y] = mt; D.ftail[y] = tl;
+    D.start[y] = A.aff_start[a] + (int64_t)q * per;
+}
+
+__device__ inline void part_first(WaveMerge& S, const Dir& D, const MergeArgs& A, int a, int doff, int q, int per,
+                                  int nout, int dp, uint64_t h, uint64_t l, uint32_t mt, const uint8_t* tl) {
+    if (q < MAXP) {
+        S.f_hi[q] = h; S.f_lo[q] = l; S.f_meta[q] = mt; S.f_tail[q] = tl; S.f_dp[q] = dp;
+    } else {
+        part_first_direct(D, A, a, doff + q, q, per, nout, dp, h, l, mt, tl);
+    }
+}
+
+__device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int p = A.aff_list[a];
-    const int pg = A.dir.page[p], cntp = A.dir.cnt[p];
     const int parts = A.parts[a];
-    if (parts == 0) {  // wholly erased: returns to the free stack in k_bmax_commit (after all pops)
-        if (tid == 0) A.freed_list[A.free_off[a]] = pg;
+    const int pg = A.aff_page[a], cntp = A.aff_cnt[a];
+    if (parts == 0) {  // wholly erased: returns to the free stack in k_bmax_commit (after every pop)
+        if (lane == 0) A.freed_list[A.free_off[a]] = pg;
         return;
     }
     const int jlo = A.jlo[a], jhi = A.jhi[a];
-    const int nj = jhi - jlo + 1;
-    const int nn = A.nn[a], nn_off = A.nn_off[a];
-    const int xoff = A.extra_off[a];
-    const int doff = A.parts_off[a];
+    const int nn = A.nn[a];
+    const int xoff = A.extra_off[a], doff = A.parts_off[a];
     const int64_t pbase = (int64_t)pg * PAGE;
-    if (tid < cntp) {
-        S.o_hi[tid] = A.pool.hi[pbase + tid];
-        S.o_lo[tid] = A.pool.lo[pbase + tid];
-        S.o_meta[tid] = A.pool.meta[pbase + tid];
-        S.o_ver[tid] = A.pool.ver[pbase + tid];
-        S.o_tail[tid] = A.pool.tail[pbase + tid];
+    // this lane's old slots i0 .. i0+3, loaded before any write: part 0 is
+    // rewritten in place (slots past cnt are ignored)
+    const int i0 = 4 * lane;
+    uint64_t ohi[4], olo[4];
+    int64_t over[4];
+    uint32_t ometa[4];
+    const uint8_t* otail[4];
+    {
+        const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(A.pool.hi + pbase + i0);
+        const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(A.pool.lo + pbase + i0);
+        const longlong2* v2 = reinterpret_cast<const longlong2*>(A.pool.ver + pbase + i0);
+        const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(A.pool.tail + pbase + i0);
+        const uint4 m4 = *reinterpret_cast<const uint4*>(A.pool.meta + pbase + i0);
+        const ulonglong2 ha = h2[0], hb = h2[1], la = l2[0], lb = l2[1], ta = t2[0], tb = t2[1];
+        const longlong2 va = v2[0], vb = v2[1];
+        ohi[0] = ha.x; ohi[1] = ha.y; ohi[2] = hb.x; ohi[3] = hb.y;
+        olo[0] = la.x; olo[1] = la.y; olo[2] = lb.x; olo[3] = lb.y;
+        over[0] = va.x; over[1] = va.y; over[2] = vb.x; over[3] = vb.y;
+        ometa[0] = m4.x; ometa[1] = m4.y; ometa[2] = m4.z; ometa[3] = m4.w;
+        otail[0] = (const uint8_t*)ta.x; otail[1] = (const uint8_t*)ta.y;
+        otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
     }
-    if (tid < MAXP) S.pmax[tid] = INT64_MIN;
-    if (FAST && tid < nj) {
-        const int j = jlo + tid;
-        S.j_pb[tid] = A.pb[j];
-        S.j_ib[tid] = A.ib[j];
-        S.j_pe[tid] = A.pe[j];
-        S.j_ie[tid] = A.ie[j];
-        S.j_need[tid] = A.need_e[j];
-        S.j_vb[tid] = A.vb[j];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        S.er[i0 + q] = 0;
+        S.ins[i0 + q] = 0;
     }
-    if (FAST) __syncthreads();
-    auto PB = [&](int j) { return FAST ? S.j_pb[j - jlo] : A.pb[j]; };
-    auto IB = [&](int j) { return FAST ? S.j_ib[j - jlo] : A.ib[j]; };
-    auto PE = [&](int j) { return FAST ? S.j_pe[j - jlo] : A.pe[j]; };
-    auto IE = [&](int j) { return FAST ? S.j_ie[j - jlo] : A.ie[j]; };
-    auto NEED = [&](int j) { return FAST ? S.j_need[j - jlo] : A.need_e[j]; };
-    auto VB = [&](int j) { return FAST ? S.j_vb[j - jlo] : A.vb[j]; };
-    // erased iff inside [(pb_j, ib_j), (pe_j, ie_j)) for the last j starting at or before (p, tid)
-    int keep = 0;
-    if (tid < cntp) {
-        int lo = jlo, hi = jhi + 1;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pos_le(PB(mid), IB(mid), p, tid)) lo = mid + 1; else hi = mid;
+    if (lane == 0) {
+        S.er[PAGE] = 0;
+        S.ins[PAGE] = 0;
+    }
+    S.pmax[lane] = INT64_MIN;
+    wave_lds_sync();
+    // ---- 1. plan lanes: erased intervals and insertion counts
+    int f = PAGE;  // first old slot a range changes
+    for (int j0 = jlo; j0 <= jhi; j0 += 64) {
+        const int j = j0 + lane;
+        if (j <= jhi) {
+            const int pb = A.pb[j], ib = A.ib[j], pe = A.pe[j], ie = A.ie[j];
+            const int s0 = pb < p ? 0 : ib, e0 = pe > p ? cntp : ie;
+            if (e0 > s0) {
+                atomicAdd(&S.er[s0], 1);
+                atomicAdd(&S.er[e0], -1);
+            }
+            if (pb == p) atomicAdd(&S.ins[ib], 1);
+            if (pe == p && A.need_e[j]) atomicAdd(&S.ins[ie], 1);
+            f = min(f, s0);
         }
-        const int j = lo - 1;
-        keep = !(j >= jlo && pos_lt(p, tid, PE(j), IE(j)));
     }
-    int kept;
-    const int kex = block_excl_scan(keep, S.tmp, kept);
-    if (tid < cntp) S.kb[tid] = kex;
-    if (tid == 0) S.kb[cntp] = kept;
-    // new entries landing here, in key order: b_j (version now), then e_j
-    uint64_t* NHI = FAST ? S.n_hi : A.ne.hi + nn_off;
-    uint64_t* NLO = FAST ? S.n_lo : A.ne.lo + nn_off;
-    uint32_t* NMETA = FAST ? S.n_meta : A.ne.meta + nn_off;
-    int64_t* NVER = FAST ? S.n_ver : A.ne.ver + nn_off;
-    const uint8_t** NTAIL = FAST ? S.n_tail : A.ne.tail + nn_off;
-    int32_t* NINS = FAST ? S.n_ins : A.ne_ins + nn_off;
-    int local = 0;
-    for (int jb = jlo; jb <= jhi; jb += blockDim.x) {
-        const int j = jb + tid;
-        const bool eb = j <= jhi && PB(j) == p;
-        const bool ee = j <= jhi && PE(j) == p && NEED(j);
-        int t2;
-        int k = local + block_excl_scan((int)eb + (int)ee, S.tmp, t2);
-        if (eb) {
-            const Key kk = A.cb.get(j);
-            NHI[k] = kk.hi; NLO[k] = kk.lo; NMETA[k] = kk.meta; NVER[k] = A.now;
-            copy_tail(kk, A.arena, A.arena_cap, sc, &NTAIL[k]);
-            NINS[k] = IB(j);
-            k++;
-        }
-        if (ee) {
-            const Key kk = A.ce.get(j);
-            NHI[k] = kk.hi; NLO[k] = kk.lo; NMETA[k] = kk.meta; NVER[k] = VB(j);
-            copy_tail(kk, A.arena, A.arena_cap, sc, &NTAIL[k]);
-            NINS[k] = IE(j);
-        }
-        local += t2;
+    f = wave_reduce_min(f);
+    wave_lds_sync();
+    // ---- 2. slot lanes: survivors and output positions
+    int ec[4], ic[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        ec[q] = S.er[i0 + q];
+        ic[q] = S.ins[i0 + q];
     }
-    __threadfence_block();
-    __syncthreads();
+    const int esum = ec[0] + ec[1] + ec[2] + ec[3], isum = ic[0] + ic[1] + ic[2] + ic[3];
+    int erun = wave_incl_scan(esum) - esum;
+    int irun = wave_incl_scan(isum) - isum;
+    uint32_t keepm = 0;
+    int newb[4];  // new entries at or before each slot
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        erun += ec[q];
+        irun += ic[q];
+        newb[q] = irun;
+        if (i0 + q < cntp && erun == 0) keepm |= 1u << q;
+    }
+    const int kc = __popc(keepm);
+    const int kinc = wave_incl_scan(kc);
+    const int kept = lane_read(kinc, 63);
+    int kb[4];
+    {
+        int run = kinc - kc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            kb[q] = run;
+            S.er[i0 + q] = run;  // now: kept old entries before slot
+            run += (keepm >> q) & 1;
+        }
+    }
+    wave_lds_sync();
+    if (lane == 0) S.er[cntp] = kept;
+    wave_lds_sync();
     const int nout = kept + nn;
     const int per = cdiv(nout, parts);
-    auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
+    // old slots before the first changed one keep their slot when the page
+    // stays one page: not rewritten
+    const int u = parts == 1 ? min(f, cntp) : 0;
     const Dir& D = A.dst;
-    auto put_dir = [&](int q, int dp, uint64_t hi, uint64_t lo, uint32_t meta, const uint8_t* tail) {
-        const int y = doff + q;
-        D.page[y] = dp; D.cnt[y] = min(per, nout - q * per);
-        D.fhi[y] = hi; D.flo[y] = lo; D.fmeta[y] = meta; D.ftail[y] = tail;
-        D.start[y] = A.aff_start[a] + (int64_t)q * per;
-    };
-    if (tid < cntp && keep) {
-        int lo = 0, hi = nn;  // new entries that go before old entry tid
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (NINS[mid] <= tid) lo = mid + 1; else hi = mid;
+    auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
+    int64_t vmax = INT64_MIN;  // parts == 1: the page maximum by a wave reduction
+    // ---- 3a. surviving old entries
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (!((keepm >> q) & 1)) continue;
+        const int i = i0 + q;
+        const int m = kb[q] + newb[q];
+        const int qq = m / per, slot = m - qq * per;
+        if (parts == 1) vmax = max(vmax, over[q]);
+        else if (qq < MAXP) atomicMax(&S.pmax[qq], (long long)over[q]);
+        if (i >= u) {
+            const int dp = dest(qq);
+            put_entry(A.pool, (int64_t)dp * PAGE + slot, ohi[q], olo[q], ometa[q], over[q], otail[q]);
+            if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, ohi[q], olo[q], ometa[q], otail[q]);
+        } else if (i == 0) {  // unchanged first slot
+            part_first(S, D, A, a, doff, 0, per, nout, pg, ohi[0], olo[0], ometa[0], otail[0]);
         }
-        const int m = S.kb[tid] + lo;
-        const int q = m / per, slot = m - q * per;
-        const int dp = dest(q);
-        put_entry(A.pool, (int64_t)dp * PAGE + slot, S.o_hi[tid], S.o_lo[tid], S.o_meta[tid], S.o_ver[tid],
-                  S.o_tail[tid]);
-        if (q < MAXP) atomicMax(&S.pmax[q], (long long)S.o_ver[tid]);
-        if (slot == 0) put_dir(q, dp, S.o_hi[tid], S.o_lo[tid], S.o_meta[tid], S.o_tail[tid]);
     }
-    for (int k = tid; k < nn; k += blockDim.x) {
-        const int m = k + S.kb[NINS[k]];
-        const int q = m / per, slot = m - q * per;
-        const int dp = dest(q);
-        const uint64_t hi = NHI[k], lo = NLO[k];
-        const uint32_t meta = NMETA[k];
-        const int64_t ver = NVER[k];
-        const uint8_t* tail = NTAIL[k];
-        put_entry(A.pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
-        if (q < MAXP) atomicMax(&S.pmax[q], (long long)ver);
-        if (slot == 0) put_dir(q, dp, hi, lo, meta, tail);
+    // ---- 3b. new entries, by the plan lanes: b_j (version now), then e_j
+    int base = 0;
+    for (int j0 = jlo; j0 <= jhi; j0 += 64) {
+        const int j = j0 + lane;
+        const bool v = j <= jhi;
+        const bool eb = v && A.pb[j] == p;
+        const bool ee = v && A.pe[j] == p && A.need_e[j];
+        const int c = (int)eb + (int)ee;
+        const int inc = wave_incl_scan(c);
+        int k = base + inc - c;  // new entries before this lane's
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            if (!(w == 0 ? eb : ee)) continue;
+            const Key kk = w == 0 ? A.rb.get(j) : A.re.get(j);
+            const int at = w == 0 ? A.ib[j] : A.ie[j];
+            const int64_t ver = w == 0 ? A.now : A.vb[j];
+            const int m = k + S.er[at];
+            const int qq = m / per, slot = m - qq * per;
+            const int dp = dest(qq);
+            const uint8_t* tl;
+            copy_tail(kk, A.arena, A.arena_cap, sc, &tl);
+            put_entry(A.pool, (int64_t)dp * PAGE + slot, kk.hi, kk.lo, kk.meta, ver, tl);
+            if (parts == 1) vmax = max(vmax, ver);
+            else if (qq < MAXP) atomicMax(&S.pmax[qq], (long long)ver);
+            if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, kk.hi, kk.lo, kk.meta, tl);
+            k++;
+        }
+        base += lane_read(inc, 63);
     }
-    __threadfence_block();
-    __syncthreads();
-    for (int q = tid; q < parts; q += blockDim.x) {
+    if (parts == 1) vmax = wave_reduce_max(vmax);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // LDS stash + own pool writes visible below
+    __builtin_amdgcn_wave_barrier();
+    for (int q = lane; q < min(parts, MAXP); q += 64) {  // directory entries of the parts
+        const int y = doff + q;
+        D.page[y] = S.f_dp[q];
+        D.cnt[y] = min(per, nout - q * per);
+        D.fhi[y] = S.f_hi[q];
+        D.flo[y] = S.f_lo[q];
+        D.fmeta[y] = S.f_meta[q];
+        D.ftail[y] = S.f_tail[q];
+        D.start[y] = A.aff_start[a] + (int64_t)q * per;
+    }
+    if (parts == 1) {
+        if (lane == 0) D.maxv[doff] = vmax;
+        return;
+    }
+    for (int q = lane; q < parts; q += 64) {
         int64_t mx;
         if (q < MAXP) {
             mx = S.pmax[q];
@@ -614,20 +691,19 @@ __device__ void merge_page(const MergeArgs& A, MergeShared& S, int a, int top0, 
         }
         D.maxv[doff + q] = mx;
     }
-    __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_page_merge(MergeArgs A) {
-    __shared__ MergeShared S;
+#ifndef FDBCS_PM_WAVES
+#define FDBCS_PM_WAVES 4
+#endif
+__global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A) {
+    __shared__ WaveMerge S[MW_WAVES];
     Scalars* sc = A.sc;
     if (sc->err) return;
     const int naff = sc->n_aff;
     const int top0 = sc->free_top;
-    const int extra_total = sc->extra_total;
-    for (int a = blockIdx.x; a < naff; a += gridDim.x) {
-        if (A.jhi[a] - A.jlo[a] + 1 <= JCAP) merge_page<true>(A, S, a, top0, extra_total);
-        else merge_page<false>(A, S, a, top0, extra_total);
-    }
+    const int w = threadIdx.x >> 6;
+    for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES) merge_page_wave(A, S[w], a, top0);
 }
 
 __device__ inline void dir_copy(const Dir& s, int x, const Dir& d, int y) {
@@ -683,8 +759,8 @@ void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStrea
     // full recompute of start[] (used after reset / load)
     Dir& d = h.dir[cur];
     scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
-    hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
-    hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
     launch_bmax_commit(h, cur, sc, s, true);
 }
 
@@ -698,7 +774,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
         hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
-                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc);
+                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
     hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
@@ -708,19 +784,21 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
     P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
     P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
+    P.aff_page = b.aff_page; P.aff_cnt = b.aff_cnt;
     hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
     if (W > 0) {
         const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
         MergeArgs A;
         A.pool = h.pool; A.dir = src; A.dst = dst; A.sc = sc; A.free_stack = h.free_stack; A.freed_list = b.freed_list;
-        A.aff_list = b.aff_list;
+        A.aff_list = b.aff_list; A.aff_page = b.aff_page; A.aff_cnt = b.aff_cnt;
         A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
         A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off; A.free_off = b.aff_free_off;
         A.aff_start = b.aff_start;
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
-        A.cb = IndirectKeys{b.keys, b.cb_slot}; A.ce = IndirectKeys{b.keys, b.ce_slot}; A.ne = b.ne; A.ne_ins = b.ne_ins;
+        A.rb = b.rkb; A.re = b.rke; A.ne = b.ne; A.ne_ins = b.ne_ins;
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
-        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, max_aff))), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)))), dim3(256),
+                           0, s, A);
     }
     launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
 }

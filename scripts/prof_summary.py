@@ -12,7 +12,7 @@ from collections import defaultdict
 def main():
     path = sys.argv[1]
     last = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    marker = sys.argv[3] if len(sys.argv) > 3 else "k_prep"
+    marker = sys.argv[3] if len(sys.argv) > 3 else "k_ingest"
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
