@@ -52,6 +52,16 @@ def main():
         extra = " ".join(f"{n}={v / batches:.0f}" for n, v in sorted(c.items()) if n not in ("FETCH_SIZE", "WRITE_SIZE"))
         print(f"{k[:32]:32s} fetch {fb / 1e6:9.2f} MB  write {wb / 1e6:9.2f} MB  {extra}")
     print(f"TOTAL fetch {tot_f / 1e6:.2f} MB write {tot_w / 1e6:.2f} MB per batch -> {(tot_f + tot_w) / 1e6:.2f} MB")
+    if len(sys.argv) > 4:  # JSON for bench.py's roofline.traffic
+        import json
+        with open(sys.argv[4], "w") as f:
+            json.dump({"bytes_per_batch": round(tot_f + tot_w), "fetch_bytes": round(tot_f), "write_bytes": round(tot_w),
+                       "batches": batches,
+                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over the bench workload; "
+                                 "FETCH_SIZE x2 (gfx950 correction), KB->bytes; summed over all kernels of a batch",
+                       "per_kernel_bytes": {k: round(2 * per_kernel[k].get("FETCH_SIZE", 0) * 1024 / batches
+                                                     + per_kernel[k].get("WRITE_SIZE", 0) * 1024 / batches)
+                                            for k in names}}, f, indent=1)
 
 
 if __name__ == "__main__":
