@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["encode", "read_check", "sort_edges", "decide_combine", "merge", "compaction"]
+STAGES = ["encode", "sort", "read_check_edges", "decide_combine", "merge", "compaction"]
 E_HIST = 28.0  # SURVEY.md §8d bytes per boundary (16-B prefix + 8-B version + 4-B meta)
 
 
@@ -117,10 +117,10 @@ def stage_bytes(name, st, key_bytes):
         return 2 * st["pages_merged"] * fill * 36.0 + 2 * st["dir_entries"] * 52.0 + st["combined"] * 64.0
     if name == "compaction":
         return st["window_pages"] * fill * 36.0 + st["window_survivors"] * 36.0 + 2 * st["dir_entries"] * 52.0
-    if name == "read_check":
-        return R * (2 * 24.0 + 4 + 8 + 2 * 36.0) + T
-    if name == "sort_edges":
-        return (R + 2 * W) * (24.0 + 4 * 32.0) + (R + W) * 48.0
+    if name == "read_check_edges":  # history search per read + the sorted endpoints the edges search
+        return R * (2 * 24.0 + 4 + 8 + 2 * 36.0) + T + (R + W) * 48.0
+    if name == "sort":
+        return (R + 2 * W) * (24.0 + 4 * 32.0)
     if name == "decide_combine":
         return T * 8.0 + 2 * W * (4.0 + 8.0)
     return key_bytes + 2 * (R + W) * 24.0  # encode

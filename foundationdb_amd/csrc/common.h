@@ -122,7 +122,12 @@ struct Pool {
     uint32_t* meta;
     int64_t* ver;
     const uint8_t** tail;
+    // page index: pidx[s / 16] = hi[s] for every slot s that is a multiple of
+    // 16 (16 per page = one 128-byte line), kept by every slot writer
+    // (put_entry); the first step of a cooperative page search reads it.
+    uint64_t* pidx;
 };
+constexpr int PIDX_STRIDE = 16;
 
 struct Dir {
     int32_t* page;      // pool page id
@@ -134,7 +139,26 @@ struct Dir {
     uint32_t* fmeta;
     const uint8_t** ftail;
     int64_t* bmax;      // max of maxv over groups of 64 directory entries
+    // search index: level l >= 1 holds fhi[i * 16^l]; levels start at
+    // 16-entry (128-byte) boundaries, so a 16-wide probe window is one cache
+    // line (hist_search.h).  Rebuilt by k_bmax_commit with the directory.
+    uint64_t* sidx;
+    int32_t cap;        // entries allocated (levels are sized from it)
 };
+
+constexpr int SIDX_B = 16;      // fan-out
+constexpr int SIDX_LOG = 4;
+constexpr int SIDX_LEVELS = 7;  // 16^7 > any directory
+
+// offset of level l (1-based) in sidx; level 0 is fhi itself
+__host__ __device__ inline int64_t sidx_off(int64_t cap, int l) {
+    int64_t o = 0;
+    for (int q = 1; q < l; q++) {
+        const int64_t n = (cap + (1ll << (SIDX_LOG * q)) - 1) >> (SIDX_LOG * q);
+        o += (n + SIDX_B - 1) & ~(int64_t)(SIDX_B - 1);
+    }
+    return o;
+}
 
 // Device-resident scalars shared between the kernels of one batch.
 struct Scalars {

@@ -130,7 +130,8 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
     h.cap_pages = pages;
     const int64_t slots = (int64_t)pages * PAGE;
     if ((r = dalloc(h.pool.hi, slots)) || (r = dalloc(h.pool.lo, slots)) || (r = dalloc(h.pool.meta, slots)) ||
-        (r = dalloc(h.pool.ver, slots)) || (r = dalloc(h.pool.tail, slots)) || (r = dalloc(h.free_stack, pages)))
+        (r = dalloc(h.pool.ver, slots)) || (r = dalloc(h.pool.tail, slots)) || (r = dalloc(h.pool.pidx, slots / PIDX_STRIDE)) ||
+        (r = dalloc(h.free_stack, pages)))
         return r;
     h.cap_dir = pages + 1;
     for (int d = 0; d < 2; d++) {
@@ -138,19 +139,20 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
         if ((r = dalloc(x.page, h.cap_dir)) || (r = dalloc(x.cnt, h.cap_dir)) || (r = dalloc(x.maxv, h.cap_dir)) ||
             (r = dalloc(x.start, h.cap_dir + 1)) || (r = dalloc(x.fhi, h.cap_dir)) || (r = dalloc(x.flo, h.cap_dir)) ||
             (r = dalloc(x.fmeta, h.cap_dir)) || (r = dalloc(x.ftail, h.cap_dir)) ||
-            (r = dalloc(x.bmax, h.cap_dir / 64 + 2)))
+            (r = dalloc(x.bmax, h.cap_dir / 64 + 2)) || (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))))
             return r;
+        x.cap = h.cap_dir;
     }
     return FDBCS_OK;
 }
 
 void free_pool(HistBufs& h) {
     dfree(h.pool.hi); dfree(h.pool.lo); dfree(h.pool.meta); dfree(h.pool.ver); dfree(h.pool.tail);
-    dfree(h.free_stack);
+    dfree(h.pool.pidx); dfree(h.free_stack);
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
         dfree(x.page); dfree(x.cnt); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
-        dfree(x.ftail); dfree(x.bmax);
+        dfree(x.ftail); dfree(x.bmax); dfree(x.sidx);
     }
 }
 
@@ -183,6 +185,7 @@ int grow_pool(fdbcs* cs, int64_t pages) {
     HIPOK(hipMemcpyAsync(h.pool.meta, old.pool.meta, os * 4, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.ver, old.pool.ver, os * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.tail, old.pool.tail, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.pidx, old.pool.pidx, os / PIDX_STRIDE * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.free_stack, old.free_stack, (size_t)old.cap_pages * 4, hipMemcpyDeviceToDevice, s));
     const size_t od = (size_t)old.cap_dir;
     for (int d = 0; d < 2; d++) {
@@ -196,6 +199,7 @@ int grow_pool(fdbcs* cs, int64_t pages) {
         HIPOK(hipMemcpyAsync(h.dir[d].ftail, old.dir[d].ftail, od * 8, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].bmax, old.dir[d].bmax, (od / 64 + 2) * 8, hipMemcpyDeviceToDevice, s));
     }
+    launch_sidx_build(h, cs->cur, cs->sc, s);  // index levels are laid out by capacity
     launch_push_free(h, (int32_t)cs->known_free, old.cap_pages, (int32_t)(np - old.cap_pages), s);
     HIPOK(hipStreamSynchronize(s));
     free_pool(old);
@@ -243,7 +247,7 @@ void free_plan(BatchBufs& b) {
 void free_batch(BatchBufs& b) {
     dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
     dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
-    dfree(b.read_txn); dfree(b.write_txn);
+    dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_bkt); dfree(b.ss_tmp);
@@ -288,8 +292,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     if (R > cs->capR) {
         int64_t n = std::max<int64_t>(R, 1024);
-        dfree(b.read_txn); dfree(b.rec_r0);
-        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.rec_r0, n))) return r;
+        dfree(b.read_txn); dfree(b.read_snap); dfree(b.rec_r0);
+        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.read_snap, n)) || (r = dalloc(b.rec_r0, n))) return r;
         cs->capR = n;
     }
     if (W > cs->capW) {
@@ -433,13 +437,12 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     record(cs, 0);
     launch_ingest(v, cs->oldest, b, sc, s);
     record(cs, 1);
-    launch_read_check(v, b, h, cs->cur, sc, cs->v0, s);
-    record(cs, 2);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), s)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
-    launch_edges(v, b, sc, s);
+    record(cs, 2);
+    launch_edges_read_check(v, b, h, cs->cur, sc, cs->v0, s);
     record(cs, 3);
     launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s);
     record(cs, 4);
@@ -842,6 +845,9 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     HIPOK(hipMemcpyAsync(h.pool.meta, meta.data(), slots * 4, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.ver, ver.data(), slots * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.tail, tail.data(), slots * 8, hipMemcpyHostToDevice, s));
+    std::vector<uint64_t> pidx(slots / PIDX_STRIDE);
+    for (int64_t i = 0; i < (int64_t)pidx.size(); i++) pidx[i] = hi[i * PIDX_STRIDE];
+    HIPOK(hipMemcpyAsync(h.pool.pidx, pidx.data(), pidx.size() * 8, hipMemcpyHostToDevice, s));
     if (toff) HIPOK(hipMemcpyAsync(h.tail_arena, arena.data(), toff, hipMemcpyHostToDevice, s));
     Dir& d = h.dir[cs->cur];
     HIPOK(hipMemcpyAsync(d.page, dpage.data(), np * 4, hipMemcpyHostToDevice, s));

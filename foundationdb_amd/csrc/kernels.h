@@ -28,6 +28,7 @@ struct BatchBufs {
     int32_t* dep_idx;    // t -> index in dep_list or -1
     // range level
     int32_t* read_txn;   // [R]
+    int64_t* read_snap;  // [R] snapshot of the read's transaction (INT64_MAX: too old)
     int32_t* write_txn;  // [W]
     // encoded keys [2R+2W]
     KeyArrays keys;
@@ -114,12 +115,13 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 
 // ---- batch stages (kernels_batch.hip) ----
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s);
-void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
-                       hipStream_t s);
+
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         hipStream_t s);
 int64_t sort_staging_records(int R, int W);
-void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+// history read check + intra-batch overlap edges, one launch
+void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
+                             hipStream_t s);
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 void configure_batch_kernels();
@@ -130,6 +132,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
                   int64_t v0, bool end_of_batch, hipStream_t s);
 void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s);
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s);
+void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s);
 void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s);
 void launch_gather(HistBufs& h, int cur, Scalars* sc, Pool out, hipStream_t s);
 void launch_push_free(HistBufs& h, int32_t from_top, int32_t first_id, int32_t count, hipStream_t s);

@@ -66,6 +66,7 @@ struct IngestArgs {
     uint8_t* too_old;
     uint8_t* hist;
     int32_t* read_txn;
+    int64_t* read_snap;
     int32_t* write_txn;
     KeyArrays keys;
     uint8_t* btail;
@@ -80,9 +81,14 @@ __global__ __launch_bounds__(256) void k_ingest(IngestArgs A) {
         if (t >= A.T) return;
         const int r0 = A.ro[t], r1 = A.ro[t + 1];
         // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
-        A.too_old[t] = (A.snap[t] < A.oldest && r1 > r0) ? 1 : 0;
+        const int64_t sn = A.snap[t];
+        const bool too = sn < A.oldest && r1 > r0;
+        A.too_old[t] = too ? 1 : 0;
         A.hist[t] = 0;
-        for (int r = r0; r < r1; r++) A.read_txn[r] = t;
+        for (int r = r0; r < r1; r++) {
+            A.read_txn[r] = t;
+            A.read_snap[r] = too ? INT64_MAX : sn;  // k_read_check skips too-old transactions
+        }
         for (int w = A.wo[t], w1 = A.wo[t + 1]; w < w1; w++) A.write_txn[w] = t;
         return;
     }
@@ -101,74 +107,71 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.prep_blocks = std::max(1, cdiv(v.txn_count, 256));
     A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
     A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
-    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.write_txn = b.write_txn;
+    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap; A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc;
     const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
     hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(256), 0, s, A);
 }
 
 // ---------------------------------------------------------- read check ----
-// One lane per read range.  conflict iff max(version over boundaries in
+// Per read range: conflict iff max(version over boundaries in
 // [b, e), plus valueBefore(b) if b is not a boundary) > snapshot -- the
 // predicate CheckMax evaluates on the skip list (SkipList.cpp:755-837;
 // SURVEY.md Appendix A step 1).  Pages fully inside the range are skipped
 // through the directory's per-page maxima (the skip list's upper-level
 // maxVersion plays this role in the reference).
-__global__ __launch_bounds__(256) void k_read_check(int R, KeyArrays keys, const int32_t* __restrict__ read_txn,
-                                                    const int64_t* __restrict__ snap,
-                                                    const uint8_t* __restrict__ too_old, uint8_t* __restrict__ hist,
-                                                    Pool pool, Dir dir, const Scalars* __restrict__ sc, int64_t v0) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    const int t = read_txn[r];
-    if (too_old[t]) return;
-    const int64_t s = snap[t];
-    const Key b = keys.get(2 * (int64_t)r), e = keys.get(2 * (int64_t)r + 1);
-    const int D = sc->D;
-    const int pb = dir_search(dir, D, b, 1);
-    const int cb = dir.cnt[pb], pgb = dir.page[pb];
-    const int64_t baseb = (int64_t)pgb * PAGE;
-    const int ib = page_lb(pool, pgb, 0, cb, b);
-    bool conflict = false;
-    const bool exact = ib < cb && kcmp(pool_key(pool, baseb + ib), b) == 0;
-    if (!exact) {
-        const int64_t vb = ib > 0 ? pool.ver[baseb + ib - 1] : v0;
-        conflict = vb > s;
-    }
-    if (!conflict) {
-        int pe = pb;
-        if (pb + 1 < D && kcmp(dir_first(dir, pb + 1), e) <= 0) pe = dir_search(dir, D, e, pb + 1);
-        if (pe == pb) {
-            const int ie = page_lb(pool, pgb, ib, cb, e);
-            for (int i = ib; i < ie && !conflict; i++) conflict = pool.ver[baseb + i] > s;
-        } else {
-            for (int i = ib; i < cb && !conflict; i++) conflict = pool.ver[baseb + i] > s;
-            int q = pb + 1;
-            while (q < pe && !conflict) {
-                if ((q & 63) == 0 && q + 64 <= pe) {
-                    conflict = dir.bmax[q >> 6] > s;
-                    q += 64;
-                } else {
-                    conflict = dir.maxv[q] > s;
-                    q++;
-                }
-            }
-            if (!conflict) {
-                const int pge = dir.page[pe], ce = dir.cnt[pe];
-                const int64_t basee = (int64_t)pge * PAGE;
-                const int ie = page_lb(pool, pge, 0, ce, e);
-                for (int i = 0; i < ie && !conflict; i++) conflict = pool.ver[basee + i] > s;
-            }
-        }
-    }
-    if (conflict) hist[t] = 1;
-}
+// A group of RC_G lanes per read: both endpoints are searched in lockstep
+// (directory, then page, hist_search.h), then the group scans the versions
+// covering [b, e) -- the slot b falls in, the slots up to e, and between the
+// two pages the directory's page maxima (64-entry block maxima for long
+// ranges) -- and ORs the result.
+static constexpr int RC_G = SIDX_B;
 
-void launch_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
-                       hipStream_t s) {
-    if (v.read_count == 0) return;
-    hipLaunchKernelGGL(k_read_check, dim3(cdiv(v.read_count, 256)), dim3(256), 0, s, v.read_count, b.keys,
-                       b.read_txn, v.snapshot, b.too_old, b.hist, h.pool, h.dir[cur], sc, v0);
+struct ReadCheckArgs {
+    int R;
+    KeyArrays keys;
+    const int32_t* read_txn;
+    const int64_t* read_snap;  // INT64_MAX: the transaction is too old, nothing to check
+    uint8_t* hist;
+    Pool pool;
+    Dir dir;
+    const Scalars* sc;
+    int64_t v0;
+};
+
+// read r, checked by the RC_G lanes of its group (g.lane)
+__device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G>& g, int r) {
+    if (r >= A.R) return;
+    const Pool& pool = A.pool;
+    const Dir& dir = A.dir;
+    const int t = A.read_txn[r];
+    const int64_t s = A.read_snap[r];
+    const Key b = A.keys.get(2 * (int64_t)r), e = A.keys.get(2 * (int64_t)r + 1);
+    const int D = A.sc->D;
+    const int64_t v0 = A.v0;
+    if (s == INT64_MAX) return;
+    DirHit hb, he;
+    grp_dir_find2(g, dir, D, b, e, hb, he);
+    const int pb = hb.x, pe = he.x, cb = hb.cnt;
+    int ib, ie;
+    bool eqb, eqe;
+    grp_page_find2(g, pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    const int64_t baseb = (int64_t)hb.page * PAGE, basee = (int64_t)he.page * PAGE;
+    const int i0 = eqb ? ib : ib - 1;  // the slot whose version covers b
+    bool c = i0 < 0 && v0 > s;
+    const int lo = max(i0, 0);
+    if (pe == pb) {
+        for (int i = lo + g.lane; i < ie; i += RC_G) c |= pool.ver[baseb + i] > s;
+    } else {
+        for (int i = lo + g.lane; i < cb; i += RC_G) c |= pool.ver[baseb + i] > s;
+        for (int i = g.lane; i < ie; i += RC_G) c |= pool.ver[basee + i] > s;
+        const int q0 = pb + 1, q1 = pe;
+        const int qa = min(q1, (q0 + 63) & ~63), qz = max(qa, q1 & ~63);
+        for (int q = q0 + g.lane; q < qa; q += RC_G) c |= dir.maxv[q] > s;
+        for (int q = (qa >> 6) + g.lane; q < (qz >> 6); q += RC_G) c |= dir.bmax[q] > s;
+        for (int q = qz + g.lane; q < q1; q += RC_G) c |= dir.maxv[q] > s;
+    }
+    if (g.ballot(c) && g.lane == 0) A.hist[t] = 1;
 }
 
 // ---------------------------------------------------------------- sort ----
@@ -560,47 +563,143 @@ __device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, in
     }
 }
 
-__global__ __launch_bounds__(256) void k_edges(int R, int W, KeyArrays keys, const SRec* __restrict__ sr,
-                                               const SRec* __restrict__ sw, const int32_t* __restrict__ read_txn,
-                                               const int32_t* __restrict__ write_txn,
-                                               const uint8_t* __restrict__ too_old, const uint8_t* __restrict__ hist,
-                                               uint32_t* bits, int row_words, int32_t* et, int32_t* eu, int64_t cap,
-                                               Scalars* sc) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Edges need not skip transactions that already conflict with the history:
+// a conflicting reader is aborted whatever its sources, and a conflicting
+// writer never commits, so its edges never fire (k_decide_combine).  That
+// keeps the edges independent of the read check, so both run in one launch.
+struct EdgesArgs {
+    int R, W;
+    KeyArrays keys;
+    const SRec* sr;
+    const SRec* sw;
+    const int32_t* read_txn;
+    const int32_t* write_txn;
+    const uint8_t* too_old;
+    uint32_t* bits;
+    int row_words;
+    int32_t* et;
+    int32_t* eu;
+    int64_t cap;
+    Scalars* sc;
+};
+
+// The two searches of an edge lane: an LDS sample of the sorted array's first
+// key words (EQ evenly spaced records, loaded by the block) narrows each key
+// to ~n/EQ records, then both keys are binary-searched in lockstep so their
+// loads overlap.
+constexpr int EQ = 1024;
+
+__device__ inline void sample_fill(uint64_t* smp, const SRec* a, int n) {
+    const int m = min(n, EQ);
+    for (int q = threadIdx.x; q < m; q += blockDim.x) smp[q] = a[(int64_t)q * n / m].hi;
+}
+
+// [lo, hi) of a[0, n) that holds every record whose key word equals k.hi
+// (records before lo are < k, records from hi on are > k)
+__device__ inline void sample_narrow(const uint64_t* smp, int n, uint64_t h, int& lo, int& hi) {
+    const int m = min(n, EQ);
+    int a = 0, len = m;  // c_lt = #samples < h
+    while (len > 0) {
+        const int half = len >> 1;
+        if (smp[a + half] < h) { a += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    int b = a;  // c_le = #samples <= h
+    if (b < m && smp[b] == h) {
+        len = m - b;
+        while (len > 0) {
+            const int half = len >> 1;
+            if (smp[b + half] <= h) { b += half + 1; len -= half + 1; }
+            else len = half;
+        }
+    }
+    lo = a > 0 ? (int)((int64_t)(a - 1) * n / m) + 1 : 0;
+    hi = b < m ? (int)((int64_t)b * n / m) : n;
+}
+
+// first i in [lo, hi) with a[i] >= k (strict1: > k1) for two keys at once
+__device__ inline void bsearch2(const SRec* a, const Key& k1, bool strict1, int lo1, int hi1, const Key& k2, int lo2,
+                                int hi2, const uint8_t* const* tails, int& r1, int& r2) {
+    while (lo1 < hi1 || lo2 < hi2) {
+        const int m1 = (lo1 + hi1) >> 1, m2 = (lo2 + hi2) >> 1;
+        const bool a1 = lo1 < hi1, a2 = lo2 < hi2;
+        SRec x1, x2;
+        if (a1) x1 = a[m1];
+        if (a2) x2 = a[m2];
+        if (a1) {
+            const int c = rec_vs_key(x1, k1, tails);
+            if (strict1 ? c <= 0 : c < 0) lo1 = m1 + 1;
+            else hi1 = m1;
+        }
+        if (a2) {
+            if (rec_vs_key(x2, k2, tails) < 0) lo2 = m2 + 1;
+            else hi2 = m2;
+        }
+    }
+    r1 = lo1;
+    r2 = lo2;
+}
+
+__device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp_r, const uint64_t* smp_w) {
+    const int R = A.R, W = A.W;
     const int64_t wbase = 2 * (int64_t)R;
-    const uint8_t* const* tails = keys.tail;
+    const uint8_t* const* tails = A.keys.tail;
     if (i < R) {
-        const int t = read_txn[i];
-        if (too_old[t] || hist[t]) return;
-        const Key b = keys.get(2 * (int64_t)i), e = keys.get(2 * (int64_t)i + 1);
-        const int lo = lb_key(sw, 2 * W, b, tails);
-        const int hi = lb_key(sw, 2 * W, e, tails);
+        const int t = A.read_txn[i];
+        if (A.too_old[t]) return;
+        const Key b = A.keys.get(2 * (int64_t)i), e = A.keys.get(2 * (int64_t)i + 1);
+        int lb, hb, le, he, lo, hi;
+        sample_narrow(smp_w, 2 * W, b.hi, lb, hb);
+        sample_narrow(smp_w, 2 * W, e.hi, le, he);
+        bsearch2(A.sw, b, false, lb, hb, e, le, he, tails, lo, hi);
         for (int k = lo; k < hi; k++) {
-            const uint32_t slot = sw[k].idx;
+            const uint32_t slot = A.sw[k].idx;
             if (slot & 1) continue;  // a write end
-            const int u = write_txn[(slot - wbase) >> 1];
-            if (u < t && !too_old[u] && !hist[u]) edge_pair(t, u, bits, row_words, et, eu, cap, sc);
+            const int u = A.write_txn[(slot - wbase) >> 1];
+            if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc);
         }
     } else if (i < R + W) {
         const int w = i - R;
-        const int u = write_txn[w];
-        if (too_old[u] || hist[u]) return;
-        const Key b = keys.get(wbase + 2 * (int64_t)w), e = keys.get(wbase + 2 * (int64_t)w + 1);
-        const int lo = ub_key(sr, R, b, tails);
-        const int hi = lb_key(sr, R, e, tails);
+        const int u = A.write_txn[w];
+        if (A.too_old[u]) return;
+        const Key b = A.keys.get(wbase + 2 * (int64_t)w), e = A.keys.get(wbase + 2 * (int64_t)w + 1);
+        int lb, hb, le, he, lo, hi;
+        sample_narrow(smp_r, R, b.hi, lb, hb);
+        sample_narrow(smp_r, R, e.hi, le, he);
+        bsearch2(A.sr, b, true, lb, hb, e, le, he, tails, lo, hi);
         for (int k = lo; k < hi; k++) {
-            const int t = read_txn[sr[k].idx >> 1];
-            if (t > u && !too_old[t] && !hist[t]) edge_pair(t, u, bits, row_words, et, eu, cap, sc);
+            const int t = A.read_txn[A.sr[k].idx >> 1];
+            if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc);
         }
     }
 }
 
-void launch_edges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
+// One launch, two kinds of blocks: read-check groups (history), then edge
+// lanes (intra-batch) -- both latency-bound searches, so they overlap.
+__global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int rc_blocks, EdgesArgs EA) {
+    __shared__ uint64_t smp_r[EQ], smp_w[EQ];
+    if ((int)blockIdx.x < rc_blocks) {
+        const Group<RC_G> g;
+        read_check_group(RA, g, (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G));
+    } else {
+        const int i0 = (blockIdx.x - rc_blocks) * blockDim.x;
+        if (i0 < EA.R) sample_fill(smp_w, EA.sw, 2 * EA.W);          // readers search the writes
+        if (i0 + (int)blockDim.x > EA.R) sample_fill(smp_r, EA.sr, EA.R);  // writers search the reads
+        __syncthreads();
+        edges_lane(EA, i0 + threadIdx.x, smp_r, smp_w);
+    }
+}
+
+void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
+                             hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
-    if (R > 0 && W > 0)
-        hipLaunchKernelGGL(k_edges, dim3(cdiv(R + W, 256)), dim3(256), 0, s, R, W, b.keys, (const SRec*)b.sr,
-                           (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old, b.hist, b.pair_bits, b.row_words,
-                           b.et, b.eu, b.edge_cap, sc);
+    ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0};
+    EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
+                 b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc};
+    const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
+    const int e_blocks = R > 0 && W > 0 ? cdiv(R + W, 256) : 0;
+    if (rc_blocks + e_blocks > 0)
+        hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks, EA);
 }
 
 // ------------------------------------------------------ decide + combine ----

@@ -87,7 +87,10 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 }
 
 // ------------------------------------------------------- insertion plan ----
-// K1 k_plan_ranges, one lane per combined range j: where b and e fall in the
+static constexpr int PR_G = SIDX_B;
+
+// K1 k_plan_ranges, a group of PR_G lanes per combined range j (searches as
+// in k_read_check, hist_search.h), lane 0 records: where b and e fall in the
 // pre-batch history, whether e needs a node and the value it keeps, and the
 // range's contribution to the pages it touches, accumulated per directory
 // entry: erased old entries, new entries, first/last range touching the page.
@@ -100,26 +103,29 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
                                                      int64_t* __restrict__ vb_o, PageAcc acc, KeyArrays rb,
                                                      KeyArrays re) {
     if (sc->err) return;
-    const int nC = sc->n_comb;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nC) return;
     const int D = sc->D;
+    const Group<PR_G> g;
+    const int nC = sc->n_comb;
+    const int j = (int)((blockIdx.x * blockDim.x + threadIdx.x) / PR_G);
+    if (j >= nC) return;
     const Key b = cb.get(j), e = ce.get(j);
-    rb.put(j, b);  // compact copies for the page merge
-    re.put(j, e);
-    const int p_b = dir_search(dir, D, b, 1);
-    const int c_b = dir.cnt[p_b], g_b = dir.page[p_b];
-    const int i_b = page_lb(pool, g_b, 0, c_b, b);
-    int p_e = p_b;
-    if (p_b + 1 < D && kcmp(dir_first(dir, p_b + 1), e) <= 0) p_e = dir_search(dir, D, e, p_b + 1);
-    const int c_e = dir.cnt[p_e], g_e = dir.page[p_e];
-    const int i_e = page_lb(pool, g_e, p_e == p_b ? i_b : 0, c_e, e);
-    const bool found = i_e < c_e && kcmp(pool_key(pool, (int64_t)g_e * PAGE + i_e), e) == 0;
+    const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
+    if (g.lane == 0) {
+        rb.put(j, b);  // compact copies for the page merge
+        re.put(j, e);
+    }
+    int i_b, i_e;
+    bool eq_b, found;
+    DirHit hb, he;
+    grp_dir_find2(g, dir, D, b, e, hb, he);
+    const int p_b = hb.x, c_b = hb.cnt, g_b = hb.page;
+    const int p_e = he.x, c_e = he.cnt, g_e = he.page;
+    grp_page_find2(g, pool, g_b, c_b, b, g_e, c_e, e, i_b, eq_b, i_e, found);
+    if (g.lane != 0) return;
     int64_t vb;
     if (i_e > 0) vb = pool.ver[(int64_t)g_e * PAGE + i_e - 1];
     else if (p_e > 0) vb = pool.ver[(int64_t)dir.page[p_e - 1] * PAGE + dir.cnt[p_e - 1] - 1];
     else vb = v0;
-    const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
     const int need = (!found && !touch) ? 1 : 0;
     pb_o[j] = p_b;
     ib_o[j] = i_b;
@@ -448,6 +454,7 @@ struct MergeArgs {
 __device__ inline void put_entry(const Pool& pool, int64_t d, uint64_t hi, uint64_t lo, uint32_t meta, int64_t ver,
                                  const uint8_t* tail) {
     pool.hi[d] = hi; pool.lo[d] = lo; pool.meta[d] = meta; pool.ver[d] = ver; pool.tail[d] = tail;
+    if ((d & (PIDX_STRIDE - 1)) == 0) pool.pidx[d / PIDX_STRIDE] = hi;
 }
 
 __device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, uint64_t hi, uint64_t lo,
@@ -719,6 +726,27 @@ __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y
 // Per-64-entry maxima of the new directory (one wavefront per group), pages
 // the merge freed back onto the free stack (above the ones it took), then
 // commit the directory size, free-stack top and history size.
+// level-1 entry i of the search index, and the entries of higher levels it
+// starts (i a multiple of 16^(l-1))
+__device__ inline void sidx_build(const Dir& d, int i) {
+    const uint64_t v = d.fhi[(int64_t)i * SIDX_B];
+    d.sidx[i] = v;
+    int ii = i;
+    for (int l = 2; l <= SIDX_LEVELS && (ii & (SIDX_B - 1)) == 0; l++) {
+        ii >>= SIDX_LOG;
+        d.sidx[sidx_off(d.cap, l) + ii] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sidx_build(Dir d, const int32_t* D) {
+    const int n1 = cdiv(*D, SIDX_B);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
+}
+
+void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
+    hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
+}
+
 __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
                                                      int32_t* free_stack, int end_of_batch) {
     const int Dn = sc->D_next;
@@ -728,6 +756,8 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x)
             free_stack[base + i] = freed_list[i];
     }
+    const int n1 = cdiv(Dn, SIDX_B);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (g * 64 < Dn) {
@@ -773,7 +803,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     Dir& dst = h.dir[cur ^ 1];
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
-        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
+        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv((int64_t)W * PR_G, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
                            b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
