@@ -15,15 +15,17 @@ from concurrent.futures import ThreadPoolExecutor
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "foundationdb_amd")
 CSRC = os.path.join(PKG, "csrc")
-OBJ = os.path.join(ROOT, "build", "obj")
+OBJ = os.path.join(ROOT, "build", os.environ.get("FDBCS_OBJ_DIR", "obj"))
 ARCH = os.environ.get("FDBCS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip", "resolvers.hip"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value"]
+HIP_FLAGS += os.environ.get("FDBCS_EXTRA_FLAGS", "").split()  # experiment variants (scripts/build_variants.sh)
 if os.environ.get("FDBCS_PHASES"):  # profiling build: kernels record phase timestamps
     HIP_FLAGS.append("-DFDBCS_PHASES")
 
-LIB = os.path.join(PKG, "libfdbcs.so")
+# FDBCS_LIB_OUT / FDBCS_OBJ_DIR: build an experiment variant beside the product library
+LIB = os.environ.get("FDBCS_LIB_OUT") or os.path.join(PKG, "libfdbcs.so")
 WL_LIB = os.path.join(PKG, "libfdbcs_workload.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle_spec.so")
 

@@ -178,6 +178,7 @@ struct Scalars {
     int32_t win_newpages;   // pages produced by the repack
     int32_t win_surv;       // survivors in the window pages
     int32_t jac_iters;      // stats: Jacobi iterations in the decision
+    int32_t blocks_done;    // last-block-commits counter (k_win_dir); zero between launches
     int32_t free_next;      // free_top after the rebuild in flight
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)
@@ -193,10 +194,17 @@ struct Scalars {
     do {                                                                                       \
         if (threadIdx.x == 0 && blockIdx.x == 0) (sc)->ph[(i)] = (int64_t)wall_clock64();     \
     } while (0)
+// per-wave cycle accumulators in ph[16..31] (cumulative across batches)
+#define PACC(sc, i, v) atomicAdd((unsigned long long*)&(sc)->ph[(i)], (unsigned long long)(v))
+#define PCLK() ((int64_t)clock64())
 #else
 #define PHASE(sc, i) \
     do {             \
     } while (0)
+#define PACC(sc, i, v) \
+    do {               \
+    } while (0)
+#define PCLK() ((int64_t)0)
 #endif
 
 __device__ inline int64_t atomic_max_i64(int64_t* addr, int64_t v) {

@@ -237,7 +237,8 @@ int alloc_keys(KeyArrays& k, int64_t n) {
 void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.tail); }
 
 void free_plan(BatchBufs& b) {
-    dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff);
+    dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff); dfree(b.acc.fmin);
+    dfree(b.aff_f);
     dfree(b.blk_agg); dfree(b.blk_diff);
     dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn); dfree(b.aff_parts);
     dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off); dfree(b.aff_free_off); dfree(b.aff_start);
@@ -366,13 +367,15 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) || (r = dalloc(b.aff_parts, n)) ||
             (r = dalloc(b.aff_nn_off, n)) || (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
             (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)) ||
-            (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)))
+            (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)) || (r = dalloc(b.acc.fmin, n)) ||
+            (r = dalloc(b.aff_f, n)))
             return r;
         HIPOK(hipMemsetAsync(b.acc.er, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.nn, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.diff, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.jlo, 0x7F, n * 4, s));  // "no range yet" (> any range index)
         HIPOK(hipMemsetAsync(b.acc.jhi, 0xFF, n * 4, s));  // -1
+        HIPOK(hipMemsetAsync(b.acc.fmin, 0x7F, n * 4, s));  // no slot changed yet
         cs->capDirB = cd;
     }
     // page descriptors: the merge makes at most cap_dir of them, the compaction

@@ -13,6 +13,7 @@ struct PageAcc {
     int32_t* jlo;   // first combined range touching the page
     int32_t* jhi;   // last one
     int32_t* diff;  // +1 / -1 marks of pages wholly inside a range
+    int32_t* fmin;  // first old slot a range changes (>= PAGE: none)
 };
 
 // Per-batch device working set (sized by the engine before each batch).
@@ -75,6 +76,7 @@ struct BatchBufs {
     int64_t* aff_start;  // start[] of its first output page
     int32_t* aff_page;   // its pool page and boundary count
     int32_t* aff_cnt;
+    int32_t* aff_f;      // first old slot a range changes
     int32_t* freed_list; // pages the merge frees, pushed after its pops
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order

@@ -401,12 +401,16 @@ __device__ inline void emit_quantiles(const SortJobs& J, int job, int64_t pos, c
 }
 
 __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
-    __shared__ uint64_t s_hi[SS_ROW], s_lo[SS_ROW], s_mi[SS_ROW];
+    __shared__ __attribute__((aligned(16))) uint64_t s_buf[3 * SS_ROW];
+    uint64_t *s_hi = s_buf, *s_lo = s_buf + SS_ROW, *s_mi = s_buf + 2 * SS_ROW;  // LDS path
+    uint4* s_r4 = reinterpret_cast<uint4*>(s_buf);  // rank path: 32-byte records
+    static_assert(3 * SS_ROW * 8 >= 2 * (SS_WAVE + 8) * 16, "rank path staging");
     const int job = blockIdx.x < J.nb[0] ? 0 : 1;
     const int b = job ? blockIdx.x - J.nb[0] : blockIdx.x;
     const int lane = threadIdx.x;
     const int32_t* cnt = J.cnt + job * SS_MAXB;
     const uint8_t* const* tails = keys.tail;
+    const int64_t c0 = PCLK();
     for (int k = blockIdx.x * 64 + lane; k < 2 * SS_MAXB; k += gridDim.x * 64) J.cnt_next[k] = 0;
     // offset = counts of the earlier buckets: lane L sums counts [16L, 16L+16)
     // below b with four independent 16-byte loads (one round trip)
@@ -422,24 +426,57 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
     }
     const int offset = wave_reduce_sum(part);
     const int c = cnt[b];
+    const int64_t c1 = PCLK();
     if (c == 0) return;
     SRec* out = J.out[job] + offset;
     const SRec* row = J.tmp + ((int64_t)job * SS_MAXB + b) * SS_ROW;
     if (c <= SS_WAVE) {
-        int P = 2;
-        while (P < c) P <<= 1;
-        SRec r[2];
-#pragma unroll
-        for (int q = 0; q < 2; q++) r[q] = 2 * lane + q < c ? row[2 * lane + q] : rec_inf();
-        wave_bitonic(r, P, tails);
+        // rank sort: the bucket's records go to LDS, every lane ranks its
+        // (up to two) records against all c of them -- the order is total, so
+        // ranks are distinct.  Broadcast LDS reads, no exchange network.
+        SRec x[2];
 #pragma unroll
         for (int q = 0; q < 2; q++) {
-            const int e = 2 * lane + q;
+            const int e = lane + 64 * q;
             if (e < c) {
-                out[e] = r[q];
-                if (job) J.out_slot[offset + e] = r[q].idx;
-                emit_quantiles(J, job, (int64_t)offset + e, r[q]);
+                x[q] = row[e];
+                s_r4[2 * e] = make_uint4((uint32_t)x[q].hi, (uint32_t)(x[q].hi >> 32), (uint32_t)x[q].lo,
+                                         (uint32_t)(x[q].lo >> 32));
+                s_r4[2 * e + 1] = make_uint4(x[q].meta, x[q].idx, 0, 0);
             }
+        }
+        const int64_t c2 = PCLK();
+        const int64_t c2b = c2;
+        __syncthreads();
+        int rank[2] = {0, 0};
+        for (int j0 = 0; j0 < c; j0 += 8) {  // eight records per round: their LDS reads overlap
+            SRec y[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint4 a = s_r4[2 * (j0 + u)], m = s_r4[2 * (j0 + u) + 1];
+                y[u] = SRec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), m.x, m.y, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (j0 + u < c)
+#pragma unroll
+                    for (int q = 0; q < 2; q++) rank[q] += (lane + 64 * q < c) && rec_lt(y[u], x[q], tails);
+        }
+        const int64_t c3 = PCLK();
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (lane + 64 * q < c) {
+                out[rank[q]] = x[q];
+                if (job) J.out_slot[offset + rank[q]] = x[q].idx;
+                emit_quantiles(J, job, (int64_t)offset + rank[q], x[q]);
+            }
+        }
+        if (lane == 0) {
+            PACC(J.sc, 16, c1 - c0);
+            PACC(J.sc, 17, c2b - c1);
+            PACC(J.sc, 18, c3 - c2b);
+            PACC(J.sc, 19, PCLK() - c3);
+            PACC(J.sc, 20, 1);
         }
         return;
     }

@@ -10,10 +10,11 @@
 // valueBefore(e) unless e is already a boundary or the next range's begin;
 // every boundary in [b, e) is erased; b gets version `now`.
 //
-// Launches per batch: merge = bounds, aff_build, aff_plan, scan, page_merge,
-// dir_rebuild, bmax_commit; compaction = win_setup, win_keep, scan,
-// win_repack, win_dir, bmax_commit.  Directory `start[]` (global index of a
-// page's first boundary) is carried forward incrementally, never rescanned.
+// Launches per batch: merge = plan_ranges, plan_aggr, plan_scan, page_merge,
+// bmax_commit (+ the compaction window setup); compaction = win_keep,
+// win_repack, win_dir (+ page-group maxima, search index, commit).  Directory
+// `start[]` (global index of a page's first boundary) is carried forward
+// incrementally, never rescanned.
 #include <algorithm>
 #include "kernels.h"
 #include "devutil.h"
@@ -133,6 +134,8 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     ie_o[j] = i_e;
     need_o[j] = (uint8_t)need;
     vb_o[j] = vb;
+    atomicMin(&acc.fmin[p_b], i_b);
+    if (p_b != p_e) atomicMin(&acc.fmin[p_e], 0);
     if (p_b == p_e) {
         atomicAdd(&acc.er[p_b], max(0, i_e - i_b));
         atomicAdd(&acc.nn[p_b], 1 + need);
@@ -171,7 +174,7 @@ static constexpr int PS_BLOCK = PS_THREADS * PS_ITEMS;
 
 struct PlanItem {
     bool affected;
-    int32_t nout, parts, nn, jlo, jhi;
+    int32_t nout, parts, nn, jlo, jhi, f;
 };
 
 __device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, bool covered) {
@@ -179,6 +182,7 @@ __device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, 
     const int cnt = dir.cnt[x];
     it.jlo = acc.jlo[x];
     it.jhi = acc.jhi[x];
+    it.f = acc.fmin[x];
     it.nn = 0;
     if (covered) {
         it.affected = true;
@@ -274,7 +278,7 @@ struct PlanArgs {
     const int64_t* blk_agg;
     const int32_t* blk_diff;
     int32_t *aff_list, *aff_jlo, *aff_jhi, *aff_nn, *aff_parts, *aff_nn_off, *aff_parts_off, *aff_extra_off,
-        *aff_free_off, *aff_page, *aff_cnt;
+        *aff_free_off, *aff_page, *aff_cnt, *aff_f;
     int64_t* aff_start;
 };
 
@@ -358,6 +362,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
                 A.aff_list[a] = x;
                 A.aff_page[a] = A.src.page[x];
                 A.aff_cnt[a] = cnt[k];
+                A.aff_f[a] = it[k].f;
                 A.aff_jlo[a] = it[k].jlo;
                 A.aff_jhi[a] = it[k].jhi;
                 A.aff_nn[a] = it[k].nn;
@@ -383,6 +388,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
             A.acc.jlo[x] = INT32_MAX;
             A.acc.jhi[x] = -1;
             A.acc.diff[x] = 0;
+            A.acc.fmin[x] = INT32_MAX;
 #pragma unroll
             for (int f = 0; f < 3; f++) ex[f] += w[k][f];
         }
@@ -437,7 +443,7 @@ struct MergeArgs {
     const int32_t* free_stack;
     int32_t* freed_list;
     const int32_t* aff_list;
-    const int32_t *aff_page, *aff_cnt;
+    const int32_t *aff_page, *aff_cnt, *aff_f;
     const int32_t *jlo, *jhi, *nn, *nn_off, *parts, *parts_off, *extra_off, *free_off;
     const int64_t* aff_start;
     const int32_t *pb, *ib, *pe, *ie;
@@ -529,27 +535,33 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     const int nn = A.nn[a];
     const int xoff = A.extra_off[a], doff = A.parts_off[a];
     const int64_t pbase = (int64_t)pg * PAGE;
-    // this lane's old slots i0 .. i0+3, loaded before any write: part 0 is
-    // rewritten in place (slots past cnt are ignored)
+    // old slots before the first changed one (f, from K1) keep their slot
+    // when the page stays one page: they are neither rewritten nor read,
+    // except for their versions (the page maximum).  This lane's old slots
+    // i0 .. i0+3 are loaded before any write: part 0 is rewritten in place.
+    const int f = min(A.aff_f[a], PAGE);
+    const int u = parts == 1 ? min(f, cntp) : 0;
     const int i0 = 4 * lane;
-    uint64_t ohi[4], olo[4];
+    uint64_t ohi[4] = {}, olo[4] = {};
     int64_t over[4];
-    uint32_t ometa[4];
-    const uint8_t* otail[4];
+    uint32_t ometa[4] = {};
+    const uint8_t* otail[4] = {};
     {
-        const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(A.pool.hi + pbase + i0);
-        const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(A.pool.lo + pbase + i0);
         const longlong2* v2 = reinterpret_cast<const longlong2*>(A.pool.ver + pbase + i0);
-        const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(A.pool.tail + pbase + i0);
-        const uint4 m4 = *reinterpret_cast<const uint4*>(A.pool.meta + pbase + i0);
-        const ulonglong2 ha = h2[0], hb = h2[1], la = l2[0], lb = l2[1], ta = t2[0], tb = t2[1];
         const longlong2 va = v2[0], vb = v2[1];
-        ohi[0] = ha.x; ohi[1] = ha.y; ohi[2] = hb.x; ohi[3] = hb.y;
-        olo[0] = la.x; olo[1] = la.y; olo[2] = lb.x; olo[3] = lb.y;
         over[0] = va.x; over[1] = va.y; over[2] = vb.x; over[3] = vb.y;
-        ometa[0] = m4.x; ometa[1] = m4.y; ometa[2] = m4.z; ometa[3] = m4.w;
-        otail[0] = (const uint8_t*)ta.x; otail[1] = (const uint8_t*)ta.y;
-        otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
+        if (i0 + 3 >= u && i0 < cntp) {
+            const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(A.pool.hi + pbase + i0);
+            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(A.pool.lo + pbase + i0);
+            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(A.pool.tail + pbase + i0);
+            const uint4 m4 = *reinterpret_cast<const uint4*>(A.pool.meta + pbase + i0);
+            const ulonglong2 ha = h2[0], hb = h2[1], la = l2[0], lb = l2[1], ta = t2[0], tb = t2[1];
+            ohi[0] = ha.x; ohi[1] = ha.y; ohi[2] = hb.x; ohi[3] = hb.y;
+            olo[0] = la.x; olo[1] = la.y; olo[2] = lb.x; olo[3] = lb.y;
+            ometa[0] = m4.x; ometa[1] = m4.y; ometa[2] = m4.z; ometa[3] = m4.w;
+            otail[0] = (const uint8_t*)ta.x; otail[1] = (const uint8_t*)ta.y;
+            otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
+        }
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -563,7 +575,6 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     S.pmax[lane] = INT64_MIN;
     wave_lds_sync();
     // ---- 1. plan lanes: erased intervals and insertion counts
-    int f = PAGE;  // first old slot a range changes
     for (int j0 = jlo; j0 <= jhi; j0 += 64) {
         const int j = j0 + lane;
         if (j <= jhi) {
@@ -575,10 +586,8 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             }
             if (pb == p) atomicAdd(&S.ins[ib], 1);
             if (pe == p && A.need_e[j]) atomicAdd(&S.ins[ie], 1);
-            f = min(f, s0);
         }
     }
-    f = wave_reduce_min(f);
     wave_lds_sync();
     // ---- 2. slot lanes: survivors and output positions
     int ec[4], ic[4];
@@ -617,9 +626,6 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     wave_lds_sync();
     const int nout = kept + nn;
     const int per = cdiv(nout, parts);
-    // old slots before the first changed one keep their slot when the page
-    // stays one page: not rewritten
-    const int u = parts == 1 ? min(f, cntp) : 0;
     const Dir& D = A.dst;
     auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
     int64_t vmax = INT64_MIN;  // parts == 1: the page maximum by a wave reduction
@@ -636,8 +642,9 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             const int dp = dest(qq);
             put_entry(A.pool, (int64_t)dp * PAGE + slot, ohi[q], olo[q], ometa[q], over[q], otail[q]);
             if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, ohi[q], olo[q], ometa[q], otail[q]);
-        } else if (i == 0) {  // unchanged first slot
-            part_first(S, D, A, a, doff, 0, per, nout, pg, ohi[0], olo[0], ometa[0], otail[0]);
+        } else if (i == 0) {  // unchanged first slot: the pre-batch directory holds its key
+            part_first(S, D, A, a, doff, 0, per, nout, pg, A.dir.fhi[p], A.dir.flo[p], A.dir.fmeta[p],
+                       A.dir.ftail[p]);
         }
     }
     // ---- 3b. new entries, by the plan lanes: b_j (version now), then e_j
@@ -726,113 +733,6 @@ __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y
 // Per-64-entry maxima of the new directory (one wavefront per group), pages
 // the merge freed back onto the free stack (above the ones it took), then
 // commit the directory size, free-stack top and history size.
-// level-1 entry i of the search index, and the entries of higher levels it
-// starts (i a multiple of 16^(l-1))
-__device__ inline void sidx_build(const Dir& d, int i) {
-    const uint64_t v = d.fhi[(int64_t)i * SIDX_B];
-    d.sidx[i] = v;
-    int ii = i;
-    for (int l = 2; l <= SIDX_LEVELS && (ii & (SIDX_B - 1)) == 0; l++) {
-        ii >>= SIDX_LOG;
-        d.sidx[sidx_off(d.cap, l) + ii] = v;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sidx_build(Dir d, const int32_t* D) {
-    const int n1 = cdiv(*D, SIDX_B);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
-}
-
-void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
-    hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
-}
-
-__global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
-                                                     int32_t* free_stack, int end_of_batch) {
-    const int Dn = sc->D_next;
-    if (freed_list) {
-        const int base = sc->free_top - sc->extra_total;
-        const int nf = sc->free_next - base;
-        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x)
-            free_stack[base + i] = freed_list[i];
-    }
-    const int n1 = cdiv(Dn, SIDX_B);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
-    const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (g * 64 < Dn) {
-        const int x = g * 64 + lane;
-        int64_t m = x < Dn ? d.maxv[x] : INT64_MIN;
-        m = wave_reduce_max(m);
-        if (lane == 0) d.bmax[g] = m;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        sc->D = Dn;
-        sc->free_top = sc->free_next;
-        sc->H = d.start[Dn];
-        if (end_of_batch) {  // the next batch's encoder allocates from these
-            sc->last_err = sc->err;
-            sc->err = 0;
-            sc->btail_used = 0;
-        }
-    }
-}
-
-static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s, bool end_of_batch,
-                               const int32_t* freed_list = nullptr) {
-    const int groups = cdiv(h.cap_dir, 64);
-    hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
-                       h.free_stack, (int)end_of_batch);
-}
-
-void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
-    // full recompute of start[] (used after reset / load)
-    Dir& d = h.dir[cur];
-    scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
-    (void)hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
-    launch_bmax_commit(h, cur, sc, s, true);
-}
-
-int plan_blocks(int cap_dir) { return cdiv(cap_dir, PS_BLOCK); }
-
-void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
-                  int64_t v0, bool end_of_batch, hipStream_t s) {
-    const int W = v.write_count;
-    Dir& src = h.dir[cur];
-    Dir& dst = h.dir[cur ^ 1];
-    if (W > 0) {
-        const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
-        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv((int64_t)W * PR_G, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
-                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
-    }
-    const int nblk = plan_blocks(h.cap_dir);
-    hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
-                       b.blk_diff);
-    PlanArgs P;
-    P.src = src; P.dst = dst; P.sc = sc; P.acc = b.acc; P.blk_agg = b.blk_agg; P.blk_diff = b.blk_diff;
-    P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
-    P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
-    P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
-    P.aff_page = b.aff_page; P.aff_cnt = b.aff_cnt;
-    hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
-    if (W > 0) {
-        const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
-        MergeArgs A;
-        A.pool = h.pool; A.dir = src; A.dst = dst; A.sc = sc; A.free_stack = h.free_stack; A.freed_list = b.freed_list;
-        A.aff_list = b.aff_list; A.aff_page = b.aff_page; A.aff_cnt = b.aff_cnt;
-        A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
-        A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off; A.free_off = b.aff_free_off;
-        A.aff_start = b.aff_start;
-        A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
-        A.rb = b.rkb; A.re = b.rke; A.ne = b.ne; A.ne_ins = b.ne_ins;
-        A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
-        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)))), dim3(256),
-                           0, s, A);
-    }
-    launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
-}
-
 // ------------------------------------------------------------ compaction ----
 // removeBefore over the window driven by ConflictBatch::detectConflicts
 // (SkipList.cpp:1198-1206, 665-702).  The window
@@ -893,10 +793,21 @@ __device__ inline int wave_start_search(const int64_t* start, int D, int64_t g) 
     return lo - 1 + __popcll(__ballot(q < hi && start[q] <= g));
 }
 
-__global__ __launch_bounds__(64) void k_win_setup(Pool pool, Dir dir, Scalars* sc, uint64_t* rk_hi, uint64_t* rk_lo,
-                                                  uint32_t* rk_meta, uint8_t* rk_tail) {
-    const int lane = threadIdx.x;
-    const int D = sc->D;
+struct RemovalKey {
+    uint64_t* hi;
+    uint64_t* lo;
+    uint32_t* meta;
+    uint8_t* tail;
+};
+
+// The compaction window over the directory `dir` of D entries, by one
+// wavefront (run by k_bmax_commit after the merge, before the commit).
+__device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars* sc, const RemovalKey& rkey) {
+    uint64_t* rk_hi = rkey.hi;
+    uint64_t* rk_lo = rkey.lo;
+    uint32_t* rk_meta = rkey.meta;
+    uint8_t* rk_tail = rkey.tail;
+    const int lane = threadIdx.x & 63;
     const int64_t H = dir.start[D];
     int64_t g0 = 0, g1 = 0;
     int pA = 1, pB = 0;
@@ -913,7 +824,7 @@ __global__ __launch_bounds__(64) void k_win_setup(Pool pool, Dir dir, Scalars* s
             pA = i0 < dir.cnt[p0] ? p0 : p0 + 1;
             pB = wave_start_search(dir.start, D, g1 - 1);
             if (g1 < H) {
-                const int q1 = wave_start_search(dir.start, D, g1);
+                const int q1 = pB + 1 < D && dir.start[pB + 1] <= g1 ? pB + 1 : pB;  // entry holding g1
                 nk = pool_key(pool, (int64_t)dir.page[q1] * PAGE + (g1 - dir.start[q1]));
                 has_key = true;
             }
@@ -939,6 +850,118 @@ __global__ __launch_bounds__(64) void k_win_setup(Pool pool, Dir dir, Scalars* s
         uint64_t* d = reinterpret_cast<uint64_t*>(rk_tail);
         for (uint32_t w = lane; w < words; w += 64) d[w] = s[w];
     }
+}
+
+// level-1 entry i of the search index, and the entries of higher levels it
+// starts (i a multiple of 16^(l-1))
+__device__ inline void sidx_build(const Dir& d, int i) {
+    const uint64_t v = d.fhi[(int64_t)i * SIDX_B];
+    d.sidx[i] = v;
+    int ii = i;
+    for (int l = 2; l <= SIDX_LEVELS && (ii & (SIDX_B - 1)) == 0; l++) {
+        ii >>= SIDX_LOG;
+        d.sidx[sidx_off(d.cap, l) + ii] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sidx_build(Dir d, const int32_t* D) {
+    const int n1 = cdiv(*D, SIDX_B);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
+}
+
+void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
+    hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
+}
+
+__global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
+                                                     int32_t* free_stack, int end_of_batch, Pool pool,
+                                                     RemovalKey rkey) {
+    const int Dn = sc->D_next;
+    // a compaction follows: its window over the new directory (one wavefront)
+    if (!end_of_batch && blockIdx.x == 0 && threadIdx.x < 64) win_setup_wave(pool, d, Dn, sc, rkey);
+    if (freed_list) {
+        const int base = sc->free_top - sc->extra_total;
+        const int nf = sc->free_next - base;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x)
+            free_stack[base + i] = freed_list[i];
+    }
+    const int n1 = cdiv(Dn, SIDX_B);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (g * 64 < Dn) {
+        const int x = g * 64 + lane;
+        int64_t m = x < Dn ? d.maxv[x] : INT64_MIN;
+        m = wave_reduce_max(m);
+        if (lane == 0) d.bmax[g] = m;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sc->D = Dn;
+        sc->free_top = sc->free_next;
+        sc->H = d.start[Dn];
+        if (end_of_batch) {  // the next batch's encoder allocates from these
+            sc->last_err = sc->err;
+            sc->err = 0;
+            sc->btail_used = 0;
+        }
+    }
+}
+
+static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s, bool end_of_batch,
+                               const int32_t* freed_list = nullptr) {
+    const int groups = cdiv(h.cap_dir, 64);
+    const RemovalKey rk{h.rk_hi, h.rk_lo, h.rk_meta, h.rk_tail};
+    hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
+                       h.free_stack, (int)end_of_batch, h.pool, rk);
+}
+
+void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
+    // full recompute of start[] (used after reset / load)
+    Dir& d = h.dir[cur];
+    scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
+    (void)hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+    launch_bmax_commit(h, cur, sc, s, true);
+}
+
+int plan_blocks(int cap_dir) { return cdiv(cap_dir, PS_BLOCK); }
+
+void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
+                  int64_t v0, bool end_of_batch, hipStream_t s) {
+    const int W = v.write_count;
+    Dir& src = h.dir[cur];
+    Dir& dst = h.dir[cur ^ 1];
+    if (W > 0) {
+        const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
+        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv((int64_t)W * PR_G, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
+                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
+    }
+    const int nblk = plan_blocks(h.cap_dir);
+    hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
+                       b.blk_diff);
+    PlanArgs P;
+    P.src = src; P.dst = dst; P.sc = sc; P.acc = b.acc; P.blk_agg = b.blk_agg; P.blk_diff = b.blk_diff;
+    P.aff_f = b.aff_f;
+    P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
+    P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
+    P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
+    P.aff_page = b.aff_page; P.aff_cnt = b.aff_cnt;
+    hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
+    if (W > 0) {
+        const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
+        MergeArgs A;
+        A.pool = h.pool; A.dir = src; A.dst = dst; A.sc = sc; A.free_stack = h.free_stack; A.freed_list = b.freed_list;
+        A.aff_list = b.aff_list; A.aff_page = b.aff_page; A.aff_cnt = b.aff_cnt; A.aff_f = b.aff_f;
+        A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
+        A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off; A.free_off = b.aff_free_off;
+        A.aff_start = b.aff_start;
+        A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
+        A.rb = b.rkb; A.re = b.rke; A.ne = b.ne; A.ne_ins = b.ne_ins;
+        A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
+        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)))), dim3(256),
+                           0, s, A);
+    }
+    launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
 }
 
 __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scalars* sc, int64_t oldest,
@@ -974,18 +997,30 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
 // survivors -> fresh pages at FILL density, with their descriptors; each
 // workgroup's survivors span at most 3 parts, reduced in LDS before one
 // global atomic per part
-__global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Scalars* sc,
-                                                    const uint8_t* __restrict__ keep, const int32_t* __restrict__ off,
+__global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars* sc,
+                                                    const uint8_t* __restrict__ keep, const int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ free_stack, DescArrays desc) {
     __shared__ int32_t tmp[256 / 64 + 1];
     __shared__ long long lmax[4];
     const int np = sc->win_np;
     const int pA = sc->win_pA;
     const int top0 = sc->free_top;
-    const int S = off[np];
+    // survivors in all window pages (S) and before this block's first page:
+    // the window is a few hundred pages, so every block sums the counts
+    int all = 0;
+    for (int v = threadIdx.x; v < np; v += blockDim.x) all += cnt[v];
+    const int S = block_reduce_sum(all, tmp);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc->win_surv = S;
     const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int per = k > 0 ? cdiv(S, k) : 1;
+    int before = 0;  // survivors in pages [0, w), advanced by the grid stride
+    int wprev = 0;
     for (int w = blockIdx.x; w < np; w += gridDim.x) {
+        int part_sum = 0;
+        for (int v = wprev + threadIdx.x; v < w; v += blockDim.x) part_sum += cnt[v];
+        before += block_reduce_sum(part_sum, tmp);
+        wprev = w;
+        const int offw = before;
         const int q = pA + w;
         const int pg = dir.page[q], c = dir.cnt[q];
         const int i = threadIdx.x;
@@ -993,9 +1028,9 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Sc
         const int kp = i < c ? keep[(int64_t)w * PAGE + i] : 0;
         int tot;
         const int ex = block_excl_scan(kp, tmp, tot);
-        const int part0 = off[w] / per;
+        const int part0 = offw / per;
         if (kp) {
-            const int m = off[w] + ex;
+            const int m = offw + ex;
             const int part = m / per, slot = m - part * per;
             const int dp = free_stack[top0 - 1 - part];
             const int64_t sidx = (int64_t)pg * PAGE + i;
@@ -1013,56 +1048,76 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, const Sc
     }
 }
 
-__global__ __launch_bounds__(256) void k_win_dir(Dir src, Dir dst, Scalars* sc, DescArrays desc,
-                                                 const int32_t* __restrict__ off, int32_t* free_stack) {
+// The directory after the compaction, its page-group maxima and search index
+// (what k_bmax_commit does after a merge), and the commit by the last block.
+__global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc, DescArrays desc,
+                                                 int32_t* free_stack) {
     const int np = sc->win_np;
-    const int S = off[np];
+    const int S = sc->win_surv;
     const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int per = k > 0 ? cdiv(S, k) : 1;
     const int D = sc->D, pA = sc->win_pA;
     const int Dn = D - np + k;
     const int64_t removed = np ? (src.start[pA + np] - src.start[pA]) - S : 0;
-    const int y = blockIdx.x * blockDim.x + threadIdx.x;
-    if (y == 0) {
-        sc->D_next = Dn;
-        sc->free_next = sc->free_top - k + np;
-        dst.start[Dn] = src.start[D] - removed;
-        sc->win_newpages = k;
-        sc->win_surv = S;
-    }
-    if (y < Dn) {
-        if (np == 0 || y < pA) {
-            dir_copy(src, y, dst, y);
-            dst.start[y] = src.start[y];
-        } else if (y < pA + k) {
-            desc_copy(desc, y - pA, dst, y);
-            dst.start[y] = src.start[pA] + (int64_t)(y - pA) * per;
-        } else {
-            dir_copy(src, y - k + np, dst, y);
-            dst.start[y] = src.start[y - k + np] - removed;
+    const int free_next = sc->free_top - k + np;
+    const int64_t H = src.start[D] - removed;
+    const int top = sc->free_top;
+    if (blockIdx.x == 0 && threadIdx.x == 0) dst.start[Dn] = H;
+    // grid-stride over entries (few blocks: each one bumps the commit counter)
+    const int n = max(Dn, np);
+    for (int y0 = blockIdx.x * blockDim.x; y0 < n; y0 += gridDim.x * blockDim.x) {
+        const int y = y0 + threadIdx.x;
+        int64_t mv = INT64_MIN;
+        if (y < Dn) {
+            if (np == 0 || y < pA) {
+                dir_copy(src, y, dst, y);
+                dst.start[y] = src.start[y];
+            } else if (y < pA + k) {
+                desc_copy(desc, y - pA, dst, y);
+                dst.start[y] = src.start[pA] + (int64_t)(y - pA) * per;
+            } else {
+                dir_copy(src, y - k + np, dst, y);
+                dst.start[y] = src.start[y - k + np] - removed;
+            }
+            mv = dst.maxv[y];
+            if ((y & (SIDX_B - 1)) == 0) sidx_build(dst, y / SIDX_B);
         }
+        if (y < np) free_stack[top - k + y] = src.page[pA + y];
+        mv = wave_reduce_max(mv);  // one wavefront = one 64-entry group
+        if ((threadIdx.x & 63) == 0 && (y & ~63) < Dn) dst.bmax[y >> 6] = mv;
     }
-    if (y < np) free_stack[sc->free_top - k + y] = src.page[pA + y];
+    // commit once every block has read the pre-compaction scalars (no fence:
+    // the values were consumed before the barrier, and the directory itself
+    // is published by the kernel boundary -- a device-scope fence would write
+    // back every XCD's L2)
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(&sc->blocks_done, 1) == (int)gridDim.x - 1) {
+        sc->blocks_done = 0;
+        sc->D = Dn;
+        sc->D_next = Dn;
+        sc->free_top = free_next;
+        sc->free_next = free_next;
+        sc->H = H;
+        sc->win_newpages = k;
+        sc->last_err = sc->err;  // end of batch: the next batch's encoder allocates from these
+        sc->err = 0;
+        sc->btail_used = 0;
+    }
 }
+
+static constexpr int WIN_DIR_BLOCKS = 128;
 
 void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s) {
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
     const int win_cap = b.win_cap_pages;
-    hipLaunchKernelGGL(k_win_setup, dim3(1), dim3(64), 0, s, h.pool, src, sc, h.rk_hi, h.rk_lo, h.rk_meta,
-                       h.rk_tail);
     hipLaunchKernelGGL(k_win_keep, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc, oldest,
                        b.win_keep, b.win_cnt, b.desc_max);
-    ScanArgs<1> sa;
-    sa.in[0] = b.win_cnt;
-    sa.out[0] = b.win_off;
-    hipLaunchKernelGGL(k_scan_small<1>, dim3(1), dim3(1024), 0, s, sa, &sc->win_np);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
-                       b.win_keep, b.win_off, h.free_stack, da);
-    hipLaunchKernelGGL(k_win_dir, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, src, dst, sc, da, b.win_off,
-                       h.free_stack);
-    launch_bmax_commit(h, cur ^ 1, sc, s, true);
+                       b.win_keep, b.win_cnt, h.free_stack, da);
+    hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
+                       sc, da, h.free_stack);
 }
 
 // ------------------------------------------------------------------ reset ----

@@ -38,9 +38,12 @@ def main():
     d = (a - base) * 0.01  # 100 MHz ticks -> us
     m = d.mean(axis=0)
     print(f"H={cs.history_size()}  phase offsets (us from phase 0), mean over {nb} batches:")
-    for i in range(a.shape[1]):
+    for i in range(min(16, a.shape[1])):
         if a[:, i].any():
             print(f"  ph[{i:2d}] {m[i]:9.2f}  (+{m[i] - (m[i - 1] if i else 0):8.2f})")
+    if a.shape[1] > 16:  # cumulative per-wave cycle accumulators: per-batch deltas
+        dd = np.diff(a[:, 16:], axis=0).mean(axis=0)
+        print("  accumulators per batch:", " ".join(f"[{16 + i}]={v:.0f}" for i, v in enumerate(dd) if v))
 
 
 if __name__ == "__main__":
