@@ -87,6 +87,7 @@ struct fdbcs {
     BatchBufs b{};
     Scalars* sc = nullptr;       // device
     Scalars* sc_host = nullptr;  // pinned mirror
+    Scalars* sc_mapped = nullptr;  // host-mapped copy the batch-ending kernel writes (HistBufs::mirror)
     int cur = 0;
     int64_t v0 = 0;
     int64_t oldest = 0;
@@ -156,9 +157,7 @@ void free_pool(HistBufs& h) {
     }
 }
 
-int sync_state(fdbcs* cs) {
-    HIPOK(hipMemcpyAsync(cs->sc_host, cs->sc, sizeof(Scalars), hipMemcpyDeviceToHost, cs->stream));
-    HIPOK(hipStreamSynchronize(cs->stream));
+void adopt_scalars(fdbcs* cs) {
     cs->known_D = cs->sc_host->D;
     cs->known_free = cs->sc_host->free_top;
     cs->known_H = cs->sc_host->H;
@@ -166,6 +165,20 @@ int sync_state(fdbcs* cs) {
     if (cs->sc_host->ss_resample) cs->have_quantiles = false;
     cs->pending_pages = 0;
     cs->pending_tail = 0;
+}
+
+int sync_state(fdbcs* cs) {
+    HIPOK(hipMemcpyAsync(cs->sc_host, cs->sc, sizeof(Scalars), hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    adopt_scalars(cs);
+    return FDBCS_OK;
+}
+
+// After a batch: its last kernel has written the scalars to the mapped copy.
+int sync_batch(fdbcs* cs) {
+    HIPOK(hipStreamSynchronize(cs->stream));
+    memcpy(cs->sc_host, (const void*)cs->sc_mapped, sizeof(Scalars));
+    adopt_scalars(cs);
     return FDBCS_OK;
 }
 
@@ -460,7 +473,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     record(cs, 6);
     if (compact) cs->oldest = new_oldest;
     if (sync) {
-        if ((r = sync_state(cs))) return r;
+        if ((r = sync_batch(cs))) return r;
         if (cs->timing) {
             float ms;
             const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
@@ -557,7 +570,7 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     const int64_t T = hv.txn_count;
     if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
     if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
-    if ((r = sync_state(cs))) return r;
+    if ((r = sync_batch(cs))) return r;
     if (cs->sc_host->last_err) return cs->sc_host->last_err;
     if (T) memcpy(verdict, cs->vpin, (size_t)T);
     if (cs->timing) {
@@ -602,6 +615,11 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if (hipHostMalloc((void**)&cs->sc_host, sizeof(Scalars), hipHostMallocDefault) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
     memset(cs->sc_host, 0, sizeof(Scalars));
+    if (hipHostMalloc((void**)&cs->sc_mapped, sizeof(Scalars), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&cs->h.mirror, cs->sc_mapped, 0) != hipSuccess)
+        return fail(FDBCS_E_NOMEM);
+    memset(cs->sc_mapped, 0, sizeof(Scalars));
     if (hipMemset(cs->sc, 0, sizeof(Scalars)) != hipSuccess) return fail(FDBCS_E_HIP);
     int64_t max_hist = cfg && cfg->max_history > 0 ? cfg->max_history : (1 << 20);
     int64_t pages = std::max<int64_t>(1024, cdiv64(max_hist, FILL) * 2);
@@ -640,6 +658,7 @@ void fdbcs_destroy(fdbcs* cs) {
     dfree(cs->sc);
     dfree(cs->din);
     if (cs->sc_host) hipHostFree(cs->sc_host);
+    if (cs->sc_mapped) hipHostFree(cs->sc_mapped);
     if (cs->pin) hipHostFree(cs->pin);
     if (cs->vpin) hipHostFree(cs->vpin);
     for (int i = 0; i < 8; i++)

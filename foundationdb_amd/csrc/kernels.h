@@ -105,6 +105,9 @@ struct HistBufs {
     uint64_t tail_cap;
     // removal key (device copy)
     uint64_t* rk_hi; uint64_t* rk_lo; uint32_t* rk_meta; uint8_t* rk_tail;  // rk_tail: 30008 bytes
+    // host-mapped copy of the scalars, written by the kernel that ends a batch
+    // (the host reads it after a stream sync instead of issuing a copy)
+    Scalars* mirror;
 };
 
 // ---- scans (scan.hip) ----

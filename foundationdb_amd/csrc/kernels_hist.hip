@@ -873,9 +873,17 @@ void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
     hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
 }
 
+// the scalars to the host-mapped mirror: one wavefront of a block whose
+// thread 0 just committed (after a barrier), 8 bytes per lane
+__device__ inline void publish_scalars(const Scalars* sc, Scalars* mirror) {
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(sc);
+    uint64_t* m = reinterpret_cast<uint64_t*>(mirror);
+    for (int i = threadIdx.x; i < (int)(sizeof(Scalars) / 8); i += 64) m[i] = s[i];
+}
+
 __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
                                                      int32_t* free_stack, int end_of_batch, Pool pool,
-                                                     RemovalKey rkey) {
+                                                     RemovalKey rkey, Scalars* mirror) {
     const int Dn = sc->D_next;
     // a compaction follows: its window over the new directory (one wavefront)
     if (!end_of_batch && blockIdx.x == 0 && threadIdx.x < 64) win_setup_wave(pool, d, Dn, sc, rkey);
@@ -905,6 +913,10 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
             sc->btail_used = 0;
         }
     }
+    if (end_of_batch && blockIdx.x == 0) {
+        __syncthreads();
+        if (threadIdx.x < 64) publish_scalars(sc, mirror);
+    }
 }
 
 static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t s, bool end_of_batch,
@@ -912,7 +924,7 @@ static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t 
     const int groups = cdiv(h.cap_dir, 64);
     const RemovalKey rk{h.rk_hi, h.rk_lo, h.rk_meta, h.rk_tail};
     hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
-                       h.free_stack, (int)end_of_batch, h.pool, rk);
+                       h.free_stack, (int)end_of_batch, h.pool, rk, h.mirror);
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
@@ -1051,7 +1063,8 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
 // The directory after the compaction, its page-group maxima and search index
 // (what k_bmax_commit does after a merge), and the commit by the last block.
 __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc, DescArrays desc,
-                                                 int32_t* free_stack) {
+                                                  int32_t* free_stack, Scalars* mirror) {
+    __shared__ int last;
     const int np = sc->win_np;
     const int S = sc->win_surv;
     const int k = S > 0 ? cdiv(S, FILL) : 0;
@@ -1091,7 +1104,10 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
     // is published by the kernel boundary -- a device-scope fence would write
     // back every XCD's L2)
     __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(&sc->blocks_done, 1) == (int)gridDim.x - 1) {
+    if (threadIdx.x == 0) last = atomicAdd(&sc->blocks_done, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
         sc->blocks_done = 0;
         sc->D = Dn;
         sc->D_next = Dn;
@@ -1103,6 +1119,8 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         sc->err = 0;
         sc->btail_used = 0;
     }
+    __syncthreads();
+    if (threadIdx.x < 64) publish_scalars(sc, mirror);
 }
 
 static constexpr int WIN_DIR_BLOCKS = 128;
@@ -1117,7 +1135,7 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
                        b.win_keep, b.win_cnt, h.free_stack, da);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
-                       sc, da, h.free_stack);
+                       sc, da, h.free_stack, h.mirror);
 }
 
 // ------------------------------------------------------------------ reset ----
