@@ -268,6 +268,8 @@ void free_batch(BatchBufs& b) {
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
+    dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
+    dfree(b.wh.vb);
     free_plan(b);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
     dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
@@ -315,6 +317,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
         dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
+        dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
+        dfree(b.wh.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_combine
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
@@ -323,7 +327,9 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
             (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||
-            (r = dalloc(b.ne_ins, 2 * n)))
+            (r = dalloc(b.ne_ins, 2 * n)) || (r = dalloc(b.wh.pb, n)) || (r = dalloc(b.wh.ib, n)) ||
+            (r = dalloc(b.wh.cb, n)) || (r = dalloc(b.wh.pe, n)) || (r = dalloc(b.wh.ie, n)) ||
+            (r = dalloc(b.wh.feq, n)) || (r = dalloc(b.wh.vb, n)))
             return r;
         cs->capW = n;
     }

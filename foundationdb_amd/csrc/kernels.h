@@ -7,6 +7,16 @@
 namespace fdbcs_dev {
 
 // Merge-plan accumulators, indexed by directory entry.
+struct WriteHits {
+    int32_t* pb;   // directory entry of b
+    int32_t* ib;   // lower bound of b in its page
+    int32_t* cb;   // boundaries in b's page
+    int32_t* pe;   // directory entry of e
+    int32_t* ie;   // lower bound of e in its page
+    uint8_t* feq;  // e is a boundary
+    int64_t* vb;   // version of the boundary before e (valueBefore(e))
+};
+
 struct PageAcc {
     int32_t* er;    // old boundaries erased
     int32_t* nn;    // new boundaries landing
@@ -58,6 +68,9 @@ struct BatchBufs {
     int32_t* cb_slot;
     int32_t* ce_slot;
     KeyArrays rkb, rke;  // [W] their keys, compact (written by k_plan_ranges)
+    // where each write's begin / end fall in the pre-batch history [W]
+    // (searched speculatively beside the read check, before the decision)
+    WriteHits wh;
     // insertion plan [W]
     int32_t* pb; int32_t* ib; int32_t* pe; int32_t* ie;
     uint8_t* need_e;

@@ -600,6 +600,43 @@ __device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, in
     }
 }
 
+// Where write w's begin and end fall in the pre-batch history, searched
+// speculatively for every write (the merge plan later picks the writes that
+// open and close each combined range, k_plan_ranges).
+struct WriteSearchArgs {
+    int R, W;
+    KeyArrays keys;
+    Pool pool;
+    Dir dir;
+    const Scalars* sc;
+    int64_t v0;
+    WriteHits wh;
+};
+
+__device__ inline void write_search_group(const WriteSearchArgs& A, const Group<RC_G>& g, int w) {
+    if (w >= A.W) return;
+    const int64_t s = 2 * (int64_t)A.R + 2 * (int64_t)w;
+    const Key b = A.keys.get(s), e = A.keys.get(s + 1);
+    const int D = A.sc->D;
+    DirHit hb, he;
+    grp_dir_find2(g, A.dir, D, b, e, hb, he);
+    int ib, ie;
+    bool eqb, eqe;
+    grp_page_find2(g, A.pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    if (g.lane != 0) return;
+    int64_t vb;
+    if (ie > 0) vb = A.pool.ver[(int64_t)he.page * PAGE + ie - 1];
+    else if (he.x > 0) vb = A.pool.ver[(int64_t)A.dir.page[he.x - 1] * PAGE + A.dir.cnt[he.x - 1] - 1];
+    else vb = A.v0;
+    A.wh.pb[w] = hb.x;
+    A.wh.ib[w] = ib;
+    A.wh.cb[w] = hb.cnt;
+    A.wh.pe[w] = he.x;
+    A.wh.ie[w] = ie;
+    A.wh.feq[w] = eqe;
+    A.wh.vb[w] = vb;
+}
+
 // Edges need not skip transactions that already conflict with the history:
 // a conflicting reader is aborted whatever its sources, and a conflicting
 // writer never commits, so its edges never fire (k_decide_combine).  That
@@ -711,15 +748,20 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
     }
 }
 
-// One launch, two kinds of blocks: read-check groups (history), then edge
-// lanes (intra-batch) -- both latency-bound searches, so they overlap.
-__global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int rc_blocks, EdgesArgs EA) {
+// One launch, three kinds of blocks: read-check groups and write-search
+// groups (history), then edge lanes (intra-batch) -- all latency-bound
+// searches, so they overlap.
+__global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int rc_blocks, WriteSearchArgs WA,
+                                                          int ws_blocks, EdgesArgs EA) {
     __shared__ uint64_t smp_r[EQ], smp_w[EQ];
     if ((int)blockIdx.x < rc_blocks) {
         const Group<RC_G> g;
         read_check_group(RA, g, (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G));
+    } else if ((int)blockIdx.x < rc_blocks + ws_blocks) {
+        const Group<RC_G> g;
+        write_search_group(WA, g, (int)(((blockIdx.x - rc_blocks) * blockDim.x + threadIdx.x) / RC_G));
     } else {
-        const int i0 = (blockIdx.x - rc_blocks) * blockDim.x;
+        const int i0 = (blockIdx.x - rc_blocks - ws_blocks) * blockDim.x;
         if (i0 < EA.R) sample_fill(smp_w, EA.sw, 2 * EA.W);          // readers search the writes
         if (i0 + (int)blockDim.x > EA.R) sample_fill(smp_r, EA.sr, EA.R);  // writers search the reads
         __syncthreads();
@@ -733,10 +775,13 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
                  b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc};
+    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
+    const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
     const int e_blocks = R > 0 && W > 0 ? cdiv(R + W, 256) : 0;
-    if (rc_blocks + e_blocks > 0)
-        hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks, EA);
+    if (rc_blocks + ws_blocks + e_blocks > 0)
+        hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks,
+                           WA, ws_blocks, EA);
 }
 
 // ------------------------------------------------------ decide + combine ----

@@ -88,45 +88,36 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 }
 
 // ------------------------------------------------------- insertion plan ----
-static constexpr int PR_G = SIDX_B;
-
-// K1 k_plan_ranges, a group of PR_G lanes per combined range j (searches as
-// in k_read_check, hist_search.h), lane 0 records: where b and e fall in the
-// pre-batch history, whether e needs a node and the value it keeps, and the
-// range's contribution to the pages it touches, accumulated per directory
-// entry: erased old entries, new entries, first/last range touching the page.
-// Pages strictly inside [pb, pe] are wholly erased; they are marked in a
-// difference array (+1 at pb+1, -1 at pe) and resolved by the scan.
-__global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, Pool pool, Dir dir,
-                                                     Scalars* sc, int64_t v0, int32_t* __restrict__ pb_o,
+// K1 k_plan_ranges, one lane per combined range j.  A combined range opens
+// with the begin of one write and closes with the end of another, so where
+// its b and e fall in the pre-batch history was already found by the
+// speculative per-write searches (k_edges_read_check, WriteHits).  The lane
+// records the range's plan -- where b and e fall, whether e needs a node and
+// the value it keeps -- and its contribution to the pages it touches,
+// accumulated per directory entry: erased old entries, new entries, first /
+// last range touching the page, first old slot changed.  Pages strictly
+// inside [pb, pe] are wholly erased; they are marked in a difference array
+// (+1 at pb+1, -1 at pe) and resolved by the scan.
+__global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, WriteHits wh, int64_t wbase,
+                                                     Scalars* sc, int32_t* __restrict__ pb_o,
                                                      int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
                                                      int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
                                                      int64_t* __restrict__ vb_o, PageAcc acc, KeyArrays rb,
                                                      KeyArrays re) {
     if (sc->err) return;
-    const int D = sc->D;
-    const Group<PR_G> g;
     const int nC = sc->n_comb;
-    const int j = (int)((blockIdx.x * blockDim.x + threadIdx.x) / PR_G);
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nC) return;
-    const Key b = cb.get(j), e = ce.get(j);
+    const int sb = cb.slot[j], se = ce.slot[j];
+    const int wb = (int)((sb - wbase) >> 1), we = (int)((se - wbase) >> 1);
+    const Key b = cb.k.get(sb), e = ce.k.get(se);
     const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
-    if (g.lane == 0) {
-        rb.put(j, b);  // compact copies for the page merge
-        re.put(j, e);
-    }
-    int i_b, i_e;
-    bool eq_b, found;
-    DirHit hb, he;
-    grp_dir_find2(g, dir, D, b, e, hb, he);
-    const int p_b = hb.x, c_b = hb.cnt, g_b = hb.page;
-    const int p_e = he.x, c_e = he.cnt, g_e = he.page;
-    grp_page_find2(g, pool, g_b, c_b, b, g_e, c_e, e, i_b, eq_b, i_e, found);
-    if (g.lane != 0) return;
-    int64_t vb;
-    if (i_e > 0) vb = pool.ver[(int64_t)g_e * PAGE + i_e - 1];
-    else if (p_e > 0) vb = pool.ver[(int64_t)dir.page[p_e - 1] * PAGE + dir.cnt[p_e - 1] - 1];
-    else vb = v0;
+    const int p_b = wh.pb[wb], i_b = wh.ib[wb], c_b = wh.cb[wb];
+    const int p_e = wh.pe[we], i_e = wh.ie[we];
+    const bool found = wh.feq[we];
+    const int64_t vb = wh.vb[we];
+    rb.put(j, b);  // compact copies for the page merge
+    re.put(j, e);
     const int need = (!found && !touch) ? 1 : 0;
     pb_o[j] = p_b;
     ib_o[j] = i_b;
@@ -945,8 +936,8 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     Dir& dst = h.dir[cur ^ 1];
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
-        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv((int64_t)W * PR_G, 256)), dim3(256), 0, s, cbk, cek, h.pool, src, sc, v0, b.pb,
-                           b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
+        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, b.wh,
+                           2 * (int64_t)v.read_count, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
     hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
