@@ -472,11 +472,11 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
             }
         }
         if (lane == 0) {
-            PACC(J.sc, 16, c1 - c0);
-            PACC(J.sc, 17, c2b - c1);
-            PACC(J.sc, 18, c3 - c2b);
-            PACC(J.sc, 19, PCLK() - c3);
-            PACC(J.sc, 20, 1);
+            PACC(J.sc, 24, c1 - c0);
+            PACC(J.sc, 25, c2b - c1);
+            PACC(J.sc, 26, c3 - c2b);
+            PACC(J.sc, 27, PCLK() - c3);
+            PACC(J.sc, 28, 1);
         }
         return;
     }

@@ -486,8 +486,11 @@ struct WaveMerge {
     int32_t f_dp[MAXP];
 };
 
+// Lanes of one wavefront exchanging data through LDS: LDS operations of a
+// wavefront complete in order, so waiting for this wavefront's LDS traffic
+// suffices (no wait on its outstanding global loads, unlike a fence).
 __device__ inline void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -512,6 +515,21 @@ __device__ inline void part_first(WaveMerge& S, const Dir& D, const MergeArgs& A
     }
 }
 
+// Plan of combined range j as one lane holds it.
+struct RangePlan {
+    int pb, ib, pe, ie;
+    bool need;
+    int64_t vb;  // (the keys are loaded where they are written: fewer live registers)
+};
+
+__device__ inline RangePlan load_plan(const MergeArgs& A, int j) {
+    RangePlan r;
+    r.pb = A.pb[j]; r.ib = A.ib[j]; r.pe = A.pe[j]; r.ie = A.ie[j];
+    r.need = A.need_e[j];
+    r.vb = A.vb[j];
+    return r;
+}
+
 __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
     const int lane = threadIdx.x & 63;
@@ -526,10 +544,13 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     const int nn = A.nn[a];
     const int xoff = A.extra_off[a], doff = A.parts_off[a];
     const int64_t pbase = (int64_t)pg * PAGE;
+    // ---- 0. every load the page needs, issued together (one round trip):
     // old slots before the first changed one (f, from K1) keep their slot
-    // when the page stays one page: they are neither rewritten nor read,
-    // except for their versions (the page maximum).  This lane's old slots
-    // i0 .. i0+3 are loaded before any write: part 0 is rewritten in place.
+    // when the page stays one page, so they are neither rewritten nor read,
+    // except for their versions (the page maximum); this lane's old slots
+    // i0 .. i0+3 are loaded before any write (part 0 is rewritten in place);
+    // the first 64 ranges' plans; the page's first key (kept if unchanged).
+    const int64_t c0 = PCLK();
     const int f = min(A.aff_f[a], PAGE);
     const int u = parts == 1 ? min(f, cntp) : 0;
     const int i0 = 4 * lane;
@@ -554,6 +575,11 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
         }
     }
+    const bool has0 = jlo + lane <= jhi;
+    RangePlan r0{};
+    if (has0) r0 = load_plan(A, jlo + lane);
+    Key first{};
+    if (u > 0 && lane == 0) first = dir_first(A.dir, p);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         S.er[i0 + q] = 0;
@@ -565,21 +591,23 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     }
     S.pmax[lane] = INT64_MIN;
     wave_lds_sync();
+    const int64_t c1 = PCLK();
     // ---- 1. plan lanes: erased intervals and insertion counts
     for (int j0 = jlo; j0 <= jhi; j0 += 64) {
         const int j = j0 + lane;
         if (j <= jhi) {
-            const int pb = A.pb[j], ib = A.ib[j], pe = A.pe[j], ie = A.ie[j];
-            const int s0 = pb < p ? 0 : ib, e0 = pe > p ? cntp : ie;
+            const RangePlan r = j0 == jlo ? r0 : load_plan(A, j);
+            const int s0 = r.pb < p ? 0 : r.ib, e0 = r.pe > p ? cntp : r.ie;
             if (e0 > s0) {
                 atomicAdd(&S.er[s0], 1);
                 atomicAdd(&S.er[e0], -1);
             }
-            if (pb == p) atomicAdd(&S.ins[ib], 1);
-            if (pe == p && A.need_e[j]) atomicAdd(&S.ins[ie], 1);
+            if (r.pb == p) atomicAdd(&S.ins[r.ib], 1);
+            if (r.pe == p && r.need) atomicAdd(&S.ins[r.ie], 1);
         }
     }
     wave_lds_sync();
+    const int64_t c2 = PCLK();
     // ---- 2. slot lanes: survivors and output positions
     int ec[4], ic[4];
 #pragma unroll
@@ -620,6 +648,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     const Dir& D = A.dst;
     auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
     int64_t vmax = INT64_MIN;  // parts == 1: the page maximum by a wave reduction
+    const int64_t c3 = PCLK();
     // ---- 3a. surviving old entries
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -634,17 +663,19 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             put_entry(A.pool, (int64_t)dp * PAGE + slot, ohi[q], olo[q], ometa[q], over[q], otail[q]);
             if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, ohi[q], olo[q], ometa[q], otail[q]);
         } else if (i == 0) {  // unchanged first slot: the pre-batch directory holds its key
-            part_first(S, D, A, a, doff, 0, per, nout, pg, A.dir.fhi[p], A.dir.flo[p], A.dir.fmeta[p],
-                       A.dir.ftail[p]);
+            part_first(S, D, A, a, doff, 0, per, nout, pg, first.hi, first.lo, first.meta, first.tail);
         }
     }
+    const int64_t c4 = PCLK();
     // ---- 3b. new entries, by the plan lanes: b_j (version now), then e_j
     int base = 0;
     for (int j0 = jlo; j0 <= jhi; j0 += 64) {
         const int j = j0 + lane;
         const bool v = j <= jhi;
-        const bool eb = v && A.pb[j] == p;
-        const bool ee = v && A.pe[j] == p && A.need_e[j];
+        RangePlan r{};
+        if (v) r = j0 == jlo ? r0 : load_plan(A, j);
+        const bool eb = v && r.pb == p;
+        const bool ee = v && r.pe == p && r.need;
         const int c = (int)eb + (int)ee;
         const int inc = wave_incl_scan(c);
         int k = base + inc - c;  // new entries before this lane's
@@ -652,8 +683,8 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         for (int w = 0; w < 2; w++) {
             if (!(w == 0 ? eb : ee)) continue;
             const Key kk = w == 0 ? A.rb.get(j) : A.re.get(j);
-            const int at = w == 0 ? A.ib[j] : A.ie[j];
-            const int64_t ver = w == 0 ? A.now : A.vb[j];
+            const int at = w == 0 ? r.ib : r.ie;
+            const int64_t ver = w == 0 ? A.now : r.vb;
             const int m = k + S.er[at];
             const int qq = m / per, slot = m - qq * per;
             const int dp = dest(qq);
@@ -667,9 +698,17 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         }
         base += lane_read(inc, 63);
     }
+    const int64_t c5 = PCLK();
+    if (lane == 0) {
+        PACC(sc, 16, c1 - c0);
+        PACC(sc, 17, c2 - c1);
+        PACC(sc, 18, c3 - c2);
+        PACC(sc, 19, c4 - c3);
+        PACC(sc, 20, c5 - c4);
+        PACC(sc, 21, 1);
+    }
     if (parts == 1) vmax = wave_reduce_max(vmax);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // LDS stash + own pool writes visible below
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();  // the LDS stash of part-first entries, written by any lane
     for (int q = lane; q < min(parts, MAXP); q += 64) {  // directory entries of the parts
         const int y = doff + q;
         D.page[y] = S.f_dp[q];
@@ -684,6 +723,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         if (lane == 0) D.maxv[doff] = vmax;
         return;
     }
+    if (parts > MAXP) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // own pool writes, read below
     for (int q = lane; q < parts; q += 64) {
         int64_t mx;
         if (q < MAXP) {
@@ -692,6 +732,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             const int64_t bq = (int64_t)dest(q) * PAGE;
             const int c = min(per, nout - q * per);
             mx = INT64_MIN;
+            // (these slots were written by this wavefront above)
             for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
         }
         D.maxv[doff + q] = mx;
