@@ -17,6 +17,7 @@
 
 namespace fdbcs_dev {
 
+constexpr int SS_QT = 64;          // tail bytes kept per sort splitter (longer ones are compared as prefixes)
 constexpr int PAGE = 256;          // history page capacity (boundaries)
 constexpr int FILL = 192;          // target fill when a page is split / repacked
 constexpr uint32_t LEN_MASK = 0xFFFFFFu;

@@ -264,7 +264,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
-    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_bkt); dfree(b.ss_tmp);
+    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
@@ -334,7 +334,10 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         cs->capW = n;
     }
     if (!b.ss_cnt) {
-        if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024))) return r;
+        if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)) ||
+            (r = dalloc(b.ss_qt, 2 * 1024 * SS_QT)))
+            return r;
+        HIPOK(hipMemsetAsync(b.ss_qt, 0, 2 * 1024 * SS_QT, s));
         HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 2 * 1024 * sizeof(int32_t), s));
         HIPOK(hipMemsetAsync(b.ss_q, 0, 2 * 1024 * sizeof(SRec), s));  // equal records: valid (sorted) splitters
     }

@@ -54,6 +54,7 @@ struct BatchBufs {
     // sample sort scratch
     int32_t* ss_cnt;     // [2 parities][2 * 1024] bucket counts; a batch zeroes the next batch's
     SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
+    uint8_t* ss_qt;      // [2 * 1024 * SS_QT] their tail bytes (the batch keys they came from are gone)
     int32_t* ss_bkt;     // [R + 2W] bucket of each record
     SRec* ss_tmp;        // bucket staging rows
     int64_t ss_tmp_cap;

@@ -252,12 +252,50 @@ struct SortJobs {
     SRec* out[2];          // sorted output
     uint32_t* out_slot;    // [n1] slots of job 1's sorted records (compact copy)
     SRec* quant;           // [2][SS_Q] quantiles (persist across batches)
+    uint8_t* qtail;        // [2][SS_Q][SS_QT] their first SS_QT tail bytes
     int32_t* cnt;          // [2][SS_MAXB] this batch's bucket counts
     int32_t* cnt_next;     // [2][SS_MAXB] the next batch's (zeroed here)
     int32_t* bkt;          // [n0 + n1] bucket of each record
     SRec* tmp;             // [2][SS_MAXB][SS_ROW] staging rows
     Scalars* sc;
 };
+
+// Quantiles outlive the batch whose keys they are, so their tails are kept
+// (first SS_QT bytes) beside them.  x < splitter q, in the record order; a
+// splitter whose tail was cut stands for the prefix it kept (the smallest key
+// with that prefix), which is still a consistent split point.
+__device__ inline void put_quantile(const SortJobs& J, int job, int q, const SRec& x, const uint8_t* const* tails) {
+    J.quant[job * SS_Q + q] = x;
+    const uint32_t L = key_len(x.meta);
+    if (L > 17) {
+        const int words = (int)min<uint32_t>((L - 17 + 7) / 8, SS_QT / 8);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(tails[x.idx]);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(J.qtail + (int64_t)(job * SS_Q + q) * SS_QT);
+        for (int w = 0; w < words; w++) dst[w] = src[w];
+    }
+}
+
+__device__ __noinline__ bool rec_lt_quant_tail(const SRec& x, const SRec& q, const uint8_t* qt,
+                                               const uint8_t* const* tails) {
+    const uint32_t lx = key_len(x.meta), lq = key_len(q.meta);
+    if (lq - 17 > (uint32_t)SS_QT) {  // q was cut: compare with its kept prefix
+        const uint32_t lp = 17 + SS_QT;
+        const int c = tail_cmp(tails[x.idx], lx, qt, lp);
+        return c < 0;  // (a key that starts with the prefix is not below it)
+    }
+    const int c = tail_cmp(tails[x.idx], lx, qt, lq);
+    if (c) return c < 0;
+    const uint32_t px = x.idx & 1, pq = q.idx & 1;
+    return px != pq ? px > pq : x.idx < q.idx;
+}
+
+__device__ inline bool rec_lt_quant(const SRec& x, const SRec& q, const uint8_t* qt, const uint8_t* const* tails) {
+    const bool heq = x.hi == q.hi, leq = x.lo == q.lo;
+    const bool tail_case = heq & leq & ((x.meta >> 24) == (q.meta >> 24)) & (key_len(x.meta) > 17) &
+                           (key_len(q.meta) > 17);
+    if (__builtin_expect(tail_case, 0)) return rec_lt_quant_tail(x, q, qt, tails);
+    return rec_lt(x, q, tails);  // (decided without tails)
+}
 
 __device__ inline SRec load_rec(const KeyArrays& keys, int64_t slot) {
     return SRec{keys.hi[slot], keys.lo[slot], keys.meta[slot], (uint32_t)slot, 0};
@@ -361,7 +399,7 @@ __global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys) 
     __syncthreads();
     lds_bitonic(L, SS_Q, keys.tail);
     for (int q = threadIdx.x; q < SS_Q; q += blockDim.x)
-        J.quant[job * SS_Q + q] = L.get((int)((int64_t)q * ns / SS_Q));
+        put_quantile(J, job, q, L.get((int)((int64_t)q * ns / SS_Q)), keys.tail);
 }
 
 __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) {
@@ -380,7 +418,8 @@ __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) 
     int lo = 0, len = nb - 1;
     while (len > 0) {
         const int half = len >> 1;
-        if (!rec_lt(x, L.get(lo + half), tails)) {
+        const int s = lo + half;
+        if (!rec_lt_quant(x, L.get(s), J.qtail + (int64_t)(job * SS_Q + (s + 1) * step) * SS_QT, tails)) {
             lo += half + 1;
             len -= half + 1;
         } else {
@@ -394,10 +433,11 @@ __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) 
 }
 
 // quantile q of the sorted output sits at position floor(q * n / SS_Q)
-__device__ inline void emit_quantiles(const SortJobs& J, int job, int64_t pos, const SRec& x) {
+__device__ inline void emit_quantiles(const SortJobs& J, int job, int64_t pos, const SRec& x,
+                                      const uint8_t* const* tails) {
     const int64_t n = J.n[job];
     for (int64_t q = (pos * SS_Q + n - 1) / n; q < SS_Q && (q * n) / SS_Q == pos; q++)
-        J.quant[job * SS_Q + q] = x;
+        put_quantile(J, job, (int)q, x, tails);
 }
 
 __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
@@ -468,7 +508,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
             if (lane + 64 * q < c) {
                 out[rank[q]] = x[q];
                 if (job) J.out_slot[offset + rank[q]] = x[q].idx;
-                emit_quantiles(J, job, (int64_t)offset + rank[q], x[q]);
+                emit_quantiles(J, job, (int64_t)offset + rank[q], x[q], tails);
             }
         }
         if (lane == 0) {
@@ -492,7 +532,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
             const SRec x = L.get(k);
             out[k] = x;
             if (job) J.out_slot[offset + k] = x.idx;
-            emit_quantiles(J, job, (int64_t)offset + k, x);
+            emit_quantiles(J, job, (int64_t)offset + k, x, tails);
         }
         return;
     }
@@ -509,7 +549,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
         }
         out[rank] = x;
         if (job) J.out_slot[offset + rank] = x.idx;
-        emit_quantiles(J, job, (int64_t)offset + rank, x);
+        emit_quantiles(J, job, (int64_t)offset + rank, x, tails);
     }
 }
 
@@ -541,6 +581,7 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     J.out[1] = b.rec_w0;
     J.out_slot = b.sw_slot;
     J.quant = b.ss_q;
+    J.qtail = b.ss_qt;
     J.cnt = b.ss_cnt + parity * 2 * SS_MAXB;
     J.cnt_next = b.ss_cnt + (parity ^ 1) * 2 * SS_MAXB;
     J.bkt = b.ss_bkt;

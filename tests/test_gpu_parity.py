@@ -121,6 +121,19 @@ def test_workload_configs_small(cs, cfg, T, nb):
         check_pair(cs, c, batch, now, nold, history=(i % 5 == 4 or i == nb - 1))
 
 
+def test_sort_splitters_outlive_their_keys(cs):
+    """Splitters are the previous batch's quantiles; with long keys sharing
+    their first 17 bytes (config 4) comparing against them needs their tails,
+    which must not be read from the current batch's key slots (a smaller
+    batch does not even have those slots)."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    big, small = Workload(4, txns=1200), Workload(4, txns=90)
+    for i in range(10):
+        batch, now, nold = (big if i % 2 == 0 else small).batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i % 3 == 2 or i == 9))
+
+
 @pytest.mark.parametrize("buckets", ["1", "2", "8"])
 def test_sort_bucket_paths(cs, buckets):
     """Few sample-sort buckets push them past the register path (128 records)
