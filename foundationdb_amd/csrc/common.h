@@ -108,6 +108,15 @@ struct KeyArrays {           // one key per slot
 
 // Key slots addressed through an index (combined write ranges point at the
 // batch's key slots instead of copying keys).
+// Key range [lo, hi) of a shard in the exact sharded mode (SURVEY.md §8e
+// protocol A); has_lo / has_hi == 0: unbounded.  Keys live in device memory.
+struct ShardBounds {
+    Key lo, hi;
+    int32_t has_lo, has_hi;
+    __device__ bool below(const Key& k) const;   // k < lo
+    __device__ bool at_or_above(const Key& k) const;  // k >= hi
+};
+
 struct IndirectKeys {
     KeyArrays k;
     const int32_t* slot;
@@ -175,6 +184,9 @@ struct Scalars {
     uint64_t tail_used;     // bytes used in the history tail arena
     uint64_t btail_used;    // bytes used in the batch tail buffer
     int64_t win_g0, win_g1; // compaction window [g0, g1) (global indices)
+    int64_t last_ver;       // version of the last boundary (INT64_MIN: empty), set at each commit
+    int64_t win_r0;         // first removable index (g0 + 1: the first scanned node stays)
+    int64_t win_prev;       // version of the node before index 0 (sharded mode: the previous shard's last)
     int32_t win_pA, win_pB; // first / last directory entry covering the window
     int32_t win_newpages;   // pages produced by the repack
     int32_t win_surv;       // survivors in the window pages
@@ -211,5 +223,8 @@ struct Scalars {
 __device__ inline int64_t atomic_max_i64(int64_t* addr, int64_t v) {
     return (int64_t)atomicMax((long long*)addr, (long long)v);
 }
+
+__device__ inline bool ShardBounds::below(const Key& k) const { return has_lo && kcmp(k, lo) < 0; }
+__device__ inline bool ShardBounds::at_or_above(const Key& k) const { return has_hi && kcmp(k, hi) >= 0; }
 
 }  // namespace fdbcs_dev

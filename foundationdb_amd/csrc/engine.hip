@@ -116,6 +116,9 @@ struct fdbcs {
     // stage timing
     bool timing = false;
     hipEvent_t ev[8] = {};
+    // exact sharded mode: scratch for a key read back at a local index
+    uint64_t* key_out = nullptr;     // hi, lo, meta
+    uint8_t* key_out_tail = nullptr;
     double stage_us[7] = {0};
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
@@ -460,9 +463,11 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     hipStream_t s = cs->stream;
     Scalars* sc = cs->sc;
     record(cs, 0);
-    launch_ingest(v, cs->oldest, b, sc, s);
+    static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
+    const bool scatter = cs->have_quantiles && !no_fuse;  // steady state: the ingest scatters the sort records
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), s);
     record(cs, 1);
-    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), s)) {
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
@@ -594,6 +599,41 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     return FDBCS_OK;
 }
 
+// removalKey from host bytes (synchronous: the host copies are temporaries)
+int set_removal_key(fdbcs* cs, const uint8_t* key, uint32_t len) {
+    if (len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+    uint64_t rh, rl;
+    uint32_t rm;
+    encode_host(key, len, rh, rl, rm);
+    std::vector<uint8_t> rt(FDBCS_MAX_KEY + 16, 0);
+    if (len > 17) memcpy(rt.data(), key + 17, len - 17);
+    hipStream_t s = cs->stream;
+    HistBufs& h = cs->h;
+    HIPOK(hipMemcpyAsync(h.rk_hi, &rh, 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_lo, &rl, 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_meta, &rm, 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.rk_tail, rt.data(), len > 17 ? ((len - 17 + 7) & ~7u) : 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipStreamSynchronize(s));
+    return FDBCS_OK;
+}
+
+// key bytes from its (hi, lo, meta) encoding and tail bytes
+std::vector<uint8_t> decode_key(uint64_t hi, uint64_t lo, uint32_t meta, const uint8_t* tail) {
+    const uint32_t len = meta & LEN_MASK;
+    std::vector<uint8_t> k(len);
+    for (uint32_t i = 0; i < len; i++) {
+        if (i < 8) k[i] = (uint8_t)(hi >> (56 - 8 * i));
+        else if (i < 16) k[i] = (uint8_t)(lo >> (56 - 8 * (i - 8)));
+        else if (i == 16) k[i] = (uint8_t)(meta >> 24);
+        else k[i] = tail[i - 17];
+    }
+    return k;
+}
+
+int check_batch_shape(const fdbcs_batch_view& v) {
+    return v.txn_count < 0 || v.read_count < 0 || v.write_count < 0 ? FDBCS_E_ARG : FDBCS_OK;
+}
+
 }  // namespace
 
 // ============================================================== C ABI ====
@@ -641,6 +681,11 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         return fail(r);
     if (hipMemset(cs->h.rk_hi, 0, 8) || hipMemset(cs->h.rk_lo, 0, 8) || hipMemset(cs->h.rk_meta, 0, 4))
         return fail(FDBCS_E_HIP);
+    if ((r = dalloc(cs->h.shard_tails, 2 * (FDBCS_MAX_KEY + 16))) || (r = dalloc(cs->key_out, 3)) ||
+        (r = dalloc(cs->key_out_tail, FDBCS_MAX_KEY + 16)))
+        return fail(r);
+    if (hipMemset(cs->h.shard_tails, 0, 2 * (FDBCS_MAX_KEY + 16)) != hipSuccess) return fail(FDBCS_E_HIP);
+    cs->h.shard = ShardBounds{};
     for (int i = 0; i < 8; i++)
         if (hipEventCreate(&cs->ev[i]) != hipSuccess) return fail(FDBCS_E_HIP);
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
@@ -664,6 +709,7 @@ void fdbcs_destroy(fdbcs* cs) {
     free_pool(cs->h);
     dfree(cs->h.tail_arena);
     dfree(cs->h.rk_hi); dfree(cs->h.rk_lo); dfree(cs->h.rk_meta); dfree(cs->h.rk_tail);
+    dfree(cs->h.shard_tails); dfree(cs->key_out); dfree(cs->key_out_tail);
     dfree(cs->sc);
     dfree(cs->din);
     if (cs->sc_host) hipHostFree(cs->sc_host);
@@ -901,16 +947,7 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     tmp.free_top = (int32_t)(h.cap_pages - np);
     HIPOK(hipMemcpyAsync(cs->sc, &tmp, sizeof(Scalars), hipMemcpyHostToDevice, s));
     launch_dir_finish(h, cs->cur, cs->sc, cs->b, s);
-    // removal key
-    uint64_t rh, rl;
-    uint32_t rm;
-    encode_host(removal_key, removal_key_len, rh, rl, rm);
-    std::vector<uint8_t> rt(FDBCS_MAX_KEY + 16, 0);
-    if (removal_key_len > 17) memcpy(rt.data(), removal_key + 17, removal_key_len - 17);
-    HIPOK(hipMemcpyAsync(h.rk_hi, &rh, 8, hipMemcpyHostToDevice, s));
-    HIPOK(hipMemcpyAsync(h.rk_lo, &rl, 8, hipMemcpyHostToDevice, s));
-    HIPOK(hipMemcpyAsync(h.rk_meta, &rm, 4, hipMemcpyHostToDevice, s));
-    HIPOK(hipMemcpyAsync(h.rk_tail, rt.data(), rt.size(), hipMemcpyHostToDevice, s));
+    if ((r = set_removal_key(cs, removal_key, removal_key_len))) return r;
     cs->v0 = v0;
     cs->oldest = oldest;
     return sync_state(cs);
@@ -994,3 +1031,116 @@ const char* fdbcs_strerror(int status) {
 const char* fdbcs_version(void) { return "fdbcs gfx950 0.1.0"; }
 
 }  // extern "C"
+
+// ===================================================== exact sharded mode ====
+// SURVEY.md §8e protocol A: every GPU holds the history of one key range,
+// receives the whole batch, and the host exchanges between the phases.
+
+int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, const uint8_t* hi, uint32_t hi_len,
+                    int has_hi) {
+    if (!cs || lo_len > FDBCS_MAX_KEY || hi_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
+    ShardBounds sb{};
+    sb.has_lo = has_lo != 0;
+    sb.has_hi = has_hi != 0;
+    const uint8_t* src[2] = {lo, hi};
+    const uint32_t len[2] = {lo_len, hi_len};
+    Key* dst[2] = {&sb.lo, &sb.hi};
+    for (int k = 0; k < 2; k++) {
+        uint32_t m;
+        encode_host(src[k], len[k], dst[k]->hi, dst[k]->lo, m);
+        dst[k]->meta = m;
+        uint8_t* t = cs->h.shard_tails + (size_t)k * (FDBCS_MAX_KEY + 16);
+        dst[k]->tail = len[k] > 17 ? t : nullptr;
+        if (len[k] > 17) {
+            std::vector<uint8_t> buf(((len[k] - 17 + 7) & ~7u), 0);
+            memcpy(buf.data(), src[k] + 17, len[k] - 17);
+            HIPOK(hipMemcpy(t, buf.data(), buf.size(), hipMemcpyHostToDevice));
+        }
+    }
+    cs->h.shard = sb;
+    return FDBCS_OK;
+}
+
+int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, uint8_t* dev_hist) {
+    (void)now;
+    (void)new_oldest;
+    if (!cs || !db) return FDBCS_E_ARG;
+    const fdbcs_batch_view& v = *db;
+    int r;
+    if ((r = check_batch_shape(v))) return r;
+    if ((r = ensure_batch(cs, v.txn_count, v.read_count, v.write_count, v.key_bytes_len))) return r;
+    if ((r = ensure_history(cs, v.write_count, v.key_bytes_len))) return r;
+    cs->last_T = v.txn_count;
+    cs->last_R = v.read_count;
+    cs->last_W = v.write_count;
+    BatchBufs& b = cs->b;
+    hipStream_t s = cs->stream;
+    const bool scatter = cs->have_quantiles;
+    launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), s);
+    if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
+        cs->sorts++;
+        cs->have_quantiles = true;
+    }
+    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, cs->v0, s);
+    if (v.txn_count && dev_hist)
+        HIPOK(hipMemcpyAsync(dev_hist, b.hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipStreamSynchronize(s));
+    return FDBCS_OK;
+}
+
+int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, const uint8_t* dev_hist,
+                      uint8_t* dev_verdict, int64_t* info) {
+    if (!cs || !db || !info) return FDBCS_E_ARG;
+    const fdbcs_batch_view& v = *db;
+    BatchBufs& b = cs->b;
+    hipStream_t s = cs->stream;
+    int r;
+    if (v.txn_count && dev_hist)
+        HIPOK(hipMemcpyAsync(b.hist, dev_hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
+    launch_decide(v, b, cs->sc, dev_verdict ? dev_verdict : b.verdict, s);
+    const bool compact = new_oldest > cs->oldest;
+    launch_merge(v, b, cs->h, cs->cur, cs->sc, now, cs->v0, !compact, s);
+    cs->cur ^= 1;
+    if ((r = compact ? sync_state(cs) : sync_batch(cs))) return r;
+    const Scalars& h = *cs->sc_host;
+    info[0] = h.H;
+    info[1] = compact ? h.win_g0 : -1;
+    info[2] = h.last_ver;
+    info[3] = h.n_comb;
+    return h.last_err ? h.last_err : (compact ? h.err : 0);
+}
+
+int32_t fdbcs_shard_key_at(fdbcs* cs, int64_t index, uint8_t* buf, int32_t cap) {
+    if (!cs || index < 0 || index >= cs->known_H) return FDBCS_E_ARG;
+    launch_key_at(cs->h, cs->cur, cs->sc, index, cs->key_out, cs->key_out_tail, cs->stream);
+    uint64_t k3[3];
+    std::vector<uint8_t> t(FDBCS_MAX_KEY + 16);
+    HIPOK(hipMemcpyAsync(k3, cs->key_out, sizeof(k3), hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    const uint32_t len = (uint32_t)k3[2] & LEN_MASK;
+    if (len > 17) HIPOK(hipMemcpy(t.data(), cs->key_out_tail, len - 17, hipMemcpyDeviceToHost));
+    const std::vector<uint8_t> k = decode_key(k3[0], k3[1], (uint32_t)k3[2], t.data());
+    if (buf && cap > 0) memcpy(buf, k.data(), std::min<int64_t>(cap, len));
+    return (int32_t)len;
+}
+
+int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
+                        int64_t* info) {
+    if (!cs || !info || a < 0 || b < a) return FDBCS_E_ARG;
+    const WinExplicit w{a, b, keep_first, prev_version};
+    launch_compact(cs->b, cs->h, cs->cur, cs->sc, new_oldest, cs->stream, &w);
+    cs->cur ^= 1;
+    if (new_oldest > cs->oldest) cs->oldest = new_oldest;
+    int r;
+    if ((r = sync_batch(cs))) return r;
+    info[0] = cs->sc_host->H;
+    info[1] = cs->sc_host->last_ver;
+    return cs->sc_host->last_err;
+}
+
+int fdbcs_shard_finish(fdbcs* cs, int64_t carry_in, const uint8_t* removal_key, uint32_t removal_key_len,
+                       int set_removal_key_) {
+    if (!cs) return FDBCS_E_ARG;
+    cs->v0 = carry_in;
+    return set_removal_key_ ? set_removal_key(cs, removal_key, removal_key_len) : FDBCS_OK;
+}

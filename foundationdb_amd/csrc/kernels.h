@@ -119,6 +119,9 @@ struct HistBufs {
     uint64_t tail_cap;
     // removal key (device copy)
     uint64_t* rk_hi; uint64_t* rk_lo; uint32_t* rk_meta; uint8_t* rk_tail;  // rk_tail: 30008 bytes
+    // exact sharded mode: this engine's key range (unbounded by default)
+    ShardBounds shard;
+    uint8_t* shard_tails;  // device copies of the bounds' tails [2][FDBCS_MAX_KEY + 16]
     // host-mapped copy of the scalars, written by the kernel that ends a batch
     // (the host reads it after a stream sync instead of issuing a copy)
     Scalars* mirror;
@@ -133,10 +136,13 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
                        int64_t* tmp, hipStream_t s);
 
 // ---- batch stages (kernels_batch.hip) ----
-void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s);
+// scatter: the sort splitters exist (an earlier batch) -- the ingest puts
+// the sort records into their buckets itself (launch_sort_ranges(scattered))
+void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
+                   hipStream_t s);
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        hipStream_t s);
+                        bool scattered, hipStream_t s);
 int64_t sort_staging_records(int R, int W);
 // history read check + intra-batch overlap edges, one launch
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
@@ -149,7 +155,15 @@ void configure_batch_kernels();
 int plan_blocks(int cap_dir);
 void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t now,
                   int64_t v0, bool end_of_batch, hipStream_t s);
-void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s);
+// sharded mode: this shard's part of the global compaction window (local indices)
+struct WinExplicit {
+    int64_t a, b;
+    int keep_first;
+    int64_t prev;
+};
+void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s,
+                    const WinExplicit* win = nullptr);
+void launch_key_at(HistBufs& h, int cur, Scalars* sc, int64_t g, uint64_t* out, uint8_t* out_tail, hipStream_t s);
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s);
 void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s);
 void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s);

@@ -74,45 +74,6 @@ struct IngestArgs {
     Scalars* sc;
 };
 
-__global__ __launch_bounds__(256) void k_ingest(IngestArgs A) {
-    if ((int)blockIdx.x < A.prep_blocks) {
-        const int t = blockIdx.x * blockDim.x + threadIdx.x;
-        if (t == 0) A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
-        if (t >= A.T) return;
-        const int r0 = A.ro[t], r1 = A.ro[t + 1];
-        // tooOld uses the previous batch's oldestVersion and needs >= 1 read (SkipList.cpp:985)
-        const int64_t sn = A.snap[t];
-        const bool too = sn < A.oldest && r1 > r0;
-        A.too_old[t] = too ? 1 : 0;
-        A.hist[t] = 0;
-        for (int r = r0; r < r1; r++) {
-            A.read_txn[r] = t;
-            A.read_snap[r] = too ? INT64_MAX : sn;  // k_read_check skips too-old transactions
-        }
-        for (int w = A.wo[t], w1 = A.wo[t + 1]; w < w1; w++) A.write_txn[w] = t;
-        return;
-    }
-    const int64_t i = (int64_t)(blockIdx.x - A.prep_blocks) * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)A.R + A.W) return;
-    const Key b = encode_key(A.bytes + A.koff[2 * i], A.klen[2 * i], A.btail, A.btail_cap, A.sc);
-    const Key e = encode_key(A.bytes + A.koff[2 * i + 1], A.klen[2 * i + 1], A.btail, A.btail_cap, A.sc);
-    A.keys.put(2 * i, b);
-    A.keys.put(2 * i + 1, e);
-    if (kcmp(b, e) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
-}
-
-void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, hipStream_t s) {
-    IngestArgs A;
-    A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
-    A.prep_blocks = std::max(1, cdiv(v.txn_count, 256));
-    A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
-    A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
-    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap; A.write_txn = b.write_txn;
-    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc;
-    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
-    hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(256), 0, s, A);
-}
-
 // ---------------------------------------------------------- read check ----
 // Per read range: conflict iff max(version over boundaries in
 // [b, e), plus valueBefore(b) if b is not a boundary) > snapshot -- the
@@ -136,7 +97,8 @@ struct ReadCheckArgs {
     Pool pool;
     Dir dir;
     const Scalars* sc;
-    int64_t v0;
+    int64_t v0;            // version before the first boundary (sharded: the shard's carry-in)
+    ShardBounds shard;     // reads are clipped to it (sharded mode)
 };
 
 // read r, checked by the RC_G lanes of its group (g.lane)
@@ -146,10 +108,15 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
     const Dir& dir = A.dir;
     const int t = A.read_txn[r];
     const int64_t s = A.read_snap[r];
-    const Key b = A.keys.get(2 * (int64_t)r), e = A.keys.get(2 * (int64_t)r + 1);
+    Key b = A.keys.get(2 * (int64_t)r), e = A.keys.get(2 * (int64_t)r + 1);
     const int D = A.sc->D;
     const int64_t v0 = A.v0;
     if (s == INT64_MAX) return;
+    if (A.shard.has_lo | A.shard.has_hi) {  // the part of [b, e) in this shard (protocol A step 2)
+        if (A.shard.below(b)) b = A.shard.lo;
+        if (A.shard.at_or_above(e)) e = A.shard.hi;
+        if (kcmp(b, e) >= 0) return;
+    }
     DirHit hb, he;
     grp_dir_find2(g, dir, D, b, e, hb, he);
     const int pb = hb.x, pe = he.x, cb = hb.cnt;
@@ -402,34 +369,106 @@ __global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys) 
         put_quantile(J, job, q, L.get((int)((int64_t)q * ns / SS_Q)), keys.tail);
 }
 
-__global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) {
-    __shared__ uint64_t s_hi[SS_MAXB], s_lo[SS_MAXB], s_mi[SS_MAXB];
-    const int job = blockIdx.x < J.blocks0 ? 0 : 1;
-    const int i = (job ? blockIdx.x - J.blocks0 : blockIdx.x) * blockDim.x + threadIdx.x;
-    const int n = J.n[job], nb = J.nb[job];
-    const uint8_t* const* tails = keys.tail;
-    const LdsRecs L{s_hi, s_lo, s_mi};
-    const int step = SS_Q / nb;
-    for (int s = threadIdx.x; s < nb - 1; s += blockDim.x) L.put(s, J.quant[job * SS_Q + (s + 1) * step]);
-    __syncthreads();
-    if (i >= n) return;
-    const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
-    // bucket = number of splitters <= x (splitters nondecreasing)
+// Splitter s of a job is quantile (s + 1) * SS_Q / nb.  Scatter kernels keep
+// the splitters' first key words in LDS and fetch the whole quantile only on
+// a tie of those words.
+__device__ inline void splitter_fill(const SortJobs& J, int job, uint64_t* sp) {
+    const int nb = J.nb[job], step = SS_Q / max(nb, 1);
+    for (int k = threadIdx.x; k < nb - 1; k += blockDim.x) sp[k] = J.quant[job * SS_Q + (k + 1) * step].hi;
+}
+
+// bucket of record x = number of splitters <= x (splitters nondecreasing)
+__device__ inline int bucket_of(const SortJobs& J, int job, const uint64_t* sp, const SRec& x,
+                                const uint8_t* const* tails) {
+    const int nb = J.nb[job], step = SS_Q / nb;
     int lo = 0, len = nb - 1;
     while (len > 0) {
-        const int half = len >> 1;
-        const int s = lo + half;
-        if (!rec_lt_quant(x, L.get(s), J.qtail + (int64_t)(job * SS_Q + (s + 1) * step) * SS_QT, tails)) {
+        const int half = len >> 1, k = lo + half;
+        const uint64_t h = sp[k];
+        bool le;
+        if (h != x.hi) {
+            le = h < x.hi;
+        } else {
+            const int q = job * SS_Q + (k + 1) * step;
+            le = !rec_lt_quant(x, J.quant[q], J.qtail + (int64_t)q * SS_QT, tails);
+        }
+        if (le) {
             lo += half + 1;
             len -= half + 1;
         } else {
             len = half;
         }
     }
-    const int b = lo;
+    return lo;
+}
+
+// record i of a job into its bucket's staging row
+__device__ inline void scatter_rec(const SortJobs& J, int job, int i, const SRec& x, const uint8_t* const* tails,
+                                   const uint64_t* sp) {
+    const int b = bucket_of(J, job, sp, x, tails);
     const int slot = atomicAdd(&J.cnt[job * SS_MAXB + b], 1);
     J.bkt[(job ? J.n[0] : 0) + i] = b;
     if (slot < SS_ROW) J.tmp[((int64_t)job * SS_MAXB + b) * SS_ROW + slot] = x;
+}
+
+__global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) {
+    __shared__ uint64_t sp[SS_MAXB];
+    const int job = blockIdx.x < J.blocks0 ? 0 : 1;
+    const int i = (job ? blockIdx.x - J.blocks0 : blockIdx.x) * blockDim.x + threadIdx.x;
+    splitter_fill(J, job, sp);
+    __syncthreads();
+    if (i >= J.n[job]) return;
+    scatter_rec(J, job, i, load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]), keys.tail, sp);
+}
+
+// Ingest: one launch, two kinds of blocks.  Transaction blocks: tooOld
+// (SkipList.cpp:985: the previous batch's oldestVersion, >= 1 read), the
+// per-range transaction maps and snapshots.  Range blocks: encode both keys
+// of a range (the begin < end precondition), and -- in steady state, when
+// splitters from an earlier batch exist (SCATTER) -- scatter the range's sort
+// records straight into their buckets (reads: the begin; writes: both ends).
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_ingest(IngestArgs A, SortJobs J) {
+    if ((int)blockIdx.x < A.prep_blocks) {
+        const int t = blockIdx.x * blockDim.x + threadIdx.x;
+        if (t == 0) A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+        if (t >= A.T) return;
+        const int r0 = A.ro[t], r1 = A.ro[t + 1];
+        const int64_t sn = A.snap[t];
+        const bool too = sn < A.oldest && r1 > r0;
+        A.too_old[t] = too ? 1 : 0;
+        A.hist[t] = 0;
+        for (int r = r0; r < r1; r++) {
+            A.read_txn[r] = t;
+            A.read_snap[r] = too ? INT64_MAX : sn;  // the read check skips too-old transactions
+        }
+        for (int w = A.wo[t], w1 = A.wo[t + 1]; w < w1; w++) A.write_txn[w] = t;
+        return;
+    }
+    const int64_t i0 = (int64_t)(blockIdx.x - A.prep_blocks) * blockDim.x;
+    const int64_t i = i0 + threadIdx.x;
+    [[maybe_unused]] __shared__ uint64_t sp[2][SCATTER ? SS_MAXB : 1];
+    if constexpr (SCATTER) {
+        if (i0 < A.R) splitter_fill(J, 0, sp[0]);
+        if (i0 + blockDim.x > A.R) splitter_fill(J, 1, sp[1]);
+        __syncthreads();
+    }
+    if (i >= (int64_t)A.R + A.W) return;
+    const Key b = encode_key(A.bytes + A.koff[2 * i], A.klen[2 * i], A.btail, A.btail_cap, A.sc);
+    const Key e = encode_key(A.bytes + A.koff[2 * i + 1], A.klen[2 * i + 1], A.btail, A.btail_cap, A.sc);
+    A.keys.put(2 * i, b);
+    A.keys.put(2 * i + 1, e);
+    if (kcmp(b, e) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
+    if constexpr (SCATTER) {
+        const uint8_t* const* tails = A.keys.tail;
+        if (i < A.R) {
+            scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
+        } else {
+            const int w = (int)(i - A.R);
+            scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
+            scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(2 * i + 1), 0}, tails, sp[1]);
+        }
+    }
 }
 
 // quantile q of the sorted output sits at position floor(q * n / SS_Q)
@@ -567,8 +606,7 @@ static int ss_buckets(int n) {
 // Staging records the sort needs (engine sizes b.ss_tmp).
 int64_t sort_staging_records(int, int) { return 2 * (int64_t)SS_MAXB * SS_ROW; }
 
-bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        hipStream_t s) {
+static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity) {
     const int R = v.read_count, W = v.write_count;
     SortJobs J;
     J.n[0] = R;
@@ -589,11 +627,37 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     J.sc = sc;
     for (int j = 0; j < 2; j++) J.nb[j] = ss_buckets(J.n[j]);
     J.blocks0 = cdiv(J.n[0], 256);
+    return J;
+}
+
+void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
+                   hipStream_t s) {
+    IngestArgs A;
+    A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
+    A.prep_blocks = std::max(1, cdiv(v.txn_count, 256));
+    A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
+    A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
+    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
+    A.write_txn = b.write_txn;
+    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc;
+    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
+    const SortJobs J = make_sort_jobs(v, b, sc, parity);
+    if (scatter)
+        hipLaunchKernelGGL(k_ingest<true>, dim3(blocks), dim3(256), 0, s, A, J);
+    else
+        hipLaunchKernelGGL(k_ingest<false>, dim3(blocks), dim3(256), 0, s, A, J);
+}
+
+bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
+                        bool scattered, hipStream_t s) {
+    const SortJobs J = make_sort_jobs(v, b, sc, parity);
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
     if (J.n[0] + J.n[1] == 0) return false;
-    if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys);
-    hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
+    if (!scattered) {  // (otherwise the ingest already put every record into its bucket)
+        if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys);
+        hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
+    }
     hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
     return true;  // the counters of the other parity are zero now
 }
@@ -813,7 +877,7 @@ __global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int 
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
-    ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0};
+    ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
                  b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};

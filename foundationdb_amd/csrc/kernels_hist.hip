@@ -99,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 // inside [pb, pe] are wholly erased; they are marked in a difference array
 // (+1 at pb+1, -1 at pe) and resolved by the scan.
 __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, WriteHits wh, int64_t wbase,
-                                                     Scalars* sc, int32_t* __restrict__ pb_o,
+                                                     ShardBounds shard, Scalars* sc, int32_t* __restrict__ pb_o,
                                                      int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
                                                      int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
                                                      int64_t* __restrict__ vb_o, PageAcc acc, KeyArrays rb,
@@ -116,25 +116,31 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     const int p_e = wh.pe[we], i_e = wh.ie[we];
     const bool found = wh.feq[we];
     const int64_t vb = wh.vb[we];
+    // sharded mode (protocol A step 5): a range acts on this shard iff b < hi
+    // and e >= lo; its begin node only if b >= lo, its end node only if e < hi
+    // (the positions of keys outside the shard clamp to the shard's ends)
+    if (shard.at_or_above(b) || shard.below(e)) return;
+    const int has_b = shard.below(b) ? 0 : 1;
+    const bool e_in = !shard.at_or_above(e);
     rb.put(j, b);  // compact copies for the page merge
     re.put(j, e);
-    const int need = (!found && !touch) ? 1 : 0;
+    const int need = (e_in && !found && !touch) ? 1 : 0;
     pb_o[j] = p_b;
     ib_o[j] = i_b;
     pe_o[j] = p_e;
     ie_o[j] = i_e;
-    need_o[j] = (uint8_t)need;
+    need_o[j] = (uint8_t)(need | has_b << 1);
     vb_o[j] = vb;
     atomicMin(&acc.fmin[p_b], i_b);
     if (p_b != p_e) atomicMin(&acc.fmin[p_e], 0);
     if (p_b == p_e) {
         atomicAdd(&acc.er[p_b], max(0, i_e - i_b));
-        atomicAdd(&acc.nn[p_b], 1 + need);
+        atomicAdd(&acc.nn[p_b], has_b + need);
         atomicMin(&acc.jlo[p_b], j);
         atomicMax(&acc.jhi[p_b], j);
     } else {
         atomicAdd(&acc.er[p_b], c_b - i_b);
-        atomicAdd(&acc.nn[p_b], 1);
+        atomicAdd(&acc.nn[p_b], has_b);
         atomicMin(&acc.jlo[p_b], j);
         atomicMax(&acc.jhi[p_b], j);
         atomicAdd(&acc.er[p_e], i_e);
@@ -518,14 +524,17 @@ __device__ inline void part_first(WaveMerge& S, const Dir& D, const MergeArgs& A
 // Plan of combined range j as one lane holds it.
 struct RangePlan {
     int pb, ib, pe, ie;
-    bool need;
+    bool need;   // a node at e
+    bool has_b;  // a node at b (not so for a range clipped at the shard's start)
     int64_t vb;  // (the keys are loaded where they are written: fewer live registers)
 };
 
 __device__ inline RangePlan load_plan(const MergeArgs& A, int j) {
     RangePlan r;
     r.pb = A.pb[j]; r.ib = A.ib[j]; r.pe = A.pe[j]; r.ie = A.ie[j];
-    r.need = A.need_e[j];
+    const uint8_t fl = A.need_e[j];
+    r.need = fl & 1;
+    r.has_b = (fl >> 1) & 1;
     r.vb = A.vb[j];
     return r;
 }
@@ -602,7 +611,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
                 atomicAdd(&S.er[s0], 1);
                 atomicAdd(&S.er[e0], -1);
             }
-            if (r.pb == p) atomicAdd(&S.ins[r.ib], 1);
+            if (r.pb == p && r.has_b) atomicAdd(&S.ins[r.ib], 1);
             if (r.pe == p && r.need) atomicAdd(&S.ins[r.ie], 1);
         }
     }
@@ -674,7 +683,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         const bool v = j <= jhi;
         RangePlan r{};
         if (v) r = j0 == jlo ? r0 : load_plan(A, j);
-        const bool eb = v && r.pb == p;
+        const bool eb = v && r.pb == p && r.has_b;
         const bool ee = v && r.pe == p && r.need;
         const int c = (int)eb + (int)ee;
         const int inc = wave_incl_scan(c);
@@ -834,7 +843,11 @@ struct RemovalKey {
 
 // The compaction window over the directory `dir` of D entries, by one
 // wavefront (run by k_bmax_commit after the merge, before the commit).
-__device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars* sc, const RemovalKey& rkey) {
+// In the sharded mode (update_rk false) only g0 -- this shard's first
+// boundary >= the global removalKey -- matters: the host assembles the global
+// window from every shard's (H, g0) and sets removalKey itself.
+__device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars* sc, const RemovalKey& rkey,
+                               bool update_rk) {
     uint64_t* rk_hi = rkey.hi;
     uint64_t* rk_lo = rkey.lo;
     uint32_t* rk_meta = rkey.meta;
@@ -866,17 +879,19 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
     }
     if (lane == 0) {
         sc->win_g0 = g0;
+        sc->win_r0 = g0 + 1;  // the first scanned node is never removed
+        sc->win_prev = 0;     // (not needed: g0 + 1 > 0)
         sc->win_g1 = g1;
         sc->win_pA = pA;
         sc->win_pB = pB;
         sc->win_np = pB - pA + 1 > 0 ? pB - pA + 1 : 0;
-        if (!sc->err) {
+        if (!sc->err && update_rk) {
             rk_hi[0] = has_key ? nk.hi : 0;
             rk_lo[0] = has_key ? nk.lo : 0;
             rk_meta[0] = has_key ? nk.meta : 0;
         }
     }
-    if (!sc->err && has_key && key_len(nk.meta) > 17) {
+    if (!sc->err && update_rk && has_key && key_len(nk.meta) > 17) {
         const uint32_t words = (key_len(nk.meta) - 17 + 7) / 8;
         const uint64_t* s = reinterpret_cast<const uint64_t*>(nk.tail);
         uint64_t* d = reinterpret_cast<uint64_t*>(rk_tail);
@@ -915,10 +930,10 @@ __device__ inline void publish_scalars(const Scalars* sc, Scalars* mirror) {
 
 __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const int32_t* freed_list,
                                                      int32_t* free_stack, int end_of_batch, Pool pool,
-                                                     RemovalKey rkey, Scalars* mirror) {
+                                                     RemovalKey rkey, Scalars* mirror, int sharded) {
     const int Dn = sc->D_next;
     // a compaction follows: its window over the new directory (one wavefront)
-    if (!end_of_batch && blockIdx.x == 0 && threadIdx.x < 64) win_setup_wave(pool, d, Dn, sc, rkey);
+    if (!end_of_batch && blockIdx.x == 0 && threadIdx.x < 64) win_setup_wave(pool, d, Dn, sc, rkey, !sharded);
     if (freed_list) {
         const int base = sc->free_top - sc->extra_total;
         const int nf = sc->free_next - base;
@@ -939,6 +954,7 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         sc->D = Dn;
         sc->free_top = sc->free_next;
         sc->H = d.start[Dn];
+        sc->last_ver = d.cnt[Dn - 1] > 0 ? pool.ver[(int64_t)d.page[Dn - 1] * PAGE + d.cnt[Dn - 1] - 1] : INT64_MIN;
         if (end_of_batch) {  // the next batch's encoder allocates from these
             sc->last_err = sc->err;
             sc->err = 0;
@@ -956,7 +972,8 @@ static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t 
     const int groups = cdiv(h.cap_dir, 64);
     const RemovalKey rk{h.rk_hi, h.rk_lo, h.rk_meta, h.rk_tail};
     hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
-                       h.free_stack, (int)end_of_batch, h.pool, rk, h.mirror);
+                       h.free_stack, (int)end_of_batch, h.pool, rk, h.mirror,
+                       (int)(h.shard.has_lo | h.shard.has_hi));
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
@@ -978,7 +995,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
         hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, b.wh,
-                           2 * (int64_t)v.read_count, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
+                           2 * (int64_t)v.read_count, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
     hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
@@ -1012,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
                                                   uint8_t* __restrict__ keep_o, int32_t* __restrict__ cnt_o,
                                                   int64_t* __restrict__ part_max) {
     __shared__ int32_t tmp[256 / 64 + 1];
-    const int64_t g0 = sc->win_g0, g1 = sc->win_g1;
+    const int64_t r0 = sc->win_r0, g1 = sc->win_g1, prev0 = sc->win_prev;
     const int pA = sc->win_pA, np = sc->win_np;
     for (int w = blockIdx.x; w < np; w += gridDim.x) {
         // the repack makes at most ceil(np * PAGE / FILL) <= 2 * np pages
@@ -1025,10 +1042,11 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
         if (i < c) {
             keep = 1;
             const int64_t g = st + i;
-            if (g > g0 && g < g1) {
+            if (g >= r0 && g < g1) {
                 const bool above = pool.ver[(int64_t)pg * PAGE + i] >= oldest;
-                const int64_t pv = i > 0 ? pool.ver[(int64_t)pg * PAGE + i - 1]
-                                         : pool.ver[(int64_t)dir.page[q - 1] * PAGE + dir.cnt[q - 1] - 1];
+                const int64_t pv = i > 0    ? pool.ver[(int64_t)pg * PAGE + i - 1]
+                                   : q > 0 ? pool.ver[(int64_t)dir.page[q - 1] * PAGE + dir.cnt[q - 1] - 1]
+                                           : prev0;  // (sharded: the previous shard's last node)
                 keep = above || pv >= oldest;
             }
             keep_o[(int64_t)w * PAGE + i] = (uint8_t)keep;
@@ -1095,7 +1113,7 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
 // The directory after the compaction, its page-group maxima and search index
 // (what k_bmax_commit does after a merge), and the commit by the last block.
 __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc, DescArrays desc,
-                                                  int32_t* free_stack, Scalars* mirror) {
+                                                  int32_t* free_stack, Scalars* mirror, const int64_t* pool_ver) {
     __shared__ int last;
     const int np = sc->win_np;
     const int S = sc->win_surv;
@@ -1146,6 +1164,22 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         sc->free_top = free_next;
         sc->free_next = free_next;
         sc->H = H;
+        {  // the last boundary: from the repacked pages when the window reached the end
+            int lp = -1, lc = 0;
+            if (np > 0 && pA + np == D) {
+                if (k > 0) {
+                    lp = desc.page[k - 1];
+                    lc = desc.cnt[k - 1];
+                } else if (pA > 0) {
+                    lp = src.page[pA - 1];
+                    lc = src.cnt[pA - 1];
+                }
+            } else {
+                lp = src.page[D - 1];
+                lc = src.cnt[D - 1];
+            }
+            sc->last_ver = lp >= 0 && lc > 0 ? pool_ver[(int64_t)lp * PAGE + lc - 1] : INT64_MIN;
+        }
         sc->win_newpages = k;
         sc->last_err = sc->err;  // end of batch: the next batch's encoder allocates from these
         sc->err = 0;
@@ -1155,19 +1189,63 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
     if (threadIdx.x < 64) publish_scalars(sc, mirror);
 }
 
+// Sharded mode: the host hands this shard its part [a, b) of the global
+// compaction window (local indices), whether a is the window's first node
+// (never removed), and the version of the node before a when a == 0.
+__global__ __launch_bounds__(64) void k_win_explicit(Dir dir, Scalars* sc, int64_t a, int64_t b, int keep_first,
+                                                     int64_t prev) {
+    const int D = sc->D;
+    const int pA = a < b ? wave_start_search(dir.start, D, a) : 1;
+    const int pB = a < b ? wave_start_search(dir.start, D, b - 1) : 0;
+    if (threadIdx.x == 0) {
+        sc->win_g0 = a;
+        sc->win_r0 = keep_first ? a + 1 : a;
+        sc->win_g1 = b;
+        sc->win_prev = prev;
+        sc->win_pA = pA;
+        sc->win_pB = pB;
+        sc->win_np = pB - pA + 1 > 0 ? pB - pA + 1 : 0;
+    }
+}
+
+// the key at local index g (0 <= g < H) into out (hi, lo, meta) + out_tail
+__global__ __launch_bounds__(64) void k_key_at(Pool pool, Dir dir, const Scalars* sc, int64_t g, uint64_t* out,
+                                               uint8_t* out_tail) {
+    const int D = sc->D;
+    const int q = wave_start_search(dir.start, D, g);
+    const Key k = pool_key(pool, (int64_t)dir.page[q] * PAGE + (g - dir.start[q]));
+    if (threadIdx.x == 0) {
+        out[0] = k.hi;
+        out[1] = k.lo;
+        out[2] = k.meta;
+    }
+    const uint32_t L = key_len(k.meta);
+    if (L > 17)
+        for (uint32_t w = threadIdx.x; w < (L - 17 + 7) / 8; w += 64)
+            reinterpret_cast<uint64_t*>(out_tail)[w] = reinterpret_cast<const uint64_t*>(k.tail)[w];
+}
+
+void launch_key_at(HistBufs& h, int cur, Scalars* sc, int64_t g, uint64_t* out, uint8_t* out_tail, hipStream_t s) {
+    hipLaunchKernelGGL(k_key_at, dim3(1), dim3(64), 0, s, h.pool, h.dir[cur], (const Scalars*)sc, g, out, out_tail);
+}
+
 static constexpr int WIN_DIR_BLOCKS = 128;
 
-void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s) {
+void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t oldest, hipStream_t s,
+                    const WinExplicit* win) {
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
     const int win_cap = b.win_cap_pages;
+    if (win)
+        hipLaunchKernelGGL(k_win_explicit, dim3(1), dim3(64), 0, s, src, sc, win->a, win->b, win->keep_first,
+                           win->prev);
     hipLaunchKernelGGL(k_win_keep, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc, oldest,
                        b.win_keep, b.win_cnt, b.desc_max);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
                        b.win_keep, b.win_cnt, h.free_stack, da);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
-                       sc, da, h.free_stack, h.mirror);
+                       sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
 }
 
 // ------------------------------------------------------------------ reset ----

@@ -182,6 +182,49 @@ int32_t fdbcs_key_owner(int32_t nres, const uint8_t* bound_bytes, const uint64_t
 int  fdbcs_scatter_verdicts(fdbcs* cs, const uint8_t* dev_sub, const int32_t* dev_index, int32_t n,
                             uint8_t* dev_global);
 
+/* ---- Exact sharded mode: one resolver over G GPUs (SURVEY.md §8e protocol A) ---- */
+
+/* The north star's node layout: GPU g holds the history of the keys in
+ * [lo, hi) (has_lo / has_hi == 0: unbounded), every GPU receives the whole
+ * batch, and the host exchanges between the phases below.  The result equals
+ * one ConflictSet's (a single Resolver, Resolver.actor.cpp:140-153) exactly.
+ * A shard's header version (fdbcs_header_version) is its carry-in: the
+ * version of the last boundary below lo anywhere, or the global v0. */
+int  fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo,
+                     const uint8_t* hi, uint32_t hi_len, int has_hi);
+
+/* Phase 1 (steps 1-2): ingest, endpoint sort, intra-batch overlaps, and the
+ * history check of every read clipped to the shard.  dev_hist receives T
+ * bytes (1: the transaction conflicts with this shard's history); the host
+ * MAX-reduces them over the shards (RCCL all-reduce). */
+int  fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now,
+                       int64_t new_oldest, uint8_t* dev_hist);
+
+/* Phase 2 (steps 4-5): the decision from the reduced flags (identical on
+ * every shard, verdicts to dev_verdict), the combine, and the shard's part of
+ * the merge.  info[0] = boundaries H, [1] = index of the shard's first
+ * boundary >= removalKey when a compaction follows (else -1), [2] = version
+ * of its last boundary (INT64_MIN: none), [3] = combined write ranges.
+ * When new_oldest > oldestVersion, fdbcs_shard_compact must follow. */
+int  fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now, int64_t new_oldest,
+                       const uint8_t* dev_hist, uint8_t* dev_verdict, int64_t* info);
+
+/* The key of the boundary at local index (after phase 2): the new
+ * removalKey, read on the shard that holds the global window's end. */
+int32_t fdbcs_shard_key_at(fdbcs* cs, int64_t index, uint8_t* buf, int32_t cap);
+
+/* Phase 3 (step 6): removeBefore over this shard's part [a, b) of the global
+ * window (local indices).  keep_first: a is the window's first node (never
+ * removed); prev_version: the version of the node before local index 0 (the
+ * previous non-empty shard's last).  info[0] = H, info[1] = last version. */
+int  fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version,
+                         int64_t new_oldest, int64_t* info);
+
+/* Step 7: the shard's carry-in for the next batch and, when set_removal_key,
+ * the global removalKey. */
+int  fdbcs_shard_finish(fdbcs* cs, int64_t carry_in, const uint8_t* removal_key, uint32_t removal_key_len,
+                        int set_removal_key);
+
 /* ---- Introspection (tests, bench, checkpoint) --------------------------------- */
 
 /* Number of boundaries in the history (skip-list nodes other than the header). */
