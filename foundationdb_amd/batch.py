@@ -99,3 +99,39 @@ def unpack_history(n, versions, key_len, key_off, key_bytes):
     """(keys list, versions list) from dump arrays."""
     keys = [key_bytes[int(key_off[i]):int(key_off[i]) + int(key_len[i])].tobytes() for i in range(n)]
     return keys, [int(v) for v in versions[:n]]
+
+
+class DeviceBatch:
+    """A batch staged in device memory: the tensors plus the ``fdbcs_batch_view``
+    over them (the input of ``fdbcs_detect_device`` and the sharded entry points).
+
+    ``src`` is a ``PackedBatch`` or a host ``BatchView``; ``device`` a torch device.
+    """
+
+    def __init__(self, src, device):
+        import torch
+
+        v = src.view() if isinstance(src, PackedBatch) else src
+        T, R, W = v.txn_count, v.read_count, v.write_count
+        slots = 2 * (R + W)
+
+        def arr(ptr, ctype, n, dtype):
+            if n == 0:
+                return torch.zeros(1, dtype=torch.uint8, device=device)
+            a = np.ctypeslib.as_array((ctype * n).from_address(ptr)).astype(dtype, copy=True)
+            return torch.from_numpy(a).to(device)
+
+        self.tensors = [arr(v.snapshot, C.c_int64, T, np.int64), arr(v.read_off, C.c_int32, T + 1, np.int32),
+                        arr(v.write_off, C.c_int32, T + 1, np.int32), arr(v.key_off, C.c_uint64, slots, np.int64),
+                        arr(v.key_len, C.c_uint32, slots, np.int32),
+                        arr(v.key_bytes, C.c_uint8, int(v.key_bytes_len), np.uint8)]
+        dv = BatchView()
+        dv.txn_count, dv.read_count, dv.write_count = T, R, W
+        t = self.tensors
+        dv.snapshot, dv.read_off, dv.write_off = t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr()
+        dv.key_off, dv.key_len, dv.key_bytes = t[3].data_ptr(), t[4].data_ptr(), t[5].data_ptr()
+        dv.key_bytes_len = int(v.key_bytes_len)
+        self.view = dv
+        self.T = T
+        if self.tensors[0].is_cuda:
+            torch.cuda.synchronize(self.tensors[0].device)  # the engines read it on their own streams

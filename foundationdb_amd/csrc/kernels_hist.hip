@@ -192,7 +192,9 @@ __device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, 
         it.affected = false;
         it.nout = cnt;
     }
-    it.parts = !it.affected ? 1 : (it.nout == 0 ? 0 : (it.nout <= PAGE ? 1 : cdiv(it.nout, FILL)));
+    // an emptied entry 0 stays (as an empty page): the directory never has
+    // zero entries (a shard's whole history can be erased in sharded mode)
+    it.parts = !it.affected ? 1 : (it.nout == 0 ? (x == 0 ? 1 : 0) : (it.nout <= PAGE ? 1 : cdiv(it.nout, FILL)));
     return it;
 }
 
@@ -654,6 +656,9 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     wave_lds_sync();
     const int nout = kept + nn;
     const int per = cdiv(nout, parts);
+    if (nout == 0 && lane == 0) {  // entry 0 emptied: an empty page whose first key sorts first
+        S.f_hi[0] = 0; S.f_lo[0] = 0; S.f_meta[0] = 0; S.f_tail[0] = nullptr; S.f_dp[0] = pg;
+    }
     const Dir& D = A.dst;
     auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
     int64_t vmax = INT64_MIN;  // parts == 1: the page maximum by a wave reduction
@@ -1120,9 +1125,12 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
     const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int per = k > 0 ? cdiv(S, k) : 1;
     const int D = sc->D, pA = sc->win_pA;
-    const int Dn = D - np + k;
+    // sharded mode can remove a shard's whole history: its first page then
+    // stays as one empty entry (the directory never has zero entries)
+    const int keep = (S == 0 && np == D && np > 0) ? 1 : 0;
+    const int Dn = D - np + k + keep;
     const int64_t removed = np ? (src.start[pA + np] - src.start[pA]) - S : 0;
-    const int free_next = sc->free_top - k + np;
+    const int free_next = sc->free_top - k + np - keep;
     const int64_t H = src.start[D] - removed;
     const int top = sc->free_top;
     if (blockIdx.x == 0 && threadIdx.x == 0) dst.start[Dn] = H;
@@ -1132,7 +1140,11 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         const int y = y0 + threadIdx.x;
         int64_t mv = INT64_MIN;
         if (y < Dn) {
-            if (np == 0 || y < pA) {
+            if (keep) {  // (Dn == 1)
+                dst.page[0] = src.page[0]; dst.cnt[0] = 0; dst.maxv[0] = INT64_MIN;
+                dst.fhi[0] = 0; dst.flo[0] = 0; dst.fmeta[0] = 0; dst.ftail[0] = nullptr;
+                dst.start[0] = 0;
+            } else if (np == 0 || y < pA) {
                 dir_copy(src, y, dst, y);
                 dst.start[y] = src.start[y];
             } else if (y < pA + k) {
@@ -1145,7 +1157,7 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
             mv = dst.maxv[y];
             if ((y & (SIDX_B - 1)) == 0) sidx_build(dst, y / SIDX_B);
         }
-        if (y < np) free_stack[top - k + y] = src.page[pA + y];
+        if (y < np - keep) free_stack[top - k + y] = src.page[pA + keep + y];
         mv = wave_reduce_max(mv);  // one wavefront = one 64-entry group
         if ((threadIdx.x & 63) == 0 && (y & ~63) < Dn) dst.bmax[y >> 6] = mv;
     }

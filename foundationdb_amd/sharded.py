@@ -102,6 +102,8 @@ def carry_ins(v0, hl):
     return out
 
 
+
+
 class Shard:
     """One engine holding the keys [lo, hi) (None: unbounded)."""
 
@@ -139,121 +141,198 @@ class Shard:
         check(self._lib.fdbcs_shard_finish(self.cs.handle, carry_in, rk, len(rk), int(removal_key is not None)),
               "shard_finish")
 
+    def clear(self, v):
+        self.cs.clear(v)
+
+    def history(self):
+        return self.cs.history()
+
+    def removal_key(self):
+        return self.cs.removal_key()
+
+    def close(self):
+        self.cs.close()
+
 
 def _shard_ranges(bounds):
     edges = [None] + list(bounds) + [None]
     return [(edges[g], edges[g + 1]) for g in range(len(bounds) + 1)]
 
 
-class ShardedConflictSet:
-    """All G shards in this process: the exchange is a few device reductions."""
+def _device(torch, d):
+    return torch.device("cpu") if d is None or d < 0 else torch.device("cuda", d)
 
-    def __init__(self, bounds, devices=None, v0=0, max_history=0):
+
+def _sync(torch, dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+class ShardedConflictSet:
+    """All G shards in this process (on one or several devices): the exchange
+    is a device reduction.  ``shard_factory`` builds a shard (tests pass a
+    CPU model of the same interface)."""
+
+    def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard):
         import torch
 
         self.torch = torch
         ranges = _shard_ranges(bounds)
-        devices = devices or [max(0, torch.cuda.current_device())] * len(ranges)
-        self.devices = devices
-        self.shards = [Shard(lo, hi, device=d, v0=v0, max_history=max_history) for (lo, hi), d in zip(ranges, devices)]
+        if devices is None:
+            d = torch.cuda.current_device() if torch.cuda.is_available() else -1
+            devices = [d] * len(ranges)
+        assert len(devices) == len(ranges)
+        self.devices = [_device(torch, d) for d in devices]
+        self.shards = [shard_factory(lo, hi, device=d, v0=v0, max_history=max_history)
+                       for (lo, hi), d in zip(ranges, devices)]
         self.v0 = v0
         self.oldest = 0
 
     def clear(self, v):
+        """clearConflictSet (SkipList.cpp:957-959): every shard empty, carry-ins v."""
         for s in self.shards:
-            s.cs.clear(v)
+            s.clear(v)
         self.v0 = v
 
-    def detect_device(self, dev_views, now, new_oldest, verdict):
-        """dev_views[g]: the batch in shard g's device memory; verdict: uint8 tensor [T] (device)."""
+    def detect_device(self, views, now, new_oldest, verdict):
+        """views[g]: the batch in shard g's device memory; verdict: uint8 tensor [>= T] on devices[0]."""
         torch = self.torch
-        T = dev_views[0].txn_count
-        hs = [torch.zeros(max(1, T), dtype=torch.uint8, device=f"cuda:{d}") for d in self.devices]
-        for s, v, h in zip(self.shards, dev_views, hs):
+        T = views[0].txn_count
+        hs = [torch.empty(max(1, T), dtype=torch.uint8, device=d) for d in self.devices]
+        for d in set(self.devices):
+            _sync(torch, d)
+        for s, v, h in zip(self.shards, views, hs):  # steps 1-2
             s.check(v, now, new_oldest, h.data_ptr())
-        flags = torch.stack([h.to(hs[0].device) for h in hs]).amax(0)  # step 3: MAX over shards
+        flags = torch.stack([h.to(self.devices[0]) for h in hs]).amax(0)  # step 3: MAX over shards
         infos, n_comb = [], 0
-        scratch = torch.empty(max(1, T), dtype=torch.uint8, device=verdict.device)
-        for g, (s, v) in enumerate(zip(self.shards, dev_views)):
-            f = flags.to(f"cuda:{self.devices[g]}")
-            out = verdict if g == 0 else scratch.to(f"cuda:{self.devices[g]}")
+        for g, (s, v) in enumerate(zip(self.shards, views)):  # steps 4-5
+            f = flags.to(self.devices[g])
+            out = verdict if g == 0 else torch.empty(max(1, T), dtype=torch.uint8, device=self.devices[g])
+            _sync(torch, self.devices[g])
             H, g0, last, n_comb = s.apply(v, now, new_oldest, f.data_ptr(), out.data_ptr())
             infos.append((H, g0, last))
         self._finish(infos, n_comb, new_oldest)
 
+    def detect_packed(self, batch, now, new_oldest):
+        """A host PackedBatch through the sharded path; returns the verdict bytes (numpy)."""
+        from .batch import DeviceBatch
+
+        staged = {}
+        for d in self.devices:
+            if d not in staged:
+                staged[d] = DeviceBatch(batch, d)
+        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.devices[0])
+        self.detect_device([staged[d].view for d in self.devices], now, new_oldest, verdict)
+        return verdict[:batch.T].cpu().numpy()
+
     def _finish(self, infos, n_comb, new_oldest):
         rk = None
-        if new_oldest > self.oldest:
+        if new_oldest > self.oldest:  # step 6
             parts, owner = plan_compaction(infos, n_comb)
             rk = self.shards[owner[0]].key_at(owner[1]) if owner else b""
             hl = [s.compact(p, new_oldest) for s, p in zip(self.shards, parts)]
             self.oldest = new_oldest
         else:
             hl = [(H, last) for H, _g0, last in infos]
-        for s, c in zip(self.shards, carry_ins(self.v0, hl)):
+        for s, c in zip(self.shards, carry_ins(self.v0, hl)):  # step 7
             s.finish(c, rk)
+
+    @property
+    def oldest_version(self):
+        return self.oldest
 
     def history(self):
         out = []
         for s in self.shards:
-            out += s.cs.history()
+            out += s.history()
         return out
 
     def removal_key(self):
-        return self.shards[0].cs.removal_key()
+        return self.shards[0].removal_key()
 
     def close(self):
         for s in self.shards:
-            s.cs.close()
+            s.close()
 
 
 class DistShardedConflictSet:
-    """One shard per torch.distributed rank (RCCL over xGMI on MI355X)."""
+    """One shard per torch.distributed rank (RCCL over xGMI on MI355X, gloo on CPU)."""
 
-    def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None):
+    def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None, shard_factory=Shard):
         import torch
         import torch.distributed as dist
 
         assert len(bounds) + 1 == world
         self.torch, self.dist, self.group = torch, dist, group
-        self.rank, self.world, self.device = rank, world, device
+        self.rank, self.world = rank, world
+        self.device = _device(torch, device)
         lo, hi = _shard_ranges(bounds)[rank]
-        self.shard = Shard(lo, hi, device=device, v0=v0, max_history=max_history)
+        self.shard = shard_factory(lo, hi, device=device, v0=v0, max_history=max_history)
         self.v0 = v0
         self.oldest = 0
         backend = dist.get_backend(group)
-        self.coll_dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
+        self.coll_dev = self.device if backend == "nccl" else torch.device("cpu")
+        self._T = -1
 
-    def detect_device(self, dev_view, now, new_oldest, verdict):
+    def clear(self, v):
+        self.shard.clear(v)
+        self.v0 = v
+
+    def _buffers(self, T):
+        if T != self._T:
+            torch = self.torch
+            self._h = torch.empty(max(1, T), dtype=torch.uint8, device=self.device)
+            self._hc = self._h if self.coll_dev == self.device else torch.empty(max(1, T), dtype=torch.uint8)
+            self._T = T
+        return self._h, self._hc
+
+    def detect_device(self, view, now, new_oldest, verdict):
+        """view: the whole batch in this rank's device memory; verdict: uint8 tensor [>= T] there."""
         torch, dist = self.torch, self.dist
-        T = dev_view.txn_count
-        h = torch.zeros(max(1, T), dtype=torch.uint8, device=verdict.device)
-        self.shard.check(dev_view, now, new_oldest, h.data_ptr())
-        hc = h.to(self.coll_dev)
+        h, hc = self._buffers(view.txn_count)
+        _sync(torch, self.device)
+        self.shard.check(view, now, new_oldest, h.data_ptr())  # steps 1-2 (synchronous)
+        if hc is not h:
+            hc.copy_(h)
         dist.all_reduce(hc, op=dist.ReduceOp.MAX, group=self.group)  # step 3
-        h.copy_(hc)
-        H, g0, last, n_comb = self.shard.apply(dev_view, now, new_oldest, h.data_ptr(), verdict.data_ptr())
+        if hc is not h:
+            h.copy_(hc)
+        _sync(torch, self.device)  # the engine reads h on its own stream
+        H, g0, last, n_comb = self.shard.apply(view, now, new_oldest, h.data_ptr(), verdict.data_ptr())  # 4-5
         infos = self._allgather([H, g0, last])
         rk = None
-        if new_oldest > self.oldest:
+        if new_oldest > self.oldest:  # step 6
             parts, owner = plan_compaction([tuple(x) for x in infos], n_comb)
-            buf = torch.zeros(_abi.MAX_KEY + 4, dtype=torch.uint8, device=self.coll_dev)
-            if owner is not None and owner[0] == self.rank:
-                k = self.shard.key_at(owner[1])
-                buf[:4] = torch.tensor(list(len(k).to_bytes(4, "little")), dtype=torch.uint8)
-                buf[4:4 + len(k)] = torch.tensor(list(k), dtype=torch.uint8) if k else buf[4:4]
-            if owner is not None:
-                dist.broadcast(buf, src=owner[0], group=self.group)
-                n = int.from_bytes(bytes(buf[:4].cpu().tolist()), "little")
-                rk = bytes(buf[4:4 + n].cpu().tolist())
-            else:
-                rk = b""
+            rk = self._broadcast_key(owner)
             Hn, lastn = self.shard.compact(parts[self.rank], new_oldest)
             hl = [tuple(x) for x in self._allgather([Hn, lastn])]
             self.oldest = new_oldest
         else:
             hl = [(x[0], x[2]) for x in infos]
-        self.shard.finish(carry_ins(self.v0, hl)[self.rank], rk)
+        self.shard.finish(carry_ins(self.v0, hl)[self.rank], rk)  # step 7
+
+    def detect_packed(self, batch, now, new_oldest):
+        from .batch import DeviceBatch
+
+        db = DeviceBatch(batch, self.device)
+        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.device)
+        self.detect_device(db.view, now, new_oldest, verdict)
+        return verdict[:batch.T].cpu().numpy()
+
+    def _broadcast_key(self, owner):
+        """The new removalKey from the shard holding the window's end ("" past the end)."""
+        if owner is None:
+            return b""
+        torch, dist = self.torch, self.dist
+        buf = torch.zeros(_abi.MAX_KEY + 4, dtype=torch.uint8)
+        if owner[0] == self.rank:
+            k = self.shard.key_at(owner[1])
+            buf[:4 + len(k)] = torch.frombuffer(bytearray(len(k).to_bytes(4, "little") + k), dtype=torch.uint8)
+        buf = buf.to(self.coll_dev)
+        dist.broadcast(buf, src=owner[0], group=self.group)
+        raw = buf.cpu().numpy()
+        n = int.from_bytes(raw[:4].tobytes(), "little")
+        return raw[4:4 + n].tobytes()
 
     def _allgather(self, vals):
         torch, dist = self.torch, self.dist
@@ -261,3 +340,16 @@ class DistShardedConflictSet:
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
         return [o.cpu().tolist() for o in out]
+
+    @property
+    def oldest_version(self):
+        return self.oldest
+
+    def history(self):
+        return self.shard.history()
+
+    def removal_key(self):
+        return self.shard.removal_key()
+
+    def close(self):
+        self.shard.close()

@@ -1,0 +1,195 @@
+"""Exact sharded mode (SURVEY.md §8e protocol A): one Resolver over G shards.
+
+The concatenated shard histories, the verdicts, removalKey and oldestVersion
+must equal ONE conflict set's (the oracle) after every batch -- the north
+star's "result matches a single-resolver reference exactly".
+
+CPU tests drive the host protocol (plan_compaction, carry-ins, removalKey
+broadcast; in-process and over gloo with world_size 2 and 3) with the CPU
+shard model (tests/shard_model.py).  GPU tests drive the HIP engines through
+the C ABI (fdbcs_shard_*), G shards on one device.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from foundationdb_amd.resolvers import uniform_bounds
+from foundationdb_amd.sharded import ShardedConflictSet, carry_ins, plan_compaction
+from gen import ALPHA, mixed_stream, rand_key, tiny_stream
+from oracle import CpuSpec
+from shard_model import ModelShard
+
+
+def random_bounds(rng, G, maxlen, alpha=ALPHA):
+    ks = set()
+    while len(ks) < G - 1:
+        ks.add(rand_key(rng, maxlen, alpha))
+    return sorted(ks)
+
+
+def check_step(sh, c, batch, now, nold, history=True):
+    vs = sh.detect_packed(batch, now, nold)
+    vc = c.detect_packed(batch, now, nold)
+    assert np.array_equal(vs, vc), (np.nonzero(vs != vc)[0][:10], vs[:20], vc[:20])
+    assert sh.oldest_version == c.oldest_version
+    if history:
+        assert sh.history() == c.history()
+        assert sh.removal_key() == c.removal_key()
+
+
+# ------------------------------------------------------------------ CPU ----
+
+def test_plan_compaction_cuts_the_global_window():
+    # shards of 3, 0, 4 boundaries; removalKey's first hit in shard 0 at index 2
+    infos = [(3, 2, 50), (0, 0, -(1 << 63)), (4, 0, 70)]
+    parts, owner = plan_compaction(infos, 0)  # window = 10 boundaries: all 5 from global 2
+    assert parts == [(2, 3, 1, 0), (0, 0, 0, 0), (0, 4, 0, 50)]
+    assert owner is None  # the scan reached the end: removalKey wraps to ""
+    parts, owner = plan_compaction([(30, 25, 9), (20, 0, 8)], 0)
+    assert parts == [(25, 30, 1, 0), (0, 5, 0, 9)]
+    assert owner == (1, 5)
+    parts, owner = plan_compaction([(3, 3, 1), (2, 2, 2)], 4)  # nothing >= removalKey anywhere
+    assert owner is None and all(p[0] == p[1] for p in parts)
+
+
+def test_carry_ins_skip_empty_shards():
+    assert carry_ins(7, [(2, 11), (0, 0), (1, 13), (0, 0)]) == [7, 11, 11, 13]
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 5])
+def test_model_shards_equal_one_conflict_set(G):
+    for seed in range(12):
+        rng = random.Random(seed * 7 + G)
+        maxlen = rng.choice([2, 3, 6])
+        sh = ShardedConflictSet(random_bounds(rng, G, maxlen), devices=[-1] * G, shard_factory=ModelShard)
+        c = CpuSpec()
+        for batch, now, nold in tiny_stream(seed * 31 + G, n_batches=25, maxlen=maxlen):
+            check_step(sh, c, batch, now, nold)
+
+
+def test_model_shards_bounds_at_written_keys_and_clear():
+    """Splitters that are themselves written/read keys (e = s_g ends), clearConflictSet mid-stream."""
+    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], devices=[-1] * 4, shard_factory=ModelShard)
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(tiny_stream(99, n_batches=40, maxlen=3)):
+        if i == 20:
+            sh.clear(now - 3)
+            c.clear(now - 3)
+        check_step(sh, c, batch, now, nold)
+
+
+def test_model_shards_mixed_streams():
+    for seed in range(2):
+        sh = ShardedConflictSet([b"k001000", b"k002500", b"k002500\x00"], devices=[-1] * 4,
+                                shard_factory=ModelShard)
+        c = CpuSpec()
+        for batch, now, nold in mixed_stream(seed, n_batches=8, max_txns=120, keyspace=4000):
+            check_step(sh, c, batch, now, nold)
+
+
+def _dist_rank(rank, world, port, bounds, seed, q):
+    import torch.distributed as dist
+
+    from foundationdb_amd.sharded import DistShardedConflictSet
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard)
+    out = []
+    for batch, now, nold in tiny_stream(seed, n_batches=25, maxlen=3):
+        v = sh.detect_packed(batch, now, nold)
+        out.append((v.tolist(), sh.history(), sh.removal_key(), sh.oldest_version))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_sharded_gloo(world):
+    """world_size 2/3 over gloo: one shard per rank; every rank's verdicts, the
+    concatenation of the ranks' histories and removalKey equal one conflict set's."""
+    rng = random.Random(world)
+    bounds = random_bounds(rng, world, 3)
+    seed = 1234 + world
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + random.Random(os.getpid() * 7 + world).randint(0, 3000)
+    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(tiny_stream(seed, n_batches=25, maxlen=3)):
+        vc = c.detect_packed(batch, now, nold).tolist()
+        hist = []
+        for r in range(world):
+            v, h, rk, old = got[r][i]
+            assert v == vc, (i, r)
+            assert rk == c.removal_key() and old == c.oldest_version
+            hist += h
+        assert hist == c.history(), i
+
+
+# ------------------------------------------------------------------ GPU ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxlen", [3, 11, 40])
+def test_gpu_shards_tiny_streams(gpu, maxlen):
+    for seed in range(8):
+        rng = random.Random(seed * 5 + maxlen)
+        G = rng.choice([2, 3, 4])
+        sh = ShardedConflictSet(random_bounds(rng, G, min(maxlen, 4)), max_history=1 << 14)
+        c = CpuSpec()
+        try:
+            for batch, now, nold in tiny_stream(seed * 13 + maxlen, n_batches=25, maxlen=maxlen):
+                check_step(sh, c, batch, now, nold)
+        finally:
+            sh.close()
+
+
+@pytest.mark.gpu
+def test_gpu_shards_bounds_at_keys_and_clear(gpu):
+    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], max_history=1 << 14)
+    c = CpuSpec()
+    try:
+        for i, (batch, now, nold) in enumerate(tiny_stream(99, n_batches=40, maxlen=3)):
+            if i == 20:
+                sh.clear(now - 3)
+                c.clear(now - 3)
+            check_step(sh, c, batch, now, nold)
+    finally:
+        sh.close()
+
+
+@pytest.mark.gpu
+def test_gpu_shards_mixed_streams(gpu):
+    sh = ShardedConflictSet([b"k001000", b"k002500", b"k002500\x00"], max_history=1 << 16)
+    c = CpuSpec()
+    try:
+        for batch, now, nold in mixed_stream(3, n_batches=12, max_txns=600, keyspace=5000):
+            check_step(sh, c, batch, now, nold)
+    finally:
+        sh.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4])
+def test_gpu_shards_config2(gpu, G):
+    """Config 2's shape (5R+2W, uniform 16-byte keys) split over G uniform key slices."""
+    from foundationdb_amd.workload import Workload
+
+    sh = ShardedConflictSet(uniform_bounds(G))
+    c = CpuSpec()
+    wl = Workload(2, txns=1500)
+    try:
+        for i in range(12):
+            batch, now, nold = wl.batch(i)
+            check_step(sh, c, batch, now, nold, history=(i % 4 == 3))
+    finally:
+        sh.close()
