@@ -12,12 +12,23 @@ N = 1: BASELINE.json configs[1] = SURVEY.md §8d config 2: 5,000-txn batches,
 keys, 5M-version MVCC window; W warmup batches grow the history to steady
 state (~19 M boundaries after ~2,500 batches), then K measured batches.
 
-N > 1: FoundationDB's multi-resolver scale-out: GPU g is the
-resolver for the g-th equal slice of the key space; one global batch of
-5,000 x N transactions is split by the proxy rule (fdbcs_split_batch,
+N > 1, --mode exact (default; the north star's layout, SURVEY.md §8e
+protocol A): ONE resolver over N GPUs.  GPU g holds the history of the g-th
+equal slice of the key space; every GPU receives the whole global batch of
+5,000 x N transactions, checks the reads clipped to its keys, an RCCL MAX
+all-reduce combines the per-transaction conflict flags, every GPU replays the
+identical ordered decision and merges its shard's part of the committed
+writes, and two tiny all-gathers drive the global compaction window.  The
+verdicts and the concatenated history equal a single conflict set's exactly.
+Per-GPU history and merge work stay ~fixed (weak scaling); the batch-wide
+stages (ingest, sort, decision) see the whole N x 5,000 batch on every GPU.
+
+N > 1, --mode resolvers: FoundationDB's multi-resolver scale-out (SURVEY.md
+§3.4): GPU g is an independent resolver for the g-th key slice; the global
+batch is split by the proxy rule (fdbcs_split_batch,
 MasterProxyServer.actor.cpp:267-307), every GPU resolves its sub-batch, and
 the proxy's min-combine (:558-569) is a scatter + RCCL MIN all-reduce of the
-verdict bytes inside the timed step.  Per-GPU work stays ~fixed: weak scaling.
+verdict bytes inside the timed step (conservative, as FDB's own).
 
 Prints ONE JSON line (rank 0).  `value` = resolved txns/s (whole node, max
 time over ranks), `p99_batch_ms` = p99 per-batch latency.  `roofline`: the
@@ -55,6 +66,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--stage-batches", type=int, default=50, help="extra instrumented batches after the timed region")
+    p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
+                   help="N > 1: one exact resolver sharded by key range, or N independent key-range resolvers")
     return p.parse_args()
 
 
@@ -84,12 +97,12 @@ def to_device(v, torch, dev):
 class Source:
     """Batches for this rank: the whole batch (N = 1) or this resolver's share."""
 
-    def __init__(self, cfg, txns, world, rank):
+    def __init__(self, cfg, txns, world, rank, split):
         from foundationdb_amd.workload import Workload
         self.world, self.rank = world, rank
         self.wl = Workload(cfg, txns=txns * world)
         self.kr = None
-        if world > 1:
+        if split:
             from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
             self.kr = KeyRangeResolvers(uniform_bounds(world))
 
@@ -145,22 +158,44 @@ def main():
             dist.init_process_group(backend)
 
     from foundationdb_amd import ConflictSet
-    from foundationdb_amd.resolvers import scatter_verdicts
+    from foundationdb_amd.batch import DeviceBatch
+    from foundationdb_amd.resolvers import scatter_verdicts, uniform_bounds
 
     cfg = args.config
-    src = Source(cfg, args.txns, world, rank)
-    cs = ConflictSet(device=local, max_history=30_000_000)
+    mode = args.mode if world > 1 else "single"
+    src = Source(cfg, args.txns, world, rank, split=(mode == "resolvers"))
+    eng = None
+    if mode == "exact":
+        from foundationdb_amd.sharded import DistShardedConflictSet
+        eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=30_000_000)
+        cs = eng.shard.cs
+    else:
+        cs = ConflictSet(device=local, max_history=30_000_000)
+
+    def global_h():
+        """History size of the whole resolver (the sum over shards in exact mode)."""
+        if mode != "exact":
+            return cs.history_size()
+        return sum(x[0] for x in eng._allgather([cs.history_size()]))
 
     # ---- warmup: grow the history to steady state (untimed) ----------------
     t_w = time.time()
     verdict_host = None
+    wverd = None
     for i in range(args.warmup):
         v, now, nold, _T, _idx, _keep = src.host(i)
-        verdict_host = cs.detect_view(v, now, nold, verdict_host)
+        if mode == "exact":
+            db = DeviceBatch(v, dev)
+            if wverd is None or wverd.numel() < max(1, v.txn_count):
+                wverd = torch.empty(max(1, v.txn_count), dtype=torch.uint8, device=dev)
+            eng.detect_device(db.view, now, nold, wverd)
+        else:
+            verdict_host = cs.detect_view(v, now, nold, verdict_host)
         if rank == 0 and (i + 1) % 500 == 0:
             print(f"# warmup {i + 1}/{args.warmup} H={cs.history_size()} {time.time() - t_w:.1f}s",
                   file=sys.stderr, flush=True)
-    H_pre = cs.history_size()
+    H_pre = global_h()
+    H_pre_local = cs.history_size()
 
     # CPU baseline needs the GPU's steady state: snapshot it before timing
     snap = None
@@ -168,7 +203,7 @@ def main():
         snap = cs.dump_arrays() + (cs.header_version, cs.oldest_version, cs.removal_key())
 
     # ---- stage the K measured batches (+ instrumented ones) in HBM -------------
-    n_stage = args.steps + args.stage_batches
+    n_stage = args.steps + (args.stage_batches if mode != "exact" else 0)
     staged = []
     for i in range(args.warmup, args.warmup + n_stage):
         v, now, nold, Tg, idx, keep = src.host(i)
@@ -184,14 +219,21 @@ def main():
     if world > 1:
         dist.barrier()
 
+    if mode == "exact" and os.environ.get("FDBCS_PHASES_HOST"):
+        eng.enable_phase_timing(True)
     # ---- timed region: K steps -------------------------------------------------
+    if os.environ.get("FDBCS_VERBOSE"):
+        print(f"# rank {rank}: timed region starts", file=sys.stderr, flush=True)
     lat = []
     t0 = time.perf_counter()
     for k in range(args.steps):
         dv, now, nold, _Tg, didx, _b, _nb = staged[k]
         ts = time.perf_counter()
-        cs.detect_device(dv, now, nold, sub_verdicts[k].data_ptr(), sync=True)
-        if world > 1:  # proxy combine: scatter this resolver's verdicts, MIN over resolvers
+        if mode == "exact":  # one resolver over N GPUs: check, MAX all-reduce, decide + merge, compaction
+            eng.detect_device(dv, now, nold, sub_verdicts[k])
+        else:
+            cs.detect_device(dv, now, nold, sub_verdicts[k].data_ptr(), sync=True)
+        if mode == "resolvers":  # proxy combine: scatter this resolver's verdicts, MIN over resolvers
             scatter_verdicts(None, sub_verdicts[k].data_ptr(), didx.data_ptr(), dv.txn_count,
                              global_verdicts[k].data_ptr())
             dist.all_reduce(global_verdicts[k], op=dist.ReduceOp.MIN)
@@ -204,14 +246,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    H_post = cs.history_size()
+    if eng is not None and eng.phase_s:
+        print(f"# rank {rank} phase us/batch: " +
+              json.dumps({k: round(v / args.steps * 1e6, 1) for k, v in eng.phase_s.items()}), file=sys.stderr,
+              flush=True)
+    H_post = global_h()
+    H_post_local = cs.history_size()
     total_txns = Tg * args.steps
     value = total_txns / elapsed
     lat_ms = np.array(lat) * 1e3
 
     # ---- instrumented pass: per-stage HIP-event times on the engine's stream ---
     roofline = None
-    if args.stage_batches > 0:
+    if mode == "exact":  # per-GPU algorithmic bytes (its shard's history) over the per-batch wall time
+        nbytes = float(np.mean([x[6] for x in staged[:args.steps]]))
+        algo = pipeline_bytes(nbytes, Tg, H_pre_local, H_post_local)
+        batch_us = elapsed / args.steps * 1e6
+        achieved = algo / (batch_us * 1e-6) / 1e9
+        roofline = {
+            "bound": "hbm",
+            "kernel": "detectConflicts pipeline per GPU (whole batch + its shard's history; SURVEY §8d bytes), "
+                      "wall time per batch including the RCCL exchanges",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "algo_bytes_per_batch": round(algo),
+            "batch_us": round(batch_us, 2),
+            "shard_history_pre": H_pre_local,
+        }
+    if args.stage_batches > 0 and mode != "exact":
         cs.enable_stage_timing(True)
         st_us, stats, hp = [], [], []
         scratch = torch.zeros(Tmax, dtype=torch.uint8, device=dev)
@@ -248,6 +313,8 @@ def main():
                 "frac": round(dom_bytes / (mean[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "measured_over": f"{args.stage_batches} batches after the timed region (HIP events per stage)",
+            "sort_rebucketed_batches": int(sum(x.get("sort_rebucketed", 0) for x in stats)),
+            "sort_max_bucket": int(max(x.get("sort_max_bucket", 0) for x in stats)),
         }
         prof = os.path.join(ROOT, "profiles", f"pmc_traffic_config{cfg}.json")
         if os.path.exists(prof):  # per-batch HBM bytes from separate rocprofv3 --pmc passes
@@ -277,7 +344,11 @@ def main():
                          f"GPU's steady-state history (H={H_pre}); verdict mismatches vs GPU: {mism}"}
 
     if rank == 0:
-        if world > 1:
+        if mode == "exact":
+            workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
+                        f"5M-version window; one exact resolver sharded by key range over {world} GPUs "
+                        f"(RCCL MAX all-reduce of conflict flags + all-gathers for the compaction window)")
+        elif mode == "resolvers":
             workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
                         f"5M-version window; {world} key-range resolvers (proxy split + RCCL MIN combine)")
         else:
@@ -298,7 +369,7 @@ def main():
             "dtype": "int64",
             "data": "synthetic (deterministic generator, SURVEY.md §8d)",
             "config": {"workload": workload, "txns_per_batch": Tg, "history_pre": H_pre, "history_post": H_post,
-                       "parallelism": f"keyrange{world}" if world > 1 else "single"},
+                       "parallelism": {"exact": f"sharded{world}", "resolvers": f"keyrange{world}"}.get(mode, "single")},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

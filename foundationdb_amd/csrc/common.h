@@ -195,7 +195,9 @@ struct Scalars {
     int32_t free_next;      // free_top after the rebuild in flight
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)
-    int32_t ss_resample;    // a sort bucket overflowed: recompute the splitter quantiles
+    int32_t ss_resample;    // stats: a sort bucket overflowed and the batch was bucketed again
+    int32_t ss_over[2];     // a sort bucket of job j overflowed its staging row (the guard re-buckets)
+    int32_t ss_maxc;        // stats: largest sort bucket above the register path (0: none)
     int32_t extra_total;    // free pages the merge takes (parts beyond each page's first)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };

@@ -165,10 +165,19 @@ void adopt_scalars(fdbcs* cs) {
     cs->known_free = cs->sc_host->free_top;
     cs->known_H = cs->sc_host->H;
     cs->known_tail = cs->sc_host->tail_used;
-    if (cs->sc_host->ss_resample) cs->have_quantiles = false;
     cs->pending_pages = 0;
     cs->pending_tail = 0;
 }
+
+// FDBCS_VERBOSE=1: log every buffer growth (reallocations stall the stream)
+static bool verbose() {
+    static const bool v = getenv("FDBCS_VERBOSE") != nullptr;
+    return v;
+}
+#define GROWLOG(...) \
+    do { \
+        if (verbose()) fprintf(stderr, "# fdbcs grow: " __VA_ARGS__); \
+    } while (0)
 
 int sync_state(fdbcs* cs) {
     HIPOK(hipMemcpyAsync(cs->sc_host, cs->sc, sizeof(Scalars), hipMemcpyDeviceToHost, cs->stream));
@@ -191,6 +200,7 @@ int grow_pool(fdbcs* cs, int64_t pages) {
     if ((r = sync_state(cs))) return r;
     HistBufs old = cs->h;
     int64_t np = std::max<int64_t>(pages, (int64_t)old.cap_pages * 2);
+    GROWLOG("pool %d -> %lld pages (asked %lld)\n", old.cap_pages, (long long)np, (long long)pages);
     if (np > INT32_MAX / 2) return FDBCS_E_CAPACITY;
     if ((r = alloc_pool(cs, (int32_t)np))) return r;
     HistBufs& h = cs->h;
@@ -233,6 +243,7 @@ int grow_tail(fdbcs* cs, uint64_t need) {
     if ((r = sync_state(cs))) return r;
     HistBufs& h = cs->h;
     uint64_t ncap = std::max<uint64_t>(need, h.tail_cap * 2);
+    GROWLOG("tail arena %llu -> %llu bytes\n", (unsigned long long)h.tail_cap, (unsigned long long)ncap);
     uint8_t* na = nullptr;
     if ((r = dalloc(na, (int64_t)ncap))) return r;
     HIPOK(hipMemcpyAsync(na, h.tail_arena, cs->known_tail, hipMemcpyDeviceToDevice, cs->stream));
@@ -290,6 +301,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (T > 65536) return FDBCS_E_CAPACITY;  // T x T pair matrix bound
     if (!b.scan_tmp && (r = dalloc(b.scan_tmp, 1024))) return r;
     if (T > cs->capT) {
+        GROWLOG("T %lld\n", (long long)T);
         int64_t n = std::max<int64_t>(T, 1024);
         dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
         dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
@@ -310,12 +322,14 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         cs->capT = n;
     }
     if (R > cs->capR) {
+        GROWLOG("R %lld\n", (long long)R);
         int64_t n = std::max<int64_t>(R, 1024);
         dfree(b.read_txn); dfree(b.read_snap); dfree(b.rec_r0);
         if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.read_snap, n)) || (r = dalloc(b.rec_r0, n))) return r;
         cs->capR = n;
     }
     if (W > cs->capW) {
+        GROWLOG("W %lld\n", (long long)W);
         int64_t n = std::max<int64_t>(W, 1024);
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
         dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
@@ -359,6 +373,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     const int64_t slots = 2 * (R + W);
     if (slots > cs->capSlots) {
+        GROWLOG("slots %lld\n", (long long)slots);
         int64_t n = std::max<int64_t>(slots, 4096);
         free_keys(b.keys);
         if ((r = alloc_keys(b.keys, n))) return r;
@@ -366,6 +381,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     const uint64_t btail_need = key_bytes + 8 * (uint64_t)slots + 64;
     if ((int64_t)btail_need > cs->capBtail) {
+        GROWLOG("btail %llu\n", (unsigned long long)btail_need);
         uint64_t n = std::max<uint64_t>(btail_need, 1 << 16);
         dfree(b.btail);
         if ((r = dalloc(b.btail, (int64_t)n))) return r;
@@ -374,6 +390,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     const int64_t win_pages = 3 * std::max<int64_t>(W, 1024) + 16;
     if (win_pages > cs->capWinPages) {
+        GROWLOG("win pages %lld\n", (long long)win_pages);
         dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
         if ((r = dalloc(b.win_keep, win_pages * PAGE)) || (r = dalloc(b.win_cnt, win_pages)) ||
             (r = dalloc(b.win_off, win_pages + 2)))
@@ -993,7 +1010,7 @@ int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
     if (!cs || !out) return FDBCS_E_ARG;
     const Scalars& h = *cs->sc_host;
     const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
-                                    h.win_surv, h.n_dep, h.jac_iters};
+                                    h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc};
     const int n = std::min(cap, (int)FDBCS_STATS);
     for (int i = 0; i < n; i++) out[i] = v[i];
     return n;

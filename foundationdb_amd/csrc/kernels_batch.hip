@@ -347,15 +347,14 @@ __device__ void wave_bitonic(SRec r[2], int P, const uint8_t* const* tails) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys) {
-    __shared__ uint64_t s_hi[SS_Q], s_lo[SS_Q], s_mi[SS_Q];
-    const int job = blockIdx.x;
+// Splitters drawn from the batch itself: SS_S strided samples (4x the
+// quantiles kept, so a bucket between two splitters holds ~4 sample gaps and
+// its size concentrates) sorted in LDS.  Returns the sample count.
+static constexpr int SS_S = 4096;
+__device__ int sample_quantiles(const SortJobs& J, int job, const KeyArrays& keys, const LdsRecs& L) {
     const int n = J.n[job];
-    if (blockIdx.x == 0 && threadIdx.x == 0) J.sc->ss_resample = 0;
-    if (n == 0) return;
-    const LdsRecs L{s_hi, s_lo, s_mi};
-    const int ns = min(n, SS_Q);
-    for (int k = threadIdx.x; k < SS_Q; k += blockDim.x) {
+    const int ns = min(n, SS_S);
+    for (int k = threadIdx.x; k < SS_S; k += blockDim.x) {
         if (k < ns) {
             const int64_t r = ((int64_t)k * n + n / (2 * ns)) / ns;
             L.put(k, load_rec(keys, J.sbase[job] + r * J.sstride[job]));
@@ -364,9 +363,57 @@ __global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys) 
         }
     }
     __syncthreads();
-    lds_bitonic(L, SS_Q, keys.tail);
+    lds_bitonic(L, SS_S, keys.tail);
     for (int q = threadIdx.x; q < SS_Q; q += blockDim.x)
         put_quantile(J, job, q, L.get((int)((int64_t)q * ns / SS_Q)), keys.tail);
+    return ns;
+}
+
+// record i of a job goes to bucket b: count, bucket id, staging row
+__device__ inline void place_rec(const SortJobs& J, int job, int i, int b, const SRec& x) {
+    const int slot = atomicAdd(&J.cnt[job * SS_MAXB + b], 1);
+    J.bkt[(job ? J.n[0] : 0) + i] = b;
+    if (slot < SS_ROW) J.tmp[((int64_t)job * SS_MAXB + b) * SS_ROW + slot] = x;
+    else if (slot == SS_ROW) J.sc->ss_over[job] = 1;  // the bucket kernel would rank it from global memory
+}
+
+// One workgroup per job.  guard == 0: the first batch -- splitters from a
+// sample of this batch.  guard == 1 (after every scatter): nothing, unless a
+// bucket overflowed its staging row (the key distribution moved away from the
+// previous batch's quantiles); then splitters from this batch's own sample
+// and every record of the job is bucketed again, so the batch keeps the fast
+// bucket paths instead of an O(bucket x n) global-memory ranking.
+__global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys, int guard) {
+    __shared__ uint64_t s_hi[SS_S], s_lo[SS_S], s_mi[SS_S];
+    const int job = blockIdx.x;
+    const int n = J.n[job];
+    if (guard && !J.sc->ss_over[job]) return;
+    if (n == 0) return;
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    const int ns = sample_quantiles(J, job, keys, L);
+    if (!guard) return;
+    const int nb = J.nb[job], step = SS_Q / nb;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) J.cnt[job * SS_MAXB + b] = 0;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) J.sc->ss_resample = 1;  // (stats: the batch was bucketed twice)
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
+        int lo = 0, len = nb - 1;  // bucket = number of splitters <= x
+        while (len > 0) {
+            const int half = len >> 1, k = lo + half;
+            const SRec sp = L.get((int)((int64_t)((k + 1) * step) * ns / SS_Q));
+            if (!rec_lt(x, sp, keys.tail)) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        place_rec(J, job, i, lo, x);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) J.sc->ss_over[job] = 0;  // (a bucket may still exceed its row: ranked globally)
 }
 
 // Splitter s of a job is quantile (s + 1) * SS_Q / nb.  Scatter kernels keep
@@ -405,10 +452,7 @@ __device__ inline int bucket_of(const SortJobs& J, int job, const uint64_t* sp, 
 // record i of a job into its bucket's staging row
 __device__ inline void scatter_rec(const SortJobs& J, int job, int i, const SRec& x, const uint8_t* const* tails,
                                    const uint64_t* sp) {
-    const int b = bucket_of(J, job, sp, x, tails);
-    const int slot = atomicAdd(&J.cnt[job * SS_MAXB + b], 1);
-    J.bkt[(job ? J.n[0] : 0) + i] = b;
-    if (slot < SS_ROW) J.tmp[((int64_t)job * SS_MAXB + b) * SS_ROW + slot] = x;
+    place_rec(J, job, i, bucket_of(J, job, sp, x, tails), x);
 }
 
 __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) {
@@ -431,7 +475,11 @@ template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_ingest(IngestArgs A, SortJobs J) {
     if ((int)blockIdx.x < A.prep_blocks) {
         const int t = blockIdx.x * blockDim.x + threadIdx.x;
-        if (t == 0) A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+        if (t == 0) {
+            A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+            A.sc->ss_resample = 0;
+            A.sc->ss_maxc = 0;
+        }
         if (t >= A.T) return;
         const int r0 = A.ro[t], r1 = A.ro[t + 1];
         const int64_t sn = A.snap[t];
@@ -559,7 +607,7 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
         }
         return;
     }
-    if (lane == 0) J.sc->ss_resample = 1;  // unbalanced: sample afresh next batch
+    if (lane == 0) atomicMax(&J.sc->ss_maxc, c);  // (stats: the largest bucket above the register path)
     if (c <= SS_ROW) {
         int P = 1;
         while (P < c) P <<= 1;
@@ -655,9 +703,10 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     b.sw = b.rec_w0;
     if (J.n[0] + J.n[1] == 0) return false;
     if (!scattered) {  // (otherwise the ingest already put every record into its bucket)
-        if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys);
+        if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 0);
         hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
     }
+    hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 1);  // overflow guard
     hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
     return true;  // the counters of the other parity are zero now
 }

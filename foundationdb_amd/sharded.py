@@ -38,6 +38,7 @@ Two exchange back ends share the logic below:
   RCCL over xGMI, or gloo on CPU.
 """
 import ctypes as C
+import time
 
 from . import _abi
 from ._abi import check
@@ -90,6 +91,18 @@ def plan_compaction(infos, n_comb):
                 owner = (g, G1 - offs[g])
                 break
     return parts, owner
+
+
+KEY_INLINE = 32  # removalKeys up to this length travel inside the compaction all-gather
+
+
+def _pack_key(key):
+    raw = key.ljust(KEY_INLINE, b"\0")
+    return [int.from_bytes(raw[i:i + 8], "little", signed=True) for i in range(0, KEY_INLINE, 8)]
+
+
+def _unpack_key(words, n):
+    return b"".join(int(w).to_bytes(8, "little", signed=True) for w in words)[:n]
 
 
 def carry_ins(v0, hl):
@@ -273,6 +286,7 @@ class DistShardedConflictSet:
         backend = dist.get_backend(group)
         self.coll_dev = self.device if backend == "nccl" else torch.device("cpu")
         self._T = -1
+        self.phase_s = None
 
     def clear(self, v):
         self.shard.clear(v)
@@ -289,27 +303,60 @@ class DistShardedConflictSet:
     def detect_device(self, view, now, new_oldest, verdict):
         """view: the whole batch in this rank's device memory; verdict: uint8 tensor [>= T] there."""
         torch, dist = self.torch, self.dist
+        tick = self._tick
+        tick(None)
         h, hc = self._buffers(view.txn_count)
         _sync(torch, self.device)
         self.shard.check(view, now, new_oldest, h.data_ptr())  # steps 1-2 (synchronous)
+        tick("check")
         if hc is not h:
             hc.copy_(h)
         dist.all_reduce(hc, op=dist.ReduceOp.MAX, group=self.group)  # step 3
         if hc is not h:
             h.copy_(hc)
         _sync(torch, self.device)  # the engine reads h on its own stream
+        tick("flags_allreduce")
         H, g0, last, n_comb = self.shard.apply(view, now, new_oldest, h.data_ptr(), verdict.data_ptr())  # 4-5
+        tick("apply")
         infos = self._allgather([H, g0, last])
+        tick("allgather1")
         rk = None
         if new_oldest > self.oldest:  # step 6
             parts, owner = plan_compaction([tuple(x) for x in infos], n_comb)
-            rk = self._broadcast_key(owner)
+            # the owner reads the new removalKey before its compaction moves the indices
+            key = self.shard.key_at(owner[1]) if owner is not None and owner[0] == self.rank else b""
+            tick("key_at")
             Hn, lastn = self.shard.compact(parts[self.rank], new_oldest)
-            hl = [tuple(x) for x in self._allgather([Hn, lastn])]
+            tick("compact")
+            # one all-gather carries (H, last version) for the carry-ins and a short removalKey
+            inline = key if len(key) <= KEY_INLINE else b""
+            words = [Hn, lastn, len(key)] + _pack_key(inline)
+            got = self._allgather(words)
+            tick("allgather2")
+            hl = [(x[0], x[1]) for x in got]
+            if owner is None:
+                rk = b""  # the scan reached the end: removalKey wraps
+            elif got[owner[0]][2] <= KEY_INLINE:
+                rk = _unpack_key(got[owner[0]][3:], got[owner[0]][2])
+            else:
+                rk = self._broadcast_key(owner, key)
             self.oldest = new_oldest
         else:
             hl = [(x[0], x[2]) for x in infos]
         self.shard.finish(carry_ins(self.v0, hl)[self.rank], rk)  # step 7
+        tick("finish")
+
+    def enable_phase_timing(self, on=True):
+        """Accumulate host wall time per protocol phase (``phase_times``)."""
+        self.phase_s = {} if on else None
+
+    def _tick(self, name):
+        if self.phase_s is None:
+            return
+        t = time.perf_counter()
+        if name is not None:
+            self.phase_s[name] = self.phase_s.get(name, 0.0) + t - self._t
+        self._t = t
 
     def detect_packed(self, batch, now, new_oldest):
         from .batch import DeviceBatch
@@ -319,15 +366,12 @@ class DistShardedConflictSet:
         self.detect_device(db.view, now, new_oldest, verdict)
         return verdict[:batch.T].cpu().numpy()
 
-    def _broadcast_key(self, owner):
-        """The new removalKey from the shard holding the window's end ("" past the end)."""
-        if owner is None:
-            return b""
+    def _broadcast_key(self, owner, key):
+        """A removalKey too long for the all-gather, from the shard that read it."""
         torch, dist = self.torch, self.dist
         buf = torch.zeros(_abi.MAX_KEY + 4, dtype=torch.uint8)
         if owner[0] == self.rank:
-            k = self.shard.key_at(owner[1])
-            buf[:4 + len(k)] = torch.frombuffer(bytearray(len(k).to_bytes(4, "little") + k), dtype=torch.uint8)
+            buf[:4 + len(key)] = torch.frombuffer(bytearray(len(key).to_bytes(4, "little") + key), dtype=torch.uint8)
         buf = buf.to(self.coll_dev)
         dist.broadcast(buf, src=owner[0], group=self.group)
         raw = buf.cpu().numpy()

@@ -260,8 +260,11 @@ int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
  * [0] T  [1] R  [2] W  [3] combined write ranges  [4] history pages the merge
  * rewrote  [5] directory entries  [6] history boundaries  [7] compaction
  * window pages  [8] boundaries surviving in them  [9] transactions with
- * intra-batch sources  [10] decision rounds.  Returns the count written. */
-#define FDBCS_STATS 11
+ * intra-batch sources  [10] decision rounds  [11] 1: a sort bucket
+ * overflowed and the batch's endpoints were bucketed again by splitters from
+ * its own sample  [12] largest sort bucket above 128 records (0: none).
+ * Returns the count written. */
+#define FDBCS_STATS 13
 int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
 
 /* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the

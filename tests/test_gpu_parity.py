@@ -250,3 +250,27 @@ def test_load_dump_roundtrip(cs):
     assert cs.history() == list(zip(keys, vers))
     assert cs.removal_key() == b"ab" * 20
     assert cs.header_version == 11 and cs.oldest_version == 2
+
+
+def test_sort_distribution_shift(cs):
+    """The sort buckets by the previous batch's quantiles; a batch whose keys
+    all lie outside them (a moved key distribution) overflows one bucket, and
+    the guard re-buckets it by splitters from its own sample in the same batch
+    (stats: sort_rebucketed).  Verdicts and history must not change."""
+    import random
+
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    rng = random.Random(7)
+    for i, prefix in enumerate([b"\x00", b"\x00", b"\xff", b"\x80", b"\x80"]):
+        txns = []
+        for _t in range(3000):
+            k = prefix + rng.getrandbits(96).to_bytes(12, "big")
+            w = prefix + rng.getrandbits(96).to_bytes(12, "big")
+            txns.append((100 + 10 * i - rng.randint(1, 15), [(k, k + b"\x00")], [(w, w + b"\x00")]))
+        check_pair(cs, c, PackedBatch.from_txns(txns), 100 + 10 * i, 90 + 10 * i)
+        st = cs.batch_stats()
+        if i in (2, 3):
+            assert st["sort_rebucketed"] == 1, st
+        if i in (1, 4):
+            assert st["sort_rebucketed"] == 0 and st["sort_max_bucket"] <= 512, st

@@ -90,7 +90,7 @@ def test_model_shards_mixed_streams():
             check_step(sh, c, batch, now, nold)
 
 
-def _dist_rank(rank, world, port, bounds, seed, q):
+def _dist_rank(rank, world, port, bounds, seed, maxlen, q):
     import torch.distributed as dist
 
     from foundationdb_amd.sharded import DistShardedConflictSet
@@ -100,24 +100,25 @@ def _dist_rank(rank, world, port, bounds, seed, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard)
     out = []
-    for batch, now, nold in tiny_stream(seed, n_batches=25, maxlen=3):
+    for batch, now, nold in tiny_stream(seed, n_batches=25, maxlen=maxlen):
         v = sh.detect_packed(batch, now, nold)
         out.append((v.tolist(), sh.history(), sh.removal_key(), sh.oldest_version))
     q.put((rank, out))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_dist_sharded_gloo(world):
+@pytest.mark.parametrize("world,maxlen", [(2, 3), (3, 3), (2, 40)])
+def test_dist_sharded_gloo(world, maxlen):
     """world_size 2/3 over gloo: one shard per rank; every rank's verdicts, the
-    concatenation of the ranks' histories and removalKey equal one conflict set's."""
+    concatenation of the ranks' histories and removalKey equal one conflict set's
+    (maxlen 40: removalKeys longer than the all-gather's inline 32 bytes)."""
     rng = random.Random(world)
     bounds = random_bounds(rng, world, 3)
-    seed = 1234 + world
+    seed = 1234 + world + maxlen
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.Random(os.getpid() * 7 + world).randint(0, 3000)
-    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, maxlen, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in range(world))
@@ -125,7 +126,7 @@ def test_dist_sharded_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     c = CpuSpec()
-    for i, (batch, now, nold) in enumerate(tiny_stream(seed, n_batches=25, maxlen=3)):
+    for i, (batch, now, nold) in enumerate(tiny_stream(seed, n_batches=25, maxlen=maxlen)):
         vc = c.detect_packed(batch, now, nold).tolist()
         hist = []
         for r in range(world):
