@@ -80,13 +80,11 @@ FDBCS_FUNCS = [
     ("fdbcs_key_owner", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     ("fdbcs_scatter_verdicts", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("fdbcs_set_shard", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32, C.c_int]),
-    ("fdbcs_shard_check", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
-    ("fdbcs_shard_apply", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
-                                    C.POINTER(C.c_int64)]),
-    ("fdbcs_shard_key_at", C.c_int32, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
-    ("fdbcs_shard_compact", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64,
-                                      C.POINTER(C.c_int64)]),
-    ("fdbcs_shard_finish", C.c_int, [C.c_void_p, C.c_int64, C.c_char_p, C.c_uint32, C.c_int]),
+    ("fdbcs_shard_check", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_shard_apply", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_int64, C.c_char_p,
+                                    C.c_int32, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
+    ("fdbcs_shard_compact", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64, C.c_int64,
+                                      C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
 ]

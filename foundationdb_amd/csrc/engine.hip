@@ -119,6 +119,7 @@ struct fdbcs {
     // exact sharded mode: scratch for a key read back at a local index
     uint64_t* key_out = nullptr;     // hi, lo, meta
     uint8_t* key_out_tail = nullptr;
+    uint8_t* rk_stage = nullptr;     // pinned: removalKey in (hi, lo, meta, tail) form, both directions
     double stage_us[7] = {0};
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
@@ -280,7 +281,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
-    dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
+    dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
     dfree(b.wh.vb);
@@ -332,14 +333,15 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         GROWLOG("W %lld\n", (long long)W);
         int64_t n = std::max<int64_t>(W, 1024);
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
-        dfree(b.cb_slot); dfree(b.ce_slot); free_keys(b.rkb); free_keys(b.rke);
+        dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
         dfree(b.wh.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_combine
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
-            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = alloc_keys(b.rkb, n)) ||
+            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.comb_blk, 2 * (n / 2048 + 2))) ||
+            (r = alloc_keys(b.rkb, n)) ||
             (r = alloc_keys(b.rke, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
@@ -701,6 +703,8 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = dalloc(cs->h.shard_tails, 2 * (FDBCS_MAX_KEY + 16))) || (r = dalloc(cs->key_out, 3)) ||
         (r = dalloc(cs->key_out_tail, FDBCS_MAX_KEY + 16)))
         return fail(r);
+    if (hipHostMalloc((void**)&cs->rk_stage, 24 + FDBCS_MAX_KEY + 64, hipHostMallocDefault) != hipSuccess)
+        return fail(FDBCS_E_NOMEM);
     if (hipMemset(cs->h.shard_tails, 0, 2 * (FDBCS_MAX_KEY + 16)) != hipSuccess) return fail(FDBCS_E_HIP);
     cs->h.shard = ShardBounds{};
     for (int i = 0; i < 8; i++)
@@ -727,6 +731,7 @@ void fdbcs_destroy(fdbcs* cs) {
     dfree(cs->h.tail_arena);
     dfree(cs->h.rk_hi); dfree(cs->h.rk_lo); dfree(cs->h.rk_meta); dfree(cs->h.rk_tail);
     dfree(cs->h.shard_tails); dfree(cs->key_out); dfree(cs->key_out_tail);
+    if (cs->rk_stage) hipHostFree(cs->rk_stage);
     dfree(cs->sc);
     dfree(cs->din);
     if (cs->sc_host) hipHostFree(cs->sc_host);
@@ -1078,7 +1083,8 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
     return FDBCS_OK;
 }
 
-int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, uint8_t* dev_hist) {
+int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
+                      uint8_t* dev_hist) {
     (void)now;
     (void)new_oldest;
     if (!cs || !db) return FDBCS_E_ARG;
@@ -1090,6 +1096,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     cs->last_T = v.txn_count;
     cs->last_R = v.read_count;
     cs->last_W = v.write_count;
+    cs->v0 = carry_in;
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     const bool scatter = cs->have_quantiles;
@@ -1098,25 +1105,43 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
         cs->sorts++;
         cs->have_quantiles = true;
     }
-    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, cs->v0, s);
+    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, carry_in, s);
     if (v.txn_count && dev_hist)
         HIPOK(hipMemcpyAsync(dev_hist, b.hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
     HIPOK(hipStreamSynchronize(s));
     return FDBCS_OK;
 }
 
-int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, const uint8_t* dev_hist,
+int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
+                      const uint8_t* removal_key, int32_t removal_key_len, const uint8_t* dev_hist,
                       uint8_t* dev_verdict, int64_t* info) {
-    if (!cs || !db || !info) return FDBCS_E_ARG;
+    if (!cs || !db || !info || removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
     const fdbcs_batch_view& v = *db;
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     int r;
+    cs->v0 = carry_in;
+    if (removal_key_len >= 0) {  // the previous compaction's removalKey, staged through pinned memory
+        HistBufs& h = cs->h;
+        uint8_t* st = cs->rk_stage;
+        uint64_t rh, rl;
+        uint32_t rm;
+        encode_host(removal_key, (uint32_t)removal_key_len, rh, rl, rm);
+        memcpy(st, &rh, 8);
+        memcpy(st + 8, &rl, 8);
+        memcpy(st + 16, &rm, 4);
+        const uint32_t tl = removal_key_len > 17 ? (uint32_t)removal_key_len - 17 : 0;
+        if (tl) memcpy(st + 24, removal_key + 17, tl);
+        HIPOK(hipMemcpyAsync(h.rk_hi, st, 8, hipMemcpyHostToDevice, s));
+        HIPOK(hipMemcpyAsync(h.rk_lo, st + 8, 8, hipMemcpyHostToDevice, s));
+        HIPOK(hipMemcpyAsync(h.rk_meta, st + 16, 4, hipMemcpyHostToDevice, s));
+        if (tl) HIPOK(hipMemcpyAsync(h.rk_tail, st + 24, (tl + 7) & ~7u, hipMemcpyHostToDevice, s));
+    }
     if (v.txn_count && dev_hist)
         HIPOK(hipMemcpyAsync(b.hist, dev_hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
     launch_decide(v, b, cs->sc, dev_verdict ? dev_verdict : b.verdict, s);
     const bool compact = new_oldest > cs->oldest;
-    launch_merge(v, b, cs->h, cs->cur, cs->sc, now, cs->v0, !compact, s);
+    launch_merge(v, b, cs->h, cs->cur, cs->sc, now, carry_in, !compact, s);
     cs->cur ^= 1;
     if ((r = compact ? sync_state(cs) : sync_batch(cs))) return r;
     const Scalars& h = *cs->sc_host;
@@ -1127,37 +1152,36 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     return h.last_err ? h.last_err : (compact ? h.err : 0);
 }
 
-int32_t fdbcs_shard_key_at(fdbcs* cs, int64_t index, uint8_t* buf, int32_t cap) {
-    if (!cs || index < 0 || index >= cs->known_H) return FDBCS_E_ARG;
-    launch_key_at(cs->h, cs->cur, cs->sc, index, cs->key_out, cs->key_out_tail, cs->stream);
-    uint64_t k3[3];
-    std::vector<uint8_t> t(FDBCS_MAX_KEY + 16);
-    HIPOK(hipMemcpyAsync(k3, cs->key_out, sizeof(k3), hipMemcpyDeviceToHost, cs->stream));
-    HIPOK(hipStreamSynchronize(cs->stream));
-    const uint32_t len = (uint32_t)k3[2] & LEN_MASK;
-    if (len > 17) HIPOK(hipMemcpy(t.data(), cs->key_out_tail, len - 17, hipMemcpyDeviceToHost));
-    const std::vector<uint8_t> k = decode_key(k3[0], k3[1], (uint32_t)k3[2], t.data());
-    if (buf && cap > 0) memcpy(buf, k.data(), std::min<int64_t>(cap, len));
-    return (int32_t)len;
-}
+static constexpr uint32_t RK_TAIL_FAST = 256;  // tail bytes fetched with the key's fixed part
 
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
-                        int64_t* info) {
-    if (!cs || !info || a < 0 || b < a) return FDBCS_E_ARG;
+                        int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {
+    if (!cs || !info || a < 0 || b < a || key_index >= cs->known_H) return FDBCS_E_ARG;
+    hipStream_t s = cs->stream;
+    if (key_index >= 0) {  // the boundary that becomes removalKey, read before the compaction moves it
+        launch_key_at(cs->h, cs->cur, cs->sc, key_index, cs->key_out, cs->key_out_tail, s);
+        HIPOK(hipMemcpyAsync(cs->rk_stage, cs->key_out, 24, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(cs->rk_stage + 24, cs->key_out_tail, RK_TAIL_FAST, hipMemcpyDeviceToHost, s));
+    }
     const WinExplicit w{a, b, keep_first, prev_version};
-    launch_compact(cs->b, cs->h, cs->cur, cs->sc, new_oldest, cs->stream, &w);
+    launch_compact(cs->b, cs->h, cs->cur, cs->sc, new_oldest, s, &w);
     cs->cur ^= 1;
     if (new_oldest > cs->oldest) cs->oldest = new_oldest;
     int r;
     if ((r = sync_batch(cs))) return r;
     info[0] = cs->sc_host->H;
     info[1] = cs->sc_host->last_ver;
+    info[2] = -1;
+    if (key_index >= 0) {
+        uint64_t k3[3];
+        memcpy(k3, cs->rk_stage, 24);
+        const uint32_t len = (uint32_t)k3[2] & LEN_MASK;
+        if (len > 17 + RK_TAIL_FAST)  // a long key: the rest of its tail
+            HIPOK(hipMemcpy(cs->rk_stage + 24 + RK_TAIL_FAST, cs->key_out_tail + RK_TAIL_FAST,
+                            len - 17 - RK_TAIL_FAST, hipMemcpyDeviceToHost));
+        const std::vector<uint8_t> k = decode_key(k3[0], k3[1], (uint32_t)k3[2], cs->rk_stage + 24);
+        info[2] = (int64_t)k.size();
+        if (key_buf && key_cap > 0) memcpy(key_buf, k.data(), std::min<size_t>((size_t)key_cap, k.size()));
+    }
     return cs->sc_host->last_err;
-}
-
-int fdbcs_shard_finish(fdbcs* cs, int64_t carry_in, const uint8_t* removal_key, uint32_t removal_key_len,
-                       int set_removal_key_) {
-    if (!cs) return FDBCS_E_ARG;
-    cs->v0 = carry_in;
-    return set_removal_key_ ? set_removal_key(cs, removal_key, removal_key_len) : FDBCS_OK;
 }

@@ -779,15 +779,17 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     grp_page_find2(g, A.pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
     if (g.lane != 0) return;
     int64_t vb;
+    bool from_v0 = false;  // no boundary below e: the header version (sharded: the carry-in)
     if (ie > 0) vb = A.pool.ver[(int64_t)he.page * PAGE + ie - 1];
-    else if (he.x > 0) vb = A.pool.ver[(int64_t)A.dir.page[he.x - 1] * PAGE + A.dir.cnt[he.x - 1] - 1];
-    else vb = A.v0;
+    else if (he.x > 0 && A.dir.cnt[he.x - 1] > 0)
+        vb = A.pool.ver[(int64_t)A.dir.page[he.x - 1] * PAGE + A.dir.cnt[he.x - 1] - 1];
+    else vb = A.v0, from_v0 = true;  // (only entry 0 can be an empty page)
     A.wh.pb[w] = hb.x;
     A.wh.ib[w] = ib;
     A.wh.cb[w] = hb.cnt;
     A.wh.pe[w] = he.x;
     A.wh.ie[w] = ie;
-    A.wh.feq[w] = eqe;
+    A.wh.feq[w] = (uint8_t)(eqe | from_v0 << 1);  // the merge substitutes its own v0 for bit 1
     A.wh.vb[w] = vb;
 }
 
@@ -959,6 +961,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
 // counter at 0 and ends at the committed END that brings it back to 0.
 struct DecideArgs {
     int T, R, W;
+    int combine;           // 0: the multi-block combine kernels follow (large batches)
     const uint8_t* too_old;
     const uint8_t* hist;
     const int32_t* et;
@@ -1090,6 +1093,14 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
         A.committed[t] = c;
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
+    if (!A.combine) {  // (committed[] is read by the multi-block combine)
+        if (tid == 0) {
+            sc->n_dep = ndep;
+            sc->jac_iters = iters;
+            sc->edges_total = 0;
+        }
+        return;
+    }
     // ---- combine ----
     // committed flag per write, 32 writes per thread-word
     for (int i = tid; i < wwords; i += nthr) {
@@ -1185,10 +1196,126 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
     }
 }
 
+// ---------------------------------------------- multi-block combine ----
+// For batches whose 2W sorted write endpoints exceed what one workgroup keeps
+// in registers: the same sweep (combineWriteConflictRanges,
+// SkipList.cpp:1320-1337) as three grid launches over blocks of CB_BLOCK
+// consecutive endpoints.  d(p) = +1 / -1 at a committed BEGIN / END, else 0;
+// the open-write counter before a block is the sum of d over its
+// predecessors; a range opens where the counter goes 0 -> 1 and closes where
+// it returns to 0.
+//   k_comb_sum  : per-block sum of d
+//   k_comb_open : counter at the block start (predecessor sums), opens per block
+//   k_comb_emit : both prefixes, every range's begin / end slot; n_comb
+static constexpr int CB_THREADS = 256, CB_ITEMS = 16, CB_BLOCK = CB_THREADS * CB_ITEMS;
+
+struct CombArgs {
+    int P;
+    int64_t wbase;
+    const uint32_t* sw_slot;
+    const int32_t* write_txn;
+    const uint8_t* committed;
+    int32_t* bsum;   // [blocks]
+    int32_t* bopen;  // [blocks]
+    int32_t* cb_slot;
+    int32_t* ce_slot;
+    Scalars* sc;
+};
+
+// this thread's CB_ITEMS endpoints: d values (and slots)
+__device__ inline int comb_load(const CombArgs& A, int8_t (&d)[CB_ITEMS], uint32_t (&slot)[CB_ITEMS]) {
+    const int p0 = blockIdx.x * CB_BLOCK + threadIdx.x * CB_ITEMS;
+    uint32_t w[CB_ITEMS];
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) slot[k] = p0 + k < A.P ? A.sw_slot[p0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) w[k] = p0 + k < A.P ? A.write_txn[(slot[k] - A.wbase) >> 1] : 0;
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) {
+        const bool com = p0 + k < A.P && A.committed[w[k]];
+        d[k] = com ? ((slot[k] & 1) ? -1 : 1) : 0;
+        sum += d[k];
+    }
+    return sum;
+}
+
+// sum of x[0 .. nblk) by wave 0, broadcast through LDS
+__device__ inline int pred_sum(const int32_t* x, int nblk, int* s_out) {
+    if (threadIdx.x < 64) {
+        int acc = 0;
+        for (int k = threadIdx.x; k < nblk; k += 64) acc += x[k];
+        acc = wave_reduce_sum(acc);
+        if (threadIdx.x == 0) *s_out = acc;
+    }
+    __syncthreads();
+    return *s_out;
+}
+
+__global__ __launch_bounds__(CB_THREADS) void k_comb_sum(CombArgs A) {
+    __shared__ int32_t red[CB_THREADS / 64 + 1];
+    int8_t d[CB_ITEMS];
+    uint32_t slot[CB_ITEMS];
+    int tot;
+    block_excl_scan(comb_load(A, d, slot), red, tot);
+    if (threadIdx.x == 0) A.bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(CB_THREADS) void k_comb_open(CombArgs A) {
+    __shared__ int32_t red[CB_THREADS / 64 + 1];
+    __shared__ int s0;
+    int8_t d[CB_ITEMS];
+    uint32_t slot[CB_ITEMS];
+    const int sum = comb_load(A, d, slot);
+    const int c0 = pred_sum(A.bsum, blockIdx.x, &s0);
+    int tot;
+    int c = c0 + block_excl_scan(sum, red, tot);
+    int opens = 0;
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) {
+        opens += d[k] == 1 && c == 0;
+        c += d[k];
+    }
+    block_excl_scan(opens, red, tot);
+    if (threadIdx.x == 0) A.bopen[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(CB_THREADS) void k_comb_emit(CombArgs A) {
+    __shared__ int32_t red[CB_THREADS / 64 + 1];
+    __shared__ int s0, s1;
+    int8_t d[CB_ITEMS];
+    uint32_t slot[CB_ITEMS];
+    const int sum = comb_load(A, d, slot);
+    const int c0 = pred_sum(A.bsum, blockIdx.x, &s0);
+    const int g0 = pred_sum(A.bopen, blockIdx.x, &s1);
+    int tot;
+    const int cs = c0 + block_excl_scan(sum, red, tot);
+    int c = cs, opens = 0;
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) {
+        opens += d[k] == 1 && c == 0;
+        c += d[k];
+    }
+    int gtot;
+    int g = g0 + block_excl_scan(opens, red, gtot);
+    c = cs;
+#pragma unroll
+    for (int k = 0; k < CB_ITEMS; k++) {
+        if (d[k] == 1 && c == 0) A.cb_slot[g++] = (int32_t)slot[k];
+        if (d[k] == -1 && c == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // (the open may lie in an earlier block)
+        c += d[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) A.sc->n_comb = g0 + gtot;
+}
+
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s) {
     const int T = v.txn_count;
     if (T == 0) return;  // n_comb was zeroed by k_prep
+    const int P = 2 * v.write_count;
+    const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
+    const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
     DecideArgs A;
+    A.combine = multi ? 0 : 1;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
     A.too_old = b.too_old; A.hist = b.hist; A.et = b.et; A.eu = b.eu; A.bits = b.pair_bits; A.row_words = b.row_words;
     A.edge_cap = b.edge_cap;
@@ -1199,6 +1326,14 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
     const size_t lds = head + dec;
     hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
+    if (multi) {
+        const int nblk = cdiv(P, CB_BLOCK);
+        CombArgs C{P, 2 * (int64_t)v.read_count, b.sw_slot, b.write_txn, b.committed, b.comb_blk,
+                   b.comb_blk + nblk + 1, b.cb_slot, b.ce_slot, sc};
+        hipLaunchKernelGGL(k_comb_sum, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+        hipLaunchKernelGGL(k_comb_open, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+        hipLaunchKernelGGL(k_comb_emit, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+    }
 }
 
 void launch_combine(const fdbcs_batch_view&, BatchBufs&, Scalars*, hipStream_t) {}

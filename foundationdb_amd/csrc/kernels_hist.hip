@@ -99,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 // inside [pb, pe] are wholly erased; they are marked in a difference array
 // (+1 at pb+1, -1 at pe) and resolved by the scan.
 __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, WriteHits wh, int64_t wbase,
-                                                     ShardBounds shard, Scalars* sc, int32_t* __restrict__ pb_o,
+                                                     int64_t v0, ShardBounds shard, Scalars* sc, int32_t* __restrict__ pb_o,
                                                      int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
                                                      int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
                                                      int64_t* __restrict__ vb_o, PageAcc acc, KeyArrays rb,
@@ -114,8 +114,10 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
     const int p_b = wh.pb[wb], i_b = wh.ib[wb], c_b = wh.cb[wb];
     const int p_e = wh.pe[we], i_e = wh.ie[we];
-    const bool found = wh.feq[we];
-    const int64_t vb = wh.vb[we];
+    const bool found = wh.feq[we] & 1;
+    // valueBefore(e) fell back to the header version: the merge's v0 (sharded
+    // mode: the exact carry-in, which may differ from the one the search saw)
+    const int64_t vb = (wh.feq[we] & 2) ? v0 : wh.vb[we];
     // sharded mode (protocol A step 5): a range acts on this shard iff b < hi
     // and e >= lo; its begin node only if b >= lo, its end node only if e < hi
     // (the positions of keys outside the shard clamp to the shard's ends)
@@ -1000,7 +1002,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     if (W > 0) {
         const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
         hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, b.wh,
-                           2 * (int64_t)v.read_count, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
+                           2 * (int64_t)v.read_count, v0, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
     hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
@@ -1050,8 +1052,10 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
             if (g >= r0 && g < g1) {
                 const bool above = pool.ver[(int64_t)pg * PAGE + i] >= oldest;
                 const int64_t pv = i > 0    ? pool.ver[(int64_t)pg * PAGE + i - 1]
-                                   : q > 0 ? pool.ver[(int64_t)dir.page[q - 1] * PAGE + dir.cnt[q - 1] - 1]
-                                           : prev0;  // (sharded: the previous shard's last node)
+                                   : q > 0 && dir.cnt[q - 1] > 0
+                                       ? pool.ver[(int64_t)dir.page[q - 1] * PAGE + dir.cnt[q - 1] - 1]
+                                       : prev0;  // (sharded: the previous shard's last node; only entry 0
+                                                 // can be an empty page)
                 keep = above || pv >= oldest;
             }
             keep_o[(int64_t)w * PAGE + i] = (uint8_t)keep;

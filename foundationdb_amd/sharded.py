@@ -13,22 +13,31 @@ Resolver.actor.cpp:140-153) bit for bit:
 - the concatenated history;
 - removalKey and oldestVersion.
 
-Per batch (the step numbers are SURVEY.md §8e's):
+Per batch (the step numbers are SURVEY.md §8e's), two exchanges:
 
 1-2. ``fdbcs_shard_check``: each shard checks every read clipped to its keys.
-     valueBefore of a clipped begin is the shard's carry-in.
-3.   MAX-reduce of the per-transaction history-conflict flags (T bytes).
-4-5. ``fdbcs_shard_apply``: an identical decision and combine on every
-     shard, then the shard's part of the merge:
-     - a begin node only where the real begin lies;
-     - an end node only in the shard holding the end.
-6.   Compaction over global boundary indices. The window starts at the first
-     boundary >= removalKey anywhere and spans ``3 * |combined| + 10``
-     boundaries. Each shard removes in its part, and the "previous node"
-     crosses shard edges. The shard holding the window's end supplies the
-     new removalKey.
-7.   Carry-ins for the next batch: the version of the nearest earlier
-     non-empty shard's last boundary, else the global header version v0.
+     valueBefore of a clipped begin is the shard's carry-in: the version of
+     the nearest earlier non-empty shard's last boundary after the previous
+     batch's MERGE (or the header version v0).  The previous compaction can
+     change that value only between two versions below oldestVersion, and a
+     checked read's snapshot is >= oldestVersion, so the check cannot tell.
+3.   Exchange 1, one MAX all-reduce of a byte buffer: the per-transaction
+     history-conflict flags (T bytes) followed by one slot per shard that
+     only its owner fills (a MAX over zeros is an all-gather): the shard's
+     (H, last version) after the previous compaction, and the new removalKey
+     from the shard that read it.
+4-5. ``fdbcs_shard_apply`` with the exact carry-in from those slots: an
+     identical decision and combine on every shard, then the shard's part of
+     the merge (a begin node only where the real begin lies, an end node only
+     in the shard holding the end; an end node with no boundary below it in
+     the shard takes the exact carry-in).
+6.   Exchange 2, an all-gather of (H, first index >= removalKey, last
+     version) after the merge.  Compaction over global boundary indices: the
+     window starts at the first boundary >= removalKey anywhere and spans
+     ``3 * |combined| + 10`` boundaries; each shard removes in its part, and
+     the "previous node" crosses shard edges.  The shard holding the window's
+     end reads the new removalKey (delivered in the next exchange 1).
+7.   Carry-ins for the next check from exchange 2's last versions.
 
 Two exchange back ends share the logic below:
 
@@ -36,9 +45,13 @@ Two exchange back ends share the logic below:
   devices). Tests use it.
 - ``DistShardedConflictSet`` is one shard per rank over torch.distributed:
   RCCL over xGMI, or gloo on CPU.
+
+``_Proto`` holds one shard's protocol state; both back ends drive it.
 """
 import ctypes as C
 import time
+
+import numpy as np
 
 from . import _abi
 from ._abi import check
@@ -93,7 +106,8 @@ def plan_compaction(infos, n_comb):
     return parts, owner
 
 
-KEY_INLINE = 32  # removalKeys up to this length travel inside the compaction all-gather
+KEY_INLINE = 32  # removalKeys up to this length travel inside exchange 1
+SLOT_WORDS = 3 + KEY_INLINE // 8  # H, last version, key length (-1: none), key words
 
 
 def _pack_key(key):
@@ -127,41 +141,33 @@ class Shard:
         check(self._lib.fdbcs_set_shard(self.cs.handle, lo_b, len(lo_b), int(lo is not None), hi_b, len(hi_b),
                                         int(hi is not None)), "set_shard")
         self.lo, self.hi = lo, hi
+        self._key = (C.c_uint8 * _abi.MAX_KEY)()
 
-    def check(self, dev_view, now, new_oldest, dev_hist):
-        check(self._lib.fdbcs_shard_check(self.cs.handle, C.byref(dev_view), now, new_oldest, dev_hist), "shard_check")
+    def check(self, dev_view, now, new_oldest, carry, dev_hist):
+        check(self._lib.fdbcs_shard_check(self.cs.handle, C.byref(dev_view), now, new_oldest, carry, dev_hist),
+              "shard_check")
 
-    def apply(self, dev_view, now, new_oldest, dev_hist, dev_verdict):
+    def apply(self, dev_view, now, new_oldest, carry, removal_key, dev_hist, dev_verdict):
         info = (C.c_int64 * 4)()
-        check(self._lib.fdbcs_shard_apply(self.cs.handle, C.byref(dev_view), now, new_oldest, dev_hist, dev_verdict,
-                                          info), "shard_apply")
-        return tuple(info)
-
-    def key_at(self, index):
-        n = check(self._lib.fdbcs_shard_key_at(self.cs.handle, index, None, 0), "shard_key_at")
-        buf = (C.c_uint8 * max(1, n))()
-        self._lib.fdbcs_shard_key_at(self.cs.handle, index, buf, n)
-        return bytes(buf[:n])
-
-    def compact(self, part, new_oldest):
-        a, b, keep_first, prev = part
-        info = (C.c_int64 * 2)()
-        check(self._lib.fdbcs_shard_compact(self.cs.handle, a, b, keep_first, prev, new_oldest, info), "shard_compact")
-        return tuple(info)
-
-    def finish(self, carry_in, removal_key=None):
         rk = removal_key if removal_key is not None else b""
-        check(self._lib.fdbcs_shard_finish(self.cs.handle, carry_in, rk, len(rk), int(removal_key is not None)),
-              "shard_finish")
+        n = len(rk) if removal_key is not None else -1
+        check(self._lib.fdbcs_shard_apply(self.cs.handle, C.byref(dev_view), now, new_oldest, carry, rk, n, dev_hist,
+                                          dev_verdict, info), "shard_apply")
+        return tuple(info)
+
+    def compact(self, part, new_oldest, key_index=-1):
+        a, b, keep_first, prev = part
+        info = (C.c_int64 * 3)()
+        check(self._lib.fdbcs_shard_compact(self.cs.handle, a, b, keep_first, prev, new_oldest, key_index, self._key,
+                                            _abi.MAX_KEY, info), "shard_compact")
+        key = bytes(self._key[:info[2]]) if info[2] >= 0 else None
+        return info[0], info[1], key
 
     def clear(self, v):
         self.cs.clear(v)
 
     def history(self):
         return self.cs.history()
-
-    def removal_key(self):
-        return self.cs.removal_key()
 
     def close(self):
         self.cs.close()
@@ -181,10 +187,67 @@ def _sync(torch, dev):
         torch.cuda.synchronize(dev)
 
 
+class _Proto:
+    """Protocol state of shard g (module docstring, steps 1-7)."""
+
+    def __init__(self, shard, g, v0):
+        self.shard, self.g = shard, g
+        self.v0 = v0                  # header version: the carry-in of a shard with nothing below it
+        self.carry_check = v0         # carry-in after the previous merge (step 7)
+        self.slot = (0, INT64_MIN, -1, b"")  # after the previous compaction: H, last, removalKey read here
+        self.rk_owner = None          # shard whose slot holds the pending removalKey (-1: ""; None: unchanged)
+        self.rk = b""                 # removalKey as delivered
+        self.oldest = 0
+
+    def slot_words(self):
+        H, last, n, key = self.slot
+        return [H, last, n] + _pack_key(key if 0 <= n <= KEY_INLINE else b"")
+
+    def check(self, view, now, new_oldest, hist_ptr):
+        self.shard.check(view, now, new_oldest, self.carry_check, hist_ptr)
+
+    def pending_key(self, slots, long_key=None):
+        """The removalKey the previous compaction produced, from exchange 1's slots (None: unchanged)."""
+        if self.rk_owner is None:
+            return None
+        if self.rk_owner < 0:
+            return b""
+        n = slots[self.rk_owner][2]
+        return _unpack_key(slots[self.rk_owner][3:], n) if n <= KEY_INLINE else long_key
+
+    def apply(self, view, now, new_oldest, slots, hist_ptr, verdict_ptr, long_key=None):
+        carry = carry_ins(self.v0, [(w[0], w[1]) for w in slots])[self.g]
+        rk = self.pending_key(slots, long_key)
+        if rk is not None:
+            self.rk, self.rk_owner = rk, None
+        H, g0, last, n_comb = self.shard.apply(view, now, new_oldest, carry, rk, hist_ptr, verdict_ptr)
+        return (H, g0, last), n_comb
+
+    def compact(self, infos, n_comb, new_oldest):
+        if new_oldest > self.oldest:  # step 6
+            parts, owner = plan_compaction(infos, n_comb)
+            ki = owner[1] if owner is not None and owner[0] == self.g else -1
+            Hn, lastn, key = self.shard.compact(parts[self.g], new_oldest, ki)
+            self.slot = (Hn, lastn, len(key) if key is not None else -1, key or b"")
+            self.rk_owner = owner[0] if owner is not None else -1
+            self.oldest = new_oldest
+        else:
+            H, _g0, last = infos[self.g]
+            self.slot = (H, last, -1, b"")
+        self.carry_check = carry_ins(self.v0, [(x[0], x[2]) for x in infos])[self.g]  # step 7
+
+    def clear(self, v):
+        """clearConflictSet (SkipList.cpp:957-959): empty history, header version v; oldestVersion and
+        removalKey (even one still in flight) are kept."""
+        self.shard.clear(v)
+        self.v0 = self.carry_check = v
+        self.slot = (0, INT64_MIN) + self.slot[2:]
+
+
 class ShardedConflictSet:
-    """All G shards in this process (on one or several devices): the exchange
-    is a device reduction.  ``shard_factory`` builds a shard (tests pass a
-    CPU model of the same interface)."""
+    """All G shards in this process (on one or several devices): the exchanges
+    are a device reduction and host lists.  ``shard_factory`` builds a shard
+    (tests pass a CPU model of the same interface)."""
 
     def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard):
         import torch
@@ -196,16 +259,13 @@ class ShardedConflictSet:
             devices = [d] * len(ranges)
         assert len(devices) == len(ranges)
         self.devices = [_device(torch, d) for d in devices]
-        self.shards = [shard_factory(lo, hi, device=d, v0=v0, max_history=max_history)
-                       for (lo, hi), d in zip(ranges, devices)]
-        self.v0 = v0
-        self.oldest = 0
+        self.protos = [_Proto(shard_factory(lo, hi, device=d, v0=v0, max_history=max_history), g, v0)
+                       for g, ((lo, hi), d) in enumerate(zip(ranges, devices))]
+        self.shards = [p.shard for p in self.protos]
 
     def clear(self, v):
-        """clearConflictSet (SkipList.cpp:957-959): every shard empty, carry-ins v."""
-        for s in self.shards:
-            s.clear(v)
-        self.v0 = v
+        for p in self.protos:
+            p.clear(v)
 
     def detect_device(self, views, now, new_oldest, verdict):
         """views[g]: the batch in shard g's device memory; verdict: uint8 tensor [>= T] on devices[0]."""
@@ -214,17 +274,21 @@ class ShardedConflictSet:
         hs = [torch.empty(max(1, T), dtype=torch.uint8, device=d) for d in self.devices]
         for d in set(self.devices):
             _sync(torch, d)
-        for s, v, h in zip(self.shards, views, hs):  # steps 1-2
-            s.check(v, now, new_oldest, h.data_ptr())
+        for p, v, h in zip(self.protos, views, hs):  # steps 1-2
+            p.check(v, now, new_oldest, h.data_ptr())
         flags = torch.stack([h.to(self.devices[0]) for h in hs]).amax(0)  # step 3: MAX over shards
+        slots = [p.slot_words() for p in self.protos]
         infos, n_comb = [], 0
-        for g, (s, v) in enumerate(zip(self.shards, views)):  # steps 4-5
+        for g, (p, v) in enumerate(zip(self.protos, views)):  # steps 4-5
             f = flags.to(self.devices[g])
             out = verdict if g == 0 else torch.empty(max(1, T), dtype=torch.uint8, device=self.devices[g])
             _sync(torch, self.devices[g])
-            H, g0, last, n_comb = s.apply(v, now, new_oldest, f.data_ptr(), out.data_ptr())
-            infos.append((H, g0, last))
-        self._finish(infos, n_comb, new_oldest)
+            o = p.rk_owner
+            long_key = self.protos[o].slot[3] if o is not None and o >= 0 else None
+            info, n_comb = p.apply(v, now, new_oldest, slots, f.data_ptr(), out.data_ptr(), long_key)
+            infos.append(info)
+        for p in self.protos:  # steps 6-7
+            p.compact(infos, n_comb, new_oldest)
 
     def detect_packed(self, batch, now, new_oldest):
         """A host PackedBatch through the sharded path; returns the verdict bytes (numpy)."""
@@ -238,21 +302,9 @@ class ShardedConflictSet:
         self.detect_device([staged[d].view for d in self.devices], now, new_oldest, verdict)
         return verdict[:batch.T].cpu().numpy()
 
-    def _finish(self, infos, n_comb, new_oldest):
-        rk = None
-        if new_oldest > self.oldest:  # step 6
-            parts, owner = plan_compaction(infos, n_comb)
-            rk = self.shards[owner[0]].key_at(owner[1]) if owner else b""
-            hl = [s.compact(p, new_oldest) for s, p in zip(self.shards, parts)]
-            self.oldest = new_oldest
-        else:
-            hl = [(H, last) for H, _g0, last in infos]
-        for s, c in zip(self.shards, carry_ins(self.v0, hl)):  # step 7
-            s.finish(c, rk)
-
     @property
     def oldest_version(self):
-        return self.oldest
+        return self.protos[0].oldest
 
     def history(self):
         out = []
@@ -261,7 +313,12 @@ class ShardedConflictSet:
         return out
 
     def removal_key(self):
-        return self.shards[0].removal_key()
+        p = self.protos[0]
+        rk = p.pending_key([q.slot_words() for q in self.protos], self._owner_key(p.rk_owner))
+        return p.rk if rk is None else rk
+
+    def _owner_key(self, o):
+        return self.protos[o].slot[3] if o is not None and o >= 0 else None
 
     def close(self):
         for s in self.shards:
@@ -269,7 +326,11 @@ class ShardedConflictSet:
 
 
 class DistShardedConflictSet:
-    """One shard per torch.distributed rank (RCCL over xGMI on MI355X, gloo on CPU)."""
+    """One shard per torch.distributed rank (RCCL over xGMI on MI355X, gloo on CPU).
+
+    Per batch: the engine's check, one MAX all-reduce (flags + slots), the
+    engine's apply, one all-gather of three integers, the engine's compaction.
+    """
 
     def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None, shard_factory=Shard):
         import torch
@@ -281,73 +342,72 @@ class DistShardedConflictSet:
         self.device = _device(torch, device)
         lo, hi = _shard_ranges(bounds)[rank]
         self.shard = shard_factory(lo, hi, device=device, v0=v0, max_history=max_history)
-        self.v0 = v0
-        self.oldest = 0
+        self.proto = _Proto(self.shard, rank, v0)
         backend = dist.get_backend(group)
         self.coll_dev = self.device if backend == "nccl" else torch.device("cpu")
         self._T = -1
         self.phase_s = None
 
     def clear(self, v):
-        self.shard.clear(v)
-        self.v0 = v
+        self.proto.clear(v)
 
     def _buffers(self, T):
         if T != self._T:
             torch = self.torch
+            n = max(1, T) + self.world * SLOT_WORDS * 8
             self._h = torch.empty(max(1, T), dtype=torch.uint8, device=self.device)
-            self._hc = self._h if self.coll_dev == self.device else torch.empty(max(1, T), dtype=torch.uint8)
+            self._x1 = torch.empty(n, dtype=torch.uint8, device=self.coll_dev)
             self._T = T
-        return self._h, self._hc
+        return self._h, self._x1
 
     def detect_device(self, view, now, new_oldest, verdict):
         """view: the whole batch in this rank's device memory; verdict: uint8 tensor [>= T] there."""
-        torch, dist = self.torch, self.dist
+        torch, dist, p = self.torch, self.dist, self.proto
         tick = self._tick
         tick(None)
-        h, hc = self._buffers(view.txn_count)
+        T = view.txn_count
+        h, x1 = self._buffers(T)
+        nT = max(1, T)
         _sync(torch, self.device)
-        self.shard.check(view, now, new_oldest, h.data_ptr())  # steps 1-2 (synchronous)
+        p.check(view, now, new_oldest, h.data_ptr())  # steps 1-2 (synchronous)
         tick("check")
-        if hc is not h:
-            hc.copy_(h)
-        dist.all_reduce(hc, op=dist.ReduceOp.MAX, group=self.group)  # step 3
-        if hc is not h:
-            h.copy_(hc)
-        _sync(torch, self.device)  # the engine reads h on its own stream
-        tick("flags_allreduce")
-        H, g0, last, n_comb = self.shard.apply(view, now, new_oldest, h.data_ptr(), verdict.data_ptr())  # 4-5
-        tick("apply")
-        infos = self._allgather([H, g0, last])
-        tick("allgather1")
-        rk = None
-        if new_oldest > self.oldest:  # step 6
-            parts, owner = plan_compaction([tuple(x) for x in infos], n_comb)
-            # the owner reads the new removalKey before its compaction moves the indices
-            key = self.shard.key_at(owner[1]) if owner is not None and owner[0] == self.rank else b""
-            tick("key_at")
-            Hn, lastn = self.shard.compact(parts[self.rank], new_oldest)
-            tick("compact")
-            # one all-gather carries (H, last version) for the carry-ins and a short removalKey
-            inline = key if len(key) <= KEY_INLINE else b""
-            words = [Hn, lastn, len(key)] + _pack_key(inline)
-            got = self._allgather(words)
-            tick("allgather2")
-            hl = [(x[0], x[1]) for x in got]
-            if owner is None:
-                rk = b""  # the scan reached the end: removalKey wraps
-            elif got[owner[0]][2] <= KEY_INLINE:
-                rk = _unpack_key(got[owner[0]][3:], got[owner[0]][2])
-            else:
-                rk = self._broadcast_key(owner, key)
-            self.oldest = new_oldest
+        # exchange 1: flags + this shard's slot, zeros elsewhere; MAX all-reduce
+        mine = np.zeros(self.world * SLOT_WORDS, np.int64)
+        mine[self.rank * SLOT_WORDS:(self.rank + 1) * SLOT_WORDS] = p.slot_words()
+        x1[nT:].copy_(torch.from_numpy(mine.view(np.uint8)))
+        x1[:nT].copy_(h)
+        dist.all_reduce(x1, op=dist.ReduceOp.MAX, group=self.group)
+        slots = torch.empty(self.world * SLOT_WORDS * 8, dtype=torch.uint8)
+        slots.copy_(x1[nT:])
+        slots = slots.numpy().view(np.int64).reshape(self.world, SLOT_WORDS).tolist()
+        if x1.device != self.device:
+            h.copy_(x1[:nT])
+            fl = h
         else:
-            hl = [(x[0], x[2]) for x in infos]
-        self.shard.finish(carry_ins(self.v0, hl)[self.rank], rk)  # step 7
-        tick("finish")
+            fl = x1
+        _sync(torch, self.device)  # the engine reads the flags on its own stream
+        tick("exchange1")
+        long_key = None
+        o = p.rk_owner
+        if o is not None and o >= 0 and slots[o][2] > KEY_INLINE:
+            long_key = self._broadcast_key(o, p.slot[3] if o == self.rank else b"")
+        info, n_comb = p.apply(view, now, new_oldest, slots, fl.data_ptr(), verdict.data_ptr(), long_key)  # 4-5
+        tick("apply")
+        infos = [tuple(x) for x in self._allgather(list(info))]  # exchange 2
+        tick("exchange2")
+        p.compact(infos, n_comb, new_oldest)  # steps 6-7
+        tick("compact")
+
+    def detect_packed(self, batch, now, new_oldest):
+        from .batch import DeviceBatch
+
+        db = DeviceBatch(batch, self.device)
+        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.device)
+        self.detect_device(db.view, now, new_oldest, verdict)
+        return verdict[:batch.T].cpu().numpy()
 
     def enable_phase_timing(self, on=True):
-        """Accumulate host wall time per protocol phase (``phase_times``)."""
+        """Accumulate host wall time per protocol phase (``phase_s``)."""
         self.phase_s = {} if on else None
 
     def _tick(self, name):
@@ -358,22 +418,14 @@ class DistShardedConflictSet:
             self.phase_s[name] = self.phase_s.get(name, 0.0) + t - self._t
         self._t = t
 
-    def detect_packed(self, batch, now, new_oldest):
-        from .batch import DeviceBatch
-
-        db = DeviceBatch(batch, self.device)
-        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.device)
-        self.detect_device(db.view, now, new_oldest, verdict)
-        return verdict[:batch.T].cpu().numpy()
-
     def _broadcast_key(self, owner, key):
-        """A removalKey too long for the all-gather, from the shard that read it."""
+        """A removalKey too long for exchange 1's slot, from the shard that read it."""
         torch, dist = self.torch, self.dist
         buf = torch.zeros(_abi.MAX_KEY + 4, dtype=torch.uint8)
-        if owner[0] == self.rank:
+        if owner == self.rank:
             buf[:4 + len(key)] = torch.frombuffer(bytearray(len(key).to_bytes(4, "little") + key), dtype=torch.uint8)
         buf = buf.to(self.coll_dev)
-        dist.broadcast(buf, src=owner[0], group=self.group)
+        dist.broadcast(buf, src=owner, group=self.group)
         raw = buf.cpu().numpy()
         n = int.from_bytes(raw[:4].tobytes(), "little")
         return raw[4:4 + n].tobytes()
@@ -387,13 +439,22 @@ class DistShardedConflictSet:
 
     @property
     def oldest_version(self):
-        return self.oldest
+        return self.proto.oldest
 
     def history(self):
         return self.shard.history()
 
+    def history_size(self):
+        return self.shard.cs.history_size()
+
     def removal_key(self):
-        return self.shard.removal_key()
+        """The global removalKey (collective when the last compaction's key is still in flight)."""
+        p = self.proto
+        if p.rk_owner is None:
+            return p.rk
+        if p.rk_owner < 0:
+            return b""
+        return self._broadcast_key(p.rk_owner, p.slot[3] if p.rk_owner == self.rank else b"")
 
     def close(self):
         self.shard.close()

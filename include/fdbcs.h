@@ -194,36 +194,39 @@ int  fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo,
                      const uint8_t* hi, uint32_t hi_len, int has_hi);
 
 /* Phase 1 (steps 1-2): ingest, endpoint sort, intra-batch overlaps, and the
- * history check of every read clipped to the shard.  dev_hist receives T
- * bytes (1: the transaction conflicts with this shard's history); the host
- * MAX-reduces them over the shards (RCCL all-reduce). */
+ * history check of every read clipped to the shard.  carry_in: the version of
+ * the last boundary below lo after the previous batch's merge (its
+ * compaction can change that only between versions below oldestVersion,
+ * which no checked read can tell apart).  dev_hist receives T bytes (1: the
+ * transaction conflicts with this shard's history); the host MAX-reduces
+ * them over the shards (RCCL all-reduce). */
 int  fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now,
-                       int64_t new_oldest, uint8_t* dev_hist);
+                       int64_t new_oldest, int64_t carry_in, uint8_t* dev_hist);
 
 /* Phase 2 (steps 4-5): the decision from the reduced flags (identical on
  * every shard, verdicts to dev_verdict), the combine, and the shard's part of
- * the merge.  info[0] = boundaries H, [1] = index of the shard's first
- * boundary >= removalKey when a compaction follows (else -1), [2] = version
- * of its last boundary (INT64_MIN: none), [3] = combined write ranges.
- * When new_oldest > oldestVersion, fdbcs_shard_compact must follow. */
+ * the merge.  carry_in: the exact carry-in after the previous batch's
+ * compaction (end nodes created with no boundary below them in the shard
+ * take it).  removal_key / removal_key_len >= 0: the removalKey the previous
+ * batch's compaction produced (-1: unchanged).  info[0] = boundaries H,
+ * [1] = index of the shard's first boundary >= removalKey when a compaction
+ * follows (else -1), [2] = version of its last boundary (INT64_MIN: none),
+ * [3] = combined write ranges (global).  When new_oldest > oldestVersion,
+ * fdbcs_shard_compact must follow. */
 int  fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now, int64_t new_oldest,
+                       int64_t carry_in, const uint8_t* removal_key, int32_t removal_key_len,
                        const uint8_t* dev_hist, uint8_t* dev_verdict, int64_t* info);
-
-/* The key of the boundary at local index (after phase 2): the new
- * removalKey, read on the shard that holds the global window's end. */
-int32_t fdbcs_shard_key_at(fdbcs* cs, int64_t index, uint8_t* buf, int32_t cap);
 
 /* Phase 3 (step 6): removeBefore over this shard's part [a, b) of the global
  * window (local indices).  keep_first: a is the window's first node (never
  * removed); prev_version: the version of the node before local index 0 (the
- * previous non-empty shard's last).  info[0] = H, info[1] = last version. */
+ * previous non-empty shard's last).  key_index >= 0: this shard holds the
+ * window's end -- the key there (the new removalKey) is read before the
+ * compaction into key_buf (key_cap bytes).  info[0] = H, info[1] = last
+ * version, info[2] = the key's length (-1: none read). */
 int  fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version,
-                         int64_t new_oldest, int64_t* info);
-
-/* Step 7: the shard's carry-in for the next batch and, when set_removal_key,
- * the global removalKey. */
-int  fdbcs_shard_finish(fdbcs* cs, int64_t carry_in, const uint8_t* removal_key, uint32_t removal_key_len,
-                        int set_removal_key);
+                         int64_t new_oldest, int64_t key_index, uint8_t* key_buf, int32_t key_cap,
+                         int64_t* info);
 
 /* ---- Introspection (tests, bench, checkpoint) --------------------------------- */
 

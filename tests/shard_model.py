@@ -1,7 +1,7 @@
 """CPU model of one shard of the exact sharded mode (test infrastructure).
 
 Implements the interface of ``foundationdb_amd.sharded.Shard`` (check / apply
-/ key_at / compact / finish) over a Python sorted list, so the host protocol
+/ compact / clear / history) over a Python sorted list, so the host protocol
 (``plan_compaction``, ``carry_ins``, the removalKey broadcast, the gloo/RCCL
 exchanges of ``DistShardedConflictSet``) runs without a GPU and is checked
 against the single-resolver oracle (``oracle.spec``).  Each step restates
@@ -50,7 +50,8 @@ class ModelShard:
         i = bisect_left(self.keys, k)
         return self.vers[i - 1] if i > 0 else self.v0
 
-    def check(self, view, now, new_oldest, dev_hist):
+    def check(self, view, now, new_oldest, carry, dev_hist):
+        self.v0 = carry
         txns = self._txns(view)
         out = _bytes_at(dev_hist, len(txns))
         for t, (snap, reads, _w) in enumerate(txns):
@@ -72,7 +73,10 @@ class ModelShard:
                 if m > snap:
                     out[t] = 1
 
-    def apply(self, view, now, new_oldest, dev_hist, dev_verdict):
+    def apply(self, view, now, new_oldest, carry, removal_key, dev_hist, dev_verdict):
+        self.v0 = carry
+        if removal_key is not None:
+            self.rk = removal_key
         txns = self._txns(view)
         T = len(txns)
         hist = _bytes_at(dev_hist, T).copy()
@@ -125,11 +129,9 @@ class ModelShard:
         g0 = bisect_left(self.keys, self.rk) if new_oldest > self.oldest else -1
         return H, g0, (self.vers[-1] if H else INT64_MIN), len(combined)
 
-    def key_at(self, index):
-        return self.keys[index]
-
-    def compact(self, part, new_oldest):
+    def compact(self, part, new_oldest, key_index=-1):
         a, b, keep_first, prev = part
+        key = self.keys[key_index] if key_index >= 0 else None
         keep_k, keep_v = self.keys[:a], self.vers[:a]
         for i in range(a, b):
             pv = self.vers[i - 1] if i > 0 else prev
@@ -139,12 +141,7 @@ class ModelShard:
         self.keys = keep_k + self.keys[b:]
         self.vers = keep_v + self.vers[b:]
         self.oldest = max(self.oldest, new_oldest)
-        return len(self.keys), (self.vers[-1] if self.keys else INT64_MIN)
-
-    def finish(self, carry_in, removal_key=None):
-        self.v0 = carry_in
-        if removal_key is not None:
-            self.rk = removal_key
+        return len(self.keys), (self.vers[-1] if self.keys else INT64_MIN), key
 
     def clear(self, v):
         self.keys, self.vers = [], []
@@ -152,9 +149,6 @@ class ModelShard:
 
     def history(self):
         return list(zip(self.keys, self.vers))
-
-    def removal_key(self):
-        return self.rk
 
     def close(self):
         pass

@@ -274,3 +274,24 @@ def test_sort_distribution_shift(cs):
             assert st["sort_rebucketed"] == 1, st
         if i in (1, 4):
             assert st["sort_rebucketed"] == 0 and st["sort_max_bucket"] <= 512, st
+
+
+@pytest.mark.parametrize("T,force", [(20000, False), (1500, True)])
+def test_large_batches_multiblock_combine(cs, T, force):
+    """Batches past one workgroup's register budget (2W > 32768 endpoints)
+    combine with the multi-block kernels; small ones can be forced onto them."""
+    if force:
+        os.environ["FDBCS_TEST_MULTIBLOCK_COMBINE"] = "1"
+    try:
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        wl = Workload(2, txns=T)
+        for i in range(6):
+            batch, now, nold = wl.batch(i)
+            check_pair(cs, c, batch, now, nold, history=(i % 2 == 1))
+        wl3 = Workload(3, txns=T)  # Zipf: long intra-batch chains, touching ranges
+        for i in range(6, 10):
+            batch, now, nold = wl3.batch(i)
+            check_pair(cs, c, batch, now, nold, history=(i % 2 == 1))
+    finally:
+        os.environ.pop("FDBCS_TEST_MULTIBLOCK_COMBINE", None)
