@@ -274,7 +274,7 @@ void free_plan(BatchBufs& b) {
 }
 
 void free_batch(BatchBufs& b) {
-    dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
+    dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict); dfree(b.dec_blk);
     dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
     dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
@@ -304,12 +304,13 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (T > cs->capT) {
         GROWLOG("T %lld\n", (long long)T);
         int64_t n = std::max<int64_t>(T, 1024);
-        dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict);
+        dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict); dfree(b.dec_blk);
         dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
         // +64: k_decide_combine reads these byte arrays as 4-byte words
         if ((r = dalloc(b.too_old, n + 64)) || (r = dalloc(b.hist, n + 64)) || (r = dalloc(b.committed, n)) ||
             (r = dalloc(b.verdict, n)) || (r = dalloc(b.deg, n)) || (r = dalloc(b.off, n + 1)) ||
-            (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)))
+            (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)) ||
+            (r = dalloc(b.dec_blk, 2 * (n / 256 + 2))))
             return r;
         // dedup matrix: rows of ceil(n/32) words, zero between batches
         dfree(b.pair_bits);

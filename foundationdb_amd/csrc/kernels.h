@@ -65,6 +65,7 @@ struct BatchBufs {
     int32_t* eu;         // [edge_cap] earlier writer
     int32_t* csr;        // [edge_cap] sources bucketed by reader
     int32_t* comb_blk;   // [2 * (combine blocks + 1)] multi-block combine: per-block sums, opens
+    int32_t* dec_blk;    // [2 * (T / 256 + 2)] grid decision: dependents and their sources per block
     int64_t edge_cap;
     // combined write ranges [W], as key slots of their begin / end
     int32_t* cb_slot;

@@ -65,6 +65,7 @@ struct IngestArgs {
     int64_t oldest;
     uint8_t* too_old;
     uint8_t* hist;
+    int32_t* deg;
     int32_t* read_txn;
     int64_t* read_snap;
     int32_t* write_txn;
@@ -486,6 +487,7 @@ __global__ __launch_bounds__(256) void k_ingest(IngestArgs A, SortJobs J) {
         const bool too = sn < A.oldest && r1 > r0;
         A.too_old[t] = too ? 1 : 0;
         A.hist[t] = 0;
+        A.deg[t] = 0;
         for (int r = r0; r < r1; r++) {
             A.read_txn[r] = t;
             A.read_snap[r] = too ? INT64_MAX : sn;  // the read check skips too-old transactions
@@ -687,7 +689,7 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
     A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
     A.write_txn = b.write_txn;
-    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc;
+    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
     const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     if (scatter)
@@ -741,11 +743,12 @@ __device__ inline int ub_key(const SRec* a, int n, const Key& k, const uint8_t* 
 }
 
 __device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, int32_t* et, int32_t* eu,
-                                 int64_t cap, Scalars* sc) {
+                                 int64_t cap, Scalars* sc, int32_t* deg) {
     uint32_t* word = bits + (int64_t)t * row_words + (u >> 5);
     const uint32_t bit = 1u << (u & 31);
     const uint32_t old = atomicOr(word, bit);
     if (!(old & bit)) {
+        atomicAdd(&deg[t], 1);  // (sources per reader, for the grid decision; zeroed by the ingest)
         const int idx = atomicAdd(&sc->edges_total, 1);
         if (idx < cap) {
             et[idx] = t;
@@ -811,6 +814,7 @@ struct EdgesArgs {
     int32_t* eu;
     int64_t cap;
     Scalars* sc;
+    int32_t* deg;
 };
 
 // The two searches of an edge lane: an LDS sample of the sorted array's first
@@ -886,7 +890,7 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
             const uint32_t slot = A.sw[k].idx;
             if (slot & 1) continue;  // a write end
             const int u = A.write_txn[(slot - wbase) >> 1];
-            if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc);
+            if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
         }
     } else if (i < R + W) {
         const int w = i - R;
@@ -899,7 +903,7 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
         bsearch2(A.sr, b, true, lb, hb, e, le, he, tails, lo, hi);
         for (int k = lo; k < hi; k++) {
             const int t = A.read_txn[A.sr[k].idx >> 1];
-            if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc);
+            if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
         }
     }
 }
@@ -930,7 +934,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const int R = v.read_count, W = v.write_count;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc};
+                 b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
@@ -1308,12 +1312,187 @@ __global__ __launch_bounds__(CB_THREADS) void k_comb_emit(CombArgs A) {
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) A.sc->n_comb = g0 + gtot;
 }
 
+static void launch_combine_grid(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
+    const int P = 2 * v.write_count;
+    const int nblk = cdiv(P, CB_BLOCK);
+    CombArgs C{P, 2 * (int64_t)v.read_count, b.sw_slot, b.write_txn, b.committed, b.comb_blk,
+               b.comb_blk + nblk + 1, b.cb_slot, b.ce_slot, sc};
+    hipLaunchKernelGGL(k_comb_sum, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+    hipLaunchKernelGGL(k_comb_open, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+    hipLaunchKernelGGL(k_comb_emit, dim3(nblk), dim3(CB_THREADS), 0, s, C);
+}
+
+// ------------------------------------------------------ grid decision ----
+// For batches past one workgroup's LDS / register budget.  The same rule
+// (checkIntraBatchConflicts, SkipList.cpp:1133-1153) in three launches:
+//   k_dec_flags : a lane per txn: undecided = !tooOld && !history conflict;
+//                 with no intra-batch source (deg from the edge kernel) it is
+//                 final; per-block counts of dependents and their sources
+//   k_dec_place : dependents' positions in index order and their CSR offsets
+//                 (predecessor sums + a block scan)
+//   k_dec_walk  : one workgroup: the CSR of the dependents' sources, the
+//                 committed bits in LDS, and the ordered walk in chunks of 64
+//                 (Jacobi on ballots, as in k_decide_combine)
+static constexpr int DG_THREADS = 256;
+
+struct DecGridArgs {
+    int T;
+    const uint8_t* too_old;
+    const uint8_t* hist;
+    const int32_t* deg;
+    const int32_t* et;
+    const int32_t* eu;
+    int64_t edge_cap;
+    uint32_t* bits;
+    int row_words;
+    int32_t* bd;        // [blocks] dependents per block
+    int32_t* be;        // [blocks] their sources per block
+    int32_t* didx;      // [T] dependent index or -1
+    int32_t* dep_list;  // [T] dependents in index order
+    int32_t* doff;      // [ndep + 1] CSR offsets per dependent
+    int32_t* cur;       // [ndep] CSR fill cursors
+    int32_t* csr;
+    uint8_t* committed;
+    uint8_t* verdict;
+    Scalars* sc;
+};
+
+__device__ inline uint8_t verdict_of(bool committed, bool too_old) {
+    return committed ? FDBCS_COMMITTED : (too_old ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+}
+
+__global__ __launch_bounds__(DG_THREADS) void k_dec_flags(DecGridArgs A) {
+    __shared__ int64_t red[DG_THREADS / 64 + 1];
+    const int t = blockIdx.x * DG_THREADS + threadIdx.x;
+    bool dep = false;
+    int d = 0;
+    if (t < A.T) {
+        const bool to = A.too_old[t];
+        const bool und = !to && !A.hist[t];
+        d = A.deg[t];
+        dep = und && d > 0;
+        A.committed[t] = und && !dep;  // (a dependent starts uncommitted: k_dec_walk reads these as bits)
+        if (!dep) A.verdict[t] = verdict_of(und, to);
+    }
+    int64_t tot;
+    block_excl_scan(dep ? ((int64_t)1 << 32) | (uint32_t)d : (int64_t)0, red, tot);
+    if (threadIdx.x == 0) {
+        A.bd[blockIdx.x] = (int32_t)(tot >> 32);
+        A.be[blockIdx.x] = (int32_t)(uint32_t)tot;
+    }
+}
+
+__global__ __launch_bounds__(DG_THREADS) void k_dec_place(DecGridArgs A) {
+    __shared__ int64_t red[DG_THREADS / 64 + 1];
+    __shared__ int s0, s1;
+    const int t = blockIdx.x * DG_THREADS + threadIdx.x;
+    const int nd0 = pred_sum(A.bd, blockIdx.x, &s0);
+    const int eo0 = pred_sum(A.be, blockIdx.x, &s1);
+    bool dep = false;
+    int d = 0;
+    if (t < A.T) {
+        d = A.deg[t];
+        dep = !A.too_old[t] && !A.hist[t] && d > 0;
+    }
+    int64_t tot;
+    const int64_t ex = block_excl_scan(dep ? ((int64_t)1 << 32) | (uint32_t)d : (int64_t)0, red, tot);
+    if (t < A.T) {
+        const int k = nd0 + (int)(ex >> 32);
+        A.didx[t] = dep ? k : -1;
+        if (dep) {
+            A.dep_list[k] = t;
+            A.doff[k] = eo0 + (int)(uint32_t)ex;
+            A.cur[k] = 0;
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        const int nd = nd0 + (int)(tot >> 32);
+        A.doff[nd] = eo0 + (int)(uint32_t)tot;
+        A.sc->n_dep = nd;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
+    extern __shared__ uint32_t cbits[];  // committed, a bit per txn
+    const int T = A.T, tid = threadIdx.x, nthr = blockDim.x;
+    Scalars* sc = A.sc;
+    const int E = (int)min((int64_t)sc->edges_total, A.edge_cap);
+    const int ndep = sc->n_dep;
+    for (int i = tid; i < (T + 31) / 32; i += nthr) {
+        uint32_t m = 0;
+        for (int k = 0; k < 32 && 32 * i + k < T; k++) m |= (uint32_t)(A.committed[32 * i + k] != 0) << k;
+        cbits[i] = m;
+    }
+    for (int e = tid; e < E; e += nthr) {
+        const int t = A.et[e], u = A.eu[e];
+        const int k = A.didx[t];
+        if (k >= 0) A.csr[A.doff[k] + atomicAdd(&A.cur[k], 1)] = u;
+        A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
+    }
+    __syncthreads();
+    int iters = 0;
+    if (tid < 64) {
+        const int lane = tid;
+        for (int c0 = 0; c0 < ndep; c0 += 64) {
+            const int k = c0 + lane;
+            const bool valid = k < ndep;
+            const int t = valid ? A.dep_list[k] : 0;
+            bool ext = false;
+            uint64_t L = 0;
+            if (valid) {
+                for (int e = A.doff[k], e1 = A.doff[k + 1]; e < e1 && !ext; e++) {
+                    const int u = A.csr[e];
+                    const int di = A.didx[u];
+                    if (di >= c0) L |= 1ull << (di - c0);
+                    else ext = (cbits[u >> 5] >> (u & 31)) & 1;
+                }
+            }
+            const uint64_t vm = __ballot(valid);
+            const uint64_t em = __ballot(valid && ext);
+            uint64_t cm = vm & ~em;
+            while (true) {
+                const bool ci = valid && !ext && (L & cm) == 0;
+                const uint64_t nm = __ballot(ci);
+                iters++;
+                if (nm == cm) break;
+                cm = nm;
+            }
+            const bool c = valid && ((cm >> lane) & 1);
+            if (c) atomicOr(&cbits[t >> 5], 1u << (t & 31));
+            if (valid) {
+                A.committed[t] = c;
+                A.verdict[t] = verdict_of(c, false);  // (a dependent is not tooOld)
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (tid == 0) {
+        sc->jac_iters = iters;
+        sc->edges_total = 0;  // next batch starts a new edge list
+    }
+}
+
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s) {
     const int T = v.txn_count;
     if (T == 0) return;  // n_comb was zeroed by k_prep
     const int P = 2 * v.write_count;
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
     const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
+    const int force_grid = getenv("FDBCS_TEST_GRID_DECISION") ? 1 : 0;  // (tests)
+    if (T > LDS_T || force_grid) {  // grid decision, then the multi-block combine
+        const int nb = cdiv(T, DG_THREADS);
+        DecGridArgs G;
+        G.T = T; G.too_old = b.too_old; G.hist = b.hist; G.deg = b.deg; G.et = b.et; G.eu = b.eu;
+        G.edge_cap = b.edge_cap; G.bits = b.pair_bits; G.row_words = b.row_words;
+        G.bd = b.dec_blk; G.be = b.dec_blk + nb + 1; G.didx = b.dep_idx; G.dep_list = b.dep_list; G.doff = b.off;
+        G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.verdict = verdict; G.sc = sc;
+        hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
+        hipLaunchKernelGGL(k_dec_place, dim3(nb), dim3(DG_THREADS), 0, s, G);
+        hipLaunchKernelGGL(k_dec_walk, dim3(1), dim3(1024), (size_t)((T + 31) / 32) * 4, s, G);
+        if (P > 0) launch_combine_grid(v, b, sc, s);
+        return;
+    }
     DecideArgs A;
     A.combine = multi ? 0 : 1;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
@@ -1326,14 +1505,7 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
     const size_t lds = head + dec;
     hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
-    if (multi) {
-        const int nblk = cdiv(P, CB_BLOCK);
-        CombArgs C{P, 2 * (int64_t)v.read_count, b.sw_slot, b.write_txn, b.committed, b.comb_blk,
-                   b.comb_blk + nblk + 1, b.cb_slot, b.ce_slot, sc};
-        hipLaunchKernelGGL(k_comb_sum, dim3(nblk), dim3(CB_THREADS), 0, s, C);
-        hipLaunchKernelGGL(k_comb_open, dim3(nblk), dim3(CB_THREADS), 0, s, C);
-        hipLaunchKernelGGL(k_comb_emit, dim3(nblk), dim3(CB_THREADS), 0, s, C);
-    }
+    if (multi) launch_combine_grid(v, b, sc, s);
 }
 
 void launch_combine(const fdbcs_batch_view&, BatchBufs&, Scalars*, hipStream_t) {}

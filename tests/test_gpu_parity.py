@@ -276,12 +276,14 @@ def test_sort_distribution_shift(cs):
             assert st["sort_rebucketed"] == 0 and st["sort_max_bucket"] <= 512, st
 
 
-@pytest.mark.parametrize("T,force", [(20000, False), (1500, True)])
+@pytest.mark.parametrize("T,force", [(20000, None), (1500, "FDBCS_TEST_MULTIBLOCK_COMBINE"),
+                                     (1500, "FDBCS_TEST_GRID_DECISION"), (9000, None)])
 def test_large_batches_multiblock_combine(cs, T, force):
     """Batches past one workgroup's register budget (2W > 32768 endpoints)
-    combine with the multi-block kernels; small ones can be forced onto them."""
+    combine with the multi-block kernels, and past its LDS budget (T > 8192)
+    decide with the grid kernels; small ones can be forced onto them."""
     if force:
-        os.environ["FDBCS_TEST_MULTIBLOCK_COMBINE"] = "1"
+        os.environ[force] = "1"
     try:
         cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
         c = CpuSpec()
@@ -294,4 +296,5 @@ def test_large_batches_multiblock_combine(cs, T, force):
             batch, now, nold = wl3.batch(i)
             check_pair(cs, c, batch, now, nold, history=(i % 2 == 1))
     finally:
-        os.environ.pop("FDBCS_TEST_MULTIBLOCK_COMBINE", None)
+        if force:
+            os.environ.pop(force, None)
