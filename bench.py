@@ -116,10 +116,20 @@ class Source:
         return sub.view(), now, nold, batch.T, idx, (sub, batch)
 
 
-def pipeline_bytes(key_bytes, T, h_pre, h_post):
+CONFIG_SHAPE = {
+    1: "skiplisttest keys (12 x '.' + BE32), 1R+1W",
+    2: "5R+2W, uniform 16-byte keys",
+    3: "5R+2W, Zipf(0.99) hot 16-byte keys over 10^6 ranks (long intra-batch chains)",
+    4: "4 point reads + 1 wide read (10^3-10^5 boundaries) + 2W, 68-100-byte keys (tail compares)",
+}
+
+
+def pipeline_bytes(key_bytes, T, h_pre, h_post, cfg=2):
     """SURVEY.md §8d algorithmic bytes per batch: inputs + 8 T snapshots + T
-    verdicts + E (H_pre + H_post) (history read once, written once)."""
-    return key_bytes + 9.0 * T + E_HIST * (h_pre + h_post)
+    verdicts + E (H_pre + H_post) (history read once, written once); E = 28 B
+    for keys <= 17 B, 32 B (8-B meta with a tail offset) for config 4."""
+    e = 32.0 if cfg == 4 else E_HIST
+    return key_bytes + 9.0 * T + e * (h_pre + h_post)
 
 
 def stage_bytes(name, st, key_bytes):
@@ -260,7 +270,7 @@ def main():
     roofline = None
     if mode == "exact":  # per-GPU algorithmic bytes (its shard's history) over the per-batch wall time
         nbytes = float(np.mean([x[6] for x in staged[:args.steps]]))
-        algo = pipeline_bytes(nbytes, Tg, H_pre_local, H_post_local)
+        algo = pipeline_bytes(nbytes, Tg, H_pre_local, H_post_local, cfg)
         batch_us = elapsed / args.steps * 1e6
         achieved = algo / (batch_us * 1e-6) / 1e9
         roofline = {
@@ -290,7 +300,7 @@ def main():
         cs.enable_stage_timing(False)
         mean = np.array(st_us).mean(axis=0)  # [6 stages..., whole batch] us
         batch_us = float(mean[6])
-        algo = float(np.mean([pipeline_bytes(nb, T, a, b) for a, b, nb, T in hp]))
+        algo = float(np.mean([pipeline_bytes(nb, T, a, b, cfg) for a, b, nb, T in hp]))
         dom = int(np.argmax(mean[:6]))
         dom_bytes = float(np.mean([stage_bytes(STAGES[dom], s, nb) for s, (_a, _b, nb, _T) in zip(stats, hp)]))
         achieved = algo / (batch_us * 1e-6) / 1e9
@@ -352,7 +362,7 @@ def main():
             workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
                         f"5M-version window; {world} key-range resolvers (proxy split + RCCL MIN combine)")
         else:
-            workload = f"config{cfg}: {Tg}-txn batches, 5R+2W, uniform 16-byte keys, 5M-version window"
+            workload = f"config{cfg}: {Tg}-txn batches, {CONFIG_SHAPE.get(cfg, '')}, 5M-version window"
         out = {
             "metric": "resolved txns/sec (whole node) at 5k-txn batches; p99 detectConflicts latency",
             "value": round(value, 1),
