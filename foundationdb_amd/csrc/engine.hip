@@ -294,12 +294,22 @@ void free_batch(BatchBufs& b) {
 }
 
 
+int grow_edges(BatchBufs& b, int64_t n) {
+    int r;
+    dfree(b.et); dfree(b.eu); dfree(b.csr);
+    b.edge_cap = 0;
+    if ((r = dalloc(b.et, n)) || (r = dalloc(b.eu, n)) || (r = dalloc(b.csr, n))) return r;
+    b.edge_cap = n;
+    return FDBCS_OK;
+}
+
 // Size the per-batch buffers (grow only).
 int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes) {
     BatchBufs& b = cs->b;
     int r;
     hipStream_t s = cs->stream;
-    if (T > 65536) return FDBCS_E_CAPACITY;  // T x T pair matrix bound
+    if (T > MAX_T) return FDBCS_E_CAPACITY;  // DESIGN.md §Large batches
+    b.large = large_batch_mode(T);
     if (!b.scan_tmp && (r = dalloc(b.scan_tmp, 1024))) return r;
     if (T > cs->capT) {
         GROWLOG("T %lld\n", (long long)T);
@@ -312,17 +322,28 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)) ||
             (r = dalloc(b.dec_blk, 2 * (n / 256 + 2))))
             return r;
-        // dedup matrix: rows of ceil(n/32) words, zero between batches
-        dfree(b.pair_bits);
-        b.row_words = (int32_t)((n + 31) / 32);
-        if ((r = dalloc(b.pair_bits, n * b.row_words))) return r;
-        HIPOK(hipMemsetAsync(b.pair_bits, 0, (size_t)n * b.row_words * 4, s));
-        dfree(b.et); dfree(b.eu); dfree(b.csr);
-        b.edge_cap = std::max<int64_t>(1, n * (n - 1) / 2);
-        if ((r = dalloc(b.et, b.edge_cap)) || (r = dalloc(b.eu, b.edge_cap)) || (r = dalloc(b.csr, b.edge_cap)))
-            return r;
         cs->capT = n;
     }
+    int64_t need_edges;
+    if (!b.large) {
+        // dedup matrix: rows of ceil(n/32) words, zero between batches; unique
+        // pairs u < t bound the edge list
+        const int64_t n = std::max<int64_t>(T, 1024);
+        if (n > b.pair_T) {
+            dfree(b.pair_bits);
+            b.row_words = (int32_t)((n + 31) / 32);
+            if ((r = dalloc(b.pair_bits, n * b.row_words))) return r;
+            HIPOK(hipMemsetAsync(b.pair_bits, 0, (size_t)n * b.row_words * 4, s));
+            b.pair_T = n;
+        }
+        need_edges = std::max<int64_t>(1, n * (n - 1) / 2);
+    } else {
+        // undeduplicated edges: a first guess linear in the batch; run_batch
+        // grows the list and re-runs the search if a batch overflows it
+        const char* test_cap = getenv("FDBCS_TEST_EDGE_CAP");  // (tests: reach the overflow path)
+        need_edges = test_cap ? std::max(1, atoi(test_cap)) : std::max<int64_t>(1 << 20, 2 * (R + W));
+    }
+    if (need_edges > b.edge_cap && (r = grow_edges(b, need_edges))) return r;
     if (R > cs->capR) {
         GROWLOG("R %lld\n", (long long)R);
         int64_t n = std::max<int64_t>(R, 1024);
@@ -367,7 +388,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         if ((r = dalloc(b.ss_bkt, n))) return r;
         cs->capSortRec = n;
     }
-    const int64_t stage = sort_staging_records((int)R, (int)W);
+    const int64_t stage = sort_staging_records((int)R, (int)W, b.large);
     if (stage > b.ss_tmp_cap) {
         const int64_t n = std::max<int64_t>(stage, 1 << 16);
         dfree(b.ss_tmp);
@@ -463,6 +484,29 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
     return FDBCS_OK;
 }
 
+// History read check + overlap edges.  Large batches keep duplicate edges in
+// a list sized linearly in the batch: if it overflowed, grow it to the count
+// the kernel reached and search again (the read check is idempotent; the
+// per-reader source counts restart from zero).
+int edges_read_check(fdbcs* cs, const fdbcs_batch_view& v, int64_t v0) {
+    BatchBufs& b = cs->b;
+    hipStream_t s = cs->stream;
+    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s);
+    if (!b.large) return FDBCS_OK;
+    int32_t total = 0;
+    HIPOK(hipMemcpyAsync(&total, &cs->sc->edges_total, sizeof(total), hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    if (total >= 0 && total <= b.edge_cap) return FDBCS_OK;
+    if (total < 0) return FDBCS_E_CAPACITY;  // (more than 2^31 overlap pairs in one batch)
+    GROWLOG("edges %d\n", total);
+    int r;
+    if ((r = grow_edges(b, (int64_t)total + total / 4 + 1024))) return r;
+    HIPOK(hipMemsetAsync(b.deg, 0, (size_t)v.txn_count * sizeof(int32_t), s));
+    HIPOK(hipMemsetAsync(&cs->sc->edges_total, 0, sizeof(int32_t), s));
+    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s);
+    return FDBCS_OK;
+}
+
 void record(fdbcs* cs, int i) {
     if (cs->timing) hipEventRecord(cs->ev[i], cs->stream);
 }
@@ -484,7 +528,8 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     Scalars* sc = cs->sc;
     record(cs, 0);
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
-    const bool scatter = cs->have_quantiles && !no_fuse;  // steady state: the ingest scatters the sort records
+    // steady state: the ingest scatters the sort records (large batches merge-sort instead)
+    const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), s);
     record(cs, 1);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
@@ -492,7 +537,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
         cs->have_quantiles = true;
     }
     record(cs, 2);
-    launch_edges_read_check(v, b, h, cs->cur, sc, cs->v0, s);
+    if ((r = edges_read_check(cs, v, cs->v0))) return r;
     record(cs, 3);
     launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s);
     record(cs, 4);
@@ -1100,13 +1145,13 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     cs->v0 = carry_in;
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
-    const bool scatter = cs->have_quantiles;
+    const bool scatter = cs->have_quantiles && !b.large;
     launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), s);
     if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
-    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, carry_in, s);
+    if ((r = edges_read_check(cs, v, carry_in))) return r;
     if (v.txn_count && dev_hist)
         HIPOK(hipMemcpyAsync(dev_hist, b.hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
     HIPOK(hipStreamSynchronize(s));

@@ -59,8 +59,10 @@ struct BatchBufs {
     SRec* ss_tmp;        // bucket staging rows
     int64_t ss_tmp_cap;
     // intra-batch overlap dedup matrix and edges
-    uint32_t* pair_bits; // [T * row_words]
+    uint32_t* pair_bits; // [pair_T * row_words] (small batches only)
     int32_t row_words;
+    int64_t pair_T;      // rows of pair_bits
+    bool large;          // large-batch mode (large_batch_mode): merge sort, undeduplicated edges
     int32_t* et;         // [edge_cap] reader of each unique overlap pair
     int32_t* eu;         // [edge_cap] earlier writer
     int32_t* csr;        // [edge_cap] sources bucketed by reader
@@ -145,7 +147,14 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s);
-int64_t sort_staging_records(int R, int W);
+int64_t sort_staging_records(int R, int W, bool large);
+// Large-batch mode (T > LARGE_T, or forced by FDBCS_TEST_LARGE_BATCH for tests):
+// the endpoint sort is a merge sort (no per-batch splitter balance limits)
+// and overlap edges are not deduplicated through the T x T pair matrix, so
+// memory stays linear in the batch.  Up to MAX_T transactions.
+constexpr int64_t LARGE_T = 65536;
+constexpr int64_t MAX_T = 1310720;  // k_dec_walk keeps a committed bit per txn in LDS (160 KiB)
+bool large_batch_mode(int64_t T);
 // history read check + intra-batch overlap edges, one launch
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s);

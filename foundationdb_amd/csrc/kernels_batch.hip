@@ -642,6 +642,154 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
     }
 }
 
+// ---- large batches: merge sort ------------------------------------------
+// Past LARGE_T transactions one batch holds millions of endpoints (config 5:
+// 5 M read begins, 4 M write endpoints), far beyond what 1,024 buckets of
+// <= 512 records can take.  The large-batch sort is a plain merge sort over
+// the same total order (rec_lt), so its output is identical:
+//   k_ms_tile  : a workgroup bitonic-sorts MS_TILE records in LDS;
+//   k_ms_merge : one pass merges sorted runs pairwise -- each workgroup takes
+//                MS_CHUNK outputs, finds where its two merge-path diagonals
+//                cut the runs (binary searches in global memory), stages the
+//                two input pieces in LDS and every lane merges MS_ITEMS
+//                outputs from its own diagonal;
+//   k_ms_finish: compact slot copy of the write endpoints, the quantiles the
+//                next (small) batch splits by, zeroed bucket counters.
+// Jobs ping-pong between their output array and a scratch array; the tile
+// sort starts in whichever makes the last pass land in the output.
+static constexpr int MS_TILE = 2048;
+static constexpr int MS_THREADS = 256;
+static constexpr int MS_ITEMS = 8;
+static constexpr int MS_CHUNK = MS_THREADS * MS_ITEMS;
+
+struct MergeSortArgs {
+    int32_t n[2];
+    int64_t sbase[2];
+    int32_t sstride[2];
+    int32_t passes[2];
+    SRec* buf[2][2];      // [job][0]: output, [job][1]: scratch
+    int32_t blocks0;      // blocks of job 0 in this launch
+};
+
+static int ms_passes(int n) {
+    int p = 0;
+    for (int64_t w = MS_TILE; w < n; w <<= 1) p++;
+    return p;
+}
+
+__global__ __launch_bounds__(MS_THREADS) void k_ms_tile(MergeSortArgs M, KeyArrays keys) {
+    __shared__ uint64_t s_hi[MS_TILE], s_lo[MS_TILE], s_mi[MS_TILE];
+    const int job = (int)blockIdx.x < M.blocks0 ? 0 : 1;
+    const int tile = job ? blockIdx.x - M.blocks0 : blockIdx.x;
+    const int n = M.n[job];
+    const int64_t i0 = (int64_t)tile * MS_TILE;
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    for (int k = threadIdx.x; k < MS_TILE; k += MS_THREADS) {
+        const int64_t i = i0 + k;
+        L.put(k, i < n ? load_rec(keys, M.sbase[job] + i * M.sstride[job]) : rec_inf());
+    }
+    __syncthreads();
+    lds_bitonic(L, MS_TILE, keys.tail);
+    SRec* dst = M.buf[job][M.passes[job] & 1];
+    for (int k = threadIdx.x; k < MS_TILE && i0 + k < n; k += MS_THREADS) dst[i0 + k] = L.get(k);
+}
+
+// number of records taken from a (the rest from b) among the first d of the
+// merge of sorted a[0, la) and b[0, lb); records are distinct
+template <typename GetA, typename GetB>
+__device__ inline int merge_path(GetA ga, int la, GetB gb, int lb, int d, const uint8_t* const* tails) {
+    int lo = max(0, d - lb), hi = min(d, la);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rec_lt(ga(mid), gb(d - 1 - mid), tails)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(MS_THREADS) void k_ms_merge(MergeSortArgs M, int pass, KeyArrays keys) {
+    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
+    __shared__ int s_cut[2];
+    const int job = (int)blockIdx.x < M.blocks0 ? 0 : 1;
+    const int chunk = job ? blockIdx.x - M.blocks0 : blockIdx.x;
+    const int n = M.n[job];
+    const int P = M.passes[job];
+    const SRec* src = M.buf[job][(P - pass) & 1];
+    SRec* dst = M.buf[job][(P - pass - 1) & 1];
+    const uint8_t* const* tails = keys.tail;
+    const int64_t w = (int64_t)MS_TILE << pass;
+    const int64_t o0 = (int64_t)chunk * MS_CHUNK;
+    const int64_t base = o0 / (2 * w) * (2 * w);
+    const int la = (int)min<int64_t>(w, n - base);
+    const int lb = (int)max<int64_t>(0, min<int64_t>(w, n - base - w));
+    const SRec* A = src + base;
+    const SRec* B = src + base + la;
+    const int d0 = (int)(o0 - base), d1 = min(d0 + MS_CHUNK, la + lb);
+    if (threadIdx.x < 2) {
+        const int d = threadIdx.x ? d1 : d0;
+        s_cut[threadIdx.x] = merge_path([&](int i) { return A[i]; }, la, [&](int i) { return B[i]; }, lb, d, tails);
+    }
+    __syncthreads();
+    const int a0 = s_cut[0], a1 = s_cut[1];
+    const int b0 = d0 - a0, b1 = d1 - a1;
+    const int na = a1 - a0, nb = b1 - b0;
+    const LdsRecs L{s_hi, s_lo, s_mi};  // [0, na): a piece, [na, na + nb): b piece
+    for (int k = threadIdx.x; k < na + nb; k += MS_THREADS) L.put(k, k < na ? A[a0 + k] : B[b0 + k - na]);
+    __syncthreads();
+    const int dl = threadIdx.x * MS_ITEMS;
+    if (dl >= na + nb) return;
+    int ia = merge_path([&](int i) { return L.get(i); }, na, [&](int i) { return L.get(na + i); }, nb, dl, tails);
+    int ib = dl - ia;
+    SRec* out = dst + base + d0 + dl;
+    const int cnt = min(MS_ITEMS, na + nb - dl);
+    for (int k = 0; k < cnt; k++) {
+        bool takeA;
+        if (ia >= na) takeA = false;
+        else if (ib >= nb) takeA = true;
+        else takeA = rec_lt(L.get(ia), L.get(na + ib), tails);
+        out[k] = takeA ? L.get(ia++) : L.get(na + ib++);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ms_finish(MergeSortArgs M, SortJobs J, KeyArrays keys) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < M.n[1]) J.out_slot[g] = M.buf[1][0][g].idx;
+    if (g < 2 * SS_Q) {
+        const int job = (int)(g / SS_Q), q = (int)(g % SS_Q);
+        const int64_t n = M.n[job];
+        if (n > 0) put_quantile(J, job, q, M.buf[job][0][q * n / SS_Q], keys.tail);
+    }
+    if (g < 2 * SS_MAXB) J.cnt_next[g] = 0;  // (this path leaves the current parity's counters zero)
+}
+
+static void launch_merge_sort(const SortJobs& J, BatchBufs& b, hipStream_t s) {
+    MergeSortArgs M;
+    for (int j = 0; j < 2; j++) {
+        M.n[j] = J.n[j];
+        M.sbase[j] = J.sbase[j];
+        M.sstride[j] = J.sstride[j];
+        M.passes[j] = ms_passes(J.n[j]);
+        M.buf[j][0] = J.out[j];
+    }
+    M.buf[0][1] = b.ss_tmp;
+    M.buf[1][1] = b.ss_tmp + J.n[0];
+    M.blocks0 = cdiv(M.n[0], MS_TILE);
+    const int tiles = M.blocks0 + cdiv(M.n[1], MS_TILE);
+    if (tiles > 0) hipLaunchKernelGGL(k_ms_tile, dim3(tiles), dim3(MS_THREADS), 0, s, M, b.keys);
+    const int P = std::max(M.passes[0], M.passes[1]);
+    for (int p = 0; p < P; p++) {
+        MergeSortArgs Mp = M;
+        for (int j = 0; j < 2; j++)
+            if (p >= M.passes[j]) Mp.n[j] = 0;  // this job is already sorted (no blocks)
+        // (n is kept for the jobs that take part: block counts from their sizes)
+        Mp.blocks0 = cdiv(Mp.n[0], MS_CHUNK);
+        const int blocks = Mp.blocks0 + cdiv(Mp.n[1], MS_CHUNK);
+        hipLaunchKernelGGL(k_ms_merge, dim3(blocks), dim3(MS_THREADS), 0, s, Mp, p, b.keys);
+    }
+    const int64_t fin = std::max<int64_t>(std::max(M.n[1], 2 * SS_MAXB), 2 * SS_Q);
+    hipLaunchKernelGGL(k_ms_finish, dim3(cdiv(fin, 256)), dim3(256), 0, s, M, J, b.keys);
+}
+
 static int ss_buckets(int n) {
     // FDBCS_TEST_SORT_BUCKETS forces few buckets so tests reach the LDS and
     // global-memory bucket paths
@@ -654,7 +802,14 @@ static int ss_buckets(int n) {
 }
 
 // Staging records the sort needs (engine sizes b.ss_tmp).
-int64_t sort_staging_records(int, int) { return 2 * (int64_t)SS_MAXB * SS_ROW; }
+int64_t sort_staging_records(int R, int W, bool large) {
+    const int64_t small = 2 * (int64_t)SS_MAXB * SS_ROW;
+    return large ? std::max<int64_t>(small, (int64_t)R + 2 * (int64_t)W) : small;
+}
+
+bool large_batch_mode(int64_t T) {
+    return T > LARGE_T || getenv("FDBCS_TEST_LARGE_BATCH") != nullptr;  // (tests: the large path at small T)
+}
 
 static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity) {
     const int R = v.read_count, W = v.write_count;
@@ -704,6 +859,10 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
     if (J.n[0] + J.n[1] == 0) return false;
+    if (b.large) {
+        launch_merge_sort(J, b, s);
+        return true;
+    }
     if (!scattered) {  // (otherwise the ingest already put every record into its bucket)
         if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 0);
         hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
@@ -744,10 +903,13 @@ __device__ inline int ub_key(const SRec* a, int n, const Key& k, const uint8_t* 
 
 __device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, int32_t* et, int32_t* eu,
                                  int64_t cap, Scalars* sc, int32_t* deg) {
-    uint32_t* word = bits + (int64_t)t * row_words + (u >> 5);
-    const uint32_t bit = 1u << (u & 31);
-    const uint32_t old = atomicOr(word, bit);
-    if (!(old & bit)) {
+    bool fresh = true;
+    if (bits) {  // small batches: dedup through the pair matrix (large batches keep duplicates, which are harmless)
+        uint32_t* word = bits + (int64_t)t * row_words + (u >> 5);
+        const uint32_t bit = 1u << (u & 31);
+        fresh = !(atomicOr(word, bit) & bit);
+    }
+    if (fresh) {
         atomicAdd(&deg[t], 1);  // (sources per reader, for the grid decision; zeroed by the ingest)
         const int idx = atomicAdd(&sc->edges_total, 1);
         if (idx < cap) {
@@ -934,7 +1096,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const int R = v.read_count, W = v.write_count;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
+                 b.large ? nullptr : b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
@@ -1427,7 +1589,7 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
         const int t = A.et[e], u = A.eu[e];
         const int k = A.didx[t];
         if (k >= 0) A.csr[A.doff[k] + atomicAdd(&A.cur[k], 1)] = u;
-        A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
+        if (A.bits) A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
     }
     __syncthreads();
     int iters = 0;
@@ -1480,11 +1642,11 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
     const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
     const int force_grid = getenv("FDBCS_TEST_GRID_DECISION") ? 1 : 0;  // (tests)
-    if (T > LDS_T || force_grid) {  // grid decision, then the multi-block combine
+    if (T > LDS_T || force_grid || b.large) {  // grid decision, then the multi-block combine
         const int nb = cdiv(T, DG_THREADS);
         DecGridArgs G;
         G.T = T; G.too_old = b.too_old; G.hist = b.hist; G.deg = b.deg; G.et = b.et; G.eu = b.eu;
-        G.edge_cap = b.edge_cap; G.bits = b.pair_bits; G.row_words = b.row_words;
+        G.edge_cap = b.edge_cap; G.bits = b.large ? nullptr : b.pair_bits; G.row_words = b.row_words;
         G.bd = b.dec_blk; G.be = b.dec_blk + nb + 1; G.didx = b.dep_idx; G.dep_list = b.dep_list; G.doff = b.off;
         G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.verdict = verdict; G.sc = sc;
         hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
