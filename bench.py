@@ -59,16 +59,31 @@ E_HIST = 28.0  # SURVEY.md §8d bytes per boundary (16-B prefix + 8-B version + 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=2500)
+    p.add_argument("--steps", type=int, default=None, help="measured batches (default 200; config 5: 10)")
+    p.add_argument("--warmup", type=int, default=None,
+                   help="untimed batches before them (default 2500; config 5: 2, after the 10^8-boundary preload)")
     p.add_argument("--config", type=int, default=2)
-    p.add_argument("--txns", type=int, default=5000, help="transactions per batch per GPU")
+    p.add_argument("--txns", type=int, default=None, help="transactions per batch per GPU (default 5000; config 5: 10^6)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--stage-batches", type=int, default=50, help="extra instrumented batches after the timed region")
+    p.add_argument("--stage-batches", type=int, default=None,
+                   help="extra instrumented batches after the timed region (default 50; config 5: 3)")
     p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
                    help="N > 1: one exact resolver sharded by key range, or N independent key-range resolvers")
-    return p.parse_args()
+    a = p.parse_args()
+    big = a.config == 5  # 1 M-txn batches over a preloaded 10^8-boundary history
+    for name, small, large in [("steps", 200, 10), ("warmup", 2500, 2), ("txns", 5000, 1_000_000),
+                               ("stage_batches", 50, 3)]:
+        if getattr(a, name) is None:
+            setattr(a, name, large if big else small)
+    return a
+
+
+PRELOAD_BATCHES = 50  # config 5: 50 blind-write batches of 10^6 point writes
+
+
+def max_history(cfg):
+    return 130_000_000 if cfg == 5 else 30_000_000
 
 
 def to_device(v, torch, dev):
@@ -121,6 +136,7 @@ CONFIG_SHAPE = {
     2: "5R+2W, uniform 16-byte keys",
     3: "5R+2W, Zipf(0.99) hot 16-byte keys over 10^6 ranks (long intra-batch chains)",
     4: "4 point reads + 1 wide read (10^3-10^5 boundaries) + 2W, 68-100-byte keys (tail compares)",
+    5: "5R+2W, uniform 16-byte keys, history preloaded to 10^8 boundaries (50 blind-write batches of 10^6)",
 }
 
 
@@ -156,7 +172,7 @@ def time_resolvers(args, world, rank, dev, torch, dist):
     from foundationdb_amd.resolvers import scatter_verdicts
 
     src = Source(args.config, args.txns, world, rank, split=True)
-    cs = ConflictSet(device=dev.index, max_history=30_000_000)
+    cs = ConflictSet(device=dev.index, max_history=max_history(args.config))
     out = None
     for i in range(args.warmup):
         v, now, nold, _T, _idx, _keep = src.host(i)
@@ -221,10 +237,10 @@ def main():
     eng = None
     if mode == "exact":
         from foundationdb_amd.sharded import DistShardedConflictSet
-        eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=30_000_000)
+        eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=max_history(cfg))
         cs = eng.shard.cs
     else:
-        cs = ConflictSet(device=local, max_history=30_000_000)
+        cs = ConflictSet(device=local, max_history=max_history(cfg))
 
     def global_h():
         """History size of the whole resolver (the sum over shards in exact mode)."""
@@ -236,8 +252,13 @@ def main():
     t_w = time.time()
     verdict_host = None
     wverd = None
-    for i in range(args.warmup):
-        v, now, nold, _T, _idx, _keep = src.host(i)
+    pre = None
+    if cfg == 5:  # preload: blind-write batches (config 50 of the generator), no compaction
+        pre = Source(50, args.txns, world, rank, split=(mode == "resolvers"))
+    n_pre = PRELOAD_BATCHES if pre is not None else 0
+    for j in range(n_pre + args.warmup):
+        i = j - n_pre
+        v, now, nold, _T, _idx, _keep = (pre.host(j) if i < 0 else src.host(i))
         if mode == "exact":
             db = DeviceBatch(v, dev)
             if wverd is None or wverd.numel() < max(1, v.txn_count):
@@ -245,8 +266,8 @@ def main():
             eng.detect_device(db.view, now, nold, wverd)
         else:
             verdict_host = cs.detect_view(v, now, nold, verdict_host)
-        if rank == 0 and (i + 1) % 500 == 0:
-            print(f"# warmup {i + 1}/{args.warmup} H={cs.history_size()} {time.time() - t_w:.1f}s",
+        if rank == 0 and ((j + 1) % 500 == 0 or pre is not None):
+            print(f"# warmup {j + 1}/{n_pre + args.warmup} H={cs.history_size()} {time.time() - t_w:.1f}s",
                   file=sys.stderr, flush=True)
     H_pre = global_h()
     H_pre_local = cs.history_size()
