@@ -77,6 +77,9 @@ FDBCS_FUNCS = [
     ("fdbcs_split_batch", C.c_int,
      [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(BatchView), C.c_void_p,
       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fdbcs_split_batch_keep_all", C.c_int,
+     [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(BatchView), C.c_void_p,
+      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fdbcs_key_owner", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     ("fdbcs_scatter_verdicts", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     ("fdbcs_set_shard", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32, C.c_int]),
@@ -85,6 +88,10 @@ FDBCS_FUNCS = [
                                     C.c_int32, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]),
     ("fdbcs_shard_compact", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64, C.c_int64,
                                       C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
+    ("fdbcs_shard_set_protocol", C.c_int, [C.c_void_p, C.c_int]),
+    ("fdbcs_shard_edge_count", C.c_int64, [C.c_void_p]),
+    ("fdbcs_shard_get_edges", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+    ("fdbcs_shard_set_edges", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
 ]

@@ -199,6 +199,7 @@ struct Scalars {
     int32_t ss_over[2];     // a sort bucket of job j overflowed its staging row (the guard re-buckets)
     int32_t ss_maxc;        // stats: largest sort bucket above the register path (0: none)
     int32_t extra_total;    // free pages the merge takes (parts beyond each page's first)
+    int32_t n_comb_own;     // combined ranges whose begin lies in this shard (all of them unsharded)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 

@@ -123,6 +123,7 @@ struct fdbcs {
     double stage_us[7] = {0};
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
+    bool sparse_edges = false;    // exact sharded protocol B: this shard exports its overlap edges
     int64_t last_T = 0, last_R = 0, last_W = 0;  // shape of the last batch (stats)
     int64_t sorts = 0;                           // sorts launched (sort-counter parity)
 };
@@ -310,6 +311,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     hipStream_t s = cs->stream;
     if (T > MAX_T) return FDBCS_E_CAPACITY;  // DESIGN.md §Large batches
     b.large = large_batch_mode(T);
+    b.dedup = !b.large && !cs->sparse_edges;
     if (!b.scan_tmp && (r = dalloc(b.scan_tmp, 1024))) return r;
     if (T > cs->capT) {
         GROWLOG("T %lld\n", (long long)T);
@@ -325,7 +327,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         cs->capT = n;
     }
     int64_t need_edges;
-    if (!b.large) {
+    if (b.dedup) {
         // dedup matrix: rows of ceil(n/32) words, zero between batches; unique
         // pairs u < t bound the edge list
         const int64_t n = std::max<int64_t>(T, 1024);
@@ -492,7 +494,7 @@ int edges_read_check(fdbcs* cs, const fdbcs_batch_view& v, int64_t v0) {
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s);
-    if (!b.large) return FDBCS_OK;
+    if (b.dedup) return FDBCS_OK;
     int32_t total = 0;
     HIPOK(hipMemcpyAsync(&total, &cs->sc->edges_total, sizeof(total), hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
@@ -1152,8 +1154,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
         cs->have_quantiles = true;
     }
     if ((r = edges_read_check(cs, v, carry_in))) return r;
-    if (v.txn_count && dev_hist)
-        HIPOK(hipMemcpyAsync(dev_hist, b.hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
+    if (dev_hist) launch_flags_out(b, v.txn_count, dev_hist, s);
     HIPOK(hipStreamSynchronize(s));
     return FDBCS_OK;
 }
@@ -1183,8 +1184,7 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
         HIPOK(hipMemcpyAsync(h.rk_meta, st + 16, 4, hipMemcpyHostToDevice, s));
         if (tl) HIPOK(hipMemcpyAsync(h.rk_tail, st + 24, (tl + 7) & ~7u, hipMemcpyHostToDevice, s));
     }
-    if (v.txn_count && dev_hist)
-        HIPOK(hipMemcpyAsync(b.hist, dev_hist, (size_t)v.txn_count, hipMemcpyDeviceToDevice, s));
+    if (dev_hist) launch_flags_in(b, v.txn_count, dev_hist, s);
     launch_decide(v, b, cs->sc, dev_verdict ? dev_verdict : b.verdict, s);
     const bool compact = new_oldest > cs->oldest;
     launch_merge(v, b, cs->h, cs->cur, cs->sc, now, carry_in, !compact, s);
@@ -1194,11 +1194,45 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     info[0] = h.H;
     info[1] = compact ? h.win_g0 : -1;
     info[2] = h.last_ver;
-    info[3] = h.n_comb;
+    info[3] = h.n_comb_own;
     return h.last_err ? h.last_err : (compact ? h.err : 0);
 }
 
 static constexpr uint32_t RK_TAIL_FAST = 256;  // tail bytes fetched with the key's fixed part
+
+int fdbcs_shard_set_protocol(fdbcs* cs, int sparse_edges) {
+    if (!cs || cs->in_batch) return FDBCS_E_ARG;
+    cs->sparse_edges = sparse_edges != 0;
+    return FDBCS_OK;
+}
+
+int64_t fdbcs_shard_edge_count(fdbcs* cs) {
+    if (!cs) return FDBCS_E_ARG;
+    int32_t n = 0;
+    HIPOK(hipMemcpyAsync(&n, &cs->sc->edges_total, sizeof(n), hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return n;
+}
+
+int fdbcs_shard_get_edges(fdbcs* cs, int32_t* dev_et, int32_t* dev_eu, int64_t n) {
+    if (!cs || n < 0 || n > cs->b.edge_cap || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
+    if (n) {
+        HIPOK(hipMemcpyAsync(dev_et, cs->b.et, (size_t)n * 4, hipMemcpyDeviceToDevice, cs->stream));
+        HIPOK(hipMemcpyAsync(dev_eu, cs->b.eu, (size_t)n * 4, hipMemcpyDeviceToDevice, cs->stream));
+    }
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return FDBCS_OK;
+}
+
+int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_eu, int64_t n) {
+    if (!cs || n < 0 || n > INT32_MAX || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
+    BatchBufs& b = cs->b;
+    if (b.dedup) return FDBCS_E_ARG;  // (protocol B only: fdbcs_shard_set_protocol)
+    int r;
+    if (n > b.edge_cap && (r = grow_edges(b, n + n / 4 + 1024))) return r;
+    launch_set_edges(b, cs->sc, (int)cs->last_T, dev_et, dev_eu, n, cs->stream);
+    return FDBCS_OK;
+}
 
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
                         int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {

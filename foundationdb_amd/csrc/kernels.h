@@ -63,6 +63,7 @@ struct BatchBufs {
     int32_t row_words;
     int64_t pair_T;      // rows of pair_bits
     bool large;          // large-batch mode (large_batch_mode): merge sort, undeduplicated edges
+    bool dedup;          // overlap pairs deduplicated through pair_bits (small batches, own decision)
     int32_t* et;         // [edge_cap] reader of each unique overlap pair
     int32_t* eu;         // [edge_cap] earlier writer
     int32_t* csr;        // [edge_cap] sources bucketed by reader
@@ -160,6 +161,12 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
                              hipStream_t s);
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
+// exact sharded mode: per-transaction exchange flags (0 / 1 history conflict /
+// 2 tooOld) out of and back into the batch state; a foreign edge list in
+void launch_flags_out(const BatchBufs& b, int T, uint8_t* flags, hipStream_t s);
+void launch_flags_in(BatchBufs& b, int T, const uint8_t* flags, hipStream_t s);
+void launch_set_edges(BatchBufs& b, Scalars* sc, int T, const int32_t* et, const int32_t* eu, int64_t n,
+                      hipStream_t s);
 void configure_batch_kernels();
 
 // ---- history stages (kernels_hist.hip) ----

@@ -478,6 +478,7 @@ __global__ __launch_bounds__(256) void k_ingest(IngestArgs A, SortJobs J) {
         const int t = blockIdx.x * blockDim.x + threadIdx.x;
         if (t == 0) {
             A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+            A.sc->n_comb_own = 0;
             A.sc->ss_resample = 0;
             A.sc->ss_maxc = 0;
         }
@@ -1096,7 +1097,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const int R = v.read_count, W = v.write_count;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.large ? nullptr : b.pair_bits, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
+                 b.dedup ? b.pair_bits : nullptr, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
@@ -1642,11 +1643,11 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
     const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
     const int force_grid = getenv("FDBCS_TEST_GRID_DECISION") ? 1 : 0;  // (tests)
-    if (T > LDS_T || force_grid || b.large) {  // grid decision, then the multi-block combine
+    if (T > LDS_T || force_grid || !b.dedup) {  // grid decision, then the multi-block combine
         const int nb = cdiv(T, DG_THREADS);
         DecGridArgs G;
         G.T = T; G.too_old = b.too_old; G.hist = b.hist; G.deg = b.deg; G.et = b.et; G.eu = b.eu;
-        G.edge_cap = b.edge_cap; G.bits = b.large ? nullptr : b.pair_bits; G.row_words = b.row_words;
+        G.edge_cap = b.edge_cap; G.bits = b.dedup ? b.pair_bits : nullptr; G.row_words = b.row_words;
         G.bd = b.dec_blk; G.be = b.dec_blk + nb + 1; G.didx = b.dep_idx; G.dep_list = b.dep_list; G.doff = b.off;
         G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.verdict = verdict; G.sc = sc;
         hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
@@ -1671,6 +1672,52 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
 }
 
 void launch_combine(const fdbcs_batch_view&, BatchBufs&, Scalars*, hipStream_t) {}
+
+// ---- exact sharded mode: exchange flags, foreign edges -------------------
+__global__ __launch_bounds__(256) void k_flags_out(int T, const uint8_t* __restrict__ too_old,
+                                                   const uint8_t* __restrict__ hist, uint8_t* __restrict__ flags) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) flags[t] = too_old[t] ? 2 : (hist[t] ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_flags_in(int T, const uint8_t* __restrict__ flags,
+                                                  uint8_t* __restrict__ too_old, uint8_t* __restrict__ hist) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) {
+        const uint8_t f = flags[t];
+        too_old[t] = f == 2;
+        hist[t] = f == 1;
+    }
+}
+
+// the union of every shard's overlap edges replaces this shard's own; the
+// per-reader source counts are recounted from it
+__global__ __launch_bounds__(256) void k_set_edges(const int32_t* __restrict__ et, const int32_t* __restrict__ eu,
+                                                   int64_t n, int32_t* __restrict__ det, int32_t* __restrict__ deu,
+                                                   int32_t* __restrict__ deg, Scalars* sc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) sc->edges_total = (int32_t)n;
+    if (i >= n) return;
+    const int32_t t = et[i];
+    det[i] = t;
+    deu[i] = eu[i];
+    atomicAdd(&deg[t], 1);
+}
+
+void launch_flags_out(const BatchBufs& b, int T, uint8_t* flags, hipStream_t s) {
+    if (T > 0) hipLaunchKernelGGL(k_flags_out, dim3(cdiv(T, 256)), dim3(256), 0, s, T, b.too_old, b.hist, flags);
+}
+
+void launch_flags_in(BatchBufs& b, int T, const uint8_t* flags, hipStream_t s) {
+    if (T > 0) hipLaunchKernelGGL(k_flags_in, dim3(cdiv(T, 256)), dim3(256), 0, s, T, flags, b.too_old, b.hist);
+}
+
+void launch_set_edges(BatchBufs& b, Scalars* sc, int T, const int32_t* et, const int32_t* eu, int64_t n,
+                      hipStream_t s) {
+    if (T > 0) hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s);
+    hipLaunchKernelGGL(k_set_edges, dim3(std::max(1, cdiv(n, 256))), dim3(256), 0, s, et, eu, n, b.et, b.eu, b.deg,
+                       sc);
+}
 
 }  // namespace fdbcs_dev
 

@@ -124,6 +124,10 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     if (shard.at_or_above(b) || shard.below(e)) return;
     const int has_b = shard.below(b) ? 0 : 1;
     const bool e_in = !shard.at_or_above(e);
+    {  // (the global compaction budget sums these over shards): one atomic per wavefront
+        const uint64_t m = __ballot(has_b);
+        if (has_b && (int)__lane_id() == __ffsll((unsigned long long)m) - 1) atomicAdd(&sc->n_comb_own, __popcll(m));
+    }
     rb.put(j, b);  // compact copies for the page merge
     re.put(j, e);
     const int need = (e_in && !found && !touch) ? 1 : 0;

@@ -56,6 +56,16 @@ struct Bounds {
         if (g < G - 1 && kcmp_host(b, bl, bytes + off[g], len[g]) >= 0) return false;      // b >= hi
         return true;
     }
+    // does a range ending at e end exactly at resolver g's first key?
+    bool ends_at_lo(int g, const uint8_t* e, uint32_t el) const {
+        return g > 0 && kcmp_host(e, el, bytes + off[g - 1], len[g - 1]) == 0;
+    }
+    // the writes an exact protocol-B shard needs: those intersecting its keys,
+    // and those ending exactly at its first key (the shard holding a range's
+    // end creates the end node, SURVEY.md §8e "splitter ends")
+    bool write_hits(int g, const uint8_t* b, uint32_t bl, const uint8_t* e, uint32_t el, bool keep_all) const {
+        return hits(g, b, bl, e, el) || (keep_all && ends_at_lo(g, e, el));
+    }
 };
 
 __global__ __launch_bounds__(256) void k_scatter_verdicts(const uint8_t* __restrict__ sub,
@@ -69,10 +79,10 @@ __global__ __launch_bounds__(256) void k_scatter_verdicts(const uint8_t* __restr
 
 extern "C" {
 
-int fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
-                      const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
-                      fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
-                      uint64_t* key_off, uint32_t* key_len, int32_t* txn_index) {
+static int split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
+                       const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
+                       fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
+                       uint64_t* key_off, uint32_t* key_len, int32_t* txn_index, bool keep_all) {
     if (!in || !out || nres < 1 || resolver < 0 || resolver >= nres) return FDBCS_E_ARG;
     if (nres > 1 && (!bound_bytes || !bound_off || !bound_len)) return FDBCS_E_ARG;
     for (int g = 1; g + 1 < nres; g++)
@@ -94,11 +104,11 @@ int fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* b
         }
         for (int32_t w = in->write_off[t]; w < in->write_off[t + 1]; w++) {
             const uint64_t s = 2 * (uint64_t)R + 2 * (uint64_t)w;
-            if (B.hits(resolver, in->key_bytes + in->key_off[s], in->key_len[s], in->key_bytes + in->key_off[s + 1],
-                       in->key_len[s + 1]))
+            if (B.write_hits(resolver, in->key_bytes + in->key_off[s], in->key_len[s],
+                             in->key_bytes + in->key_off[s + 1], in->key_len[s + 1], keep_all))
                 nw++;
         }
-        if (nr + nw == 0) continue;
+        if (nr + nw == 0 && !keep_all) continue;
         snapshot[t_out] = in->snapshot[t];
         txn_index[t_out] = (int32_t)t;
         read_off[t_out + 1] = read_off[t_out] + nr;
@@ -123,8 +133,8 @@ int fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* b
         }
         for (int32_t w = in->write_off[t]; w < in->write_off[t + 1]; w++) {
             const uint64_t s = 2 * (uint64_t)R + 2 * (uint64_t)w;
-            if (!B.hits(resolver, in->key_bytes + in->key_off[s], in->key_len[s], in->key_bytes + in->key_off[s + 1],
-                        in->key_len[s + 1]))
+            if (!B.write_hits(resolver, in->key_bytes + in->key_off[s], in->key_len[s],
+                              in->key_bytes + in->key_off[s + 1], in->key_len[s + 1], keep_all))
                 continue;
             const uint64_t d = 2 * (uint64_t)r_out + 2 * (uint64_t)ww;
             key_off[d] = in->key_off[s];
@@ -146,6 +156,22 @@ int fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* b
     out->key_bytes = in->key_bytes;
     out->key_bytes_len = in->key_bytes_len;
     return FDBCS_OK;
+}
+
+int fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
+                      const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
+                      fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
+                      uint64_t* key_off, uint32_t* key_len, int32_t* txn_index) {
+    return split_batch(in, nres, bound_bytes, bound_off, bound_len, resolver, out, snapshot, read_off, write_off,
+                       key_off, key_len, txn_index, false);
+}
+
+int fdbcs_split_batch_keep_all(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
+                               const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
+                               fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
+                               uint64_t* key_off, uint32_t* key_len, int32_t* txn_index) {
+    return split_batch(in, nres, bound_bytes, bound_off, bound_len, resolver, out, snapshot, read_off, write_off,
+                       key_off, key_len, txn_index, true);
 }
 
 int32_t fdbcs_key_owner(int32_t nres, const uint8_t* bound_bytes, const uint64_t* bound_off,

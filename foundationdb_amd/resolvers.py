@@ -48,8 +48,10 @@ class KeyRangeResolvers:
         return check(self._lib.fdbcs_key_owner(self.n, self._blob.ctypes.data, self._offs.ctypes.data,
                                                self._lens.ctypes.data, k.ctypes.data, len(key)), "key_owner")
 
-    def split(self, batch: PackedBatch, g):
-        """(sub-batch PackedBatch, txn_index int32 array) that resolver g receives."""
+    def split(self, batch: PackedBatch, g, keep_all=False):
+        """(sub-batch PackedBatch, txn_index int32 array) that resolver g receives.
+        keep_all: every transaction stays (with only its ranges intersecting g's
+        keys) -- the per-shard input of the exact sharded protocol B."""
         T, R, W = batch.T, batch.R, batch.W
         slots = 2 * (R + W)
         snap = np.zeros(max(T, 1), np.int64)
@@ -59,7 +61,8 @@ class KeyRangeResolvers:
         klen = np.zeros(max(slots, 1), np.uint32)
         idx = np.zeros(max(T, 1), np.int32)
         out = _abi.BatchView()
-        check(self._lib.fdbcs_split_batch(C.byref(batch.view()), self.n, self._blob.ctypes.data,
+        fn = self._lib.fdbcs_split_batch_keep_all if keep_all else self._lib.fdbcs_split_batch
+        check(fn(C.byref(batch.view()), self.n, self._blob.ctypes.data,
                                           self._offs.ctypes.data, self._lens.ctypes.data, g, C.byref(out),
                                           snap.ctypes.data, roff.ctypes.data, woff.ctypes.data, koff.ctypes.data,
                                           klen.ctypes.data, idx.ctypes.data), "split_batch")

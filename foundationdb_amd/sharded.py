@@ -107,7 +107,7 @@ def plan_compaction(infos, n_comb):
 
 
 KEY_INLINE = 32  # removalKeys up to this length travel inside exchange 1
-SLOT_WORDS = 3 + KEY_INLINE // 8  # H, last version, key length (-1: none), key words
+SLOT_WORDS = 4 + KEY_INLINE // 8  # H, last version, key length (-1: none), edges (protocol B), key words
 
 
 def _pack_key(key):
@@ -134,12 +134,14 @@ def carry_ins(v0, hl):
 class Shard:
     """One engine holding the keys [lo, hi) (None: unbounded)."""
 
-    def __init__(self, lo, hi, device=-1, v0=0, max_history=0):
+    def __init__(self, lo, hi, device=-1, v0=0, max_history=0, sparse=False):
         self.cs = ConflictSet(v0=v0, device=device, max_history=max_history)
         self._lib = self.cs._lib
         lo_b, hi_b = lo or b"", hi or b""
         check(self._lib.fdbcs_set_shard(self.cs.handle, lo_b, len(lo_b), int(lo is not None), hi_b, len(hi_b),
                                         int(hi is not None)), "set_shard")
+        if sparse:
+            check(self._lib.fdbcs_shard_set_protocol(self.cs.handle, 1), "shard_set_protocol")
         self.lo, self.hi = lo, hi
         self._key = (C.c_uint8 * _abi.MAX_KEY)()
 
@@ -154,6 +156,18 @@ class Shard:
         check(self._lib.fdbcs_shard_apply(self.cs.handle, C.byref(dev_view), now, new_oldest, carry, rk, n, dev_hist,
                                           dev_verdict, info), "shard_apply")
         return tuple(info)
+
+    def edge_count(self):
+        n = self._lib.fdbcs_shard_edge_count(self.cs.handle)
+        if n < 0:
+            check(int(n), "shard_edge_count")
+        return int(n)
+
+    def get_edges(self, et_ptr, eu_ptr, n):
+        check(self._lib.fdbcs_shard_get_edges(self.cs.handle, et_ptr, eu_ptr, n), "shard_get_edges")
+
+    def set_edges(self, et_ptr, eu_ptr, n):
+        check(self._lib.fdbcs_shard_set_edges(self.cs.handle, et_ptr, eu_ptr, n), "shard_set_edges")
 
     def compact(self, part, new_oldest, key_index=-1):
         a, b, keep_first, prev = part
@@ -199,9 +213,9 @@ class _Proto:
         self.rk = b""                 # removalKey as delivered
         self.oldest = 0
 
-    def slot_words(self):
+    def slot_words(self, edges=0):
         H, last, n, key = self.slot
-        return [H, last, n] + _pack_key(key if 0 <= n <= KEY_INLINE else b"")
+        return [H, last, n, edges] + _pack_key(key if 0 <= n <= KEY_INLINE else b"")
 
     def check(self, view, now, new_oldest, hist_ptr):
         self.shard.check(view, now, new_oldest, self.carry_check, hist_ptr)
@@ -213,15 +227,15 @@ class _Proto:
         if self.rk_owner < 0:
             return b""
         n = slots[self.rk_owner][2]
-        return _unpack_key(slots[self.rk_owner][3:], n) if n <= KEY_INLINE else long_key
+        return _unpack_key(slots[self.rk_owner][4:], n) if n <= KEY_INLINE else long_key
 
     def apply(self, view, now, new_oldest, slots, hist_ptr, verdict_ptr, long_key=None):
         carry = carry_ins(self.v0, [(w[0], w[1]) for w in slots])[self.g]
         rk = self.pending_key(slots, long_key)
         if rk is not None:
             self.rk, self.rk_owner = rk, None
-        H, g0, last, n_comb = self.shard.apply(view, now, new_oldest, carry, rk, hist_ptr, verdict_ptr)
-        return (H, g0, last), n_comb
+        H, g0, last, n_own = self.shard.apply(view, now, new_oldest, carry, rk, hist_ptr, verdict_ptr)
+        return (H, g0, last), n_own
 
     def compact(self, infos, n_comb, new_oldest):
         if new_oldest > self.oldest:  # step 6
@@ -249,17 +263,19 @@ class ShardedConflictSet:
     are a device reduction and host lists.  ``shard_factory`` builds a shard
     (tests pass a CPU model of the same interface)."""
 
-    def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard):
+    def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard, sparse=False):
         import torch
 
         self.torch = torch
+        self.bounds = list(bounds)
+        self.sparse = sparse  # protocol B: shard-local ranges, exchanged overlap edges
         ranges = _shard_ranges(bounds)
         if devices is None:
             d = torch.cuda.current_device() if torch.cuda.is_available() else -1
             devices = [d] * len(ranges)
         assert len(devices) == len(ranges)
         self.devices = [_device(torch, d) for d in devices]
-        self.protos = [_Proto(shard_factory(lo, hi, device=d, v0=v0, max_history=max_history), g, v0)
+        self.protos = [_Proto(shard_factory(lo, hi, device=d, v0=v0, max_history=max_history, sparse=sparse), g, v0)
                        for g, ((lo, hi), d) in enumerate(zip(ranges, devices))]
         self.shards = [p.shard for p in self.protos]
 
@@ -278,15 +294,32 @@ class ShardedConflictSet:
             p.check(v, now, new_oldest, h.data_ptr())
         flags = torch.stack([h.to(self.devices[0]) for h in hs]).amax(0)  # step 3: MAX over shards
         slots = [p.slot_words() for p in self.protos]
+        et = eu = None
+        if self.sparse:  # protocol B: the union of the shards' overlap edges
+            parts = []
+            for p, d in zip(self.protos, self.devices):
+                n = p.shard.edge_count()
+                a = torch.empty(max(1, n), dtype=torch.int32, device=d)
+                b = torch.empty(max(1, n), dtype=torch.int32, device=d)
+                p.shard.get_edges(a.data_ptr(), b.data_ptr(), n)
+                parts.append((a[:n].to(self.devices[0]), b[:n].to(self.devices[0])))
+            et = torch.cat([a for a, _ in parts] + [torch.zeros(1, dtype=torch.int32, device=self.devices[0])])
+            eu = torch.cat([b for _, b in parts] + [torch.zeros(1, dtype=torch.int32, device=self.devices[0])])
+        n_edges = et.numel() - 1 if et is not None else 0
         infos, n_comb = [], 0
         for g, (p, v) in enumerate(zip(self.protos, views)):  # steps 4-5
             f = flags.to(self.devices[g])
             out = verdict if g == 0 else torch.empty(max(1, T), dtype=torch.uint8, device=self.devices[g])
+            if et is not None:
+                ge, gu = et.to(self.devices[g]), eu.to(self.devices[g])
+                _sync(torch, self.devices[g])
+                p.shard.set_edges(ge.data_ptr(), gu.data_ptr(), n_edges)
             _sync(torch, self.devices[g])
             o = p.rk_owner
             long_key = self.protos[o].slot[3] if o is not None and o >= 0 else None
-            info, n_comb = p.apply(v, now, new_oldest, slots, f.data_ptr(), out.data_ptr(), long_key)
+            info, n_own = p.apply(v, now, new_oldest, slots, f.data_ptr(), out.data_ptr(), long_key)
             infos.append(info)
+            n_comb += n_own  # |combined ranges| of the whole batch: each begins in exactly one shard
         for p in self.protos:  # steps 6-7
             p.compact(infos, n_comb, new_oldest)
 
@@ -294,11 +327,19 @@ class ShardedConflictSet:
         """A host PackedBatch through the sharded path; returns the verdict bytes (numpy)."""
         from .batch import DeviceBatch
 
+        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.devices[0])
+        if self.sparse:  # each shard gets the ranges intersecting its keys (all transactions)
+            from .resolvers import KeyRangeResolvers
+
+            kr = KeyRangeResolvers(self.bounds)
+            subs = [kr.split(batch, g, keep_all=True)[0] for g in range(len(self.devices))]
+            staged = [DeviceBatch(sb, d) for sb, d in zip(subs, self.devices)]
+            self.detect_device([x.view for x in staged], now, new_oldest, verdict)
+            return verdict[:batch.T].cpu().numpy()
         staged = {}
         for d in self.devices:
             if d not in staged:
                 staged[d] = DeviceBatch(batch, d)
-        verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.devices[0])
         self.detect_device([staged[d].view for d in self.devices], now, new_oldest, verdict)
         return verdict[:batch.T].cpu().numpy()
 
@@ -332,16 +373,19 @@ class DistShardedConflictSet:
     engine's apply, one all-gather of three integers, the engine's compaction.
     """
 
-    def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None, shard_factory=Shard):
+    def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None, shard_factory=Shard,
+                 sparse=False):
         import torch
         import torch.distributed as dist
 
         assert len(bounds) + 1 == world
         self.torch, self.dist, self.group = torch, dist, group
         self.rank, self.world = rank, world
+        self.bounds = list(bounds)
+        self.sparse = sparse  # protocol B: this rank receives only its ranges; overlap edges are all-gathered
         self.device = _device(torch, device)
         lo, hi = _shard_ranges(bounds)[rank]
-        self.shard = shard_factory(lo, hi, device=device, v0=v0, max_history=max_history)
+        self.shard = shard_factory(lo, hi, device=device, v0=v0, max_history=max_history, sparse=sparse)
         self.proto = _Proto(self.shard, rank, v0)
         backend = dist.get_backend(group)
         self.coll_dev = self.device if backend == "nccl" else torch.device("cpu")
@@ -372,8 +416,9 @@ class DistShardedConflictSet:
         p.check(view, now, new_oldest, h.data_ptr())  # steps 1-2 (synchronous)
         tick("check")
         # exchange 1: flags + this shard's slot, zeros elsewhere; MAX all-reduce
+        n_edges = self.shard.edge_count() if self.sparse else 0
         mine = np.zeros(self.world * SLOT_WORDS, np.int64)
-        mine[self.rank * SLOT_WORDS:(self.rank + 1) * SLOT_WORDS] = p.slot_words()
+        mine[self.rank * SLOT_WORDS:(self.rank + 1) * SLOT_WORDS] = p.slot_words(n_edges)
         x1[nT:].copy_(torch.from_numpy(mine.view(np.uint8)))
         x1[:nT].copy_(h)
         dist.all_reduce(x1, op=dist.ReduceOp.MAX, group=self.group)
@@ -385,23 +430,54 @@ class DistShardedConflictSet:
             fl = h
         else:
             fl = x1
+        if self.sparse:  # protocol B: all-gather the overlap edges (counts came in the slots)
+            self._exchange_edges([int(w[3]) for w in slots], n_edges)
         _sync(torch, self.device)  # the engine reads the flags on its own stream
         tick("exchange1")
         long_key = None
         o = p.rk_owner
         if o is not None and o >= 0 and slots[o][2] > KEY_INLINE:
             long_key = self._broadcast_key(o, p.slot[3] if o == self.rank else b"")
-        info, n_comb = p.apply(view, now, new_oldest, slots, fl.data_ptr(), verdict.data_ptr(), long_key)  # 4-5
+        info, n_own = p.apply(view, now, new_oldest, slots, fl.data_ptr(), verdict.data_ptr(), long_key)  # 4-5
         tick("apply")
-        infos = [tuple(x) for x in self._allgather(list(info))]  # exchange 2
+        got = self._allgather(list(info) + [n_own])  # exchange 2
+        infos = [tuple(x[:3]) for x in got]
+        n_comb = sum(x[3] for x in got)  # each combined range begins in exactly one shard
         tick("exchange2")
         p.compact(infos, n_comb, new_oldest)  # steps 6-7
         tick("compact")
 
+    def _exchange_edges(self, counts, n_mine):
+        """One all-gather of every shard's (reader, earlier writer) pairs, padded
+        to the longest list; their concatenation replaces this shard's own."""
+        torch, dist = self.torch, self.dist
+        m = max(1, max(counts))
+        buf = torch.zeros(2 * m, dtype=torch.int32, device=self.device)
+        self.shard.get_edges(buf.data_ptr(), buf[m:].data_ptr(), n_mine)
+        send = buf.to(self.coll_dev)
+        outs = [torch.empty_like(send) for _ in range(self.world)]
+        dist.all_gather(outs, send, group=self.group)
+        out = torch.stack(outs).view(self.world, 2, m).to(self.device)
+        et = torch.cat([out[g, 0, :counts[g]] for g in range(self.world)] + [out.new_zeros(1)])
+        eu = torch.cat([out[g, 1, :counts[g]] for g in range(self.world)] + [out.new_zeros(1)])
+        _sync(torch, self.device)
+        self.shard.set_edges(et.data_ptr(), eu.data_ptr(), sum(counts))
+        self._edges_keep = (et, eu)  # (alive until the engine's copy has run)
+
+    def split(self, batch):
+        """This rank's input under protocol B: every transaction, only the ranges
+        intersecting its keys (the proxy's per-resolver split keeping batch
+        indices); the whole batch under protocol A."""
+        if not self.sparse:
+            return batch
+        from .resolvers import KeyRangeResolvers
+
+        return KeyRangeResolvers(self.bounds).split(batch, self.rank, keep_all=True)[0]
+
     def detect_packed(self, batch, now, new_oldest):
         from .batch import DeviceBatch
 
-        db = DeviceBatch(batch, self.device)
+        db = DeviceBatch(self.split(batch), self.device)
         verdict = self.torch.empty(max(1, batch.T), dtype=self.torch.uint8, device=self.device)
         self.detect_device(db.view, now, new_oldest, verdict)
         return verdict[:batch.T].cpu().numpy()

@@ -170,6 +170,16 @@ int  fdbcs_split_batch(const fdbcs_batch_view* in, int32_t nres, const uint8_t* 
                        fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
                        uint64_t* key_off, uint32_t* key_len, int32_t* txn_index);
 
+/* As fdbcs_split_batch, but every transaction of the input stays in the
+ * sub-batch (txn_index is the identity), with only the ranges intersecting
+ * the resolver's keys -- plus the writes ending exactly at its first key,
+ * whose end node it holds: the per-shard input of the exact sharded
+ * protocol B, which keeps batch transaction indices global. */
+int  fdbcs_split_batch_keep_all(const fdbcs_batch_view* in, int32_t nres, const uint8_t* bound_bytes,
+                                const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver,
+                                fdbcs_batch_view* out, int64_t* snapshot, int32_t* read_off, int32_t* write_off,
+                                uint64_t* key_off, uint32_t* key_len, int32_t* txn_index);
+
 /* The resolver owning key (keyResolvers lookup), or a negative status. */
 int32_t fdbcs_key_owner(int32_t nres, const uint8_t* bound_bytes, const uint64_t* bound_off,
                         const uint32_t* bound_len, const uint8_t* key, uint32_t key_len);
@@ -182,7 +192,7 @@ int32_t fdbcs_key_owner(int32_t nres, const uint8_t* bound_bytes, const uint64_t
 int  fdbcs_scatter_verdicts(fdbcs* cs, const uint8_t* dev_sub, const int32_t* dev_index, int32_t n,
                             uint8_t* dev_global);
 
-/* ---- Exact sharded mode: one resolver over G GPUs (SURVEY.md §8e protocol A) ---- */
+/* ---- Exact sharded mode: one resolver over G GPUs (SURVEY.md §8e protocols A, B) ---- */
 
 /* The north star's node layout: GPU g holds the history of the keys in
  * [lo, hi) (has_lo / has_hi == 0: unbounded), every GPU receives the whole
@@ -197,9 +207,13 @@ int  fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo,
  * history check of every read clipped to the shard.  carry_in: the version of
  * the last boundary below lo after the previous batch's merge (its
  * compaction can change that only between versions below oldestVersion,
- * which no checked read can tell apart).  dev_hist receives T bytes (1: the
- * transaction conflicts with this shard's history); the host MAX-reduces
- * them over the shards (RCCL all-reduce). */
+ * which no checked read can tell apart).  dev_hist receives T flag bytes
+ * (2: tooOld -- SkipList.cpp:985 -- 1: the transaction conflicts with this
+ * shard's history, 0: neither); the host MAX-reduces them over the shards
+ * (RCCL all-reduce).  Protocol B: the batch holds every transaction of the
+ * global batch but only the ranges intersecting [lo, hi)
+ * (fdbcs_split_batch_keep_all); a transaction with no read here reports 0,
+ * and the shard that holds one of its reads reports the tooOld flag. */
 int  fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now,
                        int64_t new_oldest, int64_t carry_in, uint8_t* dev_hist);
 
@@ -211,8 +225,11 @@ int  fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now
  * batch's compaction produced (-1: unchanged).  info[0] = boundaries H,
  * [1] = index of the shard's first boundary >= removalKey when a compaction
  * follows (else -1), [2] = version of its last boundary (INT64_MIN: none),
- * [3] = combined write ranges (global).  When new_oldest > oldestVersion,
- * fdbcs_shard_compact must follow. */
+ * [3] = combined write ranges whose begin lies in [lo, hi) (their sum over
+ * the shards is |combinedWriteConflictRanges|, the compaction budget's
+ * len(C), SkipList.cpp:1198-1206).  When new_oldest > oldestVersion,
+ * fdbcs_shard_compact must follow.  Protocol B: fdbcs_shard_set_edges
+ * first. */
 int  fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now, int64_t new_oldest,
                        int64_t carry_in, const uint8_t* removal_key, int32_t removal_key_len,
                        const uint8_t* dev_hist, uint8_t* dev_verdict, int64_t* info);
@@ -227,6 +244,24 @@ int  fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t now
 int  fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version,
                          int64_t new_oldest, int64_t key_index, uint8_t* key_buf, int32_t key_cap,
                          int64_t* info);
+
+/* Protocol B (for batches too large to sort on every GPU):
+ * each shard receives only the ranges intersecting its keys, so the endpoint
+ * sort, the overlap search and the history check are all shard-local.  Every
+ * intra-batch overlap (read r of t, write w of u) has a non-empty
+ * intersection inside some shard, where both ranges are present, so the union
+ * of the shards' edge lists is the whole batch's.  sparse_edges != 0 makes
+ * this shard keep its overlap pairs undeduplicated for export (before the
+ * first batch).  Per batch: fdbcs_shard_check, then fdbcs_shard_edge_count /
+ * fdbcs_shard_get_edges (the pairs (reader t, earlier writer u) in batch
+ * transaction indices, into caller device memory), an all-gather of the
+ * lists, fdbcs_shard_set_edges with their concatenation, fdbcs_shard_apply
+ * (the ordered decision over the global edges -- identical on every shard --
+ * then this shard's combine and merge). */
+int     fdbcs_shard_set_protocol(fdbcs* cs, int sparse_edges);
+int64_t fdbcs_shard_edge_count(fdbcs* cs);
+int     fdbcs_shard_get_edges(fdbcs* cs, int32_t* dev_et, int32_t* dev_eu, int64_t n);
+int     fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_eu, int64_t n);
 
 /* ---- Introspection (tests, bench, checkpoint) --------------------------------- */
 

@@ -32,8 +32,11 @@ def _bytes_at(ptr, n):
 
 
 class ModelShard:
-    def __init__(self, lo, hi, device=-1, v0=0, max_history=0):
+    def __init__(self, lo, hi, device=-1, v0=0, max_history=0, sparse=False):
         self.lo, self.hi = lo, hi
+        self.sparse = sparse
+        self.edges = []   # protocol B: this shard's (reader, earlier writer) pairs
+        self.gedges = []  # the union over the shards
         self.v0 = v0  # carry-in
         self.keys, self.vers = [], []
         self.oldest = 0
@@ -54,9 +57,16 @@ class ModelShard:
         self.v0 = carry
         txns = self._txns(view)
         out = _bytes_at(dev_hist, len(txns))
+        self.edges = []
+        if self.sparse:  # overlaps of this shard's ranges (present whole: ranges arrive unclipped)
+            for t, (snap, reads, _w) in enumerate(txns):
+                for u in range(t):
+                    if any(rb < we and wb < re_ for rb, re_ in reads for wb, we in txns[u][2]):
+                        self.edges.append((t, u))
         for t, (snap, reads, _w) in enumerate(txns):
             out[t] = 0
             if snap < self.oldest and reads:
+                out[t] = 2
                 continue  # tooOld: not checked (SkipList.cpp:985)
             for b, e in reads:
                 if self.lo is not None and b < self.lo:
@@ -79,17 +89,25 @@ class ModelShard:
             self.rk = removal_key
         txns = self._txns(view)
         T = len(txns)
-        hist = _bytes_at(dev_hist, T).copy()
-        too_old = [snap < self.oldest and bool(reads) for snap, reads, _w in txns]
-        conflict = [bool(hist[t]) for t in range(T)]
-        acc = []
-        for t, (_s, reads, writes) in enumerate(txns):
-            if conflict[t]:
-                continue
-            c = too_old[t] or any(rb < we and wb < re_ for rb, re_ in reads for wb, we in acc)
-            conflict[t] = c
-            if not c:
-                acc.extend(writes)
+        flags = _bytes_at(dev_hist, T).copy()
+        too_old = [flags[t] == 2 for t in range(T)]
+        conflict = [flags[t] != 0 for t in range(T)]
+        if self.sparse:  # the ordered decision over the global edges
+            src = {}
+            for t, u in self.gedges:
+                src.setdefault(t, []).append(u)
+            for t in range(T):
+                if not conflict[t]:
+                    conflict[t] = any(not conflict[u] for u in src.get(t, ()))
+        else:
+            acc = []
+            for t, (_s, reads, writes) in enumerate(txns):
+                if conflict[t]:
+                    continue
+                c = any(rb < we and wb < re_ for rb, re_ in reads for wb, we in acc)
+                conflict[t] = c
+                if not c:
+                    acc.extend(writes)
         verdict = _bytes_at(dev_verdict, T)
         for t in range(T):
             verdict[t] = 2 if not conflict[t] else (1 if too_old[t] else 0)
@@ -127,7 +145,22 @@ class ModelShard:
                 self.vers.insert(i, now)
         H = len(self.keys)
         g0 = bisect_left(self.keys, self.rk) if new_oldest > self.oldest else -1
-        return H, g0, (self.vers[-1] if H else INT64_MIN), len(combined)
+        own = sum(1 for b, _e in combined if self._in(b))
+        return H, g0, (self.vers[-1] if H else INT64_MIN), own
+
+    def edge_count(self):
+        return len(self.edges)
+
+    def get_edges(self, et_ptr, eu_ptr, n):
+        et = np.ctypeslib.as_array((C.c_int32 * max(1, n)).from_address(et_ptr))
+        eu = np.ctypeslib.as_array((C.c_int32 * max(1, n)).from_address(eu_ptr))
+        for i, (t, u) in enumerate(self.edges[:n]):
+            et[i], eu[i] = t, u
+
+    def set_edges(self, et_ptr, eu_ptr, n):
+        et = np.ctypeslib.as_array((C.c_int32 * max(1, n)).from_address(et_ptr))[:n]
+        eu = np.ctypeslib.as_array((C.c_int32 * max(1, n)).from_address(eu_ptr))[:n]
+        self.gedges = list(zip(et.tolist(), eu.tolist()))
 
     def compact(self, part, new_oldest, key_index=-1):
         a, b, keep_first, prev = part

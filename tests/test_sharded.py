@@ -1,4 +1,8 @@
-"""Exact sharded mode (SURVEY.md §8e protocol A): one Resolver over G shards.
+"""Exact sharded mode (SURVEY.md §8e protocols A and B): one Resolver over G shards.
+
+Protocol A: every shard receives the whole batch.  Protocol B (sparse=True):
+each shard receives only the ranges intersecting its keys, finds the overlap
+edges among them, and the edge lists are all-gathered before the decision.
 
 The concatenated shard histories, the verdicts, removalKey and oldestVersion
 must equal ONE conflict set's (the oracle) after every batch -- the north
@@ -59,20 +63,23 @@ def test_carry_ins_skip_empty_shards():
     assert carry_ins(7, [(2, 11), (0, 0), (1, 13), (0, 0)]) == [7, 11, 11, 13]
 
 
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("G", [1, 2, 3, 5])
-def test_model_shards_equal_one_conflict_set(G):
+def test_model_shards_equal_one_conflict_set(G, sparse):
     for seed in range(12):
         rng = random.Random(seed * 7 + G)
         maxlen = rng.choice([2, 3, 6])
-        sh = ShardedConflictSet(random_bounds(rng, G, maxlen), devices=[-1] * G, shard_factory=ModelShard)
+        sh = ShardedConflictSet(random_bounds(rng, G, maxlen), devices=[-1] * G, shard_factory=ModelShard,
+                                sparse=sparse)
         c = CpuSpec()
         for batch, now, nold in tiny_stream(seed * 31 + G, n_batches=25, maxlen=maxlen):
             check_step(sh, c, batch, now, nold)
 
 
-def test_model_shards_bounds_at_written_keys_and_clear():
+@pytest.mark.parametrize("sparse", [False, True])
+def test_model_shards_bounds_at_written_keys_and_clear(sparse):
     """Splitters that are themselves written/read keys (e = s_g ends), clearConflictSet mid-stream."""
-    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], devices=[-1] * 4, shard_factory=ModelShard)
+    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], devices=[-1] * 4, shard_factory=ModelShard, sparse=sparse)
     c = CpuSpec()
     for i, (batch, now, nold) in enumerate(tiny_stream(99, n_batches=40, maxlen=3)):
         if i == 20:
@@ -81,16 +88,17 @@ def test_model_shards_bounds_at_written_keys_and_clear():
         check_step(sh, c, batch, now, nold)
 
 
-def test_model_shards_mixed_streams():
+@pytest.mark.parametrize("sparse", [False, True])
+def test_model_shards_mixed_streams(sparse):
     for seed in range(2):
         sh = ShardedConflictSet([b"k001000", b"k002500", b"k002500\x00"], devices=[-1] * 4,
-                                shard_factory=ModelShard)
+                                shard_factory=ModelShard, sparse=sparse)
         c = CpuSpec()
         for batch, now, nold in mixed_stream(seed, n_batches=8, max_txns=120, keyspace=4000):
             check_step(sh, c, batch, now, nold)
 
 
-def _dist_rank(rank, world, port, bounds, seed, maxlen, q):
+def _dist_rank(rank, world, port, bounds, seed, maxlen, sparse, q):
     import torch.distributed as dist
 
     from foundationdb_amd.sharded import DistShardedConflictSet
@@ -98,7 +106,7 @@ def _dist_rank(rank, world, port, bounds, seed, maxlen, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard)
+    sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard, sparse=sparse)
     out = []
     for batch, now, nold in tiny_stream(seed, n_batches=25, maxlen=maxlen):
         v = sh.detect_packed(batch, now, nold)
@@ -107,8 +115,9 @@ def _dist_rank(rank, world, port, bounds, seed, maxlen, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,maxlen", [(2, 3), (3, 3), (2, 40)])
-def test_dist_sharded_gloo(world, maxlen):
+@pytest.mark.parametrize("world,maxlen,sparse", [(2, 3, False), (3, 3, False), (2, 40, False), (2, 3, True),
+                                                 (3, 3, True), (2, 40, True)])
+def test_dist_sharded_gloo(world, maxlen, sparse):
     """world_size 2/3 over gloo: one shard per rank; every rank's verdicts, the
     concatenation of the ranks' histories and removalKey equal one conflict set's
     (maxlen 40: removalKeys longer than the all-gather's inline 32 bytes)."""
@@ -118,7 +127,7 @@ def test_dist_sharded_gloo(world, maxlen):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.Random(os.getpid() * 7 + world).randint(0, 3000)
-    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, maxlen, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, maxlen, sparse, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in range(world))
@@ -140,12 +149,13 @@ def test_dist_sharded_gloo(world, maxlen):
 # ------------------------------------------------------------------ GPU ----
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("maxlen", [3, 11, 40])
-def test_gpu_shards_tiny_streams(gpu, maxlen):
+def test_gpu_shards_tiny_streams(gpu, maxlen, sparse):
     for seed in range(8):
         rng = random.Random(seed * 5 + maxlen)
         G = rng.choice([2, 3, 4])
-        sh = ShardedConflictSet(random_bounds(rng, G, min(maxlen, 4)), max_history=1 << 14)
+        sh = ShardedConflictSet(random_bounds(rng, G, min(maxlen, 4)), max_history=1 << 14, sparse=sparse)
         c = CpuSpec()
         try:
             for batch, now, nold in tiny_stream(seed * 13 + maxlen, n_batches=25, maxlen=maxlen):
@@ -155,8 +165,9 @@ def test_gpu_shards_tiny_streams(gpu, maxlen):
 
 
 @pytest.mark.gpu
-def test_gpu_shards_bounds_at_keys_and_clear(gpu):
-    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], max_history=1 << 14)
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_shards_bounds_at_keys_and_clear(gpu, sparse):
+    sh = ShardedConflictSet([b"a", b"b", b"b\x00"], max_history=1 << 14, sparse=sparse)
     c = CpuSpec()
     try:
         for i, (batch, now, nold) in enumerate(tiny_stream(99, n_batches=40, maxlen=3)):
@@ -169,8 +180,9 @@ def test_gpu_shards_bounds_at_keys_and_clear(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_shards_mixed_streams(gpu):
-    sh = ShardedConflictSet([b"k001000", b"k002500", b"k002500\x00"], max_history=1 << 16)
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_shards_mixed_streams(gpu, sparse):
+    sh = ShardedConflictSet([b"k001000", b"k002500", b"k002500\x00"], max_history=1 << 16, sparse=sparse)
     c = CpuSpec()
     try:
         for batch, now, nold in mixed_stream(3, n_batches=12, max_txns=600, keyspace=5000):
@@ -180,17 +192,39 @@ def test_gpu_shards_mixed_streams(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("G", [2, 4])
-def test_gpu_shards_config2(gpu, G):
+def test_gpu_shards_config2(gpu, G, sparse):
     """Config 2's shape (5R+2W, uniform 16-byte keys) split over G uniform key slices."""
     from foundationdb_amd.workload import Workload
 
-    sh = ShardedConflictSet(uniform_bounds(G))
+    sh = ShardedConflictSet(uniform_bounds(G), sparse=sparse)
     c = CpuSpec()
     wl = Workload(2, txns=1500)
     try:
         for i in range(12):
             batch, now, nold = wl.batch(i)
             check_step(sh, c, batch, now, nold, history=(i % 4 == 3))
+    finally:
+        sh.close()
+
+
+@pytest.mark.gpu
+def test_gpu_shards_protocol_b_zipf_and_large(gpu):
+    """Protocol B with Zipf hot keys (many overlap edges, duplicated across
+    shards) and a batch past LARGE_T (merge sort in every shard)."""
+    from foundationdb_amd.workload import Workload
+
+    sh = ShardedConflictSet(uniform_bounds(3), sparse=True)
+    c = CpuSpec()
+    try:
+        wl = Workload(3, txns=3000)
+        for i in range(6):
+            batch, now, nold = wl.batch(i)
+            check_step(sh, c, batch, now, nold, history=(i % 3 == 2))
+        wl = Workload(2, txns=80_000)
+        for i in range(6, 8):
+            batch, now, nold = wl.batch(i)
+            check_step(sh, c, batch, now, nold, history=(i == 7))
     finally:
         sh.close()
