@@ -70,6 +70,9 @@ def parse():
                    help="extra instrumented batches after the timed region (default 50; config 5: 3)")
     p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
                    help="N > 1: one exact resolver sharded by key range, or N independent key-range resolvers")
+    p.add_argument("--protocol", choices=["a", "b"], default="b",
+                   help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
+                        "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
     a = p.parse_args()
     big = a.config == 5  # 1 M-txn batches over a preloaded 10^8-boundary history
     for name, small, large in [("steps", 200, 10), ("warmup", 2500, 2), ("txns", 5000, 1_000_000),
@@ -112,12 +115,13 @@ def to_device(v, torch, dev):
 class Source:
     """Batches for this rank: the whole batch (N = 1) or this resolver's share."""
 
-    def __init__(self, cfg, txns, world, rank, split):
+    def __init__(self, cfg, txns, world, rank, split, keep_all=False):
         from foundationdb_amd.workload import Workload
         self.world, self.rank = world, rank
         self.wl = Workload(cfg, txns=txns * world)
         self.kr = None
-        if split:
+        self.keep_all = keep_all  # protocol B: every transaction, only this rank's ranges
+        if split and world > 1:
             from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
             self.kr = KeyRangeResolvers(uniform_bounds(world))
 
@@ -127,8 +131,8 @@ class Source:
             v, now, nold = self.wl.view(i)
             return v, now, nold, v.txn_count, None, None
         batch, now, nold = self.wl.batch(i)
-        sub, idx = self.kr.split(batch, self.rank)
-        return sub.view(), now, nold, batch.T, idx, (sub, batch)
+        sub, idx = self.kr.split(batch, self.rank, keep_all=self.keep_all)
+        return sub.view(), now, nold, batch.T, (None if self.keep_all else idx), (sub, batch)
 
 
 CONFIG_SHAPE = {
@@ -233,11 +237,13 @@ def main():
 
     cfg = args.config
     mode = args.mode if world > 1 else "single"
-    src = Source(cfg, args.txns, world, rank, split=(mode == "resolvers"))
+    sparse = mode == "exact" and args.protocol == "b"
+    src = Source(cfg, args.txns, world, rank, split=(mode == "resolvers" or sparse), keep_all=sparse)
     eng = None
     if mode == "exact":
         from foundationdb_amd.sharded import DistShardedConflictSet
-        eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=max_history(cfg))
+        eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=max_history(cfg),
+                                     sparse=sparse)
         cs = eng.shard.cs
     else:
         cs = ConflictSet(device=local, max_history=max_history(cfg))
@@ -254,7 +260,7 @@ def main():
     wverd = None
     pre = None
     if cfg == 5:  # preload: blind-write batches (config 50 of the generator), no compaction
-        pre = Source(50, args.txns, world, rank, split=(mode == "resolvers"))
+        pre = Source(50, args.txns, world, rank, split=(mode == "resolvers" or sparse), keep_all=sparse)
     n_pre = PRELOAD_BATCHES if pre is not None else 0
     for j in range(n_pre + args.warmup):
         i = j - n_pre
@@ -423,9 +429,13 @@ def main():
 
     if rank == 0:
         if mode == "exact":
-            workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
-                        f"5M-version window; one exact resolver sharded by key range over {world} GPUs "
-                        f"(RCCL MAX all-reduce of conflict flags + all-gathers for the compaction window)")
+            how = ("protocol B: each GPU receives only the ranges intersecting its keys; RCCL MAX all-reduce of "
+                   "conflict flags + all-gather of overlap edges + all-gather for the compaction window"
+                   if sparse else
+                   "protocol A: every GPU receives the whole batch; RCCL MAX all-reduce of conflict flags + "
+                   "all-gather for the compaction window")
+            workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), {CONFIG_SHAPE.get(cfg, '')}, "
+                        f"5M-version window; one exact resolver sharded by key range over {world} GPUs ({how})")
         elif mode == "resolvers":
             workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), 5R+2W, uniform 16-byte keys, "
                         f"5M-version window; {world} key-range resolvers (proxy split + RCCL MIN combine)")

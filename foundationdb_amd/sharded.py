@@ -108,6 +108,7 @@ def plan_compaction(infos, n_comb):
 
 KEY_INLINE = 32  # removalKeys up to this length travel inside exchange 1
 SLOT_WORDS = 4 + KEY_INLINE // 8  # H, last version, key length (-1: none), edges (protocol B), key words
+EDGE_INLINE = 1024  # protocol B: overlap edges per shard carried inside exchange 1 (more: a separate all-gather)
 
 
 def _pack_key(key):
@@ -374,7 +375,7 @@ class DistShardedConflictSet:
     """
 
     def __init__(self, bounds, rank, world, device, v0=0, max_history=0, group=None, shard_factory=Shard,
-                 sparse=False):
+                 sparse=False, edge_inline=EDGE_INLINE):
         import torch
         import torch.distributed as dist
 
@@ -383,6 +384,7 @@ class DistShardedConflictSet:
         self.rank, self.world = rank, world
         self.bounds = list(bounds)
         self.sparse = sparse  # protocol B: this rank receives only its ranges; overlap edges are all-gathered
+        self.ei = max(1, edge_inline)
         self.device = _device(torch, device)
         lo, hi = _shard_ranges(bounds)[rank]
         self.shard = shard_factory(lo, hi, device=device, v0=v0, max_history=max_history, sparse=sparse)
@@ -398,9 +400,12 @@ class DistShardedConflictSet:
     def _buffers(self, T):
         if T != self._T:
             torch = self.torch
-            n = max(1, T) + self.world * SLOT_WORDS * 8
+            nT8 = (max(1, T) + 7) // 8 * 8
+            n = nT8 + self.world * SLOT_WORDS * 8 + (self.world * 2 * self.ei * 4 if self.sparse else 0)
             self._h = torch.empty(max(1, T), dtype=torch.uint8, device=self.device)
-            self._x1 = torch.empty(n, dtype=torch.uint8, device=self.coll_dev)
+            self._x1 = torch.zeros(n, dtype=torch.uint8, device=self.coll_dev)
+            self._eoff = nT8 + self.world * SLOT_WORDS * 8
+            self._eb = torch.zeros(2 * self.ei, dtype=torch.int32, device=self.device)
             self._T = T
         return self._h, self._x1
 
@@ -419,19 +424,35 @@ class DistShardedConflictSet:
         n_edges = self.shard.edge_count() if self.sparse else 0
         mine = np.zeros(self.world * SLOT_WORDS, np.int64)
         mine[self.rank * SLOT_WORDS:(self.rank + 1) * SLOT_WORDS] = p.slot_words(n_edges)
-        x1[nT:].copy_(torch.from_numpy(mine.view(np.uint8)))
+        so, eo = self._eoff - self.world * SLOT_WORDS * 8, self._eoff
+        x1[so:eo].copy_(torch.from_numpy(mine.view(np.uint8)))
         x1[:nT].copy_(h)
+        if self.sparse:  # protocol B: up to self.ei edges per shard ride in this all-reduce too
+            x1[eo:].zero_()
+            if 0 < n_edges <= self.ei:
+                self.shard.get_edges(self._eb.data_ptr(), self._eb[self.ei:].data_ptr(), n_edges)
+                w = 2 * self.ei * 4
+                x1[eo + self.rank * w:eo + (self.rank + 1) * w].copy_(self._eb.view(torch.uint8))
         dist.all_reduce(x1, op=dist.ReduceOp.MAX, group=self.group)
         slots = torch.empty(self.world * SLOT_WORDS * 8, dtype=torch.uint8)
-        slots.copy_(x1[nT:])
+        slots.copy_(x1[so:eo])
         slots = slots.numpy().view(np.int64).reshape(self.world, SLOT_WORDS).tolist()
         if x1.device != self.device:
             h.copy_(x1[:nT])
             fl = h
         else:
             fl = x1
-        if self.sparse:  # protocol B: all-gather the overlap edges (counts came in the slots)
-            self._exchange_edges([int(w[3]) for w in slots], n_edges)
+        if self.sparse:  # protocol B: the union of the overlap edges (counts came in the slots)
+            counts = [int(w[3]) for w in slots]
+            if max(counts) <= self.ei:
+                ed = x1[eo:].view(torch.int32).view(self.world, 2, self.ei).to(self.device)
+                et = torch.cat([ed[g, 0, :counts[g]] for g in range(self.world)] + [ed.new_zeros(1)])
+                eu = torch.cat([ed[g, 1, :counts[g]] for g in range(self.world)] + [ed.new_zeros(1)])
+                _sync(torch, self.device)
+                self.shard.set_edges(et.data_ptr(), eu.data_ptr(), sum(counts))
+                self._edges_keep = (et, eu)
+            else:  # a long list somewhere: one more all-gather
+                self._exchange_edges(counts, n_edges)
         _sync(torch, self.device)  # the engine reads the flags on its own stream
         tick("exchange1")
         long_key = None

@@ -98,7 +98,7 @@ def test_model_shards_mixed_streams(sparse):
             check_step(sh, c, batch, now, nold)
 
 
-def _dist_rank(rank, world, port, bounds, seed, maxlen, sparse, q):
+def _dist_rank(rank, world, port, bounds, seed, maxlen, sparse, q, edge_inline=1024):
     import torch.distributed as dist
 
     from foundationdb_amd.sharded import DistShardedConflictSet
@@ -106,7 +106,8 @@ def _dist_rank(rank, world, port, bounds, seed, maxlen, sparse, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard, sparse=sparse)
+    sh = DistShardedConflictSet(bounds, rank, world, device=-1, shard_factory=ModelShard, sparse=sparse,
+                                edge_inline=edge_inline)
     out = []
     for batch, now, nold in tiny_stream(seed, n_batches=25, maxlen=maxlen):
         v = sh.detect_packed(batch, now, nold)
@@ -115,19 +116,21 @@ def _dist_rank(rank, world, port, bounds, seed, maxlen, sparse, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,maxlen,sparse", [(2, 3, False), (3, 3, False), (2, 40, False), (2, 3, True),
-                                                 (3, 3, True), (2, 40, True)])
-def test_dist_sharded_gloo(world, maxlen, sparse):
+@pytest.mark.parametrize("world,maxlen,sparse,ei", [(2, 3, False, 1024), (3, 3, False, 1024), (2, 40, False, 1024),
+                                                    (2, 3, True, 1024), (3, 3, True, 1024), (2, 40, True, 1024),
+                                                    (3, 3, True, 1)])
+def test_dist_sharded_gloo(world, maxlen, sparse, ei):
     """world_size 2/3 over gloo: one shard per rank; every rank's verdicts, the
     concatenation of the ranks' histories and removalKey equal one conflict set's
-    (maxlen 40: removalKeys longer than the all-gather's inline 32 bytes)."""
+    (maxlen 40: removalKeys longer than the all-gather's inline 32 bytes;
+    ei 1: protocol B edge lists too long to ride in exchange 1)."""
     rng = random.Random(world)
     bounds = random_bounds(rng, world, 3)
     seed = 1234 + world + maxlen
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.Random(os.getpid() * 7 + world).randint(0, 3000)
-    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, maxlen, sparse, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_rank, args=(r, world, port, bounds, seed, maxlen, sparse, q, ei)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in range(world))
