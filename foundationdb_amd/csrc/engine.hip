@@ -280,7 +280,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
-    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp);
+    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
     dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
@@ -383,6 +383,14 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         HIPOK(hipMemsetAsync(b.ss_qt, 0, 2 * 1024 * SS_QT, s));
         HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 2 * 1024 * sizeof(int32_t), s));
         HIPOK(hipMemsetAsync(b.ss_q, 0, 2 * 1024 * sizeof(SRec), s));  // equal records: valid (sorted) splitters
+    }
+    if (!b.lb_meta && (r = dalloc(b.lb_meta, lb_meta_words()))) return r;
+    if (b.large && lb_hist_words((int)R, (int)W) + 1 > b.lb_hist_cap) {
+        const int64_t n = lb_hist_words((int)R, (int)W) + 1;
+        dfree(b.lb_hist);
+        b.lb_hist_cap = 0;
+        if ((r = dalloc(b.lb_hist, 2 * n))) return r;
+        b.lb_hist_cap = n;
     }
     if (R + 2 * W > cs->capSortRec) {
         const int64_t n = std::max<int64_t>(R + 2 * W, 4096);

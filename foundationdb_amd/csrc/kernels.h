@@ -56,7 +56,10 @@ struct BatchBufs {
     SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
     uint8_t* ss_qt;      // [2 * 1024 * SS_QT] their tail bytes (the batch keys they came from are gone)
     int32_t* ss_bkt;     // [R + 2W] bucket of each record
-    SRec* ss_tmp;        // bucket staging rows
+    SRec* ss_tmp;        // bucket staging rows (large batches: merge-sort scratch)
+    int32_t* lb_meta;    // large-batch bucketed sort: offsets, passes, per-pass chunk prefixes
+    int32_t* lb_hist;    // [2 * lb_hist_cap] per-block bucket counts and their scan
+    int64_t lb_hist_cap;
     int64_t ss_tmp_cap;
     // intra-batch overlap dedup matrix and edges
     uint32_t* pair_bits; // [pair_T * row_words] (small batches only)
@@ -156,6 +159,8 @@ int64_t sort_staging_records(int R, int W, bool large);
 constexpr int64_t LARGE_T = 65536;
 constexpr int64_t MAX_T = 1310720;  // k_dec_walk keeps a committed bit per txn in LDS (160 KiB)
 bool large_batch_mode(int64_t T);
+int64_t lb_meta_words();
+int64_t lb_hist_words(int R, int W);
 // history read check + intra-batch overlap edges, one launch
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s);

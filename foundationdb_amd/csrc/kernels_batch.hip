@@ -708,18 +708,10 @@ __device__ inline int merge_path(GetA ga, int la, GetB gb, int lb, int d, const 
     return lo;
 }
 
-__global__ __launch_bounds__(MS_THREADS) void k_ms_merge(MergeSortArgs M, int pass, KeyArrays keys) {
-    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
-    __shared__ int s_cut[2];
-    const int job = (int)blockIdx.x < M.blocks0 ? 0 : 1;
-    const int chunk = job ? blockIdx.x - M.blocks0 : blockIdx.x;
-    const int n = M.n[job];
-    const int P = M.passes[job];
-    const SRec* src = M.buf[job][(P - pass) & 1];
-    SRec* dst = M.buf[job][(P - pass - 1) & 1];
-    const uint8_t* const* tails = keys.tail;
-    const int64_t w = (int64_t)MS_TILE << pass;
-    const int64_t o0 = (int64_t)chunk * MS_CHUNK;
+// One merge-sort chunk: MS_CHUNK outputs [o0, o0 + MS_CHUNK) of the pass that
+// merges runs of width w of src[0, n) into dst[0, n).
+__device__ void merge_chunk(const SRec* src, SRec* dst, int n, int64_t w, int64_t o0, const uint8_t* const* tails,
+                            const LdsRecs& L, int* s_cut) {
     const int64_t base = o0 / (2 * w) * (2 * w);
     const int la = (int)min<int64_t>(w, n - base);
     const int lb = (int)max<int64_t>(0, min<int64_t>(w, n - base - w));
@@ -734,7 +726,6 @@ __global__ __launch_bounds__(MS_THREADS) void k_ms_merge(MergeSortArgs M, int pa
     const int a0 = s_cut[0], a1 = s_cut[1];
     const int b0 = d0 - a0, b1 = d1 - a1;
     const int na = a1 - a0, nb = b1 - b0;
-    const LdsRecs L{s_hi, s_lo, s_mi};  // [0, na): a piece, [na, na + nb): b piece
     for (int k = threadIdx.x; k < na + nb; k += MS_THREADS) L.put(k, k < na ? A[a0 + k] : B[b0 + k - na]);
     __syncthreads();
     const int dl = threadIdx.x * MS_ITEMS;
@@ -752,6 +743,16 @@ __global__ __launch_bounds__(MS_THREADS) void k_ms_merge(MergeSortArgs M, int pa
     }
 }
 
+__global__ __launch_bounds__(MS_THREADS) void k_ms_merge(MergeSortArgs M, int pass, KeyArrays keys) {
+    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
+    __shared__ int s_cut[2];
+    const int job = (int)blockIdx.x < M.blocks0 ? 0 : 1;
+    const int chunk = job ? blockIdx.x - M.blocks0 : blockIdx.x;
+    const int P = M.passes[job];
+    merge_chunk(M.buf[job][(P - pass) & 1], M.buf[job][(P - pass - 1) & 1], M.n[job], (int64_t)MS_TILE << pass,
+                (int64_t)chunk * MS_CHUNK, keys.tail, LdsRecs{s_hi, s_lo, s_mi}, s_cut);
+}
+
 __global__ __launch_bounds__(256) void k_ms_finish(MergeSortArgs M, SortJobs J, KeyArrays keys) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g < M.n[1]) J.out_slot[g] = M.buf[1][0][g].idx;
@@ -762,6 +763,210 @@ __global__ __launch_bounds__(256) void k_ms_finish(MergeSortArgs M, SortJobs J, 
     }
     if (g < 2 * SS_MAXB) J.cnt_next[g] = 0;  // (this path leaves the current parity's counters zero)
 }
+
+// Bucketed large-batch sort (steady state: splitters from the previous batch's
+// quantiles exist).  The records of each job are first distributed over
+// SS_MAXB buckets by the splitters (count, scan, scatter), then every bucket
+// is merge-sorted on its own: bucket b needs only ceil(log2(size_b / MS_TILE))
+// merge passes instead of the whole job's.  Buckets ping-pong between the
+// job's output array and scratch like the jobs of the plain merge sort; a
+// bucket's scatter target is the array its tile sort must start in.
+static constexpr int LB_MAXP = 16;  // merge passes a bucket may need (2^16 tiles)
+
+static constexpr int LB_RPB = 4096;  // records per count / scatter block (16 per thread)
+
+struct BucketSortArgs {
+    SortJobs J;
+    SRec* buf[2][2];
+    int32_t* hist;  // per-block bucket counts, bucket-major per job: [job base + b * nblk + blk]
+    int32_t* hoff;  // their exclusive scan (global positions; job 1's start at n0)
+    int32_t* off;   // [2][SS_MAXB + 1] bucket starts
+    int32_t* pb;    // [2][SS_MAXB] merge passes per bucket
+    int32_t* toff;  // [2][SS_MAXB + 1] tile prefix
+    int32_t* coff;  // [LB_MAXP][2][SS_MAXB + 1] merge-chunk prefix of the buckets still merging in pass p
+    int32_t* maxp;  // [1]
+    int32_t* bkt;   // [n0 + n1]
+    int32_t nblk[2];
+    int64_t hbase[2];
+    int32_t tiles0, chunks0;  // grid split between the jobs (tile, merge launches)
+};
+
+__device__ inline int lb_find(const int32_t* pre, int nb, int x) {  // bucket with pre[b] <= x < pre[b + 1]
+    int lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// per-block histograms in LDS (no global atomics: 1,024 hot counters would
+// serialize millions of atomics in L2)
+__global__ __launch_bounds__(256) void k_lb_count(BucketSortArgs A, KeyArrays keys) {
+    __shared__ uint64_t sp[SS_MAXB];
+    __shared__ int32_t h[SS_MAXB];
+    const SortJobs& J = A.J;
+    const int job = (int)blockIdx.x < A.nblk[0] ? 0 : 1;
+    const int blk = job ? blockIdx.x - A.nblk[0] : blockIdx.x;
+    const int nb = J.nb[job];
+    splitter_fill(J, job, sp);
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const int i1 = min(J.n[job], (blk + 1) * LB_RPB);
+    int32_t* bkt = A.bkt + (job ? J.n[0] : 0);
+    for (int i = blk * LB_RPB + threadIdx.x; i < i1; i += blockDim.x) {
+        const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
+        const int b = bucket_of(J, job, sp, x, keys.tail);
+        bkt[i] = b;
+        atomicAdd(&h[b], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) A.hist[A.hbase[job] + (int64_t)b * A.nblk[job] + blk] = h[b];
+}
+
+__global__ __launch_bounds__(SS_MAXB) void k_lb_scan(BucketSortArgs A) {
+    __shared__ int64_t red[SS_MAXB / 64 + 1];
+    const int job = blockIdx.x, b = threadIdx.x;
+    const int nb = A.J.nb[job];
+    const int n = A.J.n[job];
+    const int adj = job ? A.J.n[0] : 0;
+    const int o = b < nb ? A.hoff[A.hbase[job] + (int64_t)b * A.nblk[job]] - adj : n;
+    const int o1 = b + 1 < nb ? A.hoff[A.hbase[job] + (int64_t)(b + 1) * A.nblk[job]] - adj : n;
+    const int c = b < nb ? o1 - o : 0;
+    int p = 0;
+    for (int64_t w = MS_TILE; w < c; w <<= 1) p++;
+    int64_t tot;
+    const int64_t to = block_excl_scan((int64_t)cdiv(c, MS_TILE), red, tot);
+    if (b < nb) {
+        A.off[job * (SS_MAXB + 1) + b] = o;
+        A.pb[job * SS_MAXB + b] = p;
+        A.toff[job * (SS_MAXB + 1) + b] = (int32_t)to;
+        if (p) atomicMax(A.maxp, p);
+    }
+    if (b == 0) {
+        A.off[job * (SS_MAXB + 1) + nb] = n;
+        A.toff[job * (SS_MAXB + 1) + nb] = (int32_t)tot;
+    }
+    for (int q = 0; q < LB_MAXP; q++) {
+        const int64_t co = block_excl_scan((int64_t)(p > q ? cdiv(c, MS_CHUNK) : 0), red, tot);
+        int32_t* pre = A.coff + ((int64_t)q * 2 + job) * (SS_MAXB + 1);
+        if (b < nb) pre[b] = (int32_t)co;
+        if (b == 0) pre[nb] = (int32_t)tot;
+    }
+}
+
+// the same record partition as k_lb_count: each block's slice of a bucket
+// starts at its scanned offset; ranks inside the slice by LDS atomics
+__global__ __launch_bounds__(256) void k_lb_scatter(BucketSortArgs A, KeyArrays keys) {
+    __shared__ int32_t cur[SS_MAXB];
+    __shared__ uint8_t par[SS_MAXB];
+    const SortJobs& J = A.J;
+    const int job = (int)blockIdx.x < A.nblk[0] ? 0 : 1;
+    const int blk = job ? blockIdx.x - A.nblk[0] : blockIdx.x;
+    const int nb = J.nb[job];
+    const int adj = job ? J.n[0] : 0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        cur[b] = A.hoff[A.hbase[job] + (int64_t)b * A.nblk[job] + blk] - adj;
+        par[b] = (uint8_t)(A.pb[job * SS_MAXB + b] & 1);
+    }
+    __syncthreads();
+    const int i1 = min(J.n[job], (blk + 1) * LB_RPB);
+    const int32_t* bkt = A.bkt + adj;
+    for (int i = blk * LB_RPB + threadIdx.x; i < i1; i += blockDim.x) {
+        const int b = bkt[i];
+        const int pos = atomicAdd(&cur[b], 1);
+        A.buf[job][par[b]][pos] = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
+    }
+}
+
+__global__ __launch_bounds__(MS_THREADS) void k_lb_tile(BucketSortArgs A, KeyArrays keys) {
+    __shared__ uint64_t s_hi[MS_TILE], s_lo[MS_TILE], s_mi[MS_TILE];
+    const int job = (int)blockIdx.x < A.tiles0 ? 0 : 1;
+    const int tile = job ? blockIdx.x - A.tiles0 : blockIdx.x;
+    const int nb = A.J.nb[job];
+    const int32_t* toff = A.toff + job * (SS_MAXB + 1);
+    if (nb == 0 || tile >= toff[nb]) return;
+    const int b = lb_find(toff, nb, tile);
+    const int64_t o = A.off[job * (SS_MAXB + 1) + b];
+    const int c = A.off[job * (SS_MAXB + 1) + b + 1] - (int)o;
+    const int64_t i0 = (int64_t)(tile - toff[b]) * MS_TILE;
+    SRec* a = A.buf[job][A.pb[job * SS_MAXB + b] & 1] + o;  // sorted in place
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    for (int k = threadIdx.x; k < MS_TILE; k += MS_THREADS) L.put(k, i0 + k < c ? a[i0 + k] : rec_inf());
+    __syncthreads();
+    lds_bitonic(L, MS_TILE, keys.tail);
+    for (int k = threadIdx.x; k < MS_TILE && i0 + k < c; k += MS_THREADS) a[i0 + k] = L.get(k);
+}
+
+__global__ __launch_bounds__(MS_THREADS) void k_lb_merge(BucketSortArgs A, int pass, KeyArrays keys) {
+    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
+    __shared__ int s_cut[2];
+    const int job = (int)blockIdx.x < A.chunks0 ? 0 : 1;
+    const int chunk = job ? blockIdx.x - A.chunks0 : blockIdx.x;
+    const int nb = A.J.nb[job];
+    const int32_t* pre = A.coff + ((int64_t)pass * 2 + job) * (SS_MAXB + 1);
+    if (nb == 0 || chunk >= pre[nb]) return;
+    const int b = lb_find(pre, nb, chunk);
+    const int64_t o = A.off[job * (SS_MAXB + 1) + b];
+    const int c = A.off[job * (SS_MAXB + 1) + b + 1] - (int)o;
+    const int P = A.pb[job * SS_MAXB + b];
+    merge_chunk(A.buf[job][(P - pass) & 1] + o, A.buf[job][(P - pass - 1) & 1] + o, c, (int64_t)MS_TILE << pass,
+                (int64_t)(chunk - pre[b]) * MS_CHUNK, keys.tail, LdsRecs{s_hi, s_lo, s_mi}, s_cut);
+}
+
+int64_t lb_hist_words(int R, int W) {
+    return (int64_t)SS_MAXB * (cdiv(R, LB_RPB) + cdiv(2 * (int64_t)W, LB_RPB)) + 1;
+}
+
+// returns false when a bucket would need more than LB_MAXP passes (the
+// caller falls back to the plain merge sort)
+static bool launch_bucket_sort(const SortJobs& J, BatchBufs& b, hipStream_t s) {
+    BucketSortArgs A;
+    A.J = J;
+    for (int j = 0; j < 2; j++) A.buf[j][0] = J.out[j];
+    A.buf[0][1] = b.ss_tmp;
+    A.buf[1][1] = b.ss_tmp + J.n[0];
+    int32_t* m = b.lb_meta;
+    A.pb = m;
+    A.maxp = m + 2 * SS_MAXB;
+    A.off = m + 2 * SS_MAXB + 8;
+    A.toff = A.off + 2 * (SS_MAXB + 1);
+    A.coff = A.toff + 2 * (SS_MAXB + 1);
+    A.bkt = b.ss_bkt;
+    A.hist = b.lb_hist;
+    A.hoff = b.lb_hist + b.lb_hist_cap;
+    for (int j = 0; j < 2; j++) A.nblk[j] = cdiv(J.n[j], LB_RPB);
+    A.hbase[0] = 0;
+    A.hbase[1] = (int64_t)J.nb[0] * A.nblk[0];
+    const int64_t hn = A.hbase[1] + (int64_t)J.nb[1] * A.nblk[1];
+    A.tiles0 = J.n[0] ? cdiv(J.n[0], MS_TILE) + J.nb[0] : 0;
+    A.chunks0 = J.n[0] ? cdiv(J.n[0], MS_CHUNK) + J.nb[0] : 0;
+    hipMemsetAsync(A.maxp, 0, sizeof(int32_t), s);
+    const int cblocks = A.nblk[0] + A.nblk[1];
+    hipLaunchKernelGGL(k_lb_count, dim3(cblocks), dim3(256), 0, s, A, b.keys);
+    scan_i32(A.hist, A.hoff, nullptr, (int32_t)hn, nullptr, b.scan_tmp, s);
+    hipLaunchKernelGGL(k_lb_scan, dim3(2), dim3(SS_MAXB), 0, s, A);
+    int32_t maxp = 0;
+    hipMemcpyAsync(&maxp, A.maxp, sizeof(maxp), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (maxp > LB_MAXP) return false;
+    hipLaunchKernelGGL(k_lb_scatter, dim3(cblocks), dim3(256), 0, s, A, b.keys);
+    const int tiles = A.tiles0 + (J.n[1] ? cdiv(J.n[1], MS_TILE) + J.nb[1] : 0);
+    hipLaunchKernelGGL(k_lb_tile, dim3(tiles), dim3(MS_THREADS), 0, s, A, b.keys);
+    const int chunks = A.chunks0 + (J.n[1] ? cdiv(J.n[1], MS_CHUNK) + J.nb[1] : 0);
+    for (int p = 0; p < maxp; p++) hipLaunchKernelGGL(k_lb_merge, dim3(chunks), dim3(MS_THREADS), 0, s, A, p, b.keys);
+    MergeSortArgs M;  // (only n and the output arrays matter to the finish)
+    for (int j = 0; j < 2; j++) {
+        M.n[j] = J.n[j];
+        M.buf[j][0] = J.out[j];
+    }
+    const int64_t fin = std::max<int64_t>(std::max(M.n[1], 2 * SS_MAXB), 2 * SS_Q);
+    hipLaunchKernelGGL(k_ms_finish, dim3(cdiv(fin, 256)), dim3(256), 0, s, M, J, b.keys);
+    return true;
+}
+
+int64_t lb_meta_words() { return 2 * SS_MAXB + 8 + 4 * (SS_MAXB + 1) + (int64_t)LB_MAXP * 2 * (SS_MAXB + 1); }
 
 static void launch_merge_sort(const SortJobs& J, BatchBufs& b, hipStream_t s) {
     MergeSortArgs M;
@@ -860,8 +1065,9 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
     if (J.n[0] + J.n[1] == 0) return false;
-    if (b.large) {
-        launch_merge_sort(J, b, s);
+    if (b.large) {  // bucketed merge sort once splitters exist; the plain merge sort on the first batch
+        static const bool plain = getenv("FDBCS_LARGE_SORT_PLAIN") != nullptr;  // (A/B measurements)
+        if (sample || plain || !launch_bucket_sort(J, b, s)) launch_merge_sort(J, b, s);
         return true;
     }
     if (!scattered) {  // (otherwise the ingest already put every record into its bucket)
