@@ -276,7 +276,7 @@ void free_plan(BatchBufs& b) {
 
 void free_batch(BatchBufs& b) {
     dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict); dfree(b.dec_blk);
-    dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
+    dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx); dfree(b.cbits);
     dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
@@ -317,11 +317,12 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         GROWLOG("T %lld\n", (long long)T);
         int64_t n = std::max<int64_t>(T, 1024);
         dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict); dfree(b.dec_blk);
-        dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx);
+        dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx); dfree(b.cbits);
         // +64: k_decide_combine reads these byte arrays as 4-byte words
         if ((r = dalloc(b.too_old, n + 64)) || (r = dalloc(b.hist, n + 64)) || (r = dalloc(b.committed, n)) ||
             (r = dalloc(b.verdict, n)) || (r = dalloc(b.deg, n)) || (r = dalloc(b.off, n + 1)) ||
             (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)) ||
+            (r = dalloc(b.cbits, n / 64 + 2)) ||
             (r = dalloc(b.dec_blk, 2 * (n / 256 + 2))))
             return r;
         cs->capT = n;
@@ -1202,7 +1203,7 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     info[0] = h.H;
     info[1] = compact ? h.win_g0 : -1;
     info[2] = h.last_ver;
-    info[3] = h.n_comb_own;
+    info[3] = (cs->h.shard.has_lo | cs->h.shard.has_hi) ? h.n_comb_own : h.n_comb;  // (one shard: all of them)
     return h.last_err ? h.last_err : (compact ? h.err : 0);
 }
 

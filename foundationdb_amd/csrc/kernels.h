@@ -37,6 +37,7 @@ struct BatchBufs {
     int32_t* cur;        // fill cursors
     int32_t* dep_list;   // dependents in index order
     int32_t* dep_idx;    // t -> index in dep_list or -1
+    uint64_t* cbits;     // [T / 64 + 1] committed bits (grid decision)
     // range level
     int32_t* read_txn;   // [R]
     int64_t* read_snap;  // [R] snapshot of the read's transaction (INT64_MAX: too old)

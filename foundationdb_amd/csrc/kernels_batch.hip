@@ -1722,6 +1722,7 @@ struct DecGridArgs {
     int32_t* cur;       // [ndep] CSR fill cursors
     int32_t* csr;
     uint8_t* committed;
+    uint64_t* cbits;    // [T / 64 + 1] committed as bits (k_dec_flags), for k_dec_walk's LDS copy
     uint8_t* verdict;
     Scalars* sc;
 };
@@ -1740,8 +1741,12 @@ __global__ __launch_bounds__(DG_THREADS) void k_dec_flags(DecGridArgs A) {
         const bool und = !to && !A.hist[t];
         d = A.deg[t];
         dep = und && d > 0;
-        A.committed[t] = und && !dep;  // (a dependent starts uncommitted: k_dec_walk reads these as bits)
+        A.committed[t] = und && !dep;  // (a dependent starts uncommitted)
         if (!dep) A.verdict[t] = verdict_of(und, to);
+    }
+    {  // the same as bits for k_dec_walk: a wavefront's 64 transactions are one aligned word
+        const uint64_t m = __ballot(t < A.T && !dep && A.committed[t]);
+        if ((threadIdx.x & 63) == 0 && t < A.T) A.cbits[t >> 6] = m;
     }
     int64_t tot;
     block_excl_scan(dep ? ((int64_t)1 << 32) | (uint32_t)d : (int64_t)0, red, tot);
@@ -1787,11 +1792,8 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
     Scalars* sc = A.sc;
     const int E = (int)min((int64_t)sc->edges_total, A.edge_cap);
     const int ndep = sc->n_dep;
-    for (int i = tid; i < (T + 31) / 32; i += nthr) {
-        uint32_t m = 0;
-        for (int k = 0; k < 32 && 32 * i + k < T; k++) m |= (uint32_t)(A.committed[32 * i + k] != 0) << k;
-        cbits[i] = m;
-    }
+    const uint32_t* cb32 = reinterpret_cast<const uint32_t*>(A.cbits);  // (little-endian halves of the words)
+    for (int i = tid; i < (T + 31) / 32; i += nthr) cbits[i] = cb32[i];
     for (int e = tid; e < E; e += nthr) {
         const int t = A.et[e], u = A.eu[e];
         const int k = A.didx[t];
@@ -1855,7 +1857,7 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
         G.T = T; G.too_old = b.too_old; G.hist = b.hist; G.deg = b.deg; G.et = b.et; G.eu = b.eu;
         G.edge_cap = b.edge_cap; G.bits = b.dedup ? b.pair_bits : nullptr; G.row_words = b.row_words;
         G.bd = b.dec_blk; G.be = b.dec_blk + nb + 1; G.didx = b.dep_idx; G.dep_list = b.dep_list; G.doff = b.off;
-        G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.verdict = verdict; G.sc = sc;
+        G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.cbits = b.cbits; G.verdict = verdict; G.sc = sc;
         hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
         hipLaunchKernelGGL(k_dec_place, dim3(nb), dim3(DG_THREADS), 0, s, G);
         hipLaunchKernelGGL(k_dec_walk, dim3(1), dim3(1024), (size_t)((T + 31) / 32) * 4, s, G);

@@ -124,8 +124,8 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     if (shard.at_or_above(b) || shard.below(e)) return;
     const int has_b = shard.below(b) ? 0 : 1;
     const bool e_in = !shard.at_or_above(e);
-    {  // (the global compaction budget sums these over shards): one atomic per wavefront
-        const uint64_t m = __ballot(has_b);
+    if (shard.has_lo | shard.has_hi) {  // (the global compaction budget sums these over shards)
+        const uint64_t m = __ballot(has_b);  // one atomic per wavefront
         if (has_b && (int)__lane_id() == __ffsll((unsigned long long)m) - 1) atomicAdd(&sc->n_comb_own, __popcll(m));
     }
     rb.put(j, b);  // compact copies for the page merge
