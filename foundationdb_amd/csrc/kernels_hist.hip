@@ -172,7 +172,10 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
 // at their new positions and the affected pages' merge plan, and resets the
 // accumulators for the next batch.
 static constexpr int PS_THREADS = 256;
-static constexpr int PS_ITEMS = 4;
+#ifndef FDBCS_PS_ITEMS
+#define FDBCS_PS_ITEMS 2
+#endif
+static constexpr int PS_ITEMS = FDBCS_PS_ITEMS;
 static constexpr int PS_BLOCK = PS_THREADS * PS_ITEMS;
 
 struct PlanItem {
