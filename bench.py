@@ -70,13 +70,16 @@ def parse():
                    help="extra instrumented batches after the timed region (default 50; config 5: 3)")
     p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
                    help="N > 1: one exact resolver sharded by key range, or N independent key-range resolvers")
+    p.add_argument("--pcie-batches", type=int, default=None,
+                   help="host batches timed through the PCIe-inclusive paths after the measurement (default 50; "
+                        "config 5: 2)")
     p.add_argument("--protocol", choices=["a", "b"], default="b",
                    help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
                         "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
     a = p.parse_args()
     big = a.config == 5  # 1 M-txn batches over a preloaded 10^8-boundary history
     for name, small, large in [("steps", 200, 10), ("warmup", 2500, 2), ("txns", 5000, 1_000_000),
-                               ("stage_batches", 50, 3)]:
+                               ("stage_batches", 50, 3), ("pcie_batches", 50, 2)]:
         if getattr(a, name) is None:
             setattr(a, name, large if big else small)
     return a
@@ -407,6 +410,31 @@ def main():
             roofline["traffic"] = pm.get("bytes_per_batch")
             roofline["traffic_source"] = pm.get("source")
 
+    # ---- PCIe-inclusive rate (not `value`): host SoA batches through the C ABI ----
+    pcie = None
+    if mode == "single" and args.pcie_batches > 0:
+        n = args.pcie_batches
+        first = args.warmup + n_stage
+        host = [src.wl.batch(first + j) for j in range(2 * n)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b, now, nold in host[:n]:  # synchronous: pack, H2D, pipeline, verdict D2H, then the next
+            cs.detect_packed(b, now, nold)
+        t_serial = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for j, (b, now, nold) in enumerate(host[n:]):  # two in flight: batch k+1's packing and H2D overlap k
+            cs.submit_packed(b, now, nold)
+            if j >= 1:
+                cs.wait()
+        cs.wait()
+        t_pipe = time.perf_counter() - t0
+        T0 = host[0][0].T
+        pcie = {"serial": round(n * T0 / t_serial, 1), "pipelined": round(n * T0 / t_pipe, 1), "unit": "txn/s",
+                "batches": n, "host_bytes_per_batch": int(np.mean([b.nbytes() for b, _n, _o in host])),
+                "path": "host SoA batch -> pinned staging -> H2D -> detectConflicts pipeline -> verdict D2H "
+                        "(fdbcs_batch_detect_packed; pipelined: fdbcs_batch_submit_packed / fdbcs_batch_wait)"}
+        del host
+
     # ---- CPU baseline (oracle, 1 core) on the same batches, same start state -----
     cpu = None
     if snap is not None:
@@ -460,6 +488,7 @@ def main():
                        "parallelism": {"exact": f"sharded{world}", "resolvers": f"keyrange{world}"}.get(mode, "single")},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
         }
         if alt:
             out["alt_modes"] = alt

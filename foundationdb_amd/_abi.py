@@ -59,6 +59,8 @@ FDBCS_FUNCS = [
     ("fdbcs_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_batch_txn_count", C.c_int32, [C.c_void_p]),
     ("fdbcs_batch_detect_packed", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_batch_submit_packed", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64]),
+    ("fdbcs_batch_wait", C.c_int, [C.c_void_p, C.c_void_p]),
     ("fdbcs_detect_device", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p, C.c_int]),
     ("fdbcs_history_size", C.c_int64, [C.c_void_p]),
     ("fdbcs_header_version", C.c_int64, [C.c_void_p]),

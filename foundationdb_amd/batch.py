@@ -66,6 +66,11 @@ class PackedBatch:
                    arr(v.key_len, C.c_uint32, slots, np.uint32),
                    arr(v.key_bytes, C.c_uint8, int(v.key_bytes_len), np.uint8))
 
+    def nbytes(self):
+        """Host bytes of the batch (what crosses PCIe in one staged transfer)."""
+        return sum(a.nbytes for a in (self.snapshot, self.read_off, self.write_off, self.key_off, self.key_len,
+                                      self.key_bytes))
+
     def view(self):
         if self._view is None:
             v = BatchView()

@@ -146,6 +146,23 @@ class ConflictSet:
                                                   out.ctypes.data), "detectConflicts")
         return out[:batch.T]
 
+    def submit_packed(self, batch, now, new_oldest):
+        """Pipelined detectConflicts (fdbcs_batch_submit_packed): returns at once;
+        the next submit's packing and H2D copy overlap this batch's kernels.
+        ``batch``: a PackedBatch or a raw host view (kept alive until wait())."""
+        view = batch.view() if hasattr(batch, "view") else batch
+        if not hasattr(self, "_inflight"):
+            self._inflight = []
+        check(self._lib.fdbcs_batch_submit_packed(self.handle, C.byref(view), now, new_oldest), "submit")
+        self._inflight.append((batch, view, view.txn_count))
+
+    def wait(self):
+        """Verdict bytes of the oldest submitted batch (fdbcs_batch_wait)."""
+        _b, _v, T = self._inflight.pop(0)
+        out = np.zeros(max(T, 1), np.uint8)
+        check(self._lib.fdbcs_batch_wait(self.handle, out.ctypes.data), "wait")
+        return out[:T]
+
     def detect_view(self, host_view, now, new_oldest, out=None):
         """detectConflicts on a raw host fdbcs_batch_view (e.g. generator memory)."""
         T = host_view.txn_count

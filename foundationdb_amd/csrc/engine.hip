@@ -54,7 +54,10 @@ int dalloc(T*& p, int64_t n) {
 
 template <typename T>
 void dfree(T*& p) {
-    if (p) hipFree((void*)p);
+    if (p) {
+        hipDeviceSynchronize();  // (growth only: a pipelined batch may still be using the buffer)
+        hipFree((void*)p);
+    }
     p = nullptr;
 }
 
@@ -126,6 +129,23 @@ struct fdbcs {
     bool sparse_edges = false;    // exact sharded protocol B: this shard exports its overlap edges
     int64_t last_T = 0, last_R = 0, last_W = 0;  // shape of the last batch (stats)
     int64_t sorts = 0;                           // sorts launched (sort-counter parity)
+    // pipelined host batches (fdbcs_batch_submit_packed / fdbcs_batch_wait): two
+    // staging slots, so batch k+1's host packing and H2D copy (copy stream)
+    // overlap batch k's kernels
+    struct Slot {
+        uint8_t* pin = nullptr;
+        size_t pin_cap = 0;
+        uint8_t* din = nullptr;
+        size_t din_cap = 0;
+        uint8_t* vpin = nullptr;
+        size_t vpin_cap = 0;
+        uint8_t* dverd = nullptr;
+        int64_t dverd_cap = 0;
+        hipEvent_t copied = nullptr, done = nullptr;
+        int64_t T = 0;
+    } slot[2];
+    hipStream_t copy_stream = nullptr;
+    int64_t sub_head = 0, sub_tail = 0;  // batches submitted / waited for
 };
 
 namespace {
@@ -603,50 +623,74 @@ int ensure_pinned(uint8_t*& p, size_t& cap, size_t need) {
 
 // Lay a host batch view out in one pinned buffer, copy it to the device in one
 // transfer and return the device-side view.
-int stage_batch(fdbcs* cs, const fdbcs_batch_view& hv, fdbcs_batch_view& dv) {
+struct StageLayout {
+    size_t o_snap, o_ro, o_wo, o_ko, o_kl, o_kb, total;
+};
+
+StageLayout stage_layout(const fdbcs_batch_view& hv) {
     const int64_t T = hv.txn_count, R = hv.read_count, W = hv.write_count, slots = 2 * (R + W);
     auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-    const size_t o_snap = 0;
-    const size_t o_ro = al(o_snap + 8 * T);
-    const size_t o_wo = al(o_ro + 4 * (T + 1));
-    const size_t o_ko = al(o_wo + 4 * (T + 1));
-    const size_t o_kl = al(o_ko + 8 * slots);
-    const size_t o_kb = al(o_kl + 4 * slots);
-    const size_t total = al(o_kb + hv.key_bytes_len + 16);
-    int r;
-    if ((r = ensure_pinned(cs->pin, cs->pin_cap, total))) return r;
-    if (total > cs->din_cap) {
-        dfree(cs->din);
-        size_t n = std::max(total, cs->din_cap * 2);
-        if ((r = dalloc(cs->din, (int64_t)n))) return r;
-        cs->din_cap = n;
-    }
-    // the previous batch's H2D must be done before overwriting the pinned buffer
-    HIPOK(hipStreamSynchronize(cs->stream));
-    uint8_t* p = cs->pin;
-    if (T) memcpy(p + o_snap, hv.snapshot, 8 * T);
-    memcpy(p + o_ro, hv.read_off, 4 * (T + 1));
-    memcpy(p + o_wo, hv.write_off, 4 * (T + 1));
+    StageLayout L;
+    L.o_snap = 0;
+    L.o_ro = al(L.o_snap + 8 * T);
+    L.o_wo = al(L.o_ro + 4 * (T + 1));
+    L.o_ko = al(L.o_wo + 4 * (T + 1));
+    L.o_kl = al(L.o_ko + 8 * slots);
+    L.o_kb = al(L.o_kl + 4 * slots);
+    L.total = al(L.o_kb + hv.key_bytes_len + 16);
+    return L;
+}
+
+void stage_fill(const fdbcs_batch_view& hv, const StageLayout& L, uint8_t* p) {
+    const int64_t T = hv.txn_count, slots = 2 * ((int64_t)hv.read_count + hv.write_count);
+    if (T) memcpy(p + L.o_snap, hv.snapshot, 8 * T);
+    memcpy(p + L.o_ro, hv.read_off, 4 * (T + 1));
+    memcpy(p + L.o_wo, hv.write_off, 4 * (T + 1));
     if (slots) {
-        memcpy(p + o_ko, hv.key_off, 8 * slots);
-        memcpy(p + o_kl, hv.key_len, 4 * slots);
+        memcpy(p + L.o_ko, hv.key_off, 8 * slots);
+        memcpy(p + L.o_kl, hv.key_len, 4 * slots);
     }
-    if (hv.key_bytes_len) memcpy(p + o_kb, hv.key_bytes, hv.key_bytes_len);
-    HIPOK(hipMemcpyAsync(cs->din, p, total, hipMemcpyHostToDevice, cs->stream));
-    dv = hv;
-    dv.snapshot = (const int64_t*)(cs->din + o_snap);
-    dv.read_off = (const int32_t*)(cs->din + o_ro);
-    dv.write_off = (const int32_t*)(cs->din + o_wo);
-    dv.key_off = (const uint64_t*)(cs->din + o_ko);
-    dv.key_len = (const uint32_t*)(cs->din + o_kl);
-    dv.key_bytes = cs->din + o_kb;
+    if (hv.key_bytes_len) memcpy(p + L.o_kb, hv.key_bytes, hv.key_bytes_len);
+}
+
+fdbcs_batch_view stage_view(const fdbcs_batch_view& hv, const StageLayout& L, uint8_t* din) {
+    fdbcs_batch_view dv = hv;
+    dv.snapshot = (const int64_t*)(din + L.o_snap);
+    dv.read_off = (const int32_t*)(din + L.o_ro);
+    dv.write_off = (const int32_t*)(din + L.o_wo);
+    dv.key_off = (const uint64_t*)(din + L.o_ko);
+    dv.key_len = (const uint32_t*)(din + L.o_kl);
+    dv.key_bytes = din + L.o_kb;
+    return dv;
+}
+
+int ensure_device_bytes(uint8_t*& p, size_t& cap, size_t need) {
+    if (need <= cap) return FDBCS_OK;
+    const size_t n = std::max(need, cap * 2);
+    dfree(p);
+    cap = 0;
+    int r;
+    if ((r = dalloc(p, (int64_t)n))) return r;
+    cap = n;
     return FDBCS_OK;
 }
 
-int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+int stage_batch(fdbcs* cs, const fdbcs_batch_view& hv, fdbcs_batch_view& dv) {
+    const StageLayout L = stage_layout(hv);
     int r;
+    if ((r = ensure_pinned(cs->pin, cs->pin_cap, L.total))) return r;
+    if ((r = ensure_device_bytes(cs->din, cs->din_cap, L.total))) return r;
+    // the previous batch's H2D must be done before overwriting the pinned buffer
+    HIPOK(hipStreamSynchronize(cs->stream));
+    stage_fill(hv, L, cs->pin);
+    HIPOK(hipMemcpyAsync(cs->din, cs->pin, L.total, hipMemcpyHostToDevice, cs->stream));
+    dv = stage_view(hv, L, cs->din);
+    return FDBCS_OK;
+}
+
+// preconditions checked on the host so that no device state changes on a bad batch
+int check_host_view(const fdbcs_batch_view& hv) {
     if (hv.txn_count < 0 || hv.read_count < 0 || hv.write_count < 0) return FDBCS_E_ARG;
-    // preconditions checked on the host so that no device state changes on a bad batch
     const int64_t nr = (int64_t)hv.read_count + hv.write_count;
     for (int64_t i = 0; i < 2 * nr; i++)
         if (hv.key_len[i] > FDBCS_MAX_KEY) return FDBCS_E_KEY;
@@ -654,6 +698,13 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
         if (keycmp(hv.key_bytes + hv.key_off[2 * i], hv.key_len[2 * i], hv.key_bytes + hv.key_off[2 * i + 1],
                    hv.key_len[2 * i + 1]) >= 0)
             return FDBCS_E_RANGE;
+    return FDBCS_OK;
+}
+
+int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    int r;
+    if (cs->sub_head != cs->sub_tail) return FDBCS_E_ARG;  // (pipelined batches still in flight)
+    if ((r = check_host_view(hv))) return r;
     fdbcs_batch_view dv;
     if ((r = stage_batch(cs, hv, dv))) return r;
     if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
@@ -795,6 +846,15 @@ void fdbcs_destroy(fdbcs* cs) {
     if (cs->sc_mapped) hipHostFree(cs->sc_mapped);
     if (cs->pin) hipHostFree(cs->pin);
     if (cs->vpin) hipHostFree(cs->vpin);
+    for (auto& S : cs->slot) {
+        if (S.pin) hipHostFree(S.pin);
+        if (S.vpin) hipHostFree(S.vpin);
+        dfree(S.din);
+        dfree(S.dverd);
+        if (S.copied) hipEventDestroy(S.copied);
+        if (S.done) hipEventDestroy(S.done);
+    }
+    if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
     for (int i = 0; i < 8; i++)
         if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
     if (cs->stream) hipStreamDestroy(cs->stream);
@@ -872,6 +932,60 @@ int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
     if (!cs || !hb) return FDBCS_E_ARG;
     if (hb->txn_count && !verdict) return FDBCS_E_ARG;
     return detect_host_view(cs, *hb, now, new_oldest, verdict);
+}
+
+int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest) {
+    if (!cs || !hb || cs->in_batch) return FDBCS_E_ARG;
+    if (cs->sub_head - cs->sub_tail >= 2) return FDBCS_E_ARG;  // two in flight: fdbcs_batch_wait first
+    const fdbcs_batch_view& hv = *hb;
+    int r;
+    if ((r = check_host_view(hv))) return r;
+    fdbcs::Slot& S = cs->slot[cs->sub_head & 1];
+    if (!cs->copy_stream && hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess)
+        return FDBCS_E_HIP;
+    if (!S.copied && (hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) != hipSuccess ||
+                      hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess))
+        return FDBCS_E_HIP;
+    const StageLayout L = stage_layout(hv);
+    const int64_t T = hv.txn_count;
+    // (this slot's previous batch was waited for: its buffers are free)
+    if ((r = ensure_pinned(S.pin, S.pin_cap, L.total)) || (r = ensure_device_bytes(S.din, S.din_cap, L.total)) ||
+        (r = ensure_pinned(S.vpin, S.vpin_cap, (size_t)T + 1)))
+        return r;
+    if (T + 1 > S.dverd_cap) {
+        dfree(S.dverd);
+        S.dverd_cap = 0;
+        if ((r = dalloc(S.dverd, T + 1))) return r;
+        S.dverd_cap = T + 1;
+    }
+    stage_fill(hv, L, S.pin);  // host packing overlaps the batch in flight
+    HIPOK(hipMemcpyAsync(S.din, S.pin, L.total, hipMemcpyHostToDevice, cs->copy_stream));
+    HIPOK(hipEventRecord(S.copied, cs->copy_stream));
+    HIPOK(hipStreamWaitEvent(cs->stream, S.copied, 0));
+    const fdbcs_batch_view dv = stage_view(hv, L, S.din);
+    if ((r = run_batch(cs, dv, now, new_oldest, S.dverd, false))) return r;
+    if (T) HIPOK(hipMemcpyAsync(S.vpin, S.dverd, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipEventRecord(S.done, cs->stream));
+    S.T = T;
+    cs->sub_head++;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict) {
+    if (!cs || cs->sub_tail == cs->sub_head) return FDBCS_E_ARG;
+    fdbcs::Slot& S = cs->slot[cs->sub_tail & 1];
+    int r;
+    cs->sub_tail++;
+    if (cs->sub_tail == cs->sub_head) {  // nothing else in flight: adopt the device scalars
+        if ((r = sync_batch(cs))) return r;
+        if (cs->sc_host->last_err) return cs->sc_host->last_err;
+    } else {
+        HIPOK(hipEventSynchronize(S.done));
+        const int32_t e = ((const volatile Scalars*)cs->sc_mapped)->last_err;
+        if (e) return e;
+    }
+    if (S.T && verdict) memcpy(verdict, S.vpin, (size_t)S.T);
+    return FDBCS_OK;
 }
 
 int fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest,

@@ -152,6 +152,16 @@ int  fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* dev_batch,
                          int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
                          int sync);
 
+/* Pipelined host batches (batch ingest with overlapped
+ * H2D).  The Resolver receives batches in version order while the previous one
+ * is being resolved (Resolver.actor.cpp:104-122); submitting batch k+1 packs
+ * it into a pinned staging slot and starts its host-to-device copy on a copy
+ * stream while batch k's kernels run.  At most two batches are in flight;
+ * fdbcs_batch_wait returns the oldest one's T verdict bytes (as
+ * fdbcs_batch_detect_packed).  Results equal the synchronous calls'. */
+int  fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* host_batch, int64_t now, int64_t new_oldest);
+int  fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict);
+
 /* ---- Key-range resolvers: the proxy side of multi-resolver scale-out ------------ */
 
 /* ResolutionRequestBuilder::addTransaction (MasterProxyServer.actor.cpp:267-307)

@@ -298,3 +298,26 @@ def test_large_batches_multiblock_combine(cs, T, force):
     finally:
         if force:
             os.environ.pop(force, None)
+
+
+def test_pipelined_submit_wait_matches_synchronous(cs):
+    """fdbcs_batch_submit_packed / fdbcs_batch_wait (two batches in flight,
+    overlapped host packing and H2D) give the synchronous path's verdicts and
+    history; a synchronous call while batches are in flight is refused."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    wl = Workload(2, txns=2000)
+    batches = [wl.batch(i) for i in range(12)]
+    got = []
+    for i, (b, now, nold) in enumerate(batches):
+        cs.submit_packed(b, now, nold)
+        if i == 1:
+            with pytest.raises(FdbcsError):
+                cs.detect_packed(b, now, nold)
+        if i >= 1:
+            got.append(cs.wait())
+    got.append(cs.wait())
+    for (b, now, nold), vg in zip(batches, got):
+        assert np.array_equal(vg, c.detect_packed(b, now, nold))
+    same_history(cs, c)
+    assert cs.removal_key() == c.removal_key()
