@@ -127,6 +127,7 @@ struct fdbcs {
     bool have_times = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
     bool sparse_edges = false;    // exact sharded protocol B: this shard exports its overlap edges
+    bool edges_known = false;     // sc_host->edges_total is this batch's (set by fdbcs_shard_check)
     int64_t last_T = 0, last_R = 0, last_W = 0;  // shape of the last batch (stats)
     int64_t sorts = 0;                           // sorts launched (sort-counter parity)
     // pipelined host batches (fdbcs_batch_submit_packed / fdbcs_batch_wait): two
@@ -548,6 +549,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     int r;
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
+    cs->edges_known = false;
     if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
     cs->last_T = T;
@@ -1278,7 +1280,11 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     }
     if ((r = edges_read_check(cs, v, carry_in))) return r;
     if (dev_hist) launch_flags_out(b, v.txn_count, dev_hist, s);
+    // the edge count rides the sync below (fdbcs_shard_edge_count reads it without another round trip)
+    HIPOK(hipMemcpyAsync(&cs->sc_host->edges_total, &cs->sc->edges_total, sizeof(int32_t), hipMemcpyDeviceToHost,
+                         s));
     HIPOK(hipStreamSynchronize(s));
+    cs->edges_known = true;
     return FDBCS_OK;
 }
 
@@ -1286,6 +1292,7 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
                       const uint8_t* removal_key, int32_t removal_key_len, const uint8_t* dev_hist,
                       uint8_t* dev_verdict, int64_t* info) {
     if (!cs || !db || !info || removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
+    cs->edges_known = false;
     const fdbcs_batch_view& v = *db;
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
@@ -1331,6 +1338,7 @@ int fdbcs_shard_set_protocol(fdbcs* cs, int sparse_edges) {
 
 int64_t fdbcs_shard_edge_count(fdbcs* cs) {
     if (!cs) return FDBCS_E_ARG;
+    if (cs->edges_known) return cs->sc_host->edges_total;  // (copied by fdbcs_shard_check)
     int32_t n = 0;
     HIPOK(hipMemcpyAsync(&n, &cs->sc->edges_total, sizeof(n), hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -1349,6 +1357,7 @@ int fdbcs_shard_get_edges(fdbcs* cs, int32_t* dev_et, int32_t* dev_eu, int64_t n
 
 int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_eu, int64_t n) {
     if (!cs || n < 0 || n > INT32_MAX || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
+    cs->edges_known = false;
     BatchBufs& b = cs->b;
     if (b.dedup) return FDBCS_E_ARG;  // (protocol B only: fdbcs_shard_set_protocol)
     int r;

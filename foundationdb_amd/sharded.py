@@ -444,7 +444,9 @@ class DistShardedConflictSet:
             fl = x1
         if self.sparse:  # protocol B: the union of the overlap edges (counts came in the slots)
             counts = [int(w[3]) for w in slots]
-            if max(counts) <= self.ei:
+            if sum(counts) == 0:
+                pass  # (no overlaps anywhere: this shard's own empty list is the global one)
+            elif max(counts) <= self.ei:
                 ed = x1[eo:].view(torch.int32).view(self.world, 2, self.ei).to(self.device)
                 et = torch.cat([ed[g, 0, :counts[g]] for g in range(self.world)] + [ed.new_zeros(1)])
                 eu = torch.cat([ed[g, 1, :counts[g]] for g in range(self.world)] + [ed.new_zeros(1)])
