@@ -534,7 +534,7 @@ class DistShardedConflictSet:
         t = torch.tensor(vals, dtype=torch.int64, device=self.coll_dev)
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
-        return [o.cpu().tolist() for o in out]
+        return torch.stack(out).cpu().tolist()  # (one device-to-host copy, not one per rank)
 
     @property
     def oldest_version(self):
