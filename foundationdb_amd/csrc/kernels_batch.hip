@@ -1298,6 +1298,100 @@ __global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int 
     }
 }
 
+// Large batches: the overlap edges by one merge-join of the sorted read
+// begins with the sorted write endpoints instead of two binary searches per
+// range.  In the merged order (key; a read before a write endpoint of equal
+// key) a read at merged position m with sorted index k has m - k write
+// endpoints below its begin -- lb_key(sw, r.b) -- and a write begin at m with
+// sorted index j has m - j reads at or below it -- ub_key(sr, w.b).  From
+// there each range scans forward to its end exactly as edges_lane loops
+// between its two search results.  Workgroups take MS_CHUNK merged positions
+// (merge-path cuts, the two pieces staged in LDS), lanes MS_ITEMS each.
+__device__ inline bool rd_before_wr(const SRec& r, const SRec& w, const uint8_t* const* tails) {
+    return rec_vs_key(r, Key{w.hi, w.lo, w.meta, tails[w.idx]}, tails) <= 0;  // key(r) <= key(w)
+}
+
+__global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
+    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
+    __shared__ int s_cut[2];
+    const int R = A.R, nw = 2 * A.W;
+    const int64_t wbase = 2 * (int64_t)R;
+    const uint8_t* const* tails = A.keys.tail;
+    const SRec* sr = A.sr;
+    const SRec* sw = A.sw;
+    const int d0 = blockIdx.x * MS_CHUNK, d1 = min(d0 + MS_CHUNK, R + nw);
+    auto before = [&](const SRec& r, const SRec& w) { return rd_before_wr(r, w, tails); };
+    if (threadIdx.x < 2) {  // reads among the first d merged positions
+        const int d = threadIdx.x ? d1 : d0;
+        int lo = max(0, d - nw), hi = min(d, R);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (before(sr[mid], sw[d - 1 - mid])) lo = mid + 1;
+            else hi = mid;
+        }
+        s_cut[threadIdx.x] = lo;
+    }
+    __syncthreads();
+    const int a0 = s_cut[0], a1 = s_cut[1], b0 = d0 - a0, b1 = d1 - a1;
+    const int na = a1 - a0, nb = b1 - b0;
+    const LdsRecs L{s_hi, s_lo, s_mi};
+    for (int k = threadIdx.x; k < na + nb; k += MS_THREADS) L.put(k, k < na ? sr[a0 + k] : sw[b0 + k - na]);
+    __syncthreads();
+    const int dl = threadIdx.x * MS_ITEMS;
+    if (dl >= na + nb) return;
+    int ia, ib;
+    {
+        int lo = max(0, dl - nb), hi = min(dl, na);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (before(L.get(mid), L.get(na + dl - 1 - mid))) lo = mid + 1;
+            else hi = mid;
+        }
+        ia = lo;
+        ib = dl - lo;
+    }
+    const int cnt = min(MS_ITEMS, na + nb - dl);
+    for (int q = 0; q < cnt; q++) {
+        const int m = d0 + dl + q;
+        const bool take_r = ia < na && (ib >= nb || before(L.get(ia), L.get(na + ib)));
+        // (the common case -- nothing overlaps -- costs the next record and the
+        // end key's first word: a strictly greater first word decides)
+        if (take_r) {
+            const int k = a0 + ia++;
+            const uint32_t slot = L.get(k - a0).idx;
+            int j = m - k;
+            if (j >= nw || sw[j].hi > A.keys.hi[slot + 1]) continue;
+            const Key e = A.keys.get((int64_t)slot + 1);
+            if (rec_vs_key(sw[j], e, tails) >= 0) continue;
+            const int t = A.read_txn[slot >> 1];
+            if (A.too_old[t]) continue;
+            for (; j < nw; j++) {  // write endpoints with key in [r.b, r.e)
+                const SRec x = sw[j];
+                if (rec_vs_key(x, e, tails) >= 0) break;
+                if (x.idx & 1) continue;  // a write end
+                const int u = A.write_txn[(x.idx - wbase) >> 1];
+                if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+            }
+        } else {
+            const int j = b0 + ib++;
+            const uint32_t slot = L.get(na + j - b0).idx;
+            if (slot & 1) continue;  // only write begins search the reads
+            int k = m - j;
+            if (k >= R || sr[k].hi > A.keys.hi[slot + 1]) continue;
+            const Key e = A.keys.get((int64_t)slot + 1);
+            if (rec_vs_key(sr[k], e, tails) >= 0) continue;
+            const int u = A.write_txn[(slot - wbase) >> 1];
+            if (A.too_old[u]) continue;
+            for (; k < R; k++) {  // reads beginning in (w.b, w.e)
+                const SRec x = sr[k];
+                if (rec_vs_key(x, e, tails) >= 0) break;
+                const int t = A.read_txn[x.idx >> 1];
+                if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+            }
+        }
+    }
+}
+
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
@@ -1307,10 +1401,15 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
-    const int e_blocks = R > 0 && W > 0 ? cdiv(R + W, 256) : 0;
+    static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
+    const bool join = b.large && !search_edges;
+    const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + W, 256) : 0;
     if (rc_blocks + ws_blocks + e_blocks > 0)
         hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks,
                            WA, ws_blocks, EA);
+    if (join && R > 0 && W > 0)
+        hipLaunchKernelGGL(k_edges_merge, dim3(cdiv((int64_t)R + 2 * (int64_t)W, MS_CHUNK)), dim3(MS_THREADS), 0, s,
+                           EA);
 }
 
 // ------------------------------------------------------ decide + combine ----
