@@ -415,16 +415,18 @@ def main():
     if mode == "single" and args.pcie_batches > 0:
         n = args.pcie_batches
         first = args.warmup + n_stage
-        host = [src.wl.batch(first + j) for j in range(2 * n + 1)]
+        host = [src.wl.batch(first + j) for j in range(2 * n + 2)]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for b, now, nold in host[:n]:  # synchronous: pack, H2D, pipeline, verdict D2H, then the next
             cs.detect_packed(b, now, nold)
         t_serial = time.perf_counter() - t0
-        cs.submit_packed(*host[n])  # (untimed: sizes the pipelined path's pinned and device staging slots)
+        cs.submit_packed(*host[n])  # (untimed: sizes both of the pipelined path's staging slots)
+        cs.submit_packed(*host[n + 1])
+        cs.wait()
         cs.wait()
         t0 = time.perf_counter()
-        for j, (b, now, nold) in enumerate(host[n + 1:]):  # two in flight: batch k+1's packing and H2D overlap k
+        for j, (b, now, nold) in enumerate(host[n + 2:]):  # two in flight: batch k+1's packing and H2D overlap k
             cs.submit_packed(b, now, nold)
             if j >= 1:
                 cs.wait()
