@@ -100,7 +100,19 @@ struct ReadCheckArgs {
     const Scalars* sc;
     int64_t v0;            // version before the first boundary (sharded: the shard's carry-in)
     ShardBounds shard;     // reads are clipped to it (sharded mode)
+    const int32_t* qx;     // large batches: directory entry of every read's begin (k_dir_join), else null
 };
+
+// The directory entry of e given that of b (<= e): a 16-entry window after
+// it, one 128-byte line of first keys; past the window, the full search.
+__device__ inline int dir_entry_after(const Group<RC_G>& g, const Dir& dir, int D, int xb, const Key& e) {
+    const int j = xb + 1 + g.lane;
+    const int c = __popc(g.ballot(j < D && dir_le(dir, j, e)));
+    if (c < RC_G) return xb + c;
+    DirHit h1, h2;
+    grp_dir_find2(g, dir, D, e, e, h1, h2);
+    return h1.x;
+}
 
 // read r, checked by the RC_G lanes of its group (g.lane)
 __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G>& g, int r) {
@@ -119,7 +131,14 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
         if (kcmp(b, e) >= 0) return;
     }
     DirHit hb, he;
-    grp_dir_find2(g, dir, D, b, e, hb, he);
+    if (A.qx) {  // the begin's entry from the merge-join; the end's from the entries after it
+        const int xb = A.qx[r];
+        const int xe = dir_entry_after(g, dir, D, xb, e);
+        hb = DirHit{xb, dir.page[xb], dir.cnt[xb]};
+        he = DirHit{xe, dir.page[xe], dir.cnt[xe]};
+    } else {
+        grp_dir_find2(g, dir, D, b, e, hb, he);
+    }
     const int pb = hb.x, pe = he.x, cb = hb.cnt;
     int ib, ie;
     bool eqb, eqe;
@@ -1204,6 +1223,7 @@ struct WriteSearchArgs {
     const Scalars* sc;
     int64_t v0;
     WriteHits wh;
+    const int32_t* qx;  // large batches: directory entry of every write endpoint (k_dir_join; index R + slot - 2R)
 };
 
 __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<RC_G>& g, int w) {
@@ -1212,7 +1232,13 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     const Key b = A.keys.get(s), e = A.keys.get(s + 1);
     const int D = A.sc->D;
     DirHit hb, he;
-    grp_dir_find2(g, A.dir, D, b, e, hb, he);
+    if (A.qx) {
+        const int xb = A.qx[A.R + 2 * w], xe = A.qx[A.R + 2 * w + 1];
+        hb = DirHit{xb, A.dir.page[xb], A.dir.cnt[xb]};
+        he = DirHit{xe, A.dir.page[xe], A.dir.cnt[xe]};
+    } else {
+        grp_dir_find2(g, A.dir, D, b, e, hb, he);
+    }
     int ib, ie;
     bool eqb, eqe;
     grp_page_find2(g, A.pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
@@ -1365,6 +1391,97 @@ __global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int 
     }
 }
 
+// Large batches: the directory entry of every sorted read begin and write
+// endpoint by one merge-join with the directory's first keys instead of a
+// search-index descent per key (dir_search: entry x = the number of entries
+// j >= 1 with first(j) <= k).  In the merged order (first keys before queries
+// of equal key) a query at merged position m with index i has x = m - i.
+// Job 0: sorted read begins -> qx[read index]; job 1: sorted write endpoints
+// -> qx[R + endpoint index].
+struct DirJoinArgs {
+    const SRec* q[2];
+    int32_t nq[2];
+    int32_t blocks0;
+    Dir dir;
+    const Scalars* sc;
+    KeyArrays keys;
+    int R;
+    int32_t* qx;
+};
+
+__global__ __launch_bounds__(MS_THREADS) void k_dir_join(DirJoinArgs A) {
+    __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
+    __shared__ int s_cut[2];
+    const int job = (int)blockIdx.x < A.blocks0 ? 0 : 1;
+    const int chunk = job ? blockIdx.x - A.blocks0 : blockIdx.x;
+    const Dir& d = A.dir;
+    const int nf = A.sc->D - 1;  // first keys of entries 1 .. D-1
+    const int nq = A.nq[job];
+    const SRec* Q = A.q[job];
+    const int d0 = chunk * MS_CHUNK;
+    if (d0 >= nf + nq) return;
+    const int d1 = min(d0 + MS_CHUNK, nf + nq);
+    const uint8_t* const* qt = A.keys.tail;
+    auto fkey = [&](int j) { return dir_first(d, j + 1); };
+    auto f_le_q = [&](const Key& f, const SRec& x) {
+        return kcmp(f, Key{x.hi, x.lo, x.meta, qt[x.idx]}) <= 0;
+    };
+    if (threadIdx.x < 2) {  // first keys among the first dd merged positions
+        const int dd = threadIdx.x ? d1 : d0;
+        int lo = max(0, dd - nq), hi = min(dd, nf);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (f_le_q(fkey(mid), Q[dd - 1 - mid])) lo = mid + 1;
+            else hi = mid;
+        }
+        s_cut[threadIdx.x] = lo;
+    }
+    __syncthreads();
+    const int a0 = s_cut[0], a1 = s_cut[1], b0 = d0 - a0, b1 = d1 - a1;
+    const int na = a1 - a0, nb = b1 - b0;
+    const LdsRecs L{s_hi, s_lo, s_mi};  // [0, na): first keys (idx = entry - 1), [na, na + nb): queries
+    for (int k = threadIdx.x; k < na + nb; k += MS_THREADS) {
+        if (k < na) {
+            const int j = a0 + k;
+            L.put(k, SRec{d.fhi[j + 1], d.flo[j + 1], d.fmeta[j + 1], (uint32_t)j, 0});
+        } else {
+            L.put(k, Q[b0 + k - na]);
+        }
+    }
+    __syncthreads();
+    auto lds_f_le_q = [&](int fa, int qb) {
+        const SRec f = L.get(fa);
+        return f_le_q(Key{f.hi, f.lo, f.meta, d.ftail[f.idx + 1]}, L.get(qb));
+    };
+    const int dl = threadIdx.x * MS_ITEMS;
+    if (dl >= na + nb) return;
+    int ia, ib;
+    {
+        int lo = max(0, dl - nb), hi = min(dl, na);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (lds_f_le_q(mid, na + dl - 1 - mid)) lo = mid + 1;
+            else hi = mid;
+        }
+        ia = lo;
+        ib = dl - lo;
+    }
+    const int cnt = min(MS_ITEMS, na + nb - dl);
+    for (int q = 0; q < cnt; q++) {
+        const int m = d0 + dl + q;
+        if (ia < na && (ib >= nb || lds_f_le_q(ia, na + ib))) {
+            ia++;
+        } else {
+            const int i = b0 + ib;
+            const uint32_t slot = L.get(na + ib).idx;
+            ib++;
+            const int x = m - i;
+            if (job == 0) A.qx[slot >> 1] = x;
+            else A.qx[A.R + (int)(slot - 2 * (uint32_t)A.R)] = x;
+        }
+    }
+}
+
 // Large batches: the overlap edges by one merge-join of the sorted read
 // begins with the sorted write endpoints instead of two binary searches per
 // range.  In the merged order (key; a read before a write endpoint of equal
@@ -1462,10 +1579,21 @@ __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s) {
     const int R = v.read_count, W = v.write_count;
-    ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard};
+    // large unsharded batches: directory entries by merge-join (ss_bkt is free once the sort is done)
+    static const bool dir_search = getenv("FDBCS_LARGE_DIR_SEARCH") != nullptr;  // (A/B measurements)
+    const bool dj = b.large && !(h.shard.has_lo | h.shard.has_hi) && !dir_search && R + W > 0;
+    if (dj) {
+        DirJoinArgs J{{b.sr, b.sw}, {R, 2 * W}, 0, h.dir[cur], sc, b.keys, R, b.ss_bkt};
+        const int64_t cap_f = h.cap_dir;  // (an upper bound on D: blocks past the merged length exit)
+        J.blocks0 = cdiv(cap_f + R, MS_CHUNK);
+        const int blocks = J.blocks0 + cdiv(cap_f + 2 * (int64_t)W, MS_CHUNK);
+        hipLaunchKernelGGL(k_dir_join, dim3(blocks), dim3(MS_THREADS), 0, s, J);
+    }
+    const int32_t* qx = dj ? b.ss_bkt : nullptr;
+    ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
     EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
                  b.dedup ? b.pair_bits : nullptr, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
-    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh};
+    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
