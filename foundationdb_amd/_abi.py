@@ -94,6 +94,19 @@ FDBCS_FUNCS = [
     ("fdbcs_shard_edge_count", C.c_int64, [C.c_void_p]),
     ("fdbcs_shard_get_edges", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     ("fdbcs_shard_set_edges", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+    ("fdbcs_last_device_batch", C.c_int, [C.c_void_p, C.POINTER(BatchView)]),
+    ("fdbcs_sample_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int64, C.c_uint64]),
+    ("fdbcs_sample_destroy", None, [C.c_void_p]),
+    ("fdbcs_sample_add_batch", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_double,
+                                         C.POINTER(C.c_int64)]),
+    ("fdbcs_sample_add_metric", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int64]),
+    ("fdbcs_sample_poll", C.c_int, [C.c_void_p, C.c_double]),
+    ("fdbcs_sample_estimate", C.c_int64, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]),
+    ("fdbcs_sample_split", C.c_int32, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_int64,
+                                       C.c_int, C.c_void_p, C.c_uint32]),
+    ("fdbcs_sample_size", C.c_int64, [C.c_void_p]),
+    ("fdbcs_sample_queue_size", C.c_int64, [C.c_void_p]),
+    ("fdbcs_sample_entry", C.c_int32, [C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.POINTER(C.c_int64)]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
 ]

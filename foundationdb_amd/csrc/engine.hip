@@ -125,6 +125,9 @@ struct fdbcs {
     uint8_t* rk_stage = nullptr;     // pinned: removalKey in (hi, lo, meta, tail) form, both directions
     double stage_us[7] = {0};
     bool have_times = false;
+    // device view of the last batch staged by a host path (fdbcs_last_device_batch)
+    fdbcs_batch_view last_dv{};
+    bool have_last_dv = false;
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
     bool sparse_edges = false;    // exact sharded protocol B: this shard exports its overlap edges
     bool edges_known = false;     // sc_host->edges_total is this batch's (set by fdbcs_shard_check)
@@ -708,8 +711,11 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_ARG;  // (pipelined batches still in flight)
     if ((r = check_host_view(hv))) return r;
     fdbcs_batch_view dv;
+    cs->have_last_dv = false;
     if ((r = stage_batch(cs, hv, dv))) return r;
     if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
+    cs->last_dv = dv;
+    cs->have_last_dv = true;
     const int64_t T = hv.txn_count;
     if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
     if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
@@ -937,6 +943,7 @@ int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
 }
 
 int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest) {
+    if (cs) cs->have_last_dv = false;
     if (!cs || !hb || cs->in_batch) return FDBCS_E_ARG;
     if (cs->sub_head - cs->sub_tail >= 2) return FDBCS_E_ARG;  // two in flight: fdbcs_batch_wait first
     const fdbcs_batch_view& hv = *hb;
@@ -1207,6 +1214,13 @@ int fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap) {
 }
 
 void* fdbcs_stream(fdbcs* cs) { return cs ? (void*)cs->stream : nullptr; }
+
+int fdbcs_last_device_batch(fdbcs* cs, fdbcs_batch_view* out) {
+    if (!cs || !out) return FDBCS_E_ARG;
+    if (!cs->have_last_dv) return FDBCS_E_STATE;
+    *out = cs->last_dv;
+    return FDBCS_OK;
+}
 
 const char* fdbcs_strerror(int status) {
     switch (status) {

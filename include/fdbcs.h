@@ -324,6 +324,60 @@ int  fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap);
  * want to time or order around it. */
 void* fdbcs_stream(fdbcs* cs);
 
+/* Device view of the batch most recently resolved through a host path
+ * (fdbcs_batch_detect / fdbcs_batch_detect_packed): its arrays stay valid in
+ * device memory until the next batch is staged.  FDBCS_E_STATE when there is
+ * none (nothing resolved yet, or a pipelined submit since). */
+int  fdbcs_last_device_batch(fdbcs* cs, fdbcs_batch_view* out);
+
+/* ---- Resolver load metrics ------------------------------------ */
+
+/* The Resolver's iopsSample: TransientStorageMetricSample
+ * (fdbserver/StorageMetrics.actor.h:98-182) constructed with
+ * KEY_BYTES_PER_SAMPLE (fdbserver/Knobs.cpp:269, 2e4) units per sample,
+ * Resolver.actor.cpp:47,65.  `seed` fixes the sample's draws (the reference
+ * uses the unseeded g_random; see foundationdb_amd/csrc/load_metrics.hip). */
+typedef struct fdbcs_sample fdbcs_sample;
+int  fdbcs_sample_create(fdbcs_sample** out, int64_t units_per_sample, uint64_t seed);
+void fdbcs_sample_destroy(fdbcs_sample* s);
+
+/* Resolver.actor.cpp:146-151 for one whole batch: addAndExpire(begin,
+ * offset_per_key + |begin|, expiration) for every write then every read range
+ * of each transaction in batch order (offset_per_key = SAMPLE_OFFSET_PER_KEY,
+ * Knobs.cpp:278, 100; expiration = now() + SAMPLE_EXPIRATION_TIME).  The roll
+ * and the gather of the sampled keys run on the device, over dev_batch (a
+ * device-resident batch view; NULL = fdbcs_last_device_batch(cs)), on cs's
+ * stream; synchronous.  *out_sampled (optional) = keys sampled. */
+int  fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* dev_batch,
+                            int64_t offset_per_key, double expiration, int64_t* out_sampled);
+
+/* IndexedSet::addMetric on the sample without the roll or the queue
+ * (flow/IndexedSet.h:587-598; StorageMetrics.actor.h's own test inserts this
+ * way, :81-93).  An entry whose metric reaches 0 is erased. */
+int  fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric);
+
+/* TransientStorageMetricSample::poll() (StorageMetrics.actor.h:150-164):
+ * apply every queued expiry with expiration <= now
+ * (Resolver.actor.cpp:286-289, every SAMPLE_POLL_TIME). */
+int  fdbcs_sample_poll(fdbcs_sample* s, double now);
+
+/* getEstimate(KeyRangeRef(b, e)) (StorageMetrics.actor.h:35-37): the sum of
+ * the sampled metrics of keys in [b, e).  ResolutionMetricsRequest answers
+ * getEstimate(allKeys) (Resolver.actor.cpp:276-277). */
+int64_t fdbcs_sample_estimate(const fdbcs_sample* s, const uint8_t* b, uint32_t bl, const uint8_t* e, uint32_t el);
+
+/* splitEstimate(KeyRangeRef(b, e), offset, front) (StorageMetrics.actor.h:38-73;
+ * ResolutionSplitRequest, Resolver.actor.cpp:279-283).  Writes the split key
+ * into out (cap bytes) and returns its length, or a negative status. */
+int32_t fdbcs_sample_split(const fdbcs_sample* s, const uint8_t* b, uint32_t bl, const uint8_t* e, uint32_t el,
+                           int64_t offset, int front, uint8_t* out, uint32_t cap);
+
+/* Sampled keys held, queued expiries, and entry i (ascending key order):
+ * key bytes into out (length returned), its metric into *metric. */
+int64_t fdbcs_sample_size(const fdbcs_sample* s);
+int64_t fdbcs_sample_queue_size(const fdbcs_sample* s);
+int32_t fdbcs_sample_entry(const fdbcs_sample* s, int64_t i, uint8_t* out, uint32_t cap, int64_t* metric);
+
 /* Human-readable message for a status code. */
 const char* fdbcs_strerror(int status);
 

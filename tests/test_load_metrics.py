@@ -1,0 +1,163 @@
+"""Resolver load metrics: iopsSample on the device.
+
+CPU tests pin the sample structure: the reference's own known-answer test
+(StorageMetrics.actor.h:81-93) and random differentials of getEstimate /
+splitEstimate between libfdbcs.so's host sample and the oracle restatement
+(oracle/load_sample.py).  GPU tests check the device roll of whole batches
+(the Resolver.actor.cpp:146-151 loop) against the oracle, bit for bit: the
+same sampled keys and amounts, the same queue, the same estimates and splits
+after polls.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from foundationdb_amd import _abi
+from foundationdb_amd.load_metrics import ALL_KEYS, KEY_BYTES_PER_SAMPLE, IopsSample
+from gen import mixed_stream, tiny_stream
+from oracle.load_sample import SpecSample, key_between, roll_hash
+
+
+def test_reference_known_answer_simple():
+    """TEST_CASE("/fdbserver/StorageMetricSample/simple"), StorageMetrics.actor.h:81-93."""
+    entries = [(b"Apple", 1000), (b"Banana", 2000), (b"Cat", 1000), (b"Cathode", 1000), (b"Dog", 1000)]
+    for s in (IopsSample(1000), SpecSample(1000)):
+        for k, m in entries:
+            s.add_metric(k, m)
+        assert s.get_estimate(b"A", b"D") == 5000
+        assert s.get_estimate(b"A", b"E") == 6000
+        assert s.get_estimate(b"B", b"C") == 2000
+
+
+def test_key_between_follows_reference():
+    """keyBetween (fdbclient/FDBTypes.h:304-325) cases."""
+    assert key_between(b"abc", b"abd") == b"abd"
+    assert key_between(b"ab", b"abcd") == b"abc"
+    assert key_between(b"a", b"b") == b"b"
+    assert key_between(b"", b"xyz") == b"x"
+    assert key_between(b"abc", b"abc") == b"abc"
+    assert key_between(b"x" * 6000, b"x" * 6001) == b"x" * 6001  # past SPLIT_KEY_SIZE_LIMIT
+
+
+def test_roll_hash_vectors():
+    """The draw function restated in numpy equals its definition on Python ints."""
+    def mix(seed, seq, pos):
+        M = 2**64 - 1
+        z = (seed + seq * 0xD1B54A32D192ED03 + pos * 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    pos = np.arange(1000, dtype=np.uint64)
+    h = roll_hash(12345, 7, pos)
+    assert [int(x) for x in h[:50]] == [mix(12345, 7, int(p)) for p in pos[:50]]
+    # the sampling probability is metric / units
+    frac = float(np.mean((roll_hash(1, 2, np.arange(200000, dtype=np.uint64)) % np.uint64(20000)) < 116))
+    assert abs(frac - 116 / 20000) < 0.0015
+
+
+def _rand_entries(rng, n, alpha=b"ab\x00c", maxlen=4):
+    out = []
+    for _ in range(n):
+        k = bytes(rng.choice(alpha) for _ in range(rng.randint(0, maxlen)))
+        out.append((k, rng.choice([1, 5, 100, 1000, -1, 20000])))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_sample_estimates_and_splits_match_oracle(seed):
+    rng = random.Random(seed)
+    g, o = IopsSample(1000), SpecSample(1000)
+    for k, m in _rand_entries(rng, 300):
+        if m < 0 and o.metric.get(k, 0) + m <= 0:
+            continue  # keep metrics positive, as the Resolver's are
+        g.add_metric(k, m)
+        o.add_metric(k, m)
+    assert g.items() == o.items()
+    keys = [b"", b"a", b"ab", b"b", b"c", b"\x00", b"a\x00", b"ba", b"cc", b"\xff\xff"]
+    for _ in range(200):
+        b, e = sorted(rng.sample(keys, 2))
+        assert g.get_estimate(b, e) == o.get_estimate(b, e)
+        off = rng.randint(-500, o.get_estimate(b"", b"\xff\xff") + 500)
+        for front in (True, False):
+            assert g.split_estimate(b, e, off, front) == o.split_estimate(b, e, off, front), (b, e, off, front)
+
+
+def test_empty_sample():
+    g = IopsSample()
+    assert g.get_estimate(*ALL_KEYS) == 0
+    assert g.split_estimate(b"a", b"z", 100, True) == b"z"
+    assert g.split_estimate(b"a", b"z", 100, False) == b"z"  # index() == end -> range.end (:41-42)
+    assert g.size() == 0 and g.queue_size() == 0
+    g.poll(1e9)
+
+
+def test_add_batch_without_batch_is_state_error():
+    """No batch resolved yet: fdbcs_sample_add_batch(cs, NULL) has nothing to roll."""
+    with pytest.raises(_abi.FdbcsError):
+        IopsSample().add_batch(_NoBatch(), 1.0)
+
+
+class _NoBatch:
+    handle = None
+
+
+# ---------------------------------------------------------------- GPU
+
+def _run_stream(cs, stream, units, seed, offset=100, poll_every=3):
+    g, o = IopsSample(units, seed=seed), SpecSample(units, seed=seed)
+    t = 0.0
+    for i, (batch, now, nold) in enumerate(stream):
+        cs.detect_packed(batch, now, nold)
+        t += 0.4
+        ng = g.add_batch(cs, t + 1.0, offset_per_key=offset)
+        no = o.add_batch(batch, t + 1.0, offset_per_key=offset)
+        assert ng == no, (i, ng, no)
+        assert g.queue_size() == len(o.queue)
+        if i % poll_every == 0:
+            g.poll(t)
+            o.poll(t)
+        assert g.items() == o.items(), i
+        assert g.get_estimate(*ALL_KEYS) == o.get_estimate(*ALL_KEYS)
+    return g, o
+
+
+@pytest.mark.gpu
+def test_device_roll_tiny_streams(gpu):
+    from foundationdb_amd import ConflictSet
+    cs = ConflictSet(device=0)
+    for seed in range(6):
+        # units 110: keys of length >= 10 are added whole, shorter ones rolled
+        g, o = _run_stream(cs, tiny_stream(seed, n_batches=12, maxlen=11), units=110, seed=seed)
+        rng = random.Random(seed)
+        keys = sorted({k for k, _ in o.items()} | {b"", b"a", b"b", b"c", b"\xff"})
+        for _ in range(100):
+            b, e = sorted(rng.sample(keys, 2))
+            off = rng.randint(0, max(1, o.get_estimate(b, e)))
+            for front in (True, False):
+                assert g.split_estimate(b, e, off, front) == o.split_estimate(b, e, off, front)
+    cs.close()
+
+
+@pytest.mark.gpu
+def test_device_roll_mixed_and_config2(gpu):
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd.workload import Workload
+    cs = ConflictSet(device=0)
+    _run_stream(cs, mixed_stream(3, n_batches=8, max_txns=600), units=2000, seed=99)
+    wl = Workload(2, txns=5000)
+    stream = (wl.batch(i) for i in range(6))
+    g, o = _run_stream(cs, stream, units=KEY_BYTES_PER_SAMPLE, seed=7, poll_every=2)
+    assert g.size() > 0
+    # the master's balancing queries (masterserver.actor.cpp:964-1020)
+    total = g.get_estimate(*ALL_KEYS)
+    for front in (True, False):
+        key, used = g.resolution_split(b"", b"\xff\xff", total // 3, front)
+        assert key == o.split_estimate(b"", b"\xff\xff", total // 3, front)
+        assert used == (o.get_estimate(b"", key) if front else o.get_estimate(key, b"\xff\xff"))
+    # everything expires
+    g.poll(1e9)
+    o.poll(1e9)
+    assert g.size() == 0 and g.get_estimate(*ALL_KEYS) == 0 and o.items() == []
+    cs.close()
