@@ -73,13 +73,17 @@ def parse():
     p.add_argument("--pcie-batches", type=int, default=None,
                    help="host batches timed through the PCIe-inclusive paths after the measurement (default 50; "
                         "config 5: 2)")
+    p.add_argument("--lm-batches", type=int, default=None,
+                   help="batches whose load-metrics roll (iopsSample, Resolver.actor.cpp:146-151) is timed after "
+                        "the measurement (default 50; config 5: 2)")
     p.add_argument("--protocol", choices=["a", "b"], default="b",
                    help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
                         "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
     a = p.parse_args()
     big = a.config == 5  # 1 M-txn batches over a preloaded 10^8-boundary history
     for name, small, large in [("steps", 200, 10), ("warmup", 2500, 2), ("txns", 5000, 1_000_000),
-                               ("stage_batches", 50, 3), ("pcie_batches", 50, 2)]:
+                               ("stage_batches", 50, 3), ("pcie_batches", 50, 2),
+                               ("lm_batches", 50, 2)]:
         if getattr(a, name) is None:
             setattr(a, name, large if big else small)
     return a
@@ -439,6 +443,28 @@ def main():
                         "(fdbcs_batch_detect_packed; pipelined: fdbcs_batch_submit_packed / fdbcs_batch_wait)"}
         del host
 
+    # ---- Resolver load metrics (not `value`): iopsSample roll of whole batches on the device ----
+    lm = None
+    if mode == "single" and args.lm_batches > 0:
+        from foundationdb_amd.load_metrics import KEY_BYTES_PER_SAMPLE, SAMPLE_EXPIRATION_TIME, IopsSample
+        smp = IopsSample(KEY_BYTES_PER_SAMPLE, seed=1)
+        first = args.warmup + n_stage + 2 * args.pcie_batches + 2
+        t_add, sampled, n_rng = 0.0, 0, 0
+        for j in range(args.lm_batches):
+            b, now, nold = src.wl.batch(first + j)
+            cs.detect_packed(b, now, nold)  # (untimed) leaves the batch in HBM for the roll
+            t0 = time.perf_counter()
+            sampled += smp.add_batch(cs, j * 0.01 + SAMPLE_EXPIRATION_TIME)
+            t_add += time.perf_counter() - t0
+            n_rng += b.R + b.W
+            smp.poll(j * 0.01)
+        lm = {"us_per_batch": round(t_add / args.lm_batches * 1e6, 2), "ranges_per_batch": n_rng // args.lm_batches,
+              "sampled_per_batch": round(sampled / args.lm_batches, 1), "sample_size": smp.size(),
+              "units_per_sample": KEY_BYTES_PER_SAMPLE, "batches": args.lm_batches,
+              "path": "fdbcs_sample_add_batch on the batch resident in HBM: device roll + ordered compaction + key "
+                      "gather written to pinned host memory, host sample insert (synchronous wall time)"}
+        smp.close()
+
     # ---- CPU baseline (oracle, 1 core) on the same batches, same start state -----
     cpu = None
     if snap is not None:
@@ -493,6 +519,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "load_metrics": lm,
         }
         if alt:
             out["alt_modes"] = alt

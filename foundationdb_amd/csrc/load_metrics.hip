@@ -35,7 +35,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
-#include <map>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -153,9 +153,12 @@ __global__ __launch_bounds__(RB) void k_roll_scan(uint32_t* blk_cnt, const uint3
     if (threadIdx.x == 0) { totals[0] = carry_c; totals[1] = carry_b; }
 }
 
+// Writes the sampled entries straight into pinned host memory (a few hundred
+// per 5k-txn batch: no device staging, no copy); entries past the host
+// buffers' capacities are dropped and the caller re-emits after growing them.
 __global__ __launch_bounds__(RB) void k_roll_emit(RollArgs a, const uint32_t* blk_cnt, const uint64_t* blk_boff,
-                                                  int64_t* out_pos, int64_t* out_amount, uint32_t* out_len,
-                                                  uint64_t* out_off, uint8_t* out_bytes) {
+                                                  int64_t* out_amount, uint32_t* out_len, uint64_t* out_off,
+                                                  uint8_t* out_bytes, uint64_t cap_n, uint64_t cap_b) {
     const int64_t n = (int64_t)a.R + a.W;
     const int64_t pos = (int64_t)blockIdx.x * RB + threadIdx.x;
     uint32_t c = 0, b = 0, slot = 0, len = 0;
@@ -169,12 +172,24 @@ __global__ __launch_bounds__(RB) void k_roll_emit(RollArgs a, const uint32_t* bl
     if (!c) return;
     const uint64_t i = blk_cnt[blockIdx.x] + ec;
     const uint64_t off = blk_boff[blockIdx.x] + eb;
-    out_pos[i] = pos;
+    if (i >= cap_n || off + len > cap_b) return;
     out_amount[i] = x;
     out_len[i] = len;
     out_off[i] = off;
     const uint8_t* src = a.key_bytes + a.key_off[slot];
     for (uint32_t k = 0; k < len; k++) out_bytes[off + k] = src[k];
+}
+
+template <class T>
+int grow_pinned(T*& p, size_t& cap, size_t n) {
+    if (n <= cap && p) return FDBCS_OK;
+    size_t c = std::max<size_t>(n + n / 2, 1024);
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault) != hipSuccess) return FDBCS_E_NOMEM;
+    cap = c;
+    return FDBCS_OK;
 }
 
 template <class T>
@@ -199,14 +214,16 @@ int kcmp(const std::string& a, const uint8_t* b, uint32_t bl) {
 
 }  // namespace
 
-// The sample: IndexedSet<Key, int64_t> (flow/IndexedSet.h) as a sorted map
-// plus a prefix-sum array rebuilt lazily before a query (queries are rare next
-// to adds: the master polls every MIN_BALANCE_TIME), and the expiry queue.
+// The sample: IndexedSet<Key, int64_t> (flow/IndexedSet.h) as a hash map
+// (O(1) per sampled key on the Resolver's per-batch path) plus a sorted view
+// with prefix sums rebuilt lazily before a query: queries are rare next to
+// adds (the master asks every MIN_BALANCE_TIME), the reverse of the trade the
+// reference's balanced tree makes.  And the expiry queue.
 struct fdbcs_sample {
     int64_t units = 0;
     uint64_t seed = 0;
     uint64_t seq = 0;  // batches rolled so far (draw counter)
-    std::map<std::string, int64_t> sample;
+    std::unordered_map<std::string, int64_t> sample;
     std::deque<std::pair<double, std::pair<std::string, int64_t>>> queue;
     // query view
     mutable bool dirty = true;
@@ -219,32 +236,26 @@ struct fdbcs_sample {
     size_t bytes_cap = 0;
     uint64_t* d_boff = nullptr;
     size_t boff_cap = 0;
-    uint64_t* d_tot = nullptr;
+    // pinned host outputs (written by the kernels)
+    uint64_t* h_tot = nullptr;
     size_t tot_cap = 0;
-    int64_t* d_pos = nullptr;
-    size_t pos_cap = 0;
-    int64_t* d_amt = nullptr;
+    int64_t* h_amt = nullptr;
     size_t amt_cap = 0;
-    uint32_t* d_len = nullptr;
+    uint32_t* h_len = nullptr;
     size_t len_cap = 0;
-    uint64_t* d_off = nullptr;
+    uint64_t* h_off = nullptr;
     size_t off_cap = 0;
-    uint8_t* d_out = nullptr;
+    uint8_t* h_out = nullptr;
     size_t out_cap = 0;
 
     // IndexedSet::addMetric (flow/IndexedSet.h:587-598) followed by the
     // erase-at-zero of StorageMetrics.actor.h:136-137 / :177-178.
     void add_metric(const std::string& k, int64_t m) {
         dirty = true;
-        auto it = sample.find(k);
-        const int64_t v = (it == sample.end() ? 0 : it->second) + m;
-        if (v == 0) {
-            if (it != sample.end()) sample.erase(it);
-        } else if (it == sample.end()) {
-            sample.emplace(k, v);
-        } else {
-            it->second = v;
-        }
+        auto ins = sample.try_emplace(k, 0);
+        const int64_t v = ins.first->second + m;
+        if (v == 0) sample.erase(ins.first);
+        else ins.first->second = v;
     }
     void view() const {
         if (!dirty) return;
@@ -252,10 +263,11 @@ struct fdbcs_sample {
         prefix.assign(1, 0);
         keys.reserve(sample.size());
         prefix.reserve(sample.size() + 1);
-        for (auto& kv : sample) {
-            keys.push_back(&kv.first);
-            prefix.push_back(prefix.back() + kv.second);
-        }
+        for (auto& kv : sample) keys.push_back(&kv.first);
+        std::sort(keys.begin(), keys.end(), [](const std::string* a, const std::string* b) {
+            return kcmp(*a, (const uint8_t*)b->data(), (uint32_t)b->size()) < 0;
+        });
+        for (const std::string* k : keys) prefix.push_back(prefix.back() + sample.find(*k)->second);
         dirty = false;
     }
     // index of the first key >= k (IndexedSet::lower_bound)
@@ -279,8 +291,8 @@ struct fdbcs_sample {
         return prefix[lower_bound(e, el)] - prefix[lower_bound(b, bl)];
     }
     ~fdbcs_sample() {
-        hipFree(d_cnt); hipFree(d_bytes); hipFree(d_boff); hipFree(d_tot); hipFree(d_pos);
-        hipFree(d_amt); hipFree(d_len); hipFree(d_off); hipFree(d_out);
+        hipFree(d_cnt); hipFree(d_bytes); hipFree(d_boff);
+        hipHostFree(h_tot); hipHostFree(h_amt); hipHostFree(h_len); hipHostFree(h_off); hipHostFree(h_out);
     }
 };
 
@@ -373,38 +385,38 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
     if (nblk > INT32_MAX) return FDBCS_E_CAPACITY;
     int r;
     if ((r = grow_dev(s->d_cnt, s->cnt_cap, nblk)) || (r = grow_dev(s->d_bytes, s->bytes_cap, nblk)) ||
-        (r = grow_dev(s->d_boff, s->boff_cap, nblk)) || (r = grow_dev(s->d_tot, s->tot_cap, 2)))
+        (r = grow_dev(s->d_boff, s->boff_cap, nblk)) || (r = grow_pinned(s->h_tot, s->tot_cap, 2)) ||
+        (r = grow_pinned(s->h_amt, s->amt_cap, 1)) || (r = grow_pinned(s->h_len, s->len_cap, 1)) ||
+        (r = grow_pinned(s->h_off, s->off_cap, 1)) || (r = grow_pinned(s->h_out, s->out_cap, 1)))
         return r;
     RollArgs a{dv.read_off, dv.write_off, dv.key_off, dv.key_len, dv.key_bytes, dv.txn_count, dv.read_count,
                dv.write_count, s->seed, seq, offset_per_key, s->units};
     hipLaunchKernelGGL(k_roll_count, dim3((unsigned)nblk), dim3(RB), 0, st, a, s->d_cnt, s->d_bytes);
-    hipLaunchKernelGGL(k_roll_scan, dim3(1), dim3(RB), 0, st, s->d_cnt, s->d_bytes, s->d_boff, (int)nblk, s->d_tot);
-    LM_HIPOK(hipGetLastError());
-    uint64_t tot[2];
-    LM_HIPOK(hipMemcpyAsync(tot, s->d_tot, sizeof tot, hipMemcpyDeviceToHost, st));
-    LM_HIPOK(hipStreamSynchronize(st));
-    const uint64_t m = tot[0], nb = tot[1];
+    hipLaunchKernelGGL(k_roll_scan, dim3(1), dim3(RB), 0, st, s->d_cnt, s->d_bytes, s->d_boff, (int)nblk, s->h_tot);
+    // one round trip in the common case: emit into the current host buffers,
+    // and again after growing them if the totals say they were too small
+    for (int pass = 0; pass < 2; pass++) {
+        const size_t cap_n = std::min(std::min(s->amt_cap, s->len_cap), s->off_cap);
+        hipLaunchKernelGGL(k_roll_emit, dim3((unsigned)nblk), dim3(RB), 0, st, a, s->d_cnt, s->d_boff, s->h_amt,
+                           s->h_len, s->h_off, s->h_out, (uint64_t)cap_n, (uint64_t)s->out_cap);
+        LM_HIPOK(hipGetLastError());
+        LM_HIPOK(hipStreamSynchronize(st));
+        const uint64_t m = s->h_tot[0], nb = s->h_tot[1];
+        if (m <= cap_n && nb <= s->out_cap) break;
+        if (pass == 1) return FDBCS_E_CAPACITY;
+        if ((r = grow_pinned(s->h_amt, s->amt_cap, m)) || (r = grow_pinned(s->h_len, s->len_cap, m)) ||
+            (r = grow_pinned(s->h_off, s->off_cap, m)) || (r = grow_pinned(s->h_out, s->out_cap, nb)))
+            return r;
+    }
+    const uint64_t m = s->h_tot[0];
     if (out_sampled) *out_sampled = (int64_t)m;
-    if (m == 0) return FDBCS_OK;
-    if ((r = grow_dev(s->d_pos, s->pos_cap, m)) || (r = grow_dev(s->d_amt, s->amt_cap, m)) ||
-        (r = grow_dev(s->d_len, s->len_cap, m)) || (r = grow_dev(s->d_off, s->off_cap, m)) ||
-        (r = grow_dev(s->d_out, s->out_cap, nb + 1)))
-        return r;
-    hipLaunchKernelGGL(k_roll_emit, dim3((unsigned)nblk), dim3(RB), 0, st, a, s->d_cnt, s->d_boff, s->d_pos,
-                       s->d_amt, s->d_len, s->d_off, s->d_out);
-    LM_HIPOK(hipGetLastError());
-    std::vector<int64_t> amt(m);
-    std::vector<uint32_t> len(m);
-    std::vector<uint64_t> off(m);
-    std::vector<uint8_t> bytes(nb + 1);
-    LM_HIPOK(hipMemcpyAsync(amt.data(), s->d_amt, m * 8, hipMemcpyDeviceToHost, st));
-    LM_HIPOK(hipMemcpyAsync(len.data(), s->d_len, m * 4, hipMemcpyDeviceToHost, st));
-    LM_HIPOK(hipMemcpyAsync(off.data(), s->d_off, m * 8, hipMemcpyDeviceToHost, st));
-    if (nb) LM_HIPOK(hipMemcpyAsync(bytes.data(), s->d_out, nb, hipMemcpyDeviceToHost, st));
-    LM_HIPOK(hipStreamSynchronize(st));
+    const int64_t* amt = s->h_amt;
+    const uint32_t* len = s->h_len;
+    const uint64_t* off = s->h_off;
+    const uint8_t* bytes = s->h_out;
     // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order
     for (uint64_t i = 0; i < m; i++) {
-        std::string k((const char*)bytes.data() + off[i], len[i]);
+        std::string k((const char*)bytes + off[i], len[i]);
         s->add_metric(k, amt[i]);
         s->queue.emplace_back(expiration, std::make_pair(std::move(k), -amt[i]));
     }

@@ -57,6 +57,12 @@ int device_ordinal() {
 
 }  // namespace
 
+// The engine behind a ConflictSet, for the Resolver's load-metrics binding
+// (fdbcs_sample_add_batch rolls the batch this conflict set last resolved;
+// INTEGRATION.md §4.3).  Not part of ConflictSet.h: Resolver.actor.cpp
+// declares it next to its iopsSample.
+fdbcs* conflictSetDevice(ConflictSet* cs) { return cs ? cs->h : nullptr; }
+
 // newConflictSet() -- SkipList.cpp:956
 ConflictSet* newConflictSet() {
     ConflictSet* cs = new ConflictSet;
