@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 R=${1:-r01}
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_$R.log 2> gpurun_out/bench_$R.err || { echo "bench failed"; tail -20 gpurun_out/bench_$R.err; exit 1; }
 cat gpurun_out/bench_$R.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$R -o run -- python3 -u bench.py --steps 200 --stage-batches 0 --pcie-batches 0 --no-cpu > gpurun_out/prof_$R.log 2> gpurun_out/prof_$R.err || { echo "prof failed"; tail -20 gpurun_out/prof_$R.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$R -o run -- python3 -u bench.py --steps 200 --stage-batches 0 --pcie-batches 0 --lm-batches 0 --no-cpu > gpurun_out/prof_$R.log 2> gpurun_out/prof_$R.err || { echo "prof failed"; tail -20 gpurun_out/prof_$R.err; exit 1; }
 cat gpurun_out/prof_$R.log
 python3 scripts/prof_summary.py gpurun_out/prof_$R/run_kernel_trace.csv 199 > gpurun_out/kstats_$R.txt && cat gpurun_out/kstats_$R.txt
 cp gpurun_out/prof_$R/run_kernel_stats.csv gpurun_out/kernel_stats_$R.csv 2>/dev/null
