@@ -141,6 +141,37 @@ def test_device_roll_tiny_streams(gpu):
 
 
 @pytest.mark.gpu
+def test_device_roll_long_keys(gpu):
+    """Begin keys of 0..300 B and up to 20 KB (metric >= units: added whole,
+    no roll, StorageMetrics.actor.h:171-175), at the knobs' units."""
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd.batch import PackedBatch
+    rng = random.Random(11)
+    cs = ConflictSet(device=0)
+
+    def key():
+        r = rng.random()
+        n = rng.randint(19890, 20010) if r < 0.02 else rng.randint(0, 300)
+        return bytes(rng.randrange(256) for _ in range(n)) if n < 400 else bytes([rng.randrange(4)]) * n
+
+    def rng_range():
+        a = key()
+        return (a, a + b"\x00")
+
+    def stream():
+        now = 100
+        for _ in range(6):
+            now += 10
+            txns = [(now - 5, [rng_range() for _ in range(rng.randint(0, 3))],
+                     [rng_range() for _ in range(rng.randint(0, 2))]) for _ in range(rng.randint(50, 400))]
+            yield PackedBatch.from_txns(txns), now, now - 50
+
+    g, o = _run_stream(cs, stream(), units=KEY_BYTES_PER_SAMPLE, seed=5, poll_every=2)
+    assert any(len(k) >= 19900 and m >= KEY_BYTES_PER_SAMPLE for k, m in o.items())
+    cs.close()
+
+
+@pytest.mark.gpu
 def test_device_roll_mixed_and_config2(gpu):
     from foundationdb_amd import ConflictSet
     from foundationdb_amd.workload import Workload
