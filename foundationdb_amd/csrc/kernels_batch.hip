@@ -491,8 +491,11 @@ __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) 
 // of a range (the begin < end precondition), and -- in steady state, when
 // splitters from an earlier batch exist (SCATTER) -- scatter the range's sort
 // records straight into their buckets (reads: the begin; writes: both ends).
+#ifndef FDBCS_INGEST_BLOCK
+#define FDBCS_INGEST_BLOCK 256
+#endif
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_ingest(IngestArgs A, SortJobs J) {
+__global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, SortJobs J) {
     if ((int)blockIdx.x < A.prep_blocks) {
         const int t = blockIdx.x * blockDim.x + threadIdx.x;
         if (t == 0) {
@@ -1129,20 +1132,21 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
 
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
                    hipStream_t s) {
+    constexpr int IB = FDBCS_INGEST_BLOCK;  // (A/B: scripts/build_variants.sh)
     IngestArgs A;
     A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
-    A.prep_blocks = std::max(1, cdiv(v.txn_count, 256));
+    A.prep_blocks = std::max(1, cdiv(v.txn_count, IB));
     A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
     A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
     A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
     A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
-    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, 256);
+    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     if (scatter)
-        hipLaunchKernelGGL(k_ingest<true>, dim3(blocks), dim3(256), 0, s, A, J);
+        hipLaunchKernelGGL(k_ingest<true>, dim3(blocks), dim3(IB), 0, s, A, J);
     else
-        hipLaunchKernelGGL(k_ingest<false>, dim3(blocks), dim3(256), 0, s, A, J);
+        hipLaunchKernelGGL(k_ingest<false>, dim3(blocks), dim3(IB), 0, s, A, J);
 }
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
