@@ -192,3 +192,43 @@ def test_device_roll_mixed_and_config2(gpu):
     o.poll(1e9)
     assert g.size() == 0 and g.get_estimate(*ALL_KEYS) == 0 and o.items() == []
     cs.close()
+
+
+@pytest.mark.gpu
+def test_key_range_resolvers_sample_their_sub_batches(gpu):
+    """resolverCount > 1 (Resolver.actor.cpp:146): three key-range resolvers,
+    each sampling the sub-batch the proxy split sends it; the master's
+    ResolutionMetricsRequest / ResolutionSplitRequest answers
+    (masterserver.actor.cpp:964-1020) equal three oracle samples'."""
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
+    from foundationdb_amd.workload import Workload
+
+    kr = KeyRangeResolvers(uniform_bounds(3))
+    lo_hi = [(b"", kr.bounds[0]), (kr.bounds[0], kr.bounds[1]), (kr.bounds[1], b"\xff\xff")]
+    gres = [ConflictSet(device=0) for _ in range(3)]
+    gs = [IopsSample(KEY_BYTES_PER_SAMPLE, seed=g) for g in range(3)]
+    os_ = [SpecSample(KEY_BYTES_PER_SAMPLE, seed=g) for g in range(3)]
+    wl = Workload(2, txns=3000)
+    t = 0.0
+    for i in range(8):
+        batch, now, nold = wl.batch(i)
+        t += 0.3
+        for g in range(3):
+            sub, _idx = kr.split(batch, g)
+            gres[g].detect_packed(sub, now, nold)
+            assert gs[g].add_batch(gres[g], t + 1.0) == os_[g].add_batch(sub, t + 1.0)
+            gs[g].poll(t)
+            os_[g].poll(t)
+    metrics = [s.get_estimate(*ALL_KEYS) for s in gs]
+    assert metrics == [o.get_estimate(*ALL_KEYS) for o in os_]
+    src = int(np.argmax(metrics))
+    amount = max(1, (metrics[src] - min(metrics)) // 2)
+    b, e = lo_hi[src]
+    for front in (True, False):
+        key, used = gs[src].resolution_split(b, e, amount, front)
+        assert key == os_[src].split_estimate(b, e, amount, front)
+        assert b <= key <= e
+        assert used == (os_[src].get_estimate(b, key) if front else os_[src].get_estimate(key, e))
+    for x in gres:
+        x.close()
