@@ -232,3 +232,36 @@ def test_key_range_resolvers_sample_their_sub_batches(gpu):
         assert used == (os_[src].get_estimate(b, key) if front else os_[src].get_estimate(key, e))
     for x in gres:
         x.close()
+
+
+@pytest.mark.gpu
+def test_device_roll_explicit_device_batch(gpu):
+    """fdbcs_sample_add_batch over a caller-owned device batch view (the
+    fdbcs_detect_device path); a pipelined submit leaves no 'last batch'."""
+    import torch
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd._abi import BatchView
+    from foundationdb_amd.workload import Workload
+
+    cs = ConflictSet(device=0)
+    wl = Workload(2, txns=2000)
+    g, o = IopsSample(2000, seed=3), SpecSample(2000, seed=3)
+    for i in range(4):
+        b, _now, _nold = wl.batch(i)
+        bufs = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in
+                (b.snapshot, b.read_off, b.write_off, b.key_off.view(np.int64), b.key_len.view(np.int32),
+                 b.key_bytes)]
+        torch.cuda.synchronize()
+        dv = BatchView()
+        dv.txn_count, dv.read_count, dv.write_count = b.T, b.R, b.W
+        dv.snapshot, dv.read_off, dv.write_off = bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr()
+        dv.key_off, dv.key_len, dv.key_bytes = bufs[3].data_ptr(), bufs[4].data_ptr(), bufs[5].data_ptr()
+        dv.key_bytes_len = int(b.key_bytes.size)
+        assert g.add_batch(cs, 1.0 + i, dev_batch=dv) == o.add_batch(b, 1.0 + i)
+        assert g.items() == o.items()
+    b, now, nold = wl.batch(10)
+    cs.submit_packed(b, now, nold)
+    cs.wait()
+    with pytest.raises(_abi.FdbcsError):
+        g.add_batch(cs, 9.0)
+    cs.close()
