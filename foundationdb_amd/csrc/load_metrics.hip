@@ -35,7 +35,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
-#include <unordered_map>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -214,19 +214,111 @@ int kcmp(const std::string& a, const uint8_t* b, uint32_t bl) {
 
 }  // namespace
 
-// The sample: IndexedSet<Key, int64_t> (flow/IndexedSet.h) as a hash map
-// (O(1) per sampled key on the Resolver's per-batch path) plus a sorted view
-// with prefix sums rebuilt lazily before a query: queries are rare next to
-// adds (the master asks every MIN_BALANCE_TIME), the reverse of the trade the
-// reference's balanced tree makes.  And the expiry queue.
+// The sample: IndexedSet<Key, int64_t> (flow/IndexedSet.h) as an
+// open-addressing hash table whose keys live in one byte arena (no allocation
+// per sampled key on the Resolver's per-batch path), plus a sorted view with
+// prefix sums rebuilt lazily before a query: queries are rare next to adds
+// (the master asks every MIN_BALANCE_TIME), the reverse of the trade the
+// reference's balanced tree makes.  The expiry queue holds one group per
+// batch (all its entries share one expiration).
+struct FlatSample {
+    struct E {
+        uint64_t h, off;
+        uint32_t len, st;  // st: 0 empty, 1 live, 2 erased
+        int64_t m;
+    };
+    std::vector<E> t;
+    size_t live = 0, used = 0, garbage = 0;
+    std::string arena;
+
+    static uint64_t mix(uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    static uint64_t hash(const uint8_t* p, uint32_t n) {
+        uint64_t h = mix(0x9E3779B97F4A7C15ull ^ n);
+        for (; n >= 8; p += 8, n -= 8) {
+            uint64_t w;
+            memcpy(&w, p, 8);
+            h = mix(h ^ w);
+        }
+        uint64_t w = 0;
+        if (n) memcpy(&w, p, n);
+        return mix(h ^ w);
+    }
+    void place(const E& e) {
+        const size_t mask = t.size() - 1;
+        size_t i = e.h & mask;
+        while (t[i].st) i = (i + 1) & mask;
+        t[i] = e;
+    }
+    // rebuild at capacity cap: drops erased slots and compacts the arena
+    void rehash(size_t cap) {
+        std::vector<E> old(cap, E{});
+        old.swap(t);
+        std::string na;
+        na.reserve(arena.size() - garbage);
+        for (const E& e : old)
+            if (e.st == 1) {
+                E n = e;
+                n.off = na.size();
+                na.append(arena, e.off, e.len);
+                place(n);
+            }
+        arena.swap(na);
+        garbage = 0;
+        used = live;
+    }
+    // IndexedSet::addMetric (flow/IndexedSet.h:587-598) followed by the
+    // erase-at-zero of StorageMetrics.actor.h:136-137 / :177-178
+    void add(const uint8_t* k, uint32_t len, uint64_t h, int64_t m) {
+        if (t.empty()) t.assign(1024, E{});
+        if ((used + 1) * 2 > t.size()) rehash((live + 1) * 4 > t.size() ? t.size() * 2 : t.size());
+        else if (garbage > (1u << 20) && garbage * 2 > arena.size()) rehash(t.size());
+        const size_t mask = t.size() - 1;
+        size_t i = h & mask, tomb = SIZE_MAX;
+        for (; t[i].st; i = (i + 1) & mask) {
+            E& e = t[i];
+            if (e.st == 1 && e.h == h && e.len == len && (len == 0 || !memcmp(arena.data() + e.off, k, len))) {
+                e.m += m;
+                if (e.m == 0) {
+                    e.st = 2;
+                    live--;
+                    garbage += len;
+                }
+                return;
+            }
+            if (e.st == 2 && tomb == SIZE_MAX) tomb = i;
+        }
+        if (m == 0) return;
+        if (tomb == SIZE_MAX) used++;
+        t[tomb != SIZE_MAX ? tomb : i] = E{h, arena.size(), len, 1, m};
+        arena.append((const char*)k, len);
+        live++;
+    }
+};
+
 struct fdbcs_sample {
     int64_t units = 0;
     uint64_t seed = 0;
     uint64_t seq = 0;  // batches rolled so far (draw counter)
-    std::unordered_map<std::string, int64_t> sample;
-    std::deque<std::pair<double, std::pair<std::string, int64_t>>> queue;
+    FlatSample sample;
+    struct GItem {
+        uint64_t h, off;
+        uint32_t len;
+        int64_t delta;
+    };
+    struct Group {
+        double exp;
+        std::string bytes;
+        std::vector<GItem> items;
+    };
+    std::deque<Group> queue;
+    size_t queued = 0;
     // query view
     mutable bool dirty = true;
+    mutable std::vector<std::string> vstore;
     mutable std::vector<const std::string*> keys;
     mutable std::vector<int64_t> prefix;  // prefix[i] = sumTo(i); size n+1
     // device roll buffers
@@ -248,26 +340,29 @@ struct fdbcs_sample {
     uint8_t* h_out = nullptr;
     size_t out_cap = 0;
 
-    // IndexedSet::addMetric (flow/IndexedSet.h:587-598) followed by the
-    // erase-at-zero of StorageMetrics.actor.h:136-137 / :177-178.
-    void add_metric(const std::string& k, int64_t m) {
+    void add_metric(const uint8_t* k, uint32_t len, int64_t m) {
         dirty = true;
-        auto ins = sample.try_emplace(k, 0);
-        const int64_t v = ins.first->second + m;
-        if (v == 0) sample.erase(ins.first);
-        else ins.first->second = v;
+        sample.add(k, len, FlatSample::hash(k, len), m);
     }
     void view() const {
         if (!dirty) return;
+        std::vector<std::pair<std::string, int64_t>> ents;
+        ents.reserve(sample.live);
+        for (const auto& e : sample.t)
+            if (e.st == 1) ents.emplace_back(std::string(sample.arena, e.off, e.len), e.m);
+        std::sort(ents.begin(), ents.end(), [](const auto& x, const auto& y) {
+            return kcmp(x.first, (const uint8_t*)y.first.data(), (uint32_t)y.first.size()) < 0;
+        });
+        vstore.clear();
+        vstore.reserve(ents.size());
         keys.clear();
         prefix.assign(1, 0);
-        keys.reserve(sample.size());
-        prefix.reserve(sample.size() + 1);
-        for (auto& kv : sample) keys.push_back(&kv.first);
-        std::sort(keys.begin(), keys.end(), [](const std::string* a, const std::string* b) {
-            return kcmp(*a, (const uint8_t*)b->data(), (uint32_t)b->size()) < 0;
-        });
-        for (const std::string* k : keys) prefix.push_back(prefix.back() + sample.find(*k)->second);
+        prefix.reserve(ents.size() + 1);
+        for (auto& kv : ents) {
+            vstore.push_back(std::move(kv.first));
+            prefix.push_back(prefix.back() + kv.second);
+        }
+        for (const auto& k : vstore) keys.push_back(&k);
         dirty = false;
     }
     // index of the first key >= k (IndexedSet::lower_bound)
@@ -414,28 +509,39 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
     const uint32_t* len = s->h_len;
     const uint64_t* off = s->h_off;
     const uint8_t* bytes = s->h_out;
-    // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order
+    // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order;
+    // the batch's queue entries form one group sharing its key bytes
+    fdbcs_sample::Group g{expiration, std::string((const char*)bytes, s->h_tot[1]), {}};
+    g.items.reserve(m);
+    s->dirty = true;
     for (uint64_t i = 0; i < m; i++) {
-        std::string k((const char*)bytes + off[i], len[i]);
-        s->add_metric(k, amt[i]);
-        s->queue.emplace_back(expiration, std::make_pair(std::move(k), -amt[i]));
+        const uint8_t* k = (const uint8_t*)g.bytes.data() + off[i];
+        const uint64_t h = FlatSample::hash(k, len[i]);
+        s->sample.add(k, len[i], h, amt[i]);
+        g.items.push_back({h, off[i], len[i], -amt[i]});
     }
+    s->queued += m;
+    s->queue.push_back(std::move(g));
     return FDBCS_OK;
 }
 
 int fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric) {
     if (!s || (len && !key)) return FDBCS_E_ARG;
-    s->add_metric(std::string((const char*)key, len), metric);
+    s->add_metric(key, len, metric);
     return FDBCS_OK;
 }
 
 int fdbcs_sample_poll(fdbcs_sample* s, double now) {
     if (!s) return FDBCS_E_ARG;
     // TransientStorageMetricSample::poll() (StorageMetrics.actor.h:150-164)
-    while (!s->queue.empty() && s->queue.front().first <= now) {
-        auto& q = s->queue.front();
-        if (q.second.second == 0) return FDBCS_E_STATE;  // ASSERT(delta != 0)
-        s->add_metric(q.second.first, q.second.second);
+    while (!s->queue.empty() && s->queue.front().exp <= now) {
+        const auto& g = s->queue.front();
+        s->dirty = true;
+        for (const auto& it : g.items) {
+            if (it.delta == 0) return FDBCS_E_STATE;  // ASSERT(delta != 0)
+            s->sample.add((const uint8_t*)g.bytes.data() + it.off, it.len, it.h, it.delta);
+        }
+        s->queued -= g.items.size();
         s->queue.pop_front();
     }
     return FDBCS_OK;
@@ -456,9 +562,9 @@ int32_t fdbcs_sample_split(const fdbcs_sample* s, const uint8_t* b, uint32_t bl,
     return (int32_t)k.size();
 }
 
-int64_t fdbcs_sample_size(const fdbcs_sample* s) { return s ? (int64_t)s->sample.size() : FDBCS_E_ARG; }
+int64_t fdbcs_sample_size(const fdbcs_sample* s) { return s ? (int64_t)s->sample.live : FDBCS_E_ARG; }
 
-int64_t fdbcs_sample_queue_size(const fdbcs_sample* s) { return s ? (int64_t)s->queue.size() : FDBCS_E_ARG; }
+int64_t fdbcs_sample_queue_size(const fdbcs_sample* s) { return s ? (int64_t)s->queued : FDBCS_E_ARG; }
 
 int32_t fdbcs_sample_entry(const fdbcs_sample* s, int64_t i, uint8_t* out, uint32_t cap, int64_t* metric) {
     if (!s || i < 0 || (cap && !out)) return FDBCS_E_ARG;
