@@ -116,6 +116,11 @@ WL_FUNCS = [
     ("fdbwl_destroy", None, [C.c_void_p]),
     ("fdbwl_generate", C.c_int, [C.c_void_p, C.c_int64, C.POINTER(BatchView), C.POINTER(C.c_int64),
                                  C.POINTER(C.c_int64)]),
+    ("fdbwl_run_prepare", C.c_void_p, [C.c_void_p, C.c_int64, C.c_int32]),
+    ("fdbwl_run_destroy", None, [C.c_void_p]),
+    ("fdbwl_run_txns", C.c_int32, [C.c_void_p]),
+    ("fdbwl_run_resolver", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fdbwl_prefill", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
 ]
 
 _lib = None
@@ -136,13 +141,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m foundationdb_amd.build`")
-        _lib = _bind(C.CDLL(LIB_PATH), FDBCS_FUNCS)
+        # RTLD_GLOBAL: the workload library's bench drivers call the C ABI through it
+        _lib = _bind(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL), FDBCS_FUNCS)
     return _lib
 
 
 def workload_lib():
     global _wl
     if _wl is None:
+        lib()  # (its fdbcs_* symbols resolve the workload library's)
         if not os.path.exists(WL_PATH):
             raise RuntimeError(f"{WL_PATH} is missing: build it with `python -m foundationdb_amd.build`")
         _wl = _bind(C.CDLL(WL_PATH), WL_FUNCS)

@@ -18,7 +18,8 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(ROOT, "build", os.environ.get("FDBCS_OBJ_DIR", "obj"))
 ARCH = os.environ.get("FDBCS_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip", "resolvers.hip", "load_metrics.hip"]
+HIP_SOURCES = ["scan.hip", "kernels_batch.hip", "kernels_hist.hip", "engine.hip", "stage.hip", "resolvers.hip",
+               "load_metrics.hip"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value"]
 HIP_FLAGS += os.environ.get("FDBCS_EXTRA_FLAGS", "").split()  # experiment variants (scripts/build_variants.sh)
 if os.environ.get("FDBCS_PHASES"):  # profiling build: kernels record phase timestamps

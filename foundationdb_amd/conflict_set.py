@@ -186,6 +186,7 @@ class ConflictBatch:
         self._lib = cs._lib
         check(self._lib.fdbcs_batch_begin(cs.handle), "ConflictBatch")
         self._count = 0
+        self._keep = []  # the key buffers (kept to detect_conflicts, as the reference borrows them)
 
     def add_transaction(self, read_ranges, write_ranges, read_snapshot):
         """read_ranges / write_ranges: sequences of (begin bytes, end bytes)."""
@@ -206,14 +207,18 @@ class ConflictBatch:
         rs, ws = list(read_ranges), list(write_ranges)
         check(self._lib.fdbcs_batch_add(self.cs.handle, read_snapshot, ranges(rs), len(rs), ranges(ws), len(ws)),
               "addTransaction")
+        self._keep.append(keep)
         self._count += 1
 
     def detect_conflicts(self, now, new_oldest_version, non_conflicting=None, too_old=None):
         """Appends committed indices to ``non_conflicting`` and tooOld indices to
         ``too_old`` (if given); returns the verdict byte array."""
         out = np.zeros(max(self._count, 1), np.uint8)
-        check(self._lib.fdbcs_batch_detect(self.cs.handle, now, new_oldest_version, out.ctypes.data),
-              "detectConflicts")
+        try:
+            check(self._lib.fdbcs_batch_detect(self.cs.handle, now, new_oldest_version, out.ctypes.data),
+                  "detectConflicts")
+        finally:
+            self._keep = []
         out = out[:self._count]
         if non_conflicting is not None:
             non_conflicting.extend(int(i) for i in np.nonzero(out == COMMITTED)[0])

@@ -9,6 +9,8 @@
 // compaction.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +19,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "stage.h"
 
 using namespace fdbcs_dev;
 
@@ -74,12 +77,27 @@ void encode_host(const uint8_t* p, uint32_t L, uint64_t& hi, uint64_t& lo, uint3
     meta = (b16 << 24) | L;
 }
 
+// ~35,000 ranges per config-2 batch are checked on the host: inline word
+// compares instead of a libc call per key.
+inline uint64_t ld64(const uint8_t* p) {
+    uint64_t x;
+    memcpy(&x, p, 8);
+    return x;
+}
+
+// keycmp (SkipList.cpp:113-120 order) eight bytes at a time
 int keycmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
-    uint32_t n = std::min(al, bl);
-    int c = n ? memcmp(a, b, n) : 0;
-    if (c) return c < 0 ? -1 : 1;
+    const uint32_t n = std::min(al, bl);
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint64_t x = ld64(a + i), y = ld64(b + i);
+        if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y) ? -1 : 1;
+    }
+    for (; i < n; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
     return al < bl ? -1 : (al > bl ? 1 : 0);
 }
+
 
 }  // namespace
 
@@ -102,13 +120,10 @@ struct fdbcs {
     uint64_t known_tail = 0;
     int64_t pending_pages = 0;   // worst-case pages consumed by unsynchronized batches
     uint64_t pending_tail = 0;
-    // host staging of ConflictBatch::addTransaction
+    // host staging of ConflictBatch::addTransaction (SkipList.cpp:979-1008):
+    // stage.h (pinned record stream, chunked H2D, k_unpack at detect)
     bool in_batch = false;
-    std::vector<int64_t> snap;
-    std::vector<int32_t> roff{0}, woff{0};
-    std::vector<uint64_t> rkoff, wkoff;
-    std::vector<uint32_t> rklen, wklen;
-    std::vector<uint8_t> blob;
+    TxnStage st;
     // pinned host staging + device input staging
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
@@ -212,9 +227,29 @@ int sync_state(fdbcs* cs) {
     return FDBCS_OK;
 }
 
+// Wait for the stream.  FDBCS_SYNC_SPIN=1: poll instead of the runtime's
+// blocking wait (the resolver thread stays on its core).
+int wait_stream(fdbcs* cs) {
+    static const bool spin = getenv("FDBCS_SYNC_SPIN") && atoi(getenv("FDBCS_SYNC_SPIN"));
+    if (!spin) {
+        HIPOK(hipStreamSynchronize(cs->stream));
+        return FDBCS_OK;
+    }
+    for (;;) {
+        const hipError_t e = hipStreamQuery(cs->stream);
+        if (e == hipSuccess) return FDBCS_OK;
+        if (e != hipErrorNotReady) {
+            last_hip_error() = e;
+            return FDBCS_E_HIP;
+        }
+        _mm_pause();
+    }
+}
+
 // After a batch: its last kernel has written the scalars to the mapped copy.
 int sync_batch(fdbcs* cs) {
-    HIPOK(hipStreamSynchronize(cs->stream));
+    int r;
+    if ((r = wait_stream(cs))) return r;
     memcpy(cs->sc_host, (const void*)cs->sc_mapped, sizeof(Scalars));
     adopt_scalars(cs);
     return FDBCS_OK;
@@ -546,6 +581,18 @@ void record(fdbcs* cs, int i) {
     if (cs->timing) hipEventRecord(cs->ev[i], cs->stream);
 }
 
+// per-stage HIP-event times of the batch just synchronized (stage timing on)
+void read_stage_times(fdbcs* cs) {
+    if (!cs->timing) return;
+    float ms;
+    const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
+    for (int i = 0; i < 7; i++) {
+        hipEventElapsedTime(&ms, cs->ev[map[i][0]], cs->ev[map[i][1]]);
+        cs->stage_us[i] = ms * 1000.0;
+    }
+    cs->have_times = true;
+}
+
 // The whole detectConflicts pipeline on a device-resident batch.
 int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
               bool sync) {
@@ -553,6 +600,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
     cs->edges_known = false;
+    cs->have_last_dv = false;  // (the host paths set it again once this batch succeeded)
     if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
     cs->last_T = T;
@@ -589,15 +637,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     if (compact) cs->oldest = new_oldest;
     if (sync) {
         if ((r = sync_batch(cs))) return r;
-        if (cs->timing) {
-            float ms;
-            const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
-            for (int i = 0; i < 7; i++) {
-                hipEventElapsedTime(&ms, cs->ev[map[i][0]], cs->ev[map[i][1]]);
-                cs->stage_us[i] = ms * 1000.0;
-            }
-            cs->have_times = true;
-        }
+        read_stage_times(cs);
         if (cs->sc_host->last_err) return cs->sc_host->last_err;
     }
     return FDBCS_OK;
@@ -714,23 +754,15 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     cs->have_last_dv = false;
     if ((r = stage_batch(cs, hv, dv))) return r;
     if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
-    cs->last_dv = dv;
-    cs->have_last_dv = true;
     const int64_t T = hv.txn_count;
     if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
     if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
     if ((r = sync_batch(cs))) return r;
+    read_stage_times(cs);
     if (cs->sc_host->last_err) return cs->sc_host->last_err;
     if (T) memcpy(verdict, cs->vpin, (size_t)T);
-    if (cs->timing) {
-        float ms;
-        const int map[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
-        for (int i = 0; i < 7; i++) {
-            hipEventElapsedTime(&ms, cs->ev[map[i][0]], cs->ev[map[i][1]]);
-            cs->stage_us[i] = ms * 1000.0;
-        }
-        cs->have_times = true;
-    }
+    cs->last_dv = dv;
+    cs->have_last_dv = true;
     return FDBCS_OK;
 }
 
@@ -828,6 +860,10 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
     if ((r = reset_history(cs, v0))) return fail(r);
     cs->oldest = 0;
+    if (const char* c = getenv("FDBCS_STAGE_CHUNK"))  // bytes per streamed H2D chunk of the per-transaction path
+        cs->st.configure(cs->stream, strtoull(c, nullptr, 0));
+    else
+        cs->st.configure(cs->stream, 512 << 10);
     *out = cs;
     return FDBCS_OK;
 }
@@ -871,68 +907,46 @@ void fdbcs_destroy(fdbcs* cs) {
 
 int fdbcs_batch_begin(fdbcs* cs) {
     if (!cs) return FDBCS_E_ARG;
+    if (cs->sub_head != cs->sub_tail) return FDBCS_E_STATE;  // (pipelined batches still in flight)
+    int r;
+    if ((r = cs->st.begin())) return r;
     cs->in_batch = true;
-    cs->snap.clear();
-    cs->roff.assign(1, 0);
-    cs->woff.assign(1, 0);
-    cs->rkoff.clear(); cs->rklen.clear(); cs->wkoff.clear(); cs->wklen.clear();
-    cs->blob.clear();
     return FDBCS_OK;
 }
 
+// ConflictBatch::addTransaction (SkipList.cpp:979-1008): stage.h.
 int fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
                     const fdbcs_range* writes, int32_t nwrites) {
     if (!cs) return FDBCS_E_ARG;
     if (!cs->in_batch) return FDBCS_E_STATE;
-    if (nreads < 0 || nwrites < 0 || (nreads && !reads) || (nwrites && !writes)) return FDBCS_E_ARG;
-    for (int i = 0; i < nreads + nwrites; i++) {
-        const fdbcs_range& rg = i < nreads ? reads[i] : writes[i - nreads];
-        if (rg.begin_len > FDBCS_MAX_KEY || rg.end_len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
-        if (keycmp(rg.begin, rg.begin_len, rg.end, rg.end_len) >= 0) return FDBCS_E_RANGE;
-    }
-    auto put = [&](const uint8_t* p, uint32_t n, std::vector<uint64_t>& off, std::vector<uint32_t>& len) {
-        off.push_back(cs->blob.size());
-        len.push_back(n);
-        if (n) cs->blob.insert(cs->blob.end(), p, p + n);
-    };
-    for (int i = 0; i < nreads; i++) {
-        put(reads[i].begin, reads[i].begin_len, cs->rkoff, cs->rklen);
-        put(reads[i].end, reads[i].end_len, cs->rkoff, cs->rklen);
-    }
-    for (int i = 0; i < nwrites; i++) {
-        put(writes[i].begin, writes[i].begin_len, cs->wkoff, cs->wklen);
-        put(writes[i].end, writes[i].end_len, cs->wkoff, cs->wklen);
-    }
-    cs->snap.push_back(read_snapshot);
-    cs->roff.push_back(cs->roff.back() + nreads);
-    cs->woff.push_back(cs->woff.back() + nwrites);
-    return FDBCS_OK;
+    return cs->st.add(read_snapshot, reads, nreads, writes, nwrites);
 }
 
-int32_t fdbcs_batch_txn_count(const fdbcs* cs) { return cs ? (int32_t)cs->snap.size() : 0; }
+int32_t fdbcs_batch_txn_count(const fdbcs* cs) { return cs ? (int32_t)cs->st.txns() : 0; }
 
+// ConflictBatch::detectConflicts (SkipList.cpp:1163-1208) on the staged batch:
+// the staging finishes (last chunk, record offsets, k_unpack builds the batch
+// view on the device), the pipeline runs, the verdicts come back.
 int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verdict) {
     if (!cs) return FDBCS_E_ARG;
     if (!cs->in_batch) return FDBCS_E_STATE;
-    cs->in_batch = false;
-    const int32_t T = (int32_t)cs->snap.size();
+    const int64_t T = cs->st.txns();
     if (T && !verdict) return FDBCS_E_ARG;
-    std::vector<uint64_t> koff(cs->rkoff);
-    koff.insert(koff.end(), cs->wkoff.begin(), cs->wkoff.end());
-    std::vector<uint32_t> klen(cs->rklen);
-    klen.insert(klen.end(), cs->wklen.begin(), cs->wklen.end());
-    fdbcs_batch_view hv{};
-    hv.txn_count = T;
-    hv.read_count = cs->roff.back();
-    hv.write_count = cs->woff.back();
-    hv.snapshot = cs->snap.data();
-    hv.read_off = cs->roff.data();
-    hv.write_off = cs->woff.data();
-    hv.key_off = koff.data();
-    hv.key_len = klen.data();
-    hv.key_bytes = cs->blob.data();
-    hv.key_bytes_len = cs->blob.size();
-    return detect_host_view(cs, hv, now, new_oldest, verdict);
+    cs->in_batch = false;
+    cs->have_last_dv = false;
+    int r;
+    fdbcs_batch_view dv;
+    if ((r = cs->st.finish(dv))) return r;
+    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
+    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
+    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
+    if ((r = sync_batch(cs))) return r;
+    read_stage_times(cs);
+    if (cs->sc_host->last_err) return cs->sc_host->last_err;
+    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    cs->last_dv = dv;
+    cs->have_last_dv = true;
+    return FDBCS_OK;
 }
 
 int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest,
@@ -1278,6 +1292,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     const fdbcs_batch_view& v = *db;
     int r;
     if ((r = check_batch_shape(v))) return r;
+    cs->have_last_dv = false;
     if ((r = ensure_batch(cs, v.txn_count, v.read_count, v.write_count, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, v.write_count, v.key_bytes_len))) return r;
     cs->last_T = v.txn_count;

@@ -144,6 +144,27 @@ void scan_i32(const int32_t* in, int32_t* out, const int32_t* n_ptr, int32_t n_h
 void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, int32_t n_host, int64_t* total_out,
                        int64_t* tmp, hipStream_t s);
 
+// ---- per-transaction staging (ConflictBatch::addTransaction, SkipList.cpp:979-1008) ----
+// fdbcs_batch_add appends one record per transaction to a pinned byte stream:
+// a StageHdr, then (nr + nw) pairs {begin_len, end_len} (reads first, in call
+// order), then the key bytes (begin, end of each range), padded to 8 bytes.
+// ro / wo are the reads / writes added before this transaction.
+struct StageHdr {
+    int64_t snap;
+    int32_t ro, wo, nr, nw;
+};
+static_assert(sizeof(StageHdr) == 24, "stage record header");
+// k_unpack: one lane per transaction turns the stream (device copy) into the
+// arrays of a fdbcs_batch_view (layout below, key_bytes = the stream itself)
+struct UnpackOut {
+    int64_t* snap;     // [T]
+    int32_t* ro;       // [T+1]
+    int32_t* wo;       // [T+1]
+    uint64_t* koff;    // [2R+2W]
+    uint32_t* klen;    // [2R+2W]
+};
+void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s);
+
 // ---- batch stages (kernels_batch.hip) ----
 // scatter: the sort splitters exist (an earlier batch) -- the ingest puts
 // the sort records into their buckets itself (launch_sort_ranges(scattered))

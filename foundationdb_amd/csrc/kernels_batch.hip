@@ -1130,6 +1130,41 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
     return J;
 }
 
+// Per-transaction staging stream -> batch view (kernels.h StageHdr).  Lane t
+// places its reads at slots 2(ro + k) and its writes at 2R + 2(wo + k): the
+// slot layout every later stage addresses (include/fdbcs.h fdbcs_batch_view).
+__global__ __launch_bounds__(256) void k_unpack(const uint8_t* __restrict__ stream,
+                                                const uint64_t* __restrict__ toff, int T, int R, int W,
+                                                UnpackOut o) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > T) return;
+    if (t == T) {
+        o.ro[T] = R;
+        o.wo[T] = W;
+        return;
+    }
+    const uint64_t base = toff[t];
+    const StageHdr h = *reinterpret_cast<const StageHdr*>(stream + base);
+    o.snap[t] = h.snap;
+    o.ro[t] = h.ro;
+    o.wo[t] = h.wo;
+    const uint2* lens = reinterpret_cast<const uint2*>(stream + base + sizeof(StageHdr));
+    uint64_t kp = base + sizeof(StageHdr) + 8ull * (uint32_t)(h.nr + h.nw);
+    for (int k = 0; k < h.nr + h.nw; k++) {
+        const uint2 l = lens[k];
+        const int64_t slot = k < h.nr ? 2ll * (h.ro + k) : 2ll * R + 2ll * (h.wo + k - h.nr);
+        o.koff[slot] = kp;
+        o.klen[slot] = l.x;
+        o.koff[slot + 1] = kp + l.x;
+        o.klen[slot + 1] = l.y;
+        kp += (uint64_t)l.x + l.y;
+    }
+}
+
+void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s) {
+    hipLaunchKernelGGL(k_unpack, dim3(cdiv((int64_t)T + 1, 256)), dim3(256), 0, s, stream, toff, T, R, W, o);
+}
+
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
                    hipStream_t s) {
     constexpr int IB = FDBCS_INGEST_BLOCK;  // (A/B: scripts/build_variants.sh)

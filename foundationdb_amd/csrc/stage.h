@@ -1,0 +1,63 @@
+// stage.h -- host staging of ConflictBatch::addTransaction (SkipList.cpp:979-1008)
+// for the per-transaction path (fdbcs_batch_add / fdbcs_batch_detect).
+//
+// The Resolver calls addTransaction T times on one thread, then
+// detectConflicts (Resolver.actor.cpp:140-153).  Each call checks its ranges
+// and appends one record -- a StageHdr, the range lengths, the key bytes
+// (kernels.h) -- to a pinned byte stream: the only host copy of the batch.
+// Every `chunk` bytes the new part of the stream starts its H2D copy on the
+// conflict set's stream, so most of the batch is on the device by the time
+// detectConflicts is called; finish() sends the rest plus the record offsets
+// and k_unpack builds the batch view on the device.
+//
+// (Handing the record copies to helper threads was measured and dropped:
+// with the descriptors written by one core and read by another, the
+// calling thread got slower, 185 -> 250-990 us per config-2 batch.)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace fdbcs_dev {
+
+class TxnStage {
+   public:
+    TxnStage() = default;
+    ~TxnStage();
+    TxnStage(const TxnStage&) = delete;
+    TxnStage& operator=(const TxnStage&) = delete;
+
+    // stream: where the H2D copies and k_unpack go; chunk: bytes per streamed copy
+    void configure(hipStream_t stream, uint64_t chunk);
+    int begin();
+    // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md
+    // §0.6) refuse the transaction, which is then not part of the batch.
+    int add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw);
+    // Sends the rest and unpacks on the stream; dv = the device batch view
+    // (valid until the next begin()).
+    int finish(fdbcs_batch_view& dv);
+    int64_t txns() const { return T_; }
+    bool open() const { return open_; }
+
+   private:
+    int grow(int64_t need_txns, uint64_t need_bytes);
+
+    hipStream_t stream_ = nullptr;
+    uint64_t chunk_ = 512 << 10;
+    bool open_ = false;
+    int64_t T_ = 0, R_ = 0, W_ = 0;
+    // the record stream: pinned + device copy, same capacity
+    uint8_t* pin_ = nullptr;
+    uint8_t* dev_ = nullptr;
+    uint64_t cap_ = 0;
+    uint64_t used_ = 0, sent_ = 0;
+    uint64_t* toff_ = nullptr;    // pinned [T]: record offsets
+    uint64_t* dtoff_ = nullptr;   // device copy
+    int64_t toff_cap_ = 0;
+    uint8_t* view_ = nullptr;     // device: the unpacked arrays
+    uint64_t view_cap_ = 0;
+};
+
+}  // namespace fdbcs_dev

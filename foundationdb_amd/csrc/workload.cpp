@@ -2,6 +2,7 @@
 #include "workload.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -256,6 +257,99 @@ int fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* v, int64_t* now, i
     v->key_len = g->klen.data();
     v->key_bytes = g->bytes.data();
     v->key_bytes_len = g->bytes.size();
+    return FDBCS_OK;
+}
+
+}  // extern "C"
+
+// ---- bench drivers ----------------------------------------------------------------
+
+struct fdbwl_run {
+    struct Batch {
+        std::vector<uint8_t> bytes;        // key arena (the proxy request's)
+        std::vector<fdbcs_range> reads, writes;
+        std::vector<int64_t> snap;
+        std::vector<int32_t> roff, woff;   // per transaction: its first read / write
+        int64_t now = 0, nold = 0;
+    };
+    std::vector<Batch> b;
+    int32_t T = 0;
+};
+
+extern "C" {
+
+fdbwl_run* fdbwl_run_prepare(fdbwl* g, int64_t first, int32_t n) {
+    if (!g || n < 0) return nullptr;
+    fdbwl_run* r = new fdbwl_run();
+    r->b.resize(n);
+    r->T = g->T;
+    for (int32_t i = 0; i < n; i++) {
+        fdbcs_batch_view v;
+        fdbwl_run::Batch& B = r->b[i];
+        fdbwl_generate(g, first + i, &v, &B.now, &B.nold);
+        B.bytes.assign(v.key_bytes, v.key_bytes + v.key_bytes_len);
+        B.snap.assign(v.snapshot, v.snapshot + v.txn_count);
+        B.roff.assign(v.read_off, v.read_off + v.txn_count + 1);
+        B.woff.assign(v.write_off, v.write_off + v.txn_count + 1);
+        const uint8_t* base = B.bytes.data();
+        auto rng = [&](int64_t s) {
+            return fdbcs_range{base + v.key_off[s], v.key_len[s], base + v.key_off[s + 1], v.key_len[s + 1]};
+        };
+        B.reads.resize(v.read_count);
+        B.writes.resize(v.write_count);
+        for (int64_t k = 0; k < v.read_count; k++) B.reads[k] = rng(2 * k);
+        for (int64_t k = 0; k < v.write_count; k++) B.writes[k] = rng(2 * ((int64_t)v.read_count + k));
+    }
+    return r;
+}
+
+void fdbwl_run_destroy(fdbwl_run* r) { delete r; }
+
+int32_t fdbwl_run_txns(const fdbwl_run* r) { return r ? r->T : 0; }
+
+int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts) {
+    if (!r || !cs) return FDBCS_E_ARG;
+    std::vector<uint8_t> scratch(std::max<int32_t>(r->T, 1));
+    for (size_t i = 0; i < r->b.size(); i++) {
+        const fdbwl_run::Batch& B = r->b[i];
+        uint8_t* out = verdicts ? verdicts + i * (size_t)r->T : scratch.data();
+        const auto t0 = std::chrono::steady_clock::now();
+        int st = fdbcs_batch_begin(cs);  // ConflictBatch conflictBatch(self->conflictSet)
+        const int T = (int)B.snap.size();
+        for (int t = 0; st == FDBCS_OK && t < T; t++)  // conflictBatch.addTransaction(req.transactions[t])
+            st = fdbcs_batch_add(cs, B.snap[t], B.reads.data() + B.roff[t], B.roff[t + 1] - B.roff[t],
+                                 B.writes.data() + B.woff[t], B.woff[t + 1] - B.woff[t]);
+        const auto ta = std::chrono::steady_clock::now();
+        if (st == FDBCS_OK) st = fdbcs_batch_detect(cs, B.now, B.nold, out);  // detectConflicts(...)
+        const auto t1 = std::chrono::steady_clock::now();
+        if (st != FDBCS_OK) return st;
+        if (batch_us) batch_us[i] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+        if (add_us) add_us[i] = std::chrono::duration<double, std::micro>(ta - t0).count();
+    }
+    return FDBCS_OK;
+}
+
+int fdbwl_prefill(fdbwl* g, fdbcs* cs, int64_t first, int32_t n) {
+    if (!g || !cs || n < 0) return FDBCS_E_ARG;
+    std::vector<uint8_t> verdict(std::max(g->T, 1));
+    int inflight = 0;
+    for (int32_t i = 0; i < n; i++) {
+        fdbcs_batch_view v;
+        int64_t now, nold;
+        fdbwl_generate(g, first + i, &v, &now, &nold);  // (overlaps the batch in flight)
+        if (inflight == 2) {
+            int st = fdbcs_batch_wait(cs, verdict.data());
+            if (st != FDBCS_OK) return st;
+            inflight--;
+        }
+        int st = fdbcs_batch_submit_packed(cs, &v, now, nold);  // (copies v into pinned staging)
+        if (st != FDBCS_OK) return st;
+        inflight++;
+    }
+    while (inflight--) {
+        int st = fdbcs_batch_wait(cs, verdict.data());
+        if (st != FDBCS_OK) return st;
+    }
     return FDBCS_OK;
 }
 

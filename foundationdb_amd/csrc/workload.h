@@ -44,6 +44,31 @@ void   fdbwl_destroy(fdbwl* g);
  * stays valid until the next call on g. */
 int    fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* view, int64_t* now, int64_t* new_oldest);
 
+/* ---- bench drivers (call the C ABI of libfdbcs.so, which must be loaded
+ * with RTLD_GLOBAL first: this library leaves the fdbcs_* symbols to it) ---- */
+
+/* Batches [first, first + n) generated ahead of time and kept in the
+ * Resolver's form: per transaction its read / write KeyRangeRefs into one key
+ * arena and its read_snapshot (CommitTransactionRef, fdbclient/
+ * CommitTransaction.h:89-100), plus (now, newOldest). */
+typedef struct fdbwl_run fdbwl_run;
+fdbwl_run* fdbwl_run_prepare(fdbwl* g, int64_t first, int32_t n);
+void       fdbwl_run_destroy(fdbwl_run* r);
+/* Transactions per batch (every prepared batch has the same count). */
+int32_t    fdbwl_run_txns(const fdbwl_run* r);
+
+/* The Resolver's loop (Resolver.actor.cpp:140-153) over the prepared batches:
+ * per batch ConflictBatch (fdbcs_batch_begin), T x addTransaction
+ * (fdbcs_batch_add), detectConflicts (fdbcs_batch_detect).  batch_us[i] = the
+ * wall time of batch i's window, add_us[i] its addTransaction part (both
+ * optional); verdicts (optional) = n x T bytes. */
+int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts);
+
+/* Grow a conflict set's history through n generated batches [first, first+n)
+ * (fdbcs_batch_submit_packed / fdbcs_batch_wait, generation of batch i+1
+ * overlapping batch i): the bench's steady-state prefill. */
+int fdbwl_prefill(fdbwl* g, fdbcs* cs, int64_t first, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,8 @@
 """Synthetic Resolver batches from the native generator."""
 import ctypes as C
 
+import numpy as np
+
 from . import _abi
 from .batch import PackedBatch
 
@@ -24,10 +26,53 @@ class Workload:
         v, now, nold = self.view(index)
         return PackedBatch.from_view(v), now, nold
 
+    def prefill(self, cs, first, n):
+        """Grow cs's history through batches [first, first + n) (native, pipelined)."""
+        _abi.check(self._lib.fdbwl_prefill(self._g, cs.handle, first, n), "prefill")
+
+    def prepare_run(self, first, n):
+        """Batches [first, first + n) pre-generated in the Resolver's per-transaction form."""
+        return ResolverRun(self, first, n)
+
     def close(self):
         if getattr(self, "_g", None):
             self._lib.fdbwl_destroy(self._g)
             self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ResolverRun:
+    """Prepared batches driven through the Resolver's loop in native code
+    (Resolver.actor.cpp:140-153: ConflictBatch, T x addTransaction,
+    detectConflicts), so the timed window holds no Python."""
+
+    def __init__(self, wl, first, n):
+        self._lib = wl._lib
+        self._r = self._lib.fdbwl_run_prepare(wl._g, first, n)
+        if not self._r:
+            raise RuntimeError("fdbwl_run_prepare failed")
+        self.n = n
+        self.T = self._lib.fdbwl_run_txns(self._r)
+
+    def run(self, cs, verdicts=True):
+        """Runs every batch; returns (per-batch window in us, its addTransaction
+        part in us, verdicts n x T or None)."""
+        us = np.zeros(max(self.n, 1), np.float64)
+        add = np.zeros(max(self.n, 1), np.float64)
+        out = np.zeros((max(self.n, 1), max(self.T, 1)), np.uint8) if verdicts else None
+        _abi.check(self._lib.fdbwl_run_resolver(self._r, cs.handle, us.ctypes.data, add.ctypes.data,
+                                                out.ctypes.data if verdicts else None), "resolver loop")
+        return us[:self.n], add[:self.n], (out[:self.n, :self.T] if verdicts else None)
+
+    def close(self):
+        if getattr(self, "_r", None):
+            self._lib.fdbwl_run_destroy(self._r)
+            self._r = None
 
     def __del__(self):
         try:

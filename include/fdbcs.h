@@ -123,9 +123,12 @@ void fdbcs_destroy(fdbcs* cs);
 int  fdbcs_batch_begin(fdbcs* cs);
 
 /* ConflictBatch::addTransaction(tr) (ConflictSet.h:42, SkipList.cpp:979-1008).
- * Transaction index = call order within the batch.  Key bytes are copied
- * into pinned staging memory immediately, so the caller's arena may be
- * released after this returns (stricter than the reference's borrow). */
+ * Transaction index = call order within the batch.  The key bytes are
+ * copied into pinned staging memory before this returns, so the caller's
+ * arena may be released at once (stricter than the reference, which borrows
+ * them until detectConflicts returns).  A range with begin >= end
+ * (FDBCS_E_RANGE) or a key over FDBCS_MAX_KEY (FDBCS_E_KEY) refuses the
+ * transaction: it is not added, and the batch goes on. */
 int  fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot,
                      const fdbcs_range* reads, int32_t nreads,
                      const fdbcs_range* writes, int32_t nwrites);

@@ -3,7 +3,7 @@
 // compiled and exercised outside an fdbserver build tree.  Only the members
 // the shim uses exist: KeyRangeRef::{begin,end} (fdbclient/FDBTypes.h:161),
 // StringRef::{begin(),size()} (flow/Arena.h), CommitTransactionRef::
-// {read_conflict_ranges, write_conflict_ranges, read_snapshot}
+// {read_conflict_ranges, write_conflict_ranges, read_snapshot}, Arena
 // (fdbclient/CommitTransaction.h:89-121).  Test infrastructure only.
 #pragma once
 #include <cstddef>
@@ -30,6 +30,8 @@ struct KeyRangeRef {
     KeyRangeRef(KeyRef b, KeyRef e) : begin(b), end(e) {}
 };
 
+struct Arena {};  // (flow/Arena.h: the owner of a request's memory)
+
 template <class T>
 struct VectorRef {
     std::vector<T> items;
@@ -37,6 +39,7 @@ struct VectorRef {
     const T* end() const { return items.data() + items.size(); }
     int size() const { return (int)items.size(); }
     void push_back(const T& x) { items.push_back(x); }
+    void push_back(Arena&, const T& x) { items.push_back(x); }  // (flow/Arena.h VectorRef::push_back)
 };
 
 template <class T>

@@ -15,6 +15,7 @@ import pytest
 
 from foundationdb_amd import _abi
 from foundationdb_amd.load_metrics import ALL_KEYS, KEY_BYTES_PER_SAMPLE, IopsSample
+from foundationdb_amd.workload import Workload
 from gen import mixed_stream, tiny_stream
 from oracle.load_sample import SpecSample, key_between, roll_hash
 
@@ -93,14 +94,43 @@ def test_empty_sample():
     g.poll(1e9)
 
 
-def test_add_batch_without_batch_is_state_error():
-    """No batch resolved yet: fdbcs_sample_add_batch(cs, NULL) has nothing to roll."""
-    with pytest.raises(_abi.FdbcsError):
+def test_add_batch_null_handle_is_arg_error():
+    """fdbcs_sample_add_batch with no conflict set: FDBCS_E_ARG."""
+    with pytest.raises(_abi.FdbcsError) as e:
         IopsSample().add_batch(_NoBatch(), 1.0)
+    assert e.value.status == _abi.E_ARG
 
 
 class _NoBatch:
     handle = None
+
+
+@pytest.mark.gpu
+def test_add_batch_without_resolved_batch_is_state_error(gpu):
+    """fdbcs_sample_add_batch(cs, NULL) rolls the batch the conflict set last
+    resolved through a host path; with none (a fresh set, or after a batch
+    resolved on device memory) it is FDBCS_E_STATE (fdbcs.h)."""
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd.batch import DeviceBatch
+    import torch
+
+    cs = ConflictSet()
+    with pytest.raises(_abi.FdbcsError) as e:
+        IopsSample().add_batch(cs, 1.0)
+    assert e.value.status == _abi.E_STATE
+    wl = Workload(2, txns=200)
+    b, now, nold = wl.batch(0)
+    cs.detect_packed(b, now, nold)
+    s = IopsSample()
+    s.add_batch(cs, 1.0)  # the host batch is there
+    v, now, nold = wl.view(1)
+    db = DeviceBatch(v, torch.device("cuda", 0))
+    out = torch.zeros(v.txn_count, dtype=torch.uint8, device="cuda")
+    cs.detect_device(db.view, now, nold, out.data_ptr(), sync=True)
+    with pytest.raises(_abi.FdbcsError) as e:
+        s.add_batch(cs, 2.0)  # the last resolved batch came from device memory: nothing host-staged to roll
+    assert e.value.status == _abi.E_STATE
+    cs.close()
 
 
 # ---------------------------------------------------------------- GPU
