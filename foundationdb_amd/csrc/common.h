@@ -200,6 +200,8 @@ struct Scalars {
     int32_t ss_maxc;        // stats: largest sort bucket above the register path (0: none)
     int32_t extra_total;    // free pages the merge takes (parts beyond each page's first)
     int32_t n_comb_own;     // combined ranges whose begin lies in this shard (all of them unsharded)
+    int32_t dec_wide;       // rounds mode: the candidate list overflowed (every read is a candidate)
+    int32_t n_pot;          // rounds mode: entries in the candidate read list
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 

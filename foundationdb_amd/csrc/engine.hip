@@ -340,7 +340,8 @@ void free_batch(BatchBufs& b) {
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
-    dfree(b.pair_bits); dfree(b.et); dfree(b.eu); dfree(b.csr);
+    dfree(b.et); dfree(b.eu); dfree(b.csr);
+    dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv);
     dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
@@ -370,14 +371,13 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     hipStream_t s = cs->stream;
     if (T > MAX_T) return FDBCS_E_CAPACITY;  // DESIGN.md §Large batches
     b.large = large_batch_mode(T);
-    b.dedup = !b.large && !cs->sparse_edges;
+    b.rounds = !b.large && !cs->sparse_edges && rounds_fit(T, W);
     if (!b.scan_tmp && (r = dalloc(b.scan_tmp, 1024))) return r;
     if (T > cs->capT) {
         GROWLOG("T %lld\n", (long long)T);
         int64_t n = std::max<int64_t>(T, 1024);
         dfree(b.too_old); dfree(b.hist); dfree(b.committed); dfree(b.verdict); dfree(b.dec_blk);
         dfree(b.deg); dfree(b.off); dfree(b.cur); dfree(b.dep_list); dfree(b.dep_idx); dfree(b.cbits);
-        // +64: k_decide_combine reads these byte arrays as 4-byte words
         if ((r = dalloc(b.too_old, n + 64)) || (r = dalloc(b.hist, n + 64)) || (r = dalloc(b.committed, n)) ||
             (r = dalloc(b.verdict, n)) || (r = dalloc(b.deg, n)) || (r = dalloc(b.off, n + 1)) ||
             (r = dalloc(b.cur, n)) || (r = dalloc(b.dep_list, n)) || (r = dalloc(b.dep_idx, n)) ||
@@ -386,22 +386,10 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             return r;
         cs->capT = n;
     }
-    int64_t need_edges;
-    if (b.dedup) {
-        // dedup matrix: rows of ceil(n/32) words, zero between batches; unique
-        // pairs u < t bound the edge list
-        const int64_t n = std::max<int64_t>(T, 1024);
-        if (n > b.pair_T) {
-            dfree(b.pair_bits);
-            b.row_words = (int32_t)((n + 31) / 32);
-            if ((r = dalloc(b.pair_bits, n * b.row_words))) return r;
-            HIPOK(hipMemsetAsync(b.pair_bits, 0, (size_t)n * b.row_words * 4, s));
-            b.pair_T = n;
-        }
-        need_edges = std::max<int64_t>(1, n * (n - 1) / 2);
-    } else {
-        // undeduplicated edges: a first guess linear in the batch; run_batch
-        // grows the list and re-runs the search if a batch overflows it
+    int64_t need_edges = 1;
+    if (!b.rounds) {
+        // overlap edges (duplicates kept): a first guess linear in the batch;
+        // run_batch grows the list and re-runs the search if a batch overflows it
         const char* test_cap = getenv("FDBCS_TEST_EDGE_CAP");  // (tests: reach the overflow path)
         need_edges = test_cap ? std::max(1, atoi(test_cap)) : std::max<int64_t>(1 << 20, 2 * (R + W));
     }
@@ -409,8 +397,12 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     if (R > cs->capR) {
         GROWLOG("R %lld\n", (long long)R);
         int64_t n = std::max<int64_t>(R, 1024);
-        dfree(b.read_txn); dfree(b.read_snap); dfree(b.rec_r0);
-        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.read_snap, n)) || (r = dalloc(b.rec_r0, n))) return r;
+        dfree(b.read_txn); dfree(b.read_snap); dfree(b.rec_r0); dfree(b.rq); dfree(b.rstamp);
+        if ((r = dalloc(b.read_txn, n)) || (r = dalloc(b.read_snap, n)) || (r = dalloc(b.rec_r0, n)) ||
+            (r = dalloc(b.rq, 2 * n)) || (r = dalloc(b.rstamp, n)))
+            return r;
+        if (hipMemsetAsync(b.rstamp, 0, (size_t)n * 4, cs->stream) != hipSuccess) return FDBCS_E_HIP;
+        b.rseq = 0;
         cs->capR = n;
     }
     if (W > cs->capW) {
@@ -422,7 +414,9 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
         dfree(b.wh.vb);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-        if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_combine
+        dfree(b.wnew); dfree(b.winv);
+        if ((r = dalloc(b.wnew, 2 * n + 64)) || (r = dalloc(b.winv, 2 * n))) return r;
+        if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_rounds
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
             (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.comb_blk, 2 * (n / 2048 + 2))) ||
             (r = alloc_keys(b.rkb, n)) ||
@@ -435,6 +429,17 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.wh.feq, n)) || (r = dalloc(b.wh.vb, n)))
             return r;
         cs->capW = n;
+    }
+    if (++b.rseq == 0) {  // (stamps wrapped: clear them)
+        if (b.rstamp && hipMemsetAsync(b.rstamp, 0, (size_t)cs->capR * 4, cs->stream) != hipSuccess) return FDBCS_E_HIP;
+        b.rseq = 1;
+    }
+    if (R + W > b.list_cap) {
+        const int64_t n = std::max<int64_t>(R + W, 4096);
+        dfree(b.plist); dfree(b.items);
+        b.list_cap = 0;
+        if ((r = dalloc(b.plist, n)) || (r = dalloc(b.items, 2 * n))) return r;
+        b.list_cap = n;
     }
     if (!b.ss_cnt) {
         if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)) ||
@@ -562,7 +567,7 @@ int edges_read_check(fdbcs* cs, const fdbcs_batch_view& v, int64_t v0) {
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s);
-    if (b.dedup) return FDBCS_OK;
+    if (b.rounds) return FDBCS_OK;  // (no overlap pairs: k_decide_rounds)
     int32_t total = 0;
     HIPOK(hipMemcpyAsync(&total, &cs->sc->edges_total, sizeof(total), hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
@@ -1388,7 +1393,7 @@ int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_e
     if (!cs || n < 0 || n > INT32_MAX || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
     cs->edges_known = false;
     BatchBufs& b = cs->b;
-    if (b.dedup) return FDBCS_E_ARG;  // (protocol B only: fdbcs_shard_set_protocol)
+    if (b.rounds) return FDBCS_E_ARG;  // (protocol B only: fdbcs_shard_set_protocol)
     int r;
     if (n > b.edge_cap && (r = grow_edges(b, n + n / 4 + 1024))) return r;
     launch_set_edges(b, cs->sc, (int)cs->last_T, dev_et, dev_eu, n, cs->stream);

@@ -62,13 +62,19 @@ struct BatchBufs {
     int32_t* lb_hist;    // [2 * lb_hist_cap] per-block bucket counts and their scan
     int64_t lb_hist_cap;
     int64_t ss_tmp_cap;
-    // intra-batch overlap dedup matrix and edges
-    uint32_t* pair_bits; // [pair_T * row_words] (small batches only)
-    int32_t row_words;
-    int64_t pair_T;      // rows of pair_bits
-    bool large;          // large-batch mode (large_batch_mode): merge sort, undeduplicated edges
-    bool dedup;          // overlap pairs deduplicated through pair_bits (small batches, own decision)
-    int32_t* et;         // [edge_cap] reader of each unique overlap pair
+    bool large;          // large-batch mode (large_batch_mode): merge sort, overlap edges
+    bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
+    // rounds mode (kernels_batch.hip k_decide_rounds)
+    int32_t* rq;         // [2R] sorted write endpoints <= each read's begin / < its end
+    int32_t* plist;      // [R + W] candidate reads: some write of the batch may overlap them (duplicates)
+    uint8_t* wnew;       // [2W + 64] sorted write endpoint p starts a new distinct key
+    int32_t* winv;       // [2W] sorted position of each write endpoint (by slot - 2R)
+    uint2* items;        // [R + W] the rounds' writes and reads when they do not fit in LDS
+    int64_t list_cap;    // entries of plist (items: 2 * list_cap)
+    uint32_t* rstamp;    // [R] per read: the batch (rseq) that put it on plist
+    uint32_t rseq;
+    // overlap edges (large / sparse batches)
+    int32_t* et;         // [edge_cap] reader of each overlap pair
     int32_t* eu;         // [edge_cap] earlier writer
     int32_t* csr;        // [edge_cap] sources bucketed by reader
     int32_t* comb_blk;   // [2 * (combine blocks + 1)] multi-block combine: per-block sums, opens
@@ -176,8 +182,8 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
 int64_t sort_staging_records(int R, int W, bool large);
 // Large-batch mode (T > LARGE_T, or forced by FDBCS_TEST_LARGE_BATCH for tests):
 // the endpoint sort is a merge sort (no per-batch splitter balance limits)
-// and overlap edges are not deduplicated through the T x T pair matrix, so
-// memory stays linear in the batch.  Up to MAX_T transactions.
+// and the decision walks the overlap edges on the grid (k_dec_*) instead of
+// one workgroup's rounds (k_decide_rounds).  Up to MAX_T transactions.
 constexpr int64_t LARGE_T = 65536;
 constexpr int64_t MAX_T = 1310720;  // k_dec_walk keeps a committed bit per txn in LDS (160 KiB)
 bool large_batch_mode(int64_t T);
@@ -187,6 +193,8 @@ int64_t lb_hist_words(int R, int W);
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s);
 void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
+// k_decide_rounds keeps its state in LDS: batches up to this shape
+bool rounds_fit(int64_t T, int64_t W);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);
 // exact sharded mode: per-transaction exchange flags (0 / 1 history conflict /
 // 2 tooOld) out of and back into the batch state; a foreign edge list in

@@ -1205,15 +1205,16 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
 }
 
 // --------------------------------------------------------------- edges ----
+// Large and sparse (sharded protocol B) batches list the overlap pairs.
 // A read r of t and a write w of u overlap iff r.b < w.e && w.b < r.e.
 // Split on which begin comes first (keys only, no ranks):
 //   w.b >= r.b : the write begins among the sorted write endpoints with key in
 //                [r.b, r.e)                                       (by reader)
 //   w.b <  r.b : the read begins with key in (w.b, w.e)           (by writer)
 // Only pairs u < t where both are still undecided (not tooOld, no history
-// conflict) matter.  A T x T bit matrix dedups pairs; each new pair is
-// appended to (et, eu) through one global counter.  The decision kernel
-// clears the bits it consumes, leaving the matrix zero for the next batch.
+// conflict) matter; each is appended to (et, eu) through one global counter
+// (duplicates kept).  Other batches only search each read's position among
+// the sorted write endpoints (rounds_lane) for k_decide_rounds.
 __device__ inline int lb_key(const SRec* a, int n, const Key& k, const uint8_t* const* tails) {
     int lo = 0, hi = n;
     while (lo < hi) {
@@ -1233,21 +1234,14 @@ __device__ inline int ub_key(const SRec* a, int n, const Key& k, const uint8_t* 
     return lo;
 }
 
-__device__ inline void edge_pair(int t, int u, uint32_t* bits, int row_words, int32_t* et, int32_t* eu,
-                                 int64_t cap, Scalars* sc, int32_t* deg) {
-    bool fresh = true;
-    if (bits) {  // small batches: dedup through the pair matrix (large batches keep duplicates, which are harmless)
-        uint32_t* word = bits + (int64_t)t * row_words + (u >> 5);
-        const uint32_t bit = 1u << (u & 31);
-        fresh = !(atomicOr(word, bit) & bit);
-    }
-    if (fresh) {
-        atomicAdd(&deg[t], 1);  // (sources per reader, for the grid decision; zeroed by the ingest)
-        const int idx = atomicAdd(&sc->edges_total, 1);
-        if (idx < cap) {
-            et[idx] = t;
-            eu[idx] = u;
-        }
+// an overlap pair (reader t, earlier writer u); duplicates are kept (they
+// only repeat a source in the decision's CSR)
+__device__ inline void edge_pair(int t, int u, int32_t* et, int32_t* eu, int64_t cap, Scalars* sc, int32_t* deg) {
+    atomicAdd(&deg[t], 1);  // (sources per reader, for the grid decision; zeroed by the ingest)
+    const int idx = atomicAdd(&sc->edges_total, 1);
+    if (idx < cap) {
+        et[idx] = t;
+        eu[idx] = u;
     }
 }
 
@@ -1309,13 +1303,21 @@ struct EdgesArgs {
     const int32_t* read_txn;
     const int32_t* write_txn;
     const uint8_t* too_old;
-    uint32_t* bits;
-    int row_words;
     int32_t* et;
     int32_t* eu;
     int64_t cap;
     Scalars* sc;
     int32_t* deg;
+    // rounds mode (k_decide_rounds): no pairs; per read the sorted write
+    // endpoints at or below its begin / below its end, per sorted write
+    // endpoint whether its key differs from the previous one's
+    int32_t* rq;     // [2R] or null (edges mode)
+    uint8_t* wnew;   // [2W]
+    int32_t* plist;  // candidate reads (appended at sc->n_pot; duplicates allowed)
+    int64_t plist_cap;
+    int32_t* winv;   // [2W] sorted position of each write endpoint
+    uint32_t* rstamp;  // [R] batch stamp of reads already on plist
+    uint32_t rseq;     // this batch's stamp
 };
 
 // The two searches of an edge lane: an LDS sample of the sorted array's first
@@ -1375,10 +1377,77 @@ __device__ inline void bsearch2(const SRec* a, const Key& k1, bool strict1, int 
     r2 = lo2;
 }
 
+__device__ inline bool rec_key_eq(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    if (a.hi != b.hi || a.lo != b.lo || a.meta != b.meta) return false;
+    return key_len(a.meta) <= 17 || tail_cmp(tails[a.idx], key_len(a.meta), tails[b.idx], key_len(b.meta)) == 0;
+}
+
+// rounds mode, three kinds of lanes:
+//   i < R        read i: pb = sorted write endpoints with key <= its begin (at
+//                an equal key both write endpoint types sort before a read
+//                begin, SkipList.cpp:169-172), pe = those with key < its end
+//                (a read end sorts first); a candidate if some write endpoint
+//                has a key in [begin, end) -- every overlap where the write
+//                begins at or after the read does
+//   R + p        sorted write endpoint p starts a new distinct key
+//   R + 2W + w   write w: the reads beginning strictly inside it (the other
+//                overlaps) become candidates; past RP_MARK of them, every
+//                read is one (dec_wide)
+constexpr int RP_MARK = 64;
+
+__device__ inline void candidate(const EdgesArgs& A, int r) {
+    // once per read and batch (a read inside many writes is marked by each;
+    // a race between two markers only lets a duplicate through)
+    if (A.rstamp[r] == A.rseq) return;
+    A.rstamp[r] = A.rseq;
+    const int j = atomicAdd(&A.sc->n_pot, 1);
+    if (j < A.plist_cap) A.plist[j] = r;
+    else A.sc->dec_wide = 1;  // (overflow: every read is a candidate)
+}
+
+__device__ inline void rounds_lane(const EdgesArgs& A, int i, const uint64_t* smp_r, const uint64_t* smp_w) {
+    const int R = A.R, W = A.W, P = 2 * A.W;
+    const uint8_t* const* tails = A.keys.tail;
+    if (i < R) {
+        if (A.too_old[A.read_txn[i]]) return;  // (not decided by the rounds)
+        const Key b = A.keys.get(2 * (int64_t)i), e = A.keys.get(2 * (int64_t)i + 1);
+        int lb, hb, le, he, pb, pe;
+        sample_narrow(smp_w, P, b.hi, lb, hb);
+        sample_narrow(smp_w, P, e.hi, le, he);
+        bsearch2(A.sw, b, true, lb, hb, e, le, he, tails, pb, pe);
+        A.rq[2 * i] = pb;
+        A.rq[2 * i + 1] = pe;
+        if (pe > pb || (pb > 0 && rec_vs_key(A.sw[pb - 1], b, tails) == 0)) candidate(A, i);
+    } else if (i < R + P) {
+        const int p = i - R;
+        const SRec x = A.sw[p];
+        A.wnew[p] = p == 0 || !rec_key_eq(A.sw[p - 1], x, tails);
+        A.winv[x.idx - 2 * (int64_t)R] = p;
+    } else if (i < R + P + W) {
+        const int w = i - R - P;
+        if (A.too_old[A.write_txn[w]] || R == 0) return;
+        const int64_t s = 2 * (int64_t)R + 2 * (int64_t)w;
+        const Key b = A.keys.get(s), e = A.keys.get(s + 1);
+        int lb, hb, le, he, k0, k1;
+        sample_narrow(smp_r, R, b.hi, lb, hb);
+        sample_narrow(smp_r, R, e.hi, le, he);
+        bsearch2(A.sr, b, true, lb, hb, e, le, he, tails, k0, k1);  // read begins in (b, e)
+        if (k1 - k0 > RP_MARK) {
+            A.sc->dec_wide = 1;
+        } else {
+            for (int k = k0; k < k1; k++) candidate(A, A.sr[k].idx >> 1);
+        }
+    }
+}
+
 __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp_r, const uint64_t* smp_w) {
     const int R = A.R, W = A.W;
     const int64_t wbase = 2 * (int64_t)R;
     const uint8_t* const* tails = A.keys.tail;
+    if (A.rq) {
+        rounds_lane(A, i, smp_r, smp_w);
+        return;
+    }
     if (i < R) {
         const int t = A.read_txn[i];
         if (A.too_old[t]) return;
@@ -1391,7 +1460,7 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
             const uint32_t slot = A.sw[k].idx;
             if (slot & 1) continue;  // a write end
             const int u = A.write_txn[(slot - wbase) >> 1];
-            if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+            if (u < t && !A.too_old[u]) edge_pair(t, u, A.et, A.eu, A.cap, A.sc, A.deg);
         }
     } else if (i < R + W) {
         const int w = i - R;
@@ -1404,7 +1473,7 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
         bsearch2(A.sr, b, true, lb, hb, e, le, he, tails, lo, hi);
         for (int k = lo; k < hi; k++) {
             const int t = A.read_txn[A.sr[k].idx >> 1];
-            if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+            if (t > u && !A.too_old[t]) edge_pair(t, u, A.et, A.eu, A.cap, A.sc, A.deg);
         }
     }
 }
@@ -1593,7 +1662,7 @@ __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
                 if (rec_vs_key(x, e, tails) >= 0) break;
                 if (x.idx & 1) continue;  // a write end
                 const int u = A.write_txn[(x.idx - wbase) >> 1];
-                if (u < t && !A.too_old[u]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+                if (u < t && !A.too_old[u]) edge_pair(t, u, A.et, A.eu, A.cap, A.sc, A.deg);
             }
         } else {
             const int j = b0 + ib++;
@@ -1609,7 +1678,7 @@ __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
                 const SRec x = sr[k];
                 if (rec_vs_key(x, e, tails) >= 0) break;
                 const int t = A.read_txn[x.idx >> 1];
-                if (t > u && !A.too_old[t]) edge_pair(t, u, A.bits, A.row_words, A.et, A.eu, A.cap, A.sc, A.deg);
+                if (t > u && !A.too_old[t]) edge_pair(t, u, A.et, A.eu, A.cap, A.sc, A.deg);
             }
         }
     }
@@ -1630,14 +1699,14 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     }
     const int32_t* qx = dj ? b.ss_bkt : nullptr;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
-    EdgesArgs EA{R, W, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.dedup ? b.pair_bits : nullptr, b.row_words, b.et, b.eu, b.edge_cap, sc, b.deg};
+    EdgesArgs EA{R,     W,    b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
+                 b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv, b.rstamp, b.rseq};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
     const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
-    const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + W, 256) : 0;
+    const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
     if (rc_blocks + ws_blocks + e_blocks > 0)
         hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks,
                            WA, ws_blocks, EA);
@@ -1646,167 +1715,317 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
                            EA);
 }
 
-// ------------------------------------------------------ decide + combine ----
-// One workgroup; every thread owns a contiguous chunk of transactions (and
-// later of sorted endpoints), so each phase issues its global loads together
-// and needs a single workgroup scan.
+// ------------------------------------------ decide by rounds + combine ----
+// checkIntraBatchConflicts (SkipList.cpp:1133-1153) without enumerating
+// (reader, earlier writer) pairs, then combineWriteConflictRanges
+// (:1320-1337); one workgroup, its state in LDS.
 //
-// Decision (checkIntraBatchConflicts, SkipList.cpp:1133-1153):
-//   conflict[t] = tooOld[t] || hist[t] || some source u < t committed,
-// where the sources of t are the unique (t, u) edges.  Edges are bucketed by
-// reader into CSR.  Txns without sources are decided in parallel;
-// dependents are walked in index order in chunks of 64 by one wavefront:
-// each lane folds in its sources from earlier chunks (final), then the
-// chunk's 64x64 lower-triangular dependency masks are resolved by a Jacobi
-// iteration on ballots, which reaches the unique solution of the recurrence
-// in at most depth+1 rounds.
+// The decision: U = transactions neither tooOld nor conflicting with the
+// history.  t in U commits iff no read of t overlaps a write of a committed
+// u < t.  Write C(t) for that predicate given a candidate committed set C;
+// the committed set is the unique fixed point C* = {t in U : C*(t)} (unique
+// by induction on the index).  Jacobi from C_0 = U: C_{k+1} = {t in U :
+// C_k(t)} -- even iterates contain C*, odd ones are contained in it, and
+// transaction t is final after at most t + 1 rounds -- stops at C_{k+1} =
+// C_k, which is C*.  Config 3 (Zipf) converges in ~8 rounds.  Only candidate
+// reads (k_edges_read_check marked those a write of the batch may overlap)
+// are evaluated; with none (config 2, uniform keys) there is no round.
 //
-// Combine (combineWriteConflictRanges, SkipList.cpp:1320-1337): over the
-// sorted write endpoints (END before BEGIN at equal keys), a counter of open
-// committed writes; a combined range starts at a committed BEGIN seen with the
-// counter at 0 and ends at the committed END that brings it back to 0.
-struct DecideArgs {
+// A round without pairs.  Key positions are ranks among the DISTINCT keys of
+// the sorted write endpoints: write w = [B, E), B < E its begin / end ranks;
+// read r = (Gb, Ge), Gb = distinct keys <= its begin, Ge = distinct keys <
+// its end.  [rb, re) overlaps [wb, we) (rb < we and wb < re, the half-open
+// overlap the reference's tie order encodes) iff B < Ge and Gb <= E: (a) Gb
+// <= B < Ge, the write begins inside the read, or (b) B < Gb <= E, the read
+// begins inside the write.  Per round each write of a candidate u takes the
+// min at val[B] and paints stab over (B, E] (min); a read of t conflicts iff
+// min(val[Gb, Ge)) < t or stab[Gb] < t.  A hot key is one rank, so a round
+// costs O(candidate reads + writes of U) LDS operations whatever the fan-in
+// (the pair list it replaces held ~10^6 pairs per Zipf batch).  val and stab
+// are 16-bit (transaction indices and ranks < 65535, rounds_fit); long
+// paints and range queries go through block minima of RB1 and RB2 ranks.
+//
+// Combine: over the sorted write endpoints (END before BEGIN at equal keys),
+// a counter of open committed writes; a combined range starts at a committed
+// BEGIN seen with the counter at 0 and ends at the committed END that brings
+// it back to 0.
+struct RoundArgs {
     int T, R, W;
-    int combine;           // 0: the multi-block combine kernels follow (large batches)
+    int combine;              // 0: the multi-block combine kernels follow
+    int lcap;                 // items that fit in LDS (else A.items)
     const uint8_t* too_old;
     const uint8_t* hist;
-    const int32_t* et;
-    const int32_t* eu;
-    uint32_t* bits;
-    int row_words;
-    int64_t edge_cap;
-    int32_t* g_deg;        // [T] global fallback storage (T > LDS_T)
-    int32_t* g_off;        // [T+1]
-    int32_t* g_idx;        // [T]
-    int32_t* csr;          // [E]
-    int32_t* dep_list;     // [T]
+    const int32_t* read_txn;
+    const int32_t* write_txn;
+    const int32_t* rq;        // [2R] (k_edges_read_check, rounds mode)
+    const int32_t* plist;     // candidate reads, sc->n_pot of them
+    const uint8_t* wnew;      // [2W]
+    const int32_t* winv;      // [2W]
+    const uint32_t* sw_slot;  // [2W] slots of the sorted write endpoints
+    int64_t lcap_list;        // plist entries (past it: dec_wide)
+    uint2* items;             // [2 * lcap_list] global fallback of the item list
     uint8_t* committed;
     uint8_t* verdict;
-    const uint32_t* sw_slot;  // slots of the sorted write endpoints [2W]
-    const int32_t* write_txn;
-    int32_t* cb_slot;      // combined range begins / ends, as key slots
+    int32_t* cb_slot;         // combined range begins / ends, as key slots
     int32_t* ce_slot;
     Scalars* sc;
 };
 
 static constexpr int DC_THREADS = 1024;
-static constexpr int LDS_T = 8192;  // T up to which deg/off/idx live in LDS
-static constexpr int CPMAX = 32;    // sorted endpoints per thread kept in registers
+static constexpr int CPMAX = 32;  // sorted endpoints per thread kept in registers (combine)
+static constexpr int RB1 = 64, RB2 = 4096;
+static constexpr uint16_t INF16 = 0xFFFF;
+static constexpr size_t ROUNDS_LDS_MAX = 156 * 1024;
+// Items are taken DG per lane at a time (item i + k * nthr), their loads
+// issued together: one workgroup is latency-bound on its global inputs.
+constexpr int DG = 8;
 
-__global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
+__device__ __host__ inline int64_t rank_words16(int64_t P) {  // val + stab + their block minima, in u16
+    const int64_t n = P + 3;
+    return 2 * (n + n / RB1 + 3 + n / RB2 + 3);
+}
+
+__host__ __device__ inline size_t rounds_lds_base(int64_t T, int64_t W) {
+    const int64_t P = 2 * W;
+    const int64_t bits = 3 * ((T + 31) / 32) + (W + 31) / 32;
+    return (size_t)(4 * bits + 2 * rank_words16(P) + 64);
+}
+
+bool rounds_fit(int64_t T, int64_t W) {
+    return T < INF16 && 2 * W + 2 < INF16 && 2 * W <= CPMAX * DC_THREADS &&
+           rounds_lds_base(T, W) + 8 * 1024 <= ROUNDS_LDS_MAX;
+}
+
+// 16-bit min in LDS (no ds_min_u16 on gfx950): CAS on the containing word,
+// skipped when the value there is already lower.  arr is 4-byte aligned.
+__device__ inline void lds_min16(uint16_t* arr, int idx, uint16_t v) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(arr) + (idx >> 1);
+    const int sh = (idx & 1) * 16;
+    uint32_t old = *w;
+    while (((old >> sh) & 0xFFFFu) > v) {
+        const uint32_t nw = (old & ~(0xFFFFu << sh)) | ((uint32_t)v << sh);
+        const uint32_t prev = atomicCAS(w, old, nw);
+        if (prev == old) break;
+        old = prev;
+    }
+}
+
+// f over positions [a, b): per position below RB1 / RB2 boundaries, per
+// block of RB1 / RB2 positions inside them
+template <typename F1, typename F2, typename F3>
+__device__ inline void blocks_of(int a, int b, F1 pos, F2 blk1, F3 blk2) {
+    while (a < b && (a & (RB1 - 1))) pos(a++);
+    while (a + RB1 <= b && (a & (RB2 - 1))) {
+        blk1(a / RB1);
+        a += RB1;
+    }
+    while (a + RB2 <= b) {
+        blk2(a / RB2);
+        a += RB2;
+    }
+    while (a + RB1 <= b) {
+        blk1(a / RB1);
+        a += RB1;
+    }
+    while (a < b) pos(a++);
+}
+
+__device__ inline bool bit_of(const uint32_t* bits, int t) { return (bits[t >> 5] >> (t & 31)) & 1; }
+
+__global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ int64_t red64[DC_THREADS / 64 + 1];
     __shared__ int32_t red32[DC_THREADS / 64 + 1];
-    const int T = A.T, W = A.W, P = 2 * A.W;
+    __shared__ int32_t s_nw, s_nr;
+    const int T = A.T, R = A.R, W = A.W, P = 2 * A.W;
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int nwords = (T + 31) >> 5, wwords = (W + 31) >> 5;
-    uint32_t* cbits = lds;            // committed, per txn
-    uint32_t* cwb = lds + nwords;     // committed, per write
-    uint32_t* rest = cwb + wwords;
-    const bool small = T <= LDS_T;
-    int32_t* deg = small ? (int32_t*)rest : A.g_deg;
-    int32_t* off = small ? deg + T : A.g_off;
-    int32_t* didx = small ? off + T + 1 : A.g_idx;
+    uint32_t* ubits = lds;              // U
+    uint32_t* cbits = lds + nwords;     // the candidate committed set; C* at the end
+    uint32_t* nbits = cbits + nwords;   // conflicts found this round
+    uint32_t* cwb = nbits + nwords;     // committed, per write (combine)
+    uint16_t* r16 = reinterpret_cast<uint16_t*>(cwb + wwords);  // ranks: P u16 first, then val / stab
+    uint2* litems = reinterpret_cast<uint2*>(r16 + ((rank_words16(P) + 3) & ~3));  // lcap items
     Scalars* sc = A.sc;
-    const int E = (int)min((int64_t)sc->edges_total, A.edge_cap);
+    const int64_t wbase = 2 * (int64_t)R;
+    int ncand = 0;
     PHASE(sc, 0);
 
-    for (int i = tid; i < nwords; i += nthr) cbits[i] = 0;
-    for (int t = tid; t < T; t += nthr) deg[t] = 0;
+    // ---- U: 4 transactions per lane from one 4-byte load of each flag array ----
+    for (int i = tid; i < nwords; i += nthr) nbits[i] = 0;
+    if (tid == 0) s_nw = s_nr = 0;
+    const bool wide = sc->dec_wide != 0;
+    const int npot = wide ? R : (int)min((int64_t)sc->n_pot, A.lcap_list);
     __syncthreads();
-    for (int e = tid; e < E; e += nthr) atomicAdd(&deg[A.et[e]], 1);
-    __syncthreads();
-    PHASE(sc, 1);
-
-    // ---- per-thread chunk of transactions: [t0, t1), CH a multiple of 4 ----
-    const int CH = (((T + nthr - 1) / nthr) + 3) & ~3;
-    const int t0 = min(T, tid * CH), t1 = min(T, t0 + CH);
-    uint64_t und = 0;  // bit k: txn t0+k undecided (not tooOld, no history conflict)
-    for (int t = t0; t < t1; t += 4) {
-        const uint32_t to = *reinterpret_cast<const uint32_t*>(A.too_old + t);
-        const uint32_t hs = *reinterpret_cast<const uint32_t*>(A.hist + t);
-        const uint32_t bad = to | hs;
+    for (int t4 = tid; 4 * t4 < T; t4 += nthr) {
+        const uint32_t to = reinterpret_cast<const uint32_t*>(A.too_old)[t4];
+        const uint32_t hs = reinterpret_cast<const uint32_t*>(A.hist)[t4];
+        uint32_t m = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (t + k < t1 && !((bad >> (8 * k)) & 0xFF)) und |= 1ull << (t + k - t0);
+        for (int k = 0; k < 4; k++) m |= (uint32_t)(4 * t4 + k < T && !(((to | hs) >> (8 * k)) & 0xFF)) << k;
+        if (m) atomicOr(&nbits[t4 >> 3], m << (4 * (t4 & 7)));
     }
-    int ndep_l = 0, e_l = 0;
-    for (int t = t0; t < t1; t++) {
-        const int d = deg[t];
-        const bool u = (und >> (t - t0)) & 1;
-        ndep_l += u && d > 0;
-        e_l += d;
-        if (u && d == 0) atomicOr(&cbits[t >> 5], 1u << (t & 31));
+    __syncthreads();
+    for (int i = tid; i < nwords; i += nthr) {
+        ubits[i] = cbits[i] = nbits[i];
+        nbits[i] = 0;
     }
-    int64_t tot64;
-    const int64_t ex64 = block_excl_scan(((int64_t)ndep_l << 32) | (uint32_t)e_l, red64, tot64);
-    int nd = (int)(ex64 >> 32), eo = (int)(uint32_t)ex64;
-    const int ndep = (int)(tot64 >> 32);
+    __syncthreads();
+    if (npot == 0) goto decided;  // no read can meet a write of the batch: C* = U
     PHASE(sc, 2);
-    for (int t = t0; t < t1; t++) {
-        const int d = deg[t];
-        const bool dep = ((und >> (t - t0)) & 1) && d > 0;
-        off[t] = eo;
-        didx[t] = dep ? nd : -1;
-        if (dep) A.dep_list[nd++] = t;
-        eo += d;
-        deg[t] = 0;  // reused as fill cursors
-    }
-    if (tid == nthr - 1) off[T] = (int)(uint32_t)tot64;
-    __syncthreads();
-    PHASE(sc, 3);
-    for (int e = tid; e < E; e += nthr) {
-        const int t = A.et[e], u = A.eu[e];
-        A.csr[off[t] + atomicAdd(&deg[t], 1)] = u;
-        A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
-    }
-    __syncthreads();
-    PHASE(sc, 4);
-    int iters = 0;
-    if (tid < 64) {
-        const int lane = tid;
-        for (int c0 = 0; c0 < ndep; c0 += 64) {
-            const int k = c0 + lane;
-            const bool valid = k < ndep;
-            const int t = valid ? A.dep_list[k] : 0;
-            bool ext = false;
-            uint64_t L = 0;
-            if (valid) {
-                for (int e = off[t], e1 = off[t + 1]; e < e1 && !ext; e++) {
-                    const int u = A.csr[e];
-                    const int di = didx[u];
-                    if (di >= c0) L |= 1ull << (di - c0);
-                    else ext = (cbits[u >> 5] >> (u & 31)) & 1;
+    {
+        // ---- distinct ranks of the sorted write endpoints (u16, LDS) ----
+        const int CH = ((P + nthr - 1) / nthr + 3) & ~3;
+        const int p0 = min(P, tid * CH), p1 = min(P, p0 + CH);
+        uint32_t fl[CPMAX / 4 + 1];
+        int nnew = 0;
+#pragma unroll
+        for (int k = 0; k < CPMAX / 4 + 1; k++) {
+            fl[k] = p0 + 4 * k < p1 ? reinterpret_cast<const uint32_t*>(A.wnew)[(p0 >> 2) + k] : 0;
+            nnew += __popc(fl[k] & 0x01010101u & (p0 + 4 * k + 4 <= p1 ? ~0u : (1u << (8 * (p1 - p0 - 4 * k))) - 1));
+        }
+        int tot;
+        int d = block_excl_scan(nnew, red32, tot) - 1;  // (its barriers also publish U)
+        for (int p = p0; p < p1; p++) {
+            d += (fl[(p - p0) >> 2] >> (8 * ((p - p0) & 3))) & 1;
+            r16[p] = (uint16_t)d;
+        }
+        __syncthreads();
+        // the item list: writes of U (B | E << 16, u), then candidate reads of U (Gb | Ge << 16, t)
+        for (int w0 = tid; w0 < W; w0 += DG * nthr) {
+            int u[DG], pb[DG], pe[DG];
+#pragma unroll
+            for (int k = 0; k < DG; k++) u[k] = w0 + k * nthr < W ? A.write_txn[w0 + k * nthr] : -1;
+#pragma unroll
+            for (int k = 0; k < DG; k++) {
+                const int w = w0 + k * nthr;
+                if (u[k] >= 0 && bit_of(ubits, u[k])) {
+                    pb[k] = A.winv[2 * w];
+                    pe[k] = A.winv[2 * w + 1];
+                } else {
+                    u[k] = -1;
                 }
             }
-            const uint64_t vm = __ballot(valid);
-            const uint64_t em = __ballot(valid && ext);
-            uint64_t cm = vm & ~em;
-            while (true) {
-                const bool ci = valid && !ext && (L & cm) == 0;
-                const uint64_t nm = __ballot(ci);
-                iters++;
-                if (nm == cm) break;
-                cm = nm;
+#pragma unroll
+            for (int k = 0; k < DG; k++) {
+                if (u[k] < 0) continue;
+                const int j = atomicAdd(&s_nw, 1);
+                const uint2 it{(uint32_t)r16[pb[k]] | ((uint32_t)r16[pe[k]] << 16), (uint32_t)u[k]};
+                if (j < A.lcap) litems[j] = it;
+                else A.items[j] = it;
             }
-            if (valid && ((cm >> lane) & 1)) atomicOr(&cbits[t >> 5], 1u << (t & 31));
         }
+        __syncthreads();
+        const int nw = s_nw;
+        for (int i0 = tid; i0 < npot; i0 += DG * nthr) {
+            int r[DG], t[DG], pb[DG], pe[DG];
+#pragma unroll
+            for (int k = 0; k < DG; k++) r[k] = i0 + k * nthr < npot ? (wide ? i0 + k * nthr : A.plist[i0 + k * nthr]) : -1;
+#pragma unroll
+            for (int k = 0; k < DG; k++) r[k] = r[k] < R ? r[k] : -1;
+#pragma unroll
+            for (int k = 0; k < DG; k++) t[k] = r[k] >= 0 ? A.read_txn[r[k]] : -1;
+#pragma unroll
+            for (int k = 0; k < DG; k++) {
+                if (t[k] >= 0 && bit_of(ubits, t[k]) && !A.too_old[t[k]]) {
+                    pb[k] = A.rq[2 * r[k]];
+                    pe[k] = A.rq[2 * r[k] + 1];
+                } else {
+                    t[k] = -1;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < DG; k++) {
+                if (t[k] < 0) continue;
+                const int j = nw + atomicAdd(&s_nr, 1);
+                const uint32_t gb = pb[k] > 0 ? r16[pb[k] - 1] + 1u : 0u, ge = pe[k] > 0 ? r16[pe[k] - 1] + 1u : 0u;
+                const uint2 it{gb | (ge << 16), (uint32_t)t[k]};
+                if (j < A.lcap) litems[j] = it;
+                else A.items[j] = it;
+            }
+        }
+        __syncthreads();
+        ncand = s_nr;
+        PHASE(sc, 3);
     }
-    __syncthreads();
+    {
+        // ---- rounds: val / stab over the distinct ranks, in LDS ----
+        const int ND = P + 1;  // ranks a read can ask for: 0 .. (distinct keys) <= P
+        const int n1 = ND / RB1 + 1, n2 = ND / RB2 + 1;
+        auto ev = [](int n) { return (n + 1) & ~1; };  // (every array 4-byte aligned: lds_min16)
+        uint16_t* val = r16;
+        uint16_t* vb1 = val + ev(ND + 1);
+        uint16_t* vb2 = vb1 + ev(n1 + 1);
+        uint16_t* stab = vb2 + ev(n2 + 1);
+        uint16_t* st1 = stab + ev(ND + 1);
+        uint16_t* st2 = st1 + ev(n1 + 1);
+        const int nwords16 = (int)(st2 + ev(n2 + 1) - val);
+        const int nw = s_nw, ni = s_nw + s_nr;
+        const int lcap = A.lcap;
+        auto item = [&](int j) { return j < lcap ? litems[j] : A.items[j]; };  // (past lcap: global)
+        int rounds = 0;
+        for (;;) {
+            rounds++;
+            for (int i = tid; 2 * i < nwords16; i += nthr) reinterpret_cast<uint32_t*>(val)[i] = 0xFFFFFFFFu;
+            __syncthreads();
+            for (int j = tid; j < nw; j += nthr) {  // writes of the candidates
+                const uint2 it = item(j);
+                const int u = (int)it.y;
+                if (!bit_of(cbits, u)) continue;
+                const int B = it.x & 0xFFFF, E = it.x >> 16;
+                lds_min16(val, B, (uint16_t)u);
+                blocks_of(B + 1, E + 1, [&](int q) { lds_min16(stab, q, (uint16_t)u); },
+                          [&](int q) { lds_min16(st1, q, (uint16_t)u); }, [&](int q) { lds_min16(st2, q, (uint16_t)u); });
+            }
+            __syncthreads();
+            for (int j = tid; j < n1; j += nthr) {  // block minima of val
+                uint16_t m = INF16;
+                for (int q = j * RB1; q < min(ND, (j + 1) * RB1); q++) m = min(m, val[q]);
+                vb1[j] = m;
+            }
+            __syncthreads();
+            for (int j = tid; j < n2; j += nthr) {
+                uint16_t m = INF16;
+                for (int q = j * (RB2 / RB1); q < min(n1, (j + 1) * (RB2 / RB1)); q++) m = min(m, vb1[q]);
+                vb2[j] = m;
+            }
+            __syncthreads();
+            for (int j = nw + tid; j < ni; j += nthr) {  // candidate reads
+                const uint2 it = item(j);
+                const int t = (int)it.y;
+                if (bit_of(nbits, t)) continue;
+                const int gb = it.x & 0xFFFF, ge = it.x >> 16;
+                uint16_t m = min(stab[gb], min(st1[gb / RB1], st2[gb / RB2]));
+                blocks_of(gb, ge, [&](int q) { m = min(m, val[q]); }, [&](int q) { m = min(m, vb1[q]); },
+                          [&](int q) { m = min(m, vb2[q]); });
+                if (m < t) atomicOr(&nbits[t >> 5], 1u << (t & 31));  // a committed u < t
+            }
+            __syncthreads();
+            bool changed = false;
+            for (int i = tid; i < nwords; i += nthr) {
+                const uint32_t c = ubits[i] & ~nbits[i];
+                changed |= c != cbits[i];
+                cbits[i] = c;
+                nbits[i] = 0;
+            }
+            if (!__syncthreads_or(changed)) break;
+        }
+        if (tid == 0) sc->jac_iters = rounds;
+    }
+decided:
     PHASE(sc, 5);
-    for (int t = t0; t < t1; t++) {
+    for (int t = tid; t < T; t += nthr) {
         const bool c = (cbits[t >> 5] >> (t & 31)) & 1;
         A.committed[t] = c;
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
-    if (!A.combine) {  // (committed[] is read by the multi-block combine)
-        if (tid == 0) {
-            sc->n_dep = ndep;
-            sc->jac_iters = iters;
-            sc->edges_total = 0;
-        }
-        return;
+    if (tid == 0) {
+        sc->n_dep = ncand;  // candidate reads of U (stats)
+        if (ncand == 0) sc->jac_iters = 0;
+        sc->dec_wide = 0;
+        sc->n_pot = 0;
+        sc->edges_total = 0;
     }
+    if (!A.combine) return;  // (committed[] is read by the multi-block combine)
     // ---- combine ----
     // committed flag per write, 32 writes per thread-word
     for (int i = tid; i < wwords; i += nthr) {
@@ -1830,76 +2049,42 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_combine(DecideArgs A) {
     }
     __syncthreads();
     PHASE(sc, 6);
-    const int64_t wbase = 2 * (int64_t)A.R;
     const int CP = (P + nthr - 1) / nthr;
-    const int p0 = min(P, tid * CP), p1 = min(P, p0 + CP);
+    const int q0 = min(P, tid * CP), q1 = min(P, q0 + CP);
     int gtot;
-    if (CP <= CPMAX) {
-        // this thread's endpoints live in registers for all three passes
-        uint32_t slot[CPMAX];
-        int8_t d[CPMAX];
+    // this thread's endpoints live in registers for all three passes (2W <= CPMAX * DC_THREADS)
+    uint32_t slot[CPMAX];
+    int8_t dd[CPMAX];
 #pragma unroll
-        for (int k = 0; k < CPMAX; k++) slot[k] = p0 + k < p1 ? A.sw_slot[p0 + k] : 0;
-        int dsum = 0;
+    for (int k = 0; k < CPMAX; k++) slot[k] = q0 + k < q1 ? A.sw_slot[q0 + k] : 0;
+    int dsum = 0;
 #pragma unroll
-        for (int k = 0; k < CPMAX; k++) {
-            const int w = (int)((slot[k] - wbase) >> 1);
-            const bool com = p0 + k < p1 && ((cwb[w >> 5] >> (w & 31)) & 1);
-            d[k] = com ? ((slot[k] & 1) ? -1 : 1) : 0;
-            dsum += d[k];
-        }
-        PHASE(sc, 7);
-        int dtot;
-        const int cnt0 = block_excl_scan(dsum, red32, dtot);
-        int ns = 0, c2 = cnt0;
+    for (int k = 0; k < CPMAX; k++) {
+        const int w = (int)((slot[k] - wbase) >> 1);
+        const bool com = q0 + k < q1 && ((cwb[w >> 5] >> (w & 31)) & 1);
+        dd[k] = com ? ((slot[k] & 1) ? -1 : 1) : 0;
+        dsum += dd[k];
+    }
+    PHASE(sc, 7);
+    int dtot;
+    const int cnt0 = block_excl_scan(dsum, red32, dtot);
+    int ns = 0, c2 = cnt0;
 #pragma unroll
-        for (int k = 0; k < CPMAX; k++) {
-            ns += d[k] == 1 && c2 == 0;  // counter 0 -> 1: a combined range opens
-            c2 += d[k];
-        }
-        PHASE(sc, 8);
-        int g = block_excl_scan(ns, red32, gtot);
-        c2 = cnt0;
+    for (int k = 0; k < CPMAX; k++) {
+        ns += dd[k] == 1 && c2 == 0;  // counter 0 -> 1: a combined range opens
+        c2 += dd[k];
+    }
+    PHASE(sc, 8);
+    int g = block_excl_scan(ns, red32, gtot);
+    c2 = cnt0;
 #pragma unroll
-        for (int k = 0; k < CPMAX; k++) {
-            if (d[k] == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot[k];
-            if (d[k] == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // counter 1 -> 0: it closes
-            c2 += d[k];
-        }
-    } else {
-        auto dval = [&](int p, uint32_t& slot) -> int {
-            slot = A.sw_slot[p];
-            const int w = (int)((slot - wbase) >> 1);
-            if (!((cwb[w >> 5] >> (w & 31)) & 1)) return 0;
-            return (slot & 1) ? -1 : 1;
-        };
-        int dsum = 0;
-        uint32_t slot;
-        for (int p = p0; p < p1; p++) dsum += dval(p, slot);
-        int dtot;
-        const int cnt0 = block_excl_scan(dsum, red32, dtot);
-        int ns = 0, c2 = cnt0;
-        for (int p = p0; p < p1; p++) {
-            const int dd = dval(p, slot);
-            ns += dd == 1 && c2 == 0;
-            c2 += dd;
-        }
-        int g = block_excl_scan(ns, red32, gtot);
-        c2 = cnt0;
-        for (int p = p0; p < p1; p++) {
-            const int dd = dval(p, slot);
-            if (dd == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot;
-            if (dd == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot;
-            c2 += dd;
-        }
+    for (int k = 0; k < CPMAX; k++) {
+        if (dd[k] == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot[k];
+        if (dd[k] == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // counter 1 -> 0: it closes
+        c2 += dd[k];
     }
     PHASE(sc, 9);
-    if (tid == 0) {
-        sc->n_comb = gtot;
-        sc->n_dep = ndep;
-        sc->jac_iters = iters;
-        sc->edges_total = 0;  // next batch starts a new edge list
-    }
+    if (tid == 0) sc->n_comb = gtot;
 }
 
 // ---------------------------------------------- multi-block combine ----
@@ -2045,8 +2230,6 @@ struct DecGridArgs {
     const int32_t* et;
     const int32_t* eu;
     int64_t edge_cap;
-    uint32_t* bits;
-    int row_words;
     int32_t* bd;        // [blocks] dependents per block
     int32_t* be;        // [blocks] their sources per block
     int32_t* didx;      // [T] dependent index or -1
@@ -2131,7 +2314,6 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
         const int t = A.et[e], u = A.eu[e];
         const int k = A.didx[t];
         if (k >= 0) A.csr[A.doff[k] + atomicAdd(&A.cur[k], 1)] = u;
-        if (A.bits) A.bits[(int64_t)t * A.row_words + (u >> 5)] = 0;  // leave the dedup matrix zero
     }
     __syncthreads();
     int iters = 0;
@@ -2183,12 +2365,11 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     const int P = 2 * v.write_count;
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
     const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
-    const int force_grid = getenv("FDBCS_TEST_GRID_DECISION") ? 1 : 0;  // (tests)
-    if (T > LDS_T || force_grid || !b.dedup) {  // grid decision, then the multi-block combine
+    if (!b.rounds) {  // large or sparse batches: the overlap edges' grid decision, then the multi-block combine
         const int nb = cdiv(T, DG_THREADS);
         DecGridArgs G;
         G.T = T; G.too_old = b.too_old; G.hist = b.hist; G.deg = b.deg; G.et = b.et; G.eu = b.eu;
-        G.edge_cap = b.edge_cap; G.bits = b.dedup ? b.pair_bits : nullptr; G.row_words = b.row_words;
+        G.edge_cap = b.edge_cap;
         G.bd = b.dec_blk; G.be = b.dec_blk + nb + 1; G.didx = b.dep_idx; G.dep_list = b.dep_list; G.doff = b.off;
         G.cur = b.cur; G.csr = b.csr; G.committed = b.committed; G.cbits = b.cbits; G.verdict = verdict; G.sc = sc;
         hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
@@ -2197,18 +2378,16 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
         if (P > 0) launch_combine_grid(v, b, sc, s);
         return;
     }
-    DecideArgs A;
-    A.combine = multi ? 0 : 1;
+    RoundArgs A;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
-    A.too_old = b.too_old; A.hist = b.hist; A.et = b.et; A.eu = b.eu; A.bits = b.pair_bits; A.row_words = b.row_words;
-    A.edge_cap = b.edge_cap;
-    A.g_deg = b.deg; A.g_off = b.off; A.g_idx = b.dep_idx; A.csr = b.csr; A.dep_list = b.dep_list;
-    A.committed = b.committed; A.verdict = verdict; A.sw_slot = b.sw_slot; A.write_txn = b.write_txn;
-    A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
-    const size_t head = ((size_t)(T + 31) / 32 + (size_t)(v.write_count + 31) / 32) * 4;
-    const size_t dec = T <= LDS_T ? (size_t)(3 * T + 1) * 4 : 0;
-    const size_t lds = head + dec;
-    hipLaunchKernelGGL(k_decide_combine, dim3(1), dim3(DC_THREADS), lds, s, A);
+    A.combine = multi ? 0 : 1;
+    const size_t base = rounds_lds_base(T, v.write_count);
+    A.lcap = (int)std::min<int64_t>((int64_t)(ROUNDS_LDS_MAX - base) / 8, (int64_t)v.read_count + v.write_count);
+    if (const char* c = getenv("FDBCS_TEST_ROUNDS_LCAP")) A.lcap = std::min(A.lcap, atoi(c));  // (tests: global items)
+    A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.write_txn = b.write_txn;
+    A.rq = b.rq; A.plist = b.plist; A.wnew = b.wnew; A.winv = b.winv; A.sw_slot = b.sw_slot; A.items = b.items; A.lcap_list = b.list_cap;
+    A.committed = b.committed; A.verdict = verdict; A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
+    hipLaunchKernelGGL(k_decide_rounds, dim3(1), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
     if (multi) launch_combine_grid(v, b, sc, s);
 }
 

@@ -1,7 +1,7 @@
 """Print intra-kernel phase timings (profiling build, FDBCS_PHASES=1).
 
-usage: FDBCS_PHASES=1 python -c 'from foundationdb_amd import build; build.build_all()'   # (clean build/obj first)
-       python scripts/phases.py [warmup] [batches]
+usage: bash scripts/build_variants.sh phases:-DFDBCS_PHASES
+       FDBCS_LIB_PATH=scripts/micro/var/libfdbcs_phases.so python scripts/phases.py [warmup] [batches] [config]
 """
 import ctypes as C
 import os
@@ -18,7 +18,7 @@ def main():
     warm = int(sys.argv[1]) if len(sys.argv) > 1 else 2500
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     cs = ConflictSet(device=0, max_history=30_000_000)
-    wl = Workload(2)
+    wl = Workload(int(sys.argv[3]) if len(sys.argv) > 3 else 2)
     out = None
     for i in range(warm):
         v, now, nold = wl.view(i)

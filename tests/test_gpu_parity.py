@@ -277,11 +277,11 @@ def test_sort_distribution_shift(cs):
 
 
 @pytest.mark.parametrize("T,force", [(20000, None), (1500, "FDBCS_TEST_MULTIBLOCK_COMBINE"),
-                                     (1500, "FDBCS_TEST_GRID_DECISION"), (9000, None)])
+                                     (1500, "FDBCS_TEST_LARGE_BATCH"), (9000, None)])
 def test_large_batches_multiblock_combine(cs, T, force):
     """Batches past one workgroup's register budget (2W > 32768 endpoints)
-    combine with the multi-block kernels, and past its LDS budget (T > 8192)
-    decide with the grid kernels; small ones can be forced onto them."""
+    combine with the multi-block kernels; large-batch mode (overlap edges and
+    the grid decision) can be forced onto small ones."""
     if force:
         os.environ[force] = "1"
     try:
@@ -298,6 +298,58 @@ def test_large_batches_multiblock_combine(cs, T, force):
     finally:
         if force:
             os.environ.pop(force, None)
+
+
+def test_zipf_full_batches_rounds(cs):
+    """Config 3 at its full batch size (5,000 transactions, Zipf hot keys):
+    the decision by rounds (k_decide_rounds, no overlap pairs) against the
+    oracle, with the rounds it took in the batch stats."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    wl = Workload(3, txns=5000)
+    rounds = []
+    for i in range(12):
+        batch, now, nold = wl.batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i % 4 == 3))
+        rounds.append(cs.batch_stats()["decision_rounds"])
+    assert max(rounds) > 1, rounds  # (intra-batch conflicts did occur)
+
+
+@pytest.mark.parametrize("lcap", ["0", "700"])
+def test_rounds_items_past_lds(cs, lcap):
+    """The rounds' item list (writes of U, candidate reads) partly or wholly in
+    global memory instead of LDS (FDBCS_TEST_ROUNDS_LCAP)."""
+    os.environ["FDBCS_TEST_ROUNDS_LCAP"] = lcap
+    try:
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        wl = Workload(3, txns=2000)
+        for i in range(5):
+            batch, now, nold = wl.batch(i)
+            check_pair(cs, c, batch, now, nold, history=(i == 4))
+        same_history(cs, c)
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        for batch, now, nold in mixed_stream(11, n_batches=5, max_txns=500, keyspace=1500, wide=0.3):
+            check_pair(cs, c, batch, now, nold, history=False)
+        same_history(cs, c)
+    finally:
+        os.environ.pop("FDBCS_TEST_ROUNDS_LCAP", None)
+
+
+def test_decision_long_chain(cs):
+    """An alternating chain: t reads the key t-1 wrote and writes the next one,
+    so t commits iff t-1 aborted -- every transaction flips the next, the
+    worst case for the rounds (T + 1 of them)."""
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    T = 700
+    key = [b"chain%05d" % i for i in range(T + 1)]
+    txns = [(5, [] if t == 0 else [(key[t], key[t] + b"\x00")], [(key[t + 1], key[t + 1] + b"\x00")])
+            for t in range(T)]
+    v = check_pair(cs, c, PackedBatch.from_txns(txns), 10, 0)
+    assert list(v[:6]) == [2, 0, 2, 0, 2, 0]
+    assert cs.batch_stats()["decision_rounds"] >= T // 2
 
 
 def test_pipelined_submit_wait_matches_synchronous(cs):
