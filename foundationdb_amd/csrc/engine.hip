@@ -26,6 +26,8 @@ using namespace fdbcs_dev;
 namespace {
 
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+// where the scalar snapshot of an early verdict sits in the verdict staging
+static inline size_t vpin_scalars_off(int64_t T) { return ((size_t)T + 63) & ~(size_t)63; }
 
 #define HIPOK(x)                                    \
     do {                                            \
@@ -134,6 +136,9 @@ struct fdbcs {
     // stage timing
     bool timing = false;
     hipEvent_t ev[8] = {};
+    // early verdicts: D2H of the verdicts and a scalar snapshot right after
+    // the decision; the history update keeps running behind them
+    hipEvent_t ev_verdict = nullptr;
     // exact sharded mode: scratch for a key read back at a local index
     uint64_t* key_out = nullptr;     // hi, lo, meta
     uint8_t* key_out_tail = nullptr;
@@ -210,6 +215,21 @@ void adopt_scalars(fdbcs* cs) {
     cs->pending_tail = 0;
 }
 
+int ensure_pinned(uint8_t*& p, size_t& cap, size_t need) {
+    if (need <= cap) return FDBCS_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    size_t n = std::max(need, cap * 2);
+    hipError_t e = hipHostMalloc((void**)&p, n, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        cap = 0;
+        return FDBCS_E_NOMEM;
+    }
+    cap = n;
+    return FDBCS_OK;
+}
+
 // FDBCS_VERBOSE=1: log every buffer growth (reallocations stall the stream)
 static bool verbose() {
     static const bool v = getenv("FDBCS_VERBOSE") != nullptr;
@@ -237,6 +257,24 @@ int wait_stream(fdbcs* cs) {
     }
     for (;;) {
         const hipError_t e = hipStreamQuery(cs->stream);
+        if (e == hipSuccess) return FDBCS_OK;
+        if (e != hipErrorNotReady) {
+            last_hip_error() = e;
+            return FDBCS_E_HIP;
+        }
+        _mm_pause();
+    }
+}
+
+// Wait for an event (FDBCS_SYNC_SPIN as wait_stream).
+int wait_event(hipEvent_t ev) {
+    static const bool spin = getenv("FDBCS_SYNC_SPIN") && atoi(getenv("FDBCS_SYNC_SPIN"));
+    if (!spin) {
+        HIPOK(hipEventSynchronize(ev));
+        return FDBCS_OK;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return FDBCS_OK;
         if (e != hipErrorNotReady) {
             last_hip_error() = e;
@@ -544,7 +582,7 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
         if (cs->pending_pages && (r = sync_state(cs))) return r;
         if (cs->known_free < need) {
             const int64_t used = cs->h.cap_pages - cs->known_free;
-            if ((r = grow_pool(cs, used + 2 * need + 1024))) return r;
+            if ((r = grow_pool(cs, used + 4 * need + 1024))) return r;  // (slack: fewer syncs behind early verdicts)
         }
     }
     const uint64_t tneed = write_tail_bytes + 8 * 2 * (uint64_t)W + 64;
@@ -599,8 +637,10 @@ void read_stage_times(fdbcs* cs) {
 }
 
 // The whole detectConflicts pipeline on a device-resident batch.
+// early: copy the verdicts and a scalar snapshot to cs->vpin right after the
+// decision and record ev_verdict (finish with verdict_wait).
 int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
-              bool sync) {
+              bool sync, bool early = false) {
     int r;
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
@@ -608,6 +648,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     cs->have_last_dv = false;  // (the host paths set it again once this batch succeeded)
     if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    if (early && (r = ensure_pinned(cs->vpin, cs->vpin_cap, vpin_scalars_off(T) + sizeof(Scalars)))) return r;
     cs->last_T = T;
     cs->last_R = R;
     cs->last_W = W;
@@ -628,7 +669,13 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     record(cs, 2);
     if ((r = edges_read_check(cs, v, cs->v0))) return r;
     record(cs, 3);
-    launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s);
+    launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, early);
+    if (early) {
+        if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
+        HIPOK(hipEventRecord(cs->ev_verdict, s));
+        launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
+    }
     record(cs, 4);
     const bool compact = new_oldest > cs->oldest;
     launch_merge(v, b, h, cs->cur, sc, now, cs->v0, !compact, s);
@@ -648,6 +695,20 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     return FDBCS_OK;
 }
 
+// The early verdicts of run_batch(early): wait for them (not for the history
+// update behind them) and check the scalar snapshot taken with them: err =
+// this batch's stages so far, last_err = the previous batch's history update
+// (so a failed update is reported by the next detectConflicts).
+int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
+    int r;
+    if ((r = wait_event(cs->ev_verdict))) return r;
+    const Scalars* snap = reinterpret_cast<const Scalars*>(cs->vpin + vpin_scalars_off(T));
+    if (snap->err) return snap->err;
+    if (snap->last_err) return snap->last_err;
+    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    return FDBCS_OK;
+}
+
 int reset_history(fdbcs* cs, int64_t v) {
     cs->v0 = v;
     cs->cur = 0;
@@ -656,20 +717,6 @@ int reset_history(fdbcs* cs, int64_t v) {
     return sync_state(cs);
 }
 
-int ensure_pinned(uint8_t*& p, size_t& cap, size_t need) {
-    if (need <= cap) return FDBCS_OK;
-    if (p) hipHostFree(p);
-    p = nullptr;
-    size_t n = std::max(need, cap * 2);
-    hipError_t e = hipHostMalloc((void**)&p, n, hipHostMallocDefault);
-    if (e != hipSuccess) {
-        last_hip_error() = e;
-        cap = 0;
-        return FDBCS_E_NOMEM;
-    }
-    cap = n;
-    return FDBCS_OK;
-}
 
 // Lay a host batch view out in one pinned buffer, copy it to the device in one
 // transfer and return the device-side view.
@@ -751,6 +798,26 @@ int check_host_view(const fdbcs_batch_view& hv) {
     return FDBCS_OK;
 }
 
+// detectConflicts on a staged device view, verdicts to the host.  The call
+// returns once the verdicts are back (the Resolver needs them
+// on return); the history update (merge, compaction) is still running and the
+// next batch's kernels queue behind it on the stream.  With stage timing on,
+// the whole batch is waited for (the stage events).
+int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    int r;
+    const int64_t T = dv.txn_count;
+    const bool early = !cs->timing;
+    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early))) return r;
+    if (early) return verdict_wait(cs, T, verdict);
+    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
+    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
+    if ((r = sync_batch(cs))) return r;
+    read_stage_times(cs);
+    if (cs->sc_host->last_err) return cs->sc_host->last_err;
+    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    return FDBCS_OK;
+}
+
 int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
     int r;
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_ARG;  // (pipelined batches still in flight)
@@ -758,14 +825,7 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     fdbcs_batch_view dv;
     cs->have_last_dv = false;
     if ((r = stage_batch(cs, hv, dv))) return r;
-    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
-    const int64_t T = hv.txn_count;
-    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
-    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
-    if ((r = sync_batch(cs))) return r;
-    read_stage_times(cs);
-    if (cs->sc_host->last_err) return cs->sc_host->last_err;
-    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    if ((r = finish_detect(cs, dv, now, new_oldest, verdict))) return r;
     cs->last_dv = dv;
     cs->have_last_dv = true;
     return FDBCS_OK;
@@ -862,6 +922,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     cs->h.shard = ShardBounds{};
     for (int i = 0; i < 8; i++)
         if (hipEventCreate(&cs->ev[i]) != hipSuccess) return fail(FDBCS_E_HIP);
+    if (hipEventCreateWithFlags(&cs->ev_verdict, hipEventDisableTiming) != hipSuccess) return fail(FDBCS_E_HIP);
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
     if ((r = reset_history(cs, v0))) return fail(r);
     cs->oldest = 0;
@@ -906,6 +967,7 @@ void fdbcs_destroy(fdbcs* cs) {
     if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
     for (int i = 0; i < 8; i++)
         if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
+    if (cs->ev_verdict) hipEventDestroy(cs->ev_verdict);
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -942,13 +1004,7 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     int r;
     fdbcs_batch_view dv;
     if ((r = cs->st.finish(dv))) return r;
-    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false))) return r;
-    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
-    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
-    if ((r = sync_batch(cs))) return r;
-    read_stage_times(cs);
-    if (cs->sc_host->last_err) return cs->sc_host->last_err;
-    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    if ((r = finish_detect(cs, dv, now, new_oldest, verdict))) return r;
     cs->last_dv = dv;
     cs->have_last_dv = true;
     return FDBCS_OK;
@@ -1212,6 +1268,8 @@ int fdbcs_stage_times(fdbcs* cs, double* out_us, int cap) {
 
 int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
     if (!cs || !out) return FDBCS_E_ARG;
+    int r;
+    if ((r = sync_state(cs))) return r;  // (detect returns before the history update ends)
     const Scalars& h = *cs->sc_host;
     const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
                                     h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc};
@@ -1224,6 +1282,8 @@ int fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap) {
 #ifdef FDBCS_PHASES
     if (!cs || !out) return FDBCS_E_ARG;
     const int n = std::min(cap, 32);
+    int r;
+    if ((r = sync_state(cs))) return r;
     for (int i = 0; i < n; i++) out[i] = cs->sc_host->ph[i];
     return n;
 #else

@@ -192,7 +192,9 @@ int64_t lb_hist_words(int R, int W);
 // history read check + intra-batch overlap edges, one launch
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s);
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s);
+// split: the combine is left to launch_combine (issued after the verdict copy)
+void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
+                   bool split = false);
 // k_decide_rounds keeps its state in LDS: batches up to this shape
 bool rounds_fit(int64_t T, int64_t W);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);

@@ -2008,6 +2008,7 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
                 nbits[i] = 0;
             }
             if (!__syncthreads_or(changed)) break;
+            if (rounds == 1) PHASE(sc, 4);
         }
         if (tid == 0) sc->jac_iters = rounds;
     }
@@ -2359,12 +2360,13 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
     }
 }
 
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s) {
+void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
+                   bool split) {
     const int T = v.txn_count;
     if (T == 0) return;  // n_comb was zeroed by k_prep
     const int P = 2 * v.write_count;
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
-    const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi);
+    const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi || split);
     if (!b.rounds) {  // large or sparse batches: the overlap edges' grid decision, then the multi-block combine
         const int nb = cdiv(T, DG_THREADS);
         DecGridArgs G;
@@ -2375,7 +2377,7 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
         hipLaunchKernelGGL(k_dec_flags, dim3(nb), dim3(DG_THREADS), 0, s, G);
         hipLaunchKernelGGL(k_dec_place, dim3(nb), dim3(DG_THREADS), 0, s, G);
         hipLaunchKernelGGL(k_dec_walk, dim3(1), dim3(1024), (size_t)((T + 31) / 32) * 4, s, G);
-        if (P > 0) launch_combine_grid(v, b, sc, s);
+        if (P > 0 && !split) launch_combine_grid(v, b, sc, s);
         return;
     }
     RoundArgs A;
@@ -2388,10 +2390,13 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     A.rq = b.rq; A.plist = b.plist; A.wnew = b.wnew; A.winv = b.winv; A.sw_slot = b.sw_slot; A.items = b.items; A.lcap_list = b.list_cap;
     A.committed = b.committed; A.verdict = verdict; A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
     hipLaunchKernelGGL(k_decide_rounds, dim3(1), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
-    if (multi) launch_combine_grid(v, b, sc, s);
+    if (multi && !split) launch_combine_grid(v, b, sc, s);
 }
 
-void launch_combine(const fdbcs_batch_view&, BatchBufs&, Scalars*, hipStream_t) {}
+// the combine of a split launch_decide (after the verdicts have been sent)
+void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
+    if (v.txn_count > 0 && v.write_count > 0) launch_combine_grid(v, b, sc, s);
+}
 
 // ---- exact sharded mode: exchange flags, foreign edges -------------------
 __global__ __launch_bounds__(256) void k_flags_out(int T, const uint8_t* __restrict__ too_old,

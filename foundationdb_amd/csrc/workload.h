@@ -67,6 +67,8 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
 /* Grow a conflict set's history through n generated batches [first, first+n)
  * (fdbcs_batch_submit_packed / fdbcs_batch_wait, generation of batch i+1
  * overlapping batch i): the bench's steady-state prefill. */
+// (measurement) the adds of fdbwl_run_resolver alone, no detect
+int fdbwl_run_adds(fdbwl_run* r, fdbcs* cs, double* add_us);
 int fdbwl_prefill(fdbwl* g, fdbcs* cs, int64_t first, int32_t n);
 
 #ifdef __cplusplus
