@@ -12,6 +12,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -139,6 +140,14 @@ struct fdbcs {
     // early verdicts: D2H of the verdicts and a scalar snapshot right after
     // the decision; the history update keeps running behind them
     hipEvent_t ev_verdict = nullptr;
+    // host-mapped verdict area the decision kernel writes (kernels.h EarlyOut):
+    // [0] flag, [4] err, [8] last_err, verdicts from byte 64
+    uint8_t* vmap = nullptr;
+    uint8_t* vmap_dev = nullptr;
+    size_t vmap_cap = 0;
+    uint32_t vseq = 0;
+    bool early_mapped = false;  // the batch in flight writes vmap
+
     // exact sharded mode: scratch for a key read back at a local index
     uint64_t* key_out = nullptr;     // hi, lo, meta
     uint8_t* key_out_tail = nullptr;
@@ -649,6 +658,18 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
     if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
     if (early && (r = ensure_pinned(cs->vpin, cs->vpin_cap, vpin_scalars_off(T) + sizeof(Scalars)))) return r;
+    if (early && (size_t)T + 64 > cs->vmap_cap) {
+        if (cs->vmap) hipHostFree(cs->vmap);
+        cs->vmap = cs->vmap_dev = nullptr;
+        cs->vmap_cap = 0;
+        const size_t n = std::max<size_t>((size_t)T + 64, 2 * cs->vmap_cap) + 4096;
+        if (hipHostMalloc((void**)&cs->vmap, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        memset(cs->vmap, 0, n);
+        HIPOK(hipHostGetDevicePointer((void**)&cs->vmap_dev, cs->vmap, 0));
+        cs->vmap_cap = n;
+        cs->vseq = 0;
+    }
     cs->last_T = T;
     cs->last_R = R;
     cs->last_W = W;
@@ -669,10 +690,19 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     record(cs, 2);
     if ((r = edges_read_check(cs, v, cs->v0))) return r;
     record(cs, 3);
-    launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, early);
+    EarlyOut eo{};
+    if (early && !dev_verdict) {
+        if (++cs->vseq == 0) cs->vseq = 1;
+        eo = EarlyOut{cs->vmap_dev + 64, reinterpret_cast<int32_t*>(cs->vmap_dev + 4),
+                      reinterpret_cast<uint32_t*>(cs->vmap_dev), cs->vseq};
+    }
+    cs->early_mapped =
+        launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, early, eo.flag ? &eo : nullptr);
     if (early) {
-        if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
+        if (!cs->early_mapped) {  // (the grid decision of large batches: copies)
+            if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
+            HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
+        }
         HIPOK(hipEventRecord(cs->ev_verdict, s));
         launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
     }
@@ -701,6 +731,25 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
 // (so a failed update is reported by the next detectConflicts).
 int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
     int r;
+    if (cs->early_mapped) {
+        // poll the flag the decision kernel sets after its verdicts (no copy,
+        // no interrupt); past ~2 ms block on the event behind it instead
+        const uint32_t* flag = reinterpret_cast<const uint32_t*>(cs->vmap);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int it = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != cs->vseq; it++) {
+            _mm_pause();
+            if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                if ((r = wait_event(cs->ev_verdict))) return r;
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != cs->vseq) return FDBCS_E_HIP;
+                break;
+            }
+        }
+        const int32_t* err = reinterpret_cast<const int32_t*>(cs->vmap + 4);
+        if (err[0]) return err[0];
+        if (err[1]) return err[1];
+        if (T) memcpy(verdict, cs->vmap + 64, (size_t)T);
+        return FDBCS_OK;
+    }
     if ((r = wait_event(cs->ev_verdict))) return r;
     const Scalars* snap = reinterpret_cast<const Scalars*>(cs->vpin + vpin_scalars_off(T));
     if (snap->err) return snap->err;
@@ -930,6 +979,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         cs->st.configure(cs->stream, strtoull(c, nullptr, 0));
     else
         cs->st.configure(cs->stream, 512 << 10);
+
     *out = cs;
     return FDBCS_OK;
 }
@@ -968,6 +1018,7 @@ void fdbcs_destroy(fdbcs* cs) {
     for (int i = 0; i < 8; i++)
         if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
     if (cs->ev_verdict) hipEventDestroy(cs->ev_verdict);
+    if (cs->vmap) hipHostFree(cs->vmap);
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }

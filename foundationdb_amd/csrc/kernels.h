@@ -192,9 +192,20 @@ int64_t lb_hist_words(int R, int W);
 // history read check + intra-batch overlap edges, one launch
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s);
-// split: the combine is left to launch_combine (issued after the verdict copy)
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
-                   bool split = false);
+// Host-mapped verdict output of the decision (early verdicts): the verdicts,
+// then err[0] = sc->err, err[1] = sc->last_err, then *flag = seq (release,
+// system scope).
+struct EarlyOut {
+    uint8_t* verdict;
+    int32_t* err;
+    uint32_t* flag;
+    uint32_t seq;
+};
+// split: the combine is left to launch_combine (issued after the verdicts).
+// eo: write the verdicts there (returns true if this batch's decision does;
+// the grid decision of large batches does not).
+bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
+                   bool split = false, const EarlyOut* eo = nullptr);
 // k_decide_rounds keeps its state in LDS: batches up to this shape
 bool rounds_fit(int64_t T, int64_t W);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);

@@ -1751,6 +1751,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
 // it back to 0.
 struct RoundArgs {
     int T, R, W;
+    EarlyOut eo;              // eo.flag: verdicts go to host-mapped memory, then the flag
     int combine;              // 0: the multi-block combine kernels follow
     int lcap;                 // items that fit in LDS (else A.items)
     const uint8_t* too_old;
@@ -2018,6 +2019,16 @@ decided:
         const bool c = (cbits[t >> 5] >> (t & 31)) & 1;
         A.committed[t] = c;
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+    }
+    if (A.eo.flag) {  // host-mapped verdicts: every lane's stores, then the error words, then the flag
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) {
+            A.eo.err[0] = sc->err;
+            A.eo.err[1] = sc->last_err;
+            __threadfence_system();
+            __hip_atomic_store(A.eo.flag, A.eo.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     if (tid == 0) {
         sc->n_dep = ncand;  // candidate reads of U (stats)
@@ -2360,10 +2371,10 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
     }
 }
 
-void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
-                   bool split) {
+bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
+                   bool split, const EarlyOut* eo) {
     const int T = v.txn_count;
-    if (T == 0) return;  // n_comb was zeroed by k_prep
+    if (T == 0) return false;  // n_comb was zeroed by k_prep
     const int P = 2 * v.write_count;
     const int force_multi = getenv("FDBCS_TEST_MULTIBLOCK_COMBINE") ? 1 : 0;  // (tests)
     const bool multi = P > 0 && (P > CPMAX * DC_THREADS || force_multi || split);
@@ -2378,7 +2389,7 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
         hipLaunchKernelGGL(k_dec_place, dim3(nb), dim3(DG_THREADS), 0, s, G);
         hipLaunchKernelGGL(k_dec_walk, dim3(1), dim3(1024), (size_t)((T + 31) / 32) * 4, s, G);
         if (P > 0 && !split) launch_combine_grid(v, b, sc, s);
-        return;
+        return false;
     }
     RoundArgs A;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
@@ -2389,8 +2400,14 @@ void launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.write_txn = b.write_txn;
     A.rq = b.rq; A.plist = b.plist; A.wnew = b.wnew; A.winv = b.winv; A.sw_slot = b.sw_slot; A.items = b.items; A.lcap_list = b.list_cap;
     A.committed = b.committed; A.verdict = verdict; A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
+    A.eo = EarlyOut{};
+    if (eo) {
+        A.eo = *eo;
+        A.verdict = eo->verdict;
+    }
     hipLaunchKernelGGL(k_decide_rounds, dim3(1), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
     if (multi && !split) launch_combine_grid(v, b, sc, s);
+    return eo != nullptr;
 }
 
 // the combine of a split launch_decide (after the verdicts have been sent)

@@ -10,9 +10,12 @@
 // detectConflicts is called; finish() sends the rest plus the record offsets
 // and k_unpack builds the batch view on the device.
 //
-// (Handing the record copies to helper threads was measured and dropped:
-// with the descriptors written by one core and read by another, the
-// calling thread got slower, 185 -> 250-990 us per config-2 batch.)
+// (Measured and dropped: handing the record copies to helper threads during
+// the adds -- the calling thread got slower, 185 -> 250-990 us per config-2
+// batch -- and a parallel gather at detect by 8 host threads over borrowed
+// ranges: 52-65 us for the gather, but the 1.5 MB H2D no longer overlapped
+// the adds (~25 GB/s) and the caller's add loop slowed 3x while the helper
+// threads lived, for no net gain.)
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -31,6 +34,7 @@ class TxnStage {
 
     // stream: where the H2D copies and k_unpack go; chunk: bytes per streamed copy
     void configure(hipStream_t stream, uint64_t chunk);
+
     int begin();
     // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md
     // §0.6) refuse the transaction, which is then not part of the batch.
