@@ -386,7 +386,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.read_txn); dfree(b.read_snap); dfree(b.write_txn);
     dfree(b.keys.hi); dfree(b.keys.lo); dfree(b.keys.meta); dfree(b.keys.tail); dfree(b.btail);
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
-    dfree(b.ss_cnt); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
+    dfree(b.ss_cnt); dfree(b.ss_gsamp); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
     dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv);
     dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
@@ -490,7 +490,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
     }
     if (!b.ss_cnt) {
         if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)) ||
-            (r = dalloc(b.ss_qt, 2 * 1024 * SS_QT)))
+            (r = dalloc(b.ss_qt, 2 * 1024 * SS_QT)) || (r = dalloc(b.ss_gsamp, 2 * 3 * 4096)))
             return r;
         HIPOK(hipMemsetAsync(b.ss_qt, 0, 2 * 1024 * SS_QT, s));
         HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 2 * 1024 * sizeof(int32_t), s));
@@ -610,10 +610,10 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
 // a list sized linearly in the batch: if it overflowed, grow it to the count
 // the kernel reached and search again (the read check is idempotent; the
 // per-reader source counts restart from zero).
-int edges_read_check(fdbcs* cs, const fdbcs_batch_view& v, int64_t v0) {
+int edges_read_check(fdbcs* cs, const fdbcs_batch_view& v, int64_t v0, bool defer_ws = false) {
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
-    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s);
+    launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, v0, s, defer_ws && b.rounds);
     if (b.rounds) return FDBCS_OK;  // (no overlap pairs: k_decide_rounds)
     int32_t total = 0;
     HIPOK(hipMemcpyAsync(&total, &cs->sc->edges_total, sizeof(total), hipMemcpyDeviceToHost, s));
@@ -688,13 +688,12 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
         cs->have_quantiles = true;
     }
     record(cs, 2);
-    if ((r = edges_read_check(cs, v, cs->v0))) return r;
+    if ((r = edges_read_check(cs, v, cs->v0, early))) return r;
     record(cs, 3);
     EarlyOut eo{};
     if (early && !dev_verdict) {
         if (++cs->vseq == 0) cs->vseq = 1;
-        eo = EarlyOut{cs->vmap_dev + 64, reinterpret_cast<int32_t*>(cs->vmap_dev + 4),
-                      reinterpret_cast<uint32_t*>(cs->vmap_dev), cs->vseq};
+        eo = EarlyOut{cs->vmap_dev + 64, reinterpret_cast<uint32_t*>(cs->vmap_dev), cs->vseq};
     }
     cs->early_mapped =
         launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, early, eo.flag ? &eo : nullptr);
@@ -704,6 +703,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
             HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
         }
         HIPOK(hipEventRecord(cs->ev_verdict, s));
+        launch_write_search(v, b, cs->h, cs->cur, sc, cs->v0, s);  // (for the merge: after the verdicts)
         launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
     }
     record(cs, 4);

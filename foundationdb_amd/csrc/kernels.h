@@ -71,6 +71,8 @@ struct BatchBufs {
     int32_t* winv;       // [2W] sorted position of each write endpoint (by slot - 2R)
     uint2* items;        // [R + W] the rounds' writes and reads when they do not fit in LDS
     int64_t list_cap;    // entries of plist (items: 2 * list_cap)
+    bool ws_deferred;    // this batch's write searches wait for launch_write_search
+    uint64_t* ss_gsamp;  // [2 * 3 * 4096] global sample scratch of the sort's overflow guard
     uint32_t* rstamp;    // [R] per read: the batch (rseq) that put it on plist
     uint32_t rseq;
     // overlap edges (large / sparse batches)
@@ -190,14 +192,17 @@ bool large_batch_mode(int64_t T);
 int64_t lb_meta_words();
 int64_t lb_hist_words(int R, int W);
 // history read check + intra-batch overlap edges, one launch
+// defer_ws: leave the write searches (WriteHits, for the merge) to
+// launch_write_search, after the verdicts
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
-                             hipStream_t s);
+                             hipStream_t s, bool defer_ws = false);
+void launch_write_search(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
+                         hipStream_t s);
 // Host-mapped verdict output of the decision (early verdicts): the verdicts,
-// then err[0] = sc->err, err[1] = sc->last_err, then *flag = seq (release,
-// system scope).
+// a system-scope fence, then one 16-byte store {seq, sc->err, sc->last_err, 0}
+// at flag (16-byte aligned).
 struct EarlyOut {
     uint8_t* verdict;
-    int32_t* err;
     uint32_t* flag;
     uint32_t seq;
 };

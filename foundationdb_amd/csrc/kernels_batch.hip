@@ -403,13 +403,11 @@ __device__ inline void place_rec(const SortJobs& J, int job, int i, int b, const
 // previous batch's quantiles); then splitters from this batch's own sample
 // and every record of the job is bucketed again, so the batch keeps the fast
 // bucket paths instead of an O(bucket x n) global-memory ranking.
-__global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys, int guard) {
-    __shared__ uint64_t s_hi[SS_S], s_lo[SS_S], s_mi[SS_S];
+__device__ void ss_sample_job(const SortJobs& J, const KeyArrays& keys, const LdsRecs& L, int guard) {
     const int job = blockIdx.x;
     const int n = J.n[job];
     if (guard && !J.sc->ss_over[job]) return;
     if (n == 0) return;
-    const LdsRecs L{s_hi, s_lo, s_mi};
     const int ns = sample_quantiles(J, job, keys, L);
     if (!guard) return;
     const int nb = J.nb[job], step = SS_Q / nb;
@@ -434,6 +432,19 @@ __global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys, 
     }
     __syncthreads();
     if (threadIdx.x == 0) J.sc->ss_over[job] = 0;  // (a bucket may still exceed its row: ranked globally)
+}
+
+__global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys, int guard) {
+    __shared__ uint64_t s_hi[SS_S], s_lo[SS_S], s_mi[SS_S];
+    ss_sample_job(J, keys, LdsRecs{s_hi, s_lo, s_mi}, guard);
+}
+
+// The guard after every scatter, without the 96 KiB of LDS (whose allocation
+// made even the usual immediate return cost ~4.6 us): the rare resample sorts
+// its sample in global scratch (3 * SS_S words per job).
+__global__ __launch_bounds__(1024) void k_ss_guard(SortJobs J, KeyArrays keys, uint64_t* scratch) {
+    uint64_t* g = scratch + (int64_t)blockIdx.x * 3 * SS_S;
+    ss_sample_job(J, keys, LdsRecs{g, g + SS_S, g + 2 * SS_S}, 1);
 }
 
 // Splitter s of a job is quantile (s + 1) * SS_Q / nb.  Scatter kernels keep
@@ -1199,7 +1210,7 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
         if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 0);
         hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
     }
-    hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 1);  // overflow guard
+    hipLaunchKernelGGL(k_ss_guard, dim3(2), dim3(1024), 0, s, J, b.keys, b.ss_gsamp);  // overflow guard
     hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
     return true;  // the counters of the other parity are zero now
 }
@@ -1684,8 +1695,25 @@ __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_write_search(WriteSearchArgs WA) {
+    const Group<RC_G> g;
+    write_search_group(WA, g, (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G));
+}
+
+// the write searches held back by launch_edges_read_check(defer_ws): only
+// the merge needs them, so they run after the verdicts
+void launch_write_search(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
+                         hipStream_t s) {
+    if (!b.ws_deferred) return;
+    b.ws_deferred = false;
+    const int R = v.read_count, W = v.write_count;
+    if (W == 0) return;
+    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, nullptr};
+    hipLaunchKernelGGL(k_write_search, dim3(cdiv((int64_t)W * RC_G, 256)), dim3(256), 0, s, WA);
+}
+
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
-                             hipStream_t s) {
+                             hipStream_t s, bool defer_ws) {
     const int R = v.read_count, W = v.write_count;
     // large unsharded batches: directory entries by merge-join (ss_bkt is free once the sort is done)
     static const bool dir_search = getenv("FDBCS_LARGE_DIR_SEARCH") != nullptr;  // (A/B measurements)
@@ -1703,7 +1731,8 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
                  b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv, b.rstamp, b.rseq};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
     const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
-    const int ws_blocks = cdiv((int64_t)W * RC_G, 256);
+    b.ws_deferred = defer_ws && !dj;
+    const int ws_blocks = b.ws_deferred ? 0 : cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
@@ -2020,15 +2049,10 @@ decided:
         A.committed[t] = c;
         A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
     }
-    if (A.eo.flag) {  // host-mapped verdicts: every lane's stores, then the error words, then the flag
+    if (A.eo.flag) {  // host-mapped verdicts: every lane's stores, then flag + error words in one 16-byte store
         __threadfence_system();
         __syncthreads();
-        if (tid == 0) {
-            A.eo.err[0] = sc->err;
-            A.eo.err[1] = sc->last_err;
-            __threadfence_system();
-            __hip_atomic_store(A.eo.flag, A.eo.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (tid == 0) *reinterpret_cast<int4*>(A.eo.flag) = make_int4((int)A.eo.seq, sc->err, sc->last_err, 0);
     }
     if (tid == 0) {
         sc->n_dep = ncand;  // candidate reads of U (stats)
