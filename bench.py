@@ -67,6 +67,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="key-range shards of the N-core CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-shim", action="store_true", help="skip the shim's skipListTest rate")
     p.add_argument("--stage-batches", type=int, default=None,
                    help="instrumented HBM-resident batches after the timed region (default 50; config 5: 3)")
     p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
@@ -127,7 +128,7 @@ def stage_bytes(name, st, key_bytes):
 
 
 def host_cpu():
-    """(model name, CPUs this process may run on)."""
+    """(model name, CPUs this process may use: affinity, capped by a cgroup quota)."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -141,6 +142,13 @@ def host_cpu():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
+    try:  # a cgroup CPU quota (the GPU box: 16 CPUs' worth of time over 256 visible CPUs)
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
     return model, n
 
 
@@ -231,6 +239,31 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts):
     return one
 
 
+def shim_skiplisttest():
+    """skipListTest() (SkipList.cpp:1394-1486) through the drop-in shim, as
+    fdbserver -r skiplisttest would call it: its own rate line."""
+    import re
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "shim", "shim_smoke")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe, "skiplisttest"], capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    out = r.stdout
+    m = re.search(r"New conflict set:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
+    d = re.search(r"Detect only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
+    h = re.search(r"(\d+) entries in version history", out)
+    if r.returncode != 0 or not m:
+        return {"error": f"rc={r.returncode}", "tail": out[-300:] + r.stderr[-300:]}
+    return {"new_conflict_set_mtxn_s": float(m.group(2)), "detect_only_mtxn_s": float(d.group(2)) if d else None,
+            "history_entries": int(h.group(1)) if h else None,
+            "reference_here_mtxn_s": 0.155,
+            "path": "tests/shim/shim_smoke skiplisttest: ConflictSetShim.cpp skipListTest() (config 1: 500 x 2,500 "
+                    "txns) -> addTransaction / detectConflicts -> libfdbcs"}
+
+
 def run_single(args):
     """N = 1: steady-state prefill, then the Resolver's per-transaction window."""
     import torch
@@ -275,6 +308,23 @@ def run_single(args):
     lat_ms = us / 1e3
     del run
     next_i = first + args.steps
+
+    # ---- packed path (secondary): whole host batch views through fdbcs_batch_detect_packed ----
+    packed = None
+    n_pk = min(50, args.steps)
+    if n_pk > 0:
+        pk = [wl.batch(next_i + j) for j in range(n_pk)]  # (generated before the clock)
+        t_pk = []
+        for b, now, nold in pk:
+            t1 = time.perf_counter()
+            cs.detect_packed(b, now, nold)
+            t_pk.append(time.perf_counter() - t1)
+        next_i += n_pk
+        del pk
+        pk_ms = float(np.mean(t_pk)) * 1e3
+        packed = {"ms_per_step": round(pk_ms, 4), "value": round(T / (pk_ms * 1e-3), 1), "unit": "txn/s",
+                  "batches": n_pk, "per_txn_over_packed": round(elapsed / args.steps * 1e3 / pk_ms, 3),
+                  "path": "fdbcs_batch_detect_packed: the whole batch as one host view (pinned staging, one H2D)"}
 
     # ---- HBM-resident pipeline (secondary): staged batches, per-stage HIP events ----
     n_st = args.stage_batches
@@ -370,6 +420,7 @@ def run_single(args):
     cpu = None
     if snap is not None:
         cpu = cpu_baselines(args, snap, wl, first, args.steps, verdicts)
+    shim = shim_skiplisttest() if cfg == 2 and not args.no_shim else None
     workload = f"config{cfg}: {T}-txn batches, {CONFIG_SHAPE.get(cfg, '')}, 5M-version window"
     out = {
         "metric": "resolved txns/sec (whole node) at 5k-txn batches; p99 detectConflicts latency",
@@ -392,6 +443,8 @@ def run_single(args):
                    "window": "Resolver.actor.cpp:139-154: fdbcs_batch_begin + T x fdbcs_batch_add (pinned append, "
                              "chunked H2D) + fdbcs_batch_detect (device pipeline, verdict D2H), native loop"},
         "hbm_resident": hbm,
+        "packed_path": packed,
+        "shim_skiplisttest": shim,
         "roofline": roofline,
         "cpu_baseline": cpu,
         "load_metrics": lm,

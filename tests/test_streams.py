@@ -1,0 +1,87 @@
+"""Stream fixtures (tests/golden/stream_*.json) replayed.
+
+CPU: the generator still produces the recorded inputs (every batch's input
+SHA-256) and the CPU restatement reproduces the recorded verdicts and
+post-batch histories on a prefix of each stream.  GPU: the whole stream
+through the engine -- config 2 and 3 through the Resolver's per-transaction
+loop (fdbwl_run_resolver: fdbcs_batch_begin / add / detect), the others as
+packed batches -- bit-exact after every batch: verdicts, H, the history's
+SHA-256, 32 sampled boundaries, removalKey, oldestVersion.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden.streams import STREAMS, batch_sha, history_record, unpack_verdicts
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CPU_PREFIX = {"skiplisttest": 20, "config2": 8, "config3": 20, "config4": 20}
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, f"stream_{name}.json")) as f:
+        return json.load(f)
+
+
+def check_record(got, want, name, i):
+    for k in ("H", "history_sha256", "removal_key", "oldest", "v0"):
+        assert got[k] == want[k], f"{name} batch {i}: {k} {got[k]} != {want[k]}"
+    assert got["samples"] == want["samples"], f"{name} batch {i}: sampled boundaries differ"
+
+
+@pytest.mark.parametrize("name", list(STREAMS))
+def test_generator_inputs_unchanged(name):
+    from foundationdb_amd.workload import Workload
+    fx = load(name)
+    wl = Workload(fx["config"], txns=fx["txns"])
+    for rec in fx["batches_out"]:
+        b, now, nold = wl.batch(rec["index"])
+        assert (now, nold) == (rec["now"], rec["new_oldest"])
+        assert batch_sha(b) == rec["input_sha256"], f"{name} batch {rec['index']}: generator output changed"
+    wl.close()
+
+
+@pytest.mark.parametrize("name", list(STREAMS))
+def test_cpu_spec_reproduces_stream(name):
+    from foundationdb_amd.workload import Workload
+    from oracle import CpuSpec
+    fx = load(name)
+    wl = Workload(fx["config"], txns=fx["txns"])
+    cs = CpuSpec()
+    for rec in fx["batches_out"][:CPU_PREFIX[name]]:
+        b, now, nold = wl.batch(rec["index"])
+        v = cs.detect_packed(b, now, nold)
+        assert np.array_equal(v, unpack_verdicts(rec["verdict_b64"], b.T)), f"{name} batch {rec['index']}"
+        check_record(history_record(cs), rec, name, rec["index"])
+    cs.close()
+    wl.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(STREAMS))
+def test_gpu_replays_stream(name):
+    from foundationdb_amd import ConflictSet
+    from foundationdb_amd.workload import Workload
+    fx = load(name)
+    wl = Workload(fx["config"], txns=fx["txns"])
+    cs = ConflictSet(device=0, max_history=4_000_000)
+    per_txn = name in ("config2", "config3")
+    for rec in fx["batches_out"]:
+        i = rec["index"]
+        if per_txn:  # the Resolver's loop: begin, T x add, detect (native)
+            run = wl.prepare_run(i, 1)
+            _us, _add, v = run.run(cs, verdicts=True)
+            v = v[0]
+            del run
+        else:
+            b, now, nold = wl.batch(i)
+            v = cs.detect_packed(b, now, nold)
+        want = unpack_verdicts(rec["verdict_b64"], len(v))
+        assert np.array_equal(np.asarray(v, np.uint8), want), \
+            f"{name} batch {i}: {int((np.asarray(v) != want).sum())} verdicts differ"
+        assert [int((np.asarray(v) == k).sum()) for k in range(3)] == rec["verdict_counts"]
+        check_record(history_record(cs), rec, name, i)
+    cs.close()
+    wl.close()
