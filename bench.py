@@ -68,6 +68,8 @@ def parse():
                    help="key-range shards of the N-core CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-shim", action="store_true", help="skip the shim's skipListTest rate")
+    p.add_argument("--impl", choices=["abi", "py"], default="abi",
+                   help="exact protocol A: fdbcs_sharded (C ABI, RCCL inside libfdbcs) or the Python orchestration")
     p.add_argument("--stage-batches", type=int, default=None,
                    help="instrumented HBM-resident batches after the timed region (default 50; config 5: 3)")
     p.add_argument("--mode", choices=["exact", "resolvers"], default="exact",
@@ -504,7 +506,15 @@ def run_multi(args, rank, world):
     sparse = mode == "exact" and args.protocol == "b"
     src = Source(cfg, args.txns, world, rank, split=(mode == "resolvers" or sparse), keep_all=sparse)
     eng = None
-    if mode == "exact":
+    abi = mode == "exact" and args.protocol == "a" and args.impl == "abi"
+    if abi:  # fdbcs_sharded: the protocol inside libfdbcs, RCCL on the engine's stream
+        from foundationdb_amd.sharded import ShardedResolver
+        obj = [ShardedResolver.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        eng = ShardedResolver(uniform_bounds(world), rank, world, device=local, max_history=max_history(cfg),
+                              comm_id=obj[0])
+        cs = eng.local
+    elif mode == "exact":
         from foundationdb_amd.sharded import DistShardedConflictSet
         eng = DistShardedConflictSet(uniform_bounds(world), rank, world, local, max_history=max_history(cfg),
                                      sparse=sparse)
@@ -515,6 +525,10 @@ def run_multi(args, rank, world):
     def global_h():
         if mode != "exact":
             return cs.history_size()
+        if abi:
+            t = torch.tensor([cs.history_size()], dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            return int(t.item())
         return sum(x[0] for x in eng._allgather([cs.history_size()]))
 
     t_w = time.time()
@@ -528,7 +542,9 @@ def run_multi(args, rank, world):
     for j in range(n_pre + n_warm):
         i = j - n_pre
         v, now, nold, _T, _idx, _keep = (pre.host(j) if i < 0 else src.host(i))
-        if mode == "exact":
+        if abi:
+            eng.detect_device(DeviceBatch(v, dev).view, now, nold)
+        elif mode == "exact":
             db = DeviceBatch(v, dev)
             if wverd is None or wverd.numel() < max(1, v.txn_count):
                 wverd = torch.empty(max(1, v.txn_count), dtype=torch.uint8, device=dev)
@@ -557,7 +573,9 @@ def run_multi(args, rank, world):
     for k in range(args.steps):
         dv, now, nold, _Tg, didx, _b = staged[k]
         ts = time.perf_counter()
-        if mode == "exact":
+        if abi:
+            eng.detect_device(dv, now, nold)  # (host verdicts: the one wait per batch)
+        elif mode == "exact":
             eng.detect_device(dv, now, nold, sub_verdicts[k])
         else:
             cs.detect_device(dv, now, nold, sub_verdicts[k].data_ptr(), sync=True)
@@ -576,7 +594,12 @@ def run_multi(args, rank, world):
     value = Tg * args.steps / elapsed
     lat_ms = np.array(lat) * 1e3
     if rank == 0:
-        if mode == "exact":
+        if abi:
+            workload = (f"config{cfg}: {Tg}-txn global batches ({args.txns}/GPU), {CONFIG_SHAPE.get(cfg, '')}, "
+                        f"5M-version window; one exact resolver sharded by key range over {world} GPUs (fdbcs_sharded "
+                        f"C ABI, protocol A: RCCL MAX all-reduce + all-gather on the engine's stream, carry-ins and "
+                        f"compaction plan on the device, one host wait per batch)")
+        elif mode == "exact":
             how = ("protocol B: each GPU receives only the ranges intersecting its keys; RCCL MAX all-reduce of "
                    "conflict flags + all-gather of overlap edges + all-gather for the compaction window"
                    if sparse else

@@ -48,6 +48,16 @@ class Config(C.Structure):
     ]
 
 
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.c_uint64)
+
+
+class CommOps(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("allreduce_max_u8", ALLREDUCE_FN), ("allgather_u8", ALLGATHER_FN)]
+
+
+COMM_ID_BYTES = 128
+
 # (name, restype, argtypes) for every function declared in include/fdbcs.h
 FDBCS_FUNCS = [
     ("fdbcs_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int64, C.POINTER(Config)]),
@@ -109,6 +119,18 @@ FDBCS_FUNCS = [
     ("fdbcs_sample_entry", C.c_int32, [C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.POINTER(C.c_int64)]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
+    ("fdbcs_comm_unique_id", C.c_int, [C.c_void_p]),
+    ("fdbcs_sharded_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int64, C.POINTER(Config), C.c_void_p, C.POINTER(CommOps)]),
+    ("fdbcs_sharded_destroy", None, [C.c_void_p]),
+    ("fdbcs_sharded_clear", C.c_int, [C.c_void_p, C.c_int64]),
+    ("fdbcs_sharded_batch_begin", C.c_int, [C.c_void_p]),
+    ("fdbcs_sharded_batch_add", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
+    ("fdbcs_sharded_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_sharded_detect_device", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
+    ("fdbcs_sharded_local", C.c_void_p, [C.c_void_p]),
+    ("fdbcs_sharded_removal_key_owner", C.c_int32, [C.c_void_p]),
+    ("fdbcs_sharded_header_version", C.c_int64, [C.c_void_p]),
 ]
 
 WL_FUNCS = [

@@ -68,7 +68,8 @@ def build_hip(verbose=False):
     with ThreadPoolExecutor(workers) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if _stale(LIB, objs):
-        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs], verbose)
+        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl"],
+             verbose)
     return LIB
 
 

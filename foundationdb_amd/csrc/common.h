@@ -202,6 +202,11 @@ struct Scalars {
     int32_t n_comb_own;     // combined ranges whose begin lies in this shard (all of them unsharded)
     int32_t dec_wide;       // rounds mode: the candidate list overflowed (every read is a candidate)
     int32_t n_pot;          // rounds mode: entries in the candidate read list
+    // fdbcs_sharded (SURVEY.md §8e protocol A, exchanges on the device)
+    int32_t carry_dev;      // nonzero: the read check / merge take valueBefore-of-shard from carry_check / carry_apply
+    int32_t sh_rk_owner;    // shard holding removalKey (-1: "")
+    int64_t carry_check;    // after the previous merge (step 7)
+    int64_t carry_apply;    // after the previous compaction (from exchange 1)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 

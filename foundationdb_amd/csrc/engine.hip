@@ -1542,3 +1542,288 @@ int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t
     }
     return cs->sc_host->last_err;
 }
+
+// ============================================= exact sharded resolver ====
+// fdbcs_sharded: one Resolver over G GPUs (SURVEY.md §8e protocol A) behind
+// the C ABI.  Rank g's engine holds the keys [bound[g-1], bound[g]); every
+// rank receives the whole batch.  Per batch, all on the engine's stream:
+//   check (history read check clipped to the shard, carry-in from the
+//   device) -> exchange 1: MAX all-reduce of [G slots | T abort flags] ->
+//   k_sh_carry -> the decision (identical on every rank; verdicts to
+//   host-mapped memory) -> combine -> this shard's merge -> exchange 2:
+//   all-gather of (H, g0, last, own begins) -> k_sh_plan (compaction part,
+//   next removalKey's owner, next check's carry-in) -> compaction ->
+//   k_sh_slot_out for the next exchange 1.
+// The host waits once per batch, for the verdicts.  Exchanges: RCCL on the
+// stream (one GPU per rank), or host callbacks (fdbcs_comm_ops: tests, gloo).
+#include <rccl/rccl.h>
+
+struct fdbcs_sharded {
+    fdbcs* cs = nullptr;
+    int rank = 0, world = 1;
+    int64_t v0 = 0;
+    ncclComm_t comm = nullptr;
+    fdbcs_comm_ops ops{};
+    bool host_ops = false;
+    uint8_t* x1 = nullptr;      // device: [G slots | T flags]
+    int64_t x1_cap = 0;
+    int64_t* x2 = nullptr;      // device: [SH_WORDS send | G x SH_WORDS gathered]
+    uint8_t* hx = nullptr;      // pinned staging of the host-callback exchanges
+    size_t hx_cap = 0;
+    bool in_batch = false;
+};
+
+namespace {
+
+size_t sh_slot_bytes(const fdbcs_sharded* sh) { return (size_t)sh->world * SH_WORDS * 8; }
+
+int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
+    hipStream_t s = sh->cs->stream;
+    if (!sh->host_ops) {
+        if (ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
+        return FDBCS_OK;
+    }
+    int r;
+    if ((r = ensure_pinned(sh->hx, sh->hx_cap, n))) return r;
+    HIPOK(hipMemcpyAsync(sh->hx, dev, n, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    if (sh->ops.allreduce_max_u8(sh->ops.ctx, sh->hx, n)) return FDBCS_E_HIP;
+    HIPOK(hipMemcpyAsync(dev, sh->hx, n, hipMemcpyHostToDevice, s));
+    HIPOK(hipStreamSynchronize(s));  // (hx is reused by the next exchange)
+    return FDBCS_OK;
+}
+
+int sh_allgather(fdbcs_sharded* sh, const int64_t* dev_send, int64_t* dev_recv) {
+    hipStream_t s = sh->cs->stream;
+    const size_t n = SH_WORDS * 8;
+    if (!sh->host_ops) {
+        if (ncclAllGather(dev_send, dev_recv, n, ncclUint8, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
+        return FDBCS_OK;
+    }
+    int r;
+    if ((r = ensure_pinned(sh->hx, sh->hx_cap, n * (sh->world + 1)))) return r;
+    HIPOK(hipMemcpyAsync(sh->hx, dev_send, n, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    if (sh->ops.allgather_u8(sh->ops.ctx, sh->hx, sh->hx + n, n)) return FDBCS_E_HIP;
+    HIPOK(hipMemcpyAsync(dev_recv, sh->hx + n, n * sh->world, hipMemcpyHostToDevice, s));
+    HIPOK(hipStreamSynchronize(s));
+    return FDBCS_OK;
+}
+
+// one batch of the sharded resolver on the device-resident view v
+int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    fdbcs* cs = sh->cs;
+    int r;
+    if ((r = check_batch_shape(v))) return r;
+    const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
+    if (T && !verdict) return FDBCS_E_ARG;
+    cs->have_last_dv = false;
+    cs->edges_known = false;
+    if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
+    if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    const size_t slots = sh_slot_bytes(sh), nx = slots + (size_t)std::max<int64_t>(T, 1);
+    if ((int64_t)nx > sh->x1_cap) {  // (the slots written after the last batch are kept)
+        uint8_t* nb = nullptr;
+        if (hipMalloc((void**)&nb, 2 * nx) != hipSuccess) return FDBCS_E_NOMEM;
+        HIPOK(hipMemsetAsync(nb, 0, 2 * nx, cs->stream));
+        if (sh->x1) {
+            HIPOK(hipMemcpyAsync(nb, sh->x1, slots, hipMemcpyDeviceToDevice, cs->stream));
+            HIPOK(hipStreamSynchronize(cs->stream));
+            hipFree(sh->x1);
+        }
+        sh->x1 = nb;
+        sh->x1_cap = (int64_t)(2 * nx);
+    }
+    if (T + 64 > (int64_t)cs->vmap_cap) {
+        if (cs->vmap) hipHostFree(cs->vmap);
+        cs->vmap = cs->vmap_dev = nullptr;
+        cs->vmap_cap = 0;
+        const size_t n = (size_t)T + 64 + 4096;
+        if (hipHostMalloc((void**)&cs->vmap, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        memset(cs->vmap, 0, n);
+        HIPOK(hipHostGetDevicePointer((void**)&cs->vmap_dev, cs->vmap, 0));
+        cs->vmap_cap = n;
+        cs->vseq = 0;
+    }
+    cs->last_T = T;
+    cs->last_R = R;
+    cs->last_W = W;
+    BatchBufs& b = cs->b;
+    HistBufs& h = cs->h;
+    hipStream_t s = cs->stream;
+    Scalars* sc = cs->sc;
+    uint8_t* flags = sh->x1 + slots;
+    // 1-2: the check, clipped to this shard (carry-in: sc->carry_check)
+    const bool scatter = cs->have_quantiles && !b.large;
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), s);
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
+        cs->sorts++;
+        cs->have_quantiles = true;
+    }
+    if ((r = edges_read_check(cs, v, sh->v0))) return r;
+    if (T) launch_flags_out(b, (int)T, flags, s);
+    // 3: exchange 1
+    if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
+    launch_sh_carry(sc, reinterpret_cast<const int64_t*>(sh->x1), sh->rank, sh->v0, s);
+    if (T) launch_flags_in(b, (int)T, flags, s);
+    // 4: the decision, verdicts to host-mapped memory
+    if (++cs->vseq == 0) cs->vseq = 1;
+    const EarlyOut eo{cs->vmap_dev + 64, reinterpret_cast<uint32_t*>(cs->vmap_dev), cs->vseq};
+    cs->early_mapped = launch_decide(v, b, sc, b.verdict, s, true, T ? &eo : nullptr);
+    if (!cs->early_mapped && T) {
+        if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, vpin_scalars_off(T) + sizeof(Scalars)))) return r;
+        HIPOK(hipMemcpyAsync(cs->vpin, b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
+    }
+    HIPOK(hipEventRecord(cs->ev_verdict, s));
+    launch_combine(v, b, sc, s);
+    // 5: this shard's part of the merge (carry-in: sc->carry_apply)
+    const bool compact = new_oldest > cs->oldest;
+    launch_merge(v, b, h, cs->cur, sc, now, sh->v0, !compact, s);
+    cs->cur ^= 1;
+    // 6: exchange 2, the plan, the compaction
+    int64_t* send = sh->x2;
+    int64_t* infos = sh->x2 + SH_WORDS;
+    launch_sh_info_out(sc, send, sh->rank, s);
+    if ((r = sh_allgather(sh, send, infos))) return r;
+    launch_sh_plan(h, cs->cur, sc, infos, sh->rank, sh->world, sh->v0, compact, s);
+    if (compact) {
+        launch_compact(b, h, cs->cur, sc, new_oldest, s);  // (the window: k_sh_plan)
+        cs->cur ^= 1;
+        cs->oldest = new_oldest;
+    }
+    launch_sh_slot_out(sc, reinterpret_cast<int64_t*>(sh->x1), sh->rank, sh->world, s);
+    // the one wait: the verdicts
+    if (!T) return FDBCS_OK;
+    if ((r = verdict_wait(cs, T, verdict))) return r;
+    cs->last_dv = v;
+    cs->have_last_dv = true;
+    return FDBCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fdbcs_comm_unique_id(uint8_t* id) {
+    if (!id) return FDBCS_E_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return FDBCS_E_HIP;
+    memcpy(id, u.internal, FDBCS_COMM_ID_BYTES);
+    return FDBCS_OK;
+}
+
+int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const uint8_t* bound_bytes,
+                         const uint64_t* bound_off, const uint32_t* bound_len, int64_t v0, const fdbcs_config* cfg,
+                         const uint8_t* comm_id, const fdbcs_comm_ops* ops) {
+    if (!out) return FDBCS_E_ARG;
+    *out = nullptr;
+    if (world < 1 || world > 64 || rank < 0 || rank >= world || (!comm_id) == (!ops)) return FDBCS_E_ARG;
+    if (world > 1 && (!bound_bytes || !bound_off || !bound_len)) return FDBCS_E_ARG;
+    if (ops && (!ops->allreduce_max_u8 || !ops->allgather_u8)) return FDBCS_E_ARG;
+    fdbcs_sharded* sh = new (std::nothrow) fdbcs_sharded();
+    if (!sh) return FDBCS_E_NOMEM;
+    sh->rank = rank;
+    sh->world = world;
+    sh->v0 = v0;
+    auto fail = [&](int code) {
+        fdbcs_sharded_destroy(sh);
+        return code;
+    };
+    int r;
+    if ((r = fdbcs_create(&sh->cs, v0, cfg))) return fail(r);
+    fdbcs* cs = sh->cs;
+    // this rank's keys: [bound[rank-1], bound[rank])
+    const uint8_t* lo = rank > 0 ? bound_bytes + bound_off[rank - 1] : nullptr;
+    const uint8_t* hi = rank < world - 1 ? bound_bytes + bound_off[rank] : nullptr;
+    if ((r = fdbcs_set_shard(cs, lo, rank > 0 ? bound_len[rank - 1] : 0, rank > 0, hi,
+                             rank < world - 1 ? bound_len[rank] : 0, rank < world - 1)))
+        return fail(r);
+    if (hipMalloc((void**)&sh->x2, (size_t)(world + 1) * SH_WORDS * 8) != hipSuccess) return fail(FDBCS_E_NOMEM);
+    launch_sh_init(cs->sc, v0, true, cs->stream);
+    if (ops) {
+        sh->ops = *ops;
+        sh->host_ops = true;
+    } else {
+        ncclUniqueId u;
+        memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
+        if (ncclCommInitRank(&sh->comm, world, u, rank) != ncclSuccess) return fail(FDBCS_E_HIP);
+    }
+    // the first exchange 1: this shard's (empty) slot
+    const size_t slots = sh_slot_bytes(sh);
+    if (hipMalloc((void**)&sh->x1, 2 * (slots + 8192)) != hipSuccess) return fail(FDBCS_E_NOMEM);
+    sh->x1_cap = (int64_t)(2 * (slots + 8192));
+    HIPOK(hipMemsetAsync(sh->x1, 0, (size_t)sh->x1_cap, cs->stream));
+    launch_sh_slot_out(cs->sc, reinterpret_cast<int64_t*>(sh->x1), rank, world, cs->stream);
+    if ((r = sync_state(cs))) return fail(r);
+    *out = sh;
+    return FDBCS_OK;
+}
+
+void fdbcs_sharded_destroy(fdbcs_sharded* sh) {
+    if (!sh) return;
+    if (sh->cs) hipStreamSynchronize(sh->cs->stream);
+    if (sh->comm) ncclCommDestroy(sh->comm);
+    if (sh->x1) hipFree(sh->x1);
+    if (sh->x2) hipFree(sh->x2);
+    if (sh->hx) hipHostFree(sh->hx);
+    if (sh->cs) fdbcs_destroy(sh->cs);
+    delete sh;
+}
+
+fdbcs* fdbcs_sharded_local(fdbcs_sharded* sh) { return sh ? sh->cs : nullptr; }
+
+int fdbcs_sharded_clear(fdbcs_sharded* sh, int64_t v) {
+    if (!sh || sh->in_batch) return FDBCS_E_ARG;
+    int r;
+    if ((r = reset_history(sh->cs, v))) return r;  // oldestVersion and removalKey are kept
+    sh->v0 = v;
+    launch_sh_init(sh->cs->sc, v, false, sh->cs->stream);
+    launch_sh_slot_out(sh->cs->sc, reinterpret_cast<int64_t*>(sh->x1), sh->rank, sh->world, sh->cs->stream);
+    return sync_state(sh->cs);
+}
+
+int fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_batch, int64_t now,
+                                int64_t new_oldest, uint8_t* verdict) {
+    if (!sh || !dev_batch || sh->in_batch) return FDBCS_E_ARG;
+    return sh_run(sh, *dev_batch, now, new_oldest, verdict);
+}
+
+int fdbcs_sharded_batch_begin(fdbcs_sharded* sh) {
+    if (!sh) return FDBCS_E_ARG;
+    int r;
+    if ((r = fdbcs_batch_begin(sh->cs))) return r;
+    sh->in_batch = true;
+    return FDBCS_OK;
+}
+
+int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
+                            const fdbcs_range* writes, int32_t nwrites) {
+    if (!sh) return FDBCS_E_ARG;
+    if (!sh->in_batch) return FDBCS_E_STATE;
+    return fdbcs_batch_add(sh->cs, read_snapshot, reads, nreads, writes, nwrites);
+}
+
+int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    if (!sh) return FDBCS_E_ARG;
+    if (!sh->in_batch) return FDBCS_E_STATE;
+    fdbcs* cs = sh->cs;
+    sh->in_batch = false;
+    cs->in_batch = false;
+    fdbcs_batch_view dv;
+    int r;
+    if ((r = cs->st.finish(dv))) return r;
+    return sh_run(sh, dv, now, new_oldest, verdict);
+}
+
+int32_t fdbcs_sharded_removal_key_owner(fdbcs_sharded* sh) {
+    if (!sh) return FDBCS_E_ARG;
+    int r;
+    if ((r = sync_state(sh->cs))) return r;
+    return sh->cs->sc_host->sh_rk_owner;
+}
+
+int64_t fdbcs_sharded_header_version(const fdbcs_sharded* sh) { return sh ? sh->v0 : 0; }
+
+}  // extern "C"

@@ -123,7 +123,7 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
     const int64_t s = A.read_snap[r];
     Key b = A.keys.get(2 * (int64_t)r), e = A.keys.get(2 * (int64_t)r + 1);
     const int D = A.sc->D;
-    const int64_t v0 = A.v0;
+    const int64_t v0 = A.sc->carry_dev ? A.sc->carry_check : A.v0;
     if (s == INT64_MAX) return;
     if (A.shard.has_lo | A.shard.has_hi) {  // the part of [b, e) in this shard (protocol A step 2)
         if (A.shard.below(b)) b = A.shard.lo;

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     const bool found = wh.feq[we] & 1;
     // valueBefore(e) fell back to the header version: the merge's v0 (sharded
     // mode: the exact carry-in, which may differ from the one the search saw)
-    const int64_t vb = (wh.feq[we] & 2) ? v0 : wh.vb[we];
+    const int64_t vb = (wh.feq[we] & 2) ? (sc->carry_dev ? sc->carry_apply : v0) : wh.vb[we];
     // sharded mode (protocol A step 5): a range acts on this shard iff b < hi
     // and e >= lo; its begin node only if b >= lo, its end node only if e < hi
     // (the positions of keys outside the shard clamp to the shard's ends)
@@ -1269,6 +1269,160 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        b.win_keep, b.win_cnt, h.free_stack, da);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
+}
+
+// ------------------------------------------------ fdbcs_sharded (device) ----
+// SURVEY.md §8e protocol A with its exchanges and host-side arithmetic moved
+// onto the device (foundationdb_amd/sharded.py holds the same steps in
+// Python): slots of exchange 1 (k_sh_slot_out), the apply carry-in
+// (k_sh_carry), this shard's (H, g0, last, own begins) for exchange 2
+// (k_sh_info_out), and the compaction plan over global indices + the next
+// removalKey's owner (k_sh_plan, SkipList.cpp:665-702 over the concatenated
+// shards).  Slots / infos are SH_WORDS int64 per shard.
+__global__ __launch_bounds__(64) void k_sh_init(Scalars* sc, int64_t v0, int reset_owner) {
+    if (threadIdx.x == 0) {
+        sc->carry_dev = 1;
+        sc->carry_check = v0;
+        sc->carry_apply = v0;
+        if (reset_owner) sc->sh_rk_owner = -1;
+    }
+}
+
+// after a batch: this shard's (H, last version) in its slot, zeros elsewhere
+// (exchange 1 is a byte-wise MAX all-reduce, so it delivers every slot)
+__global__ __launch_bounds__(64) void k_sh_slot_out(const Scalars* sc, int64_t* slots, int rank, int G) {
+    for (int i = threadIdx.x; i < SH_WORDS * G; i += blockDim.x) {
+        const int k = i % SH_WORDS;
+        int64_t v = 0;
+        if (i / SH_WORDS == rank) v = k == 0 ? sc->H : (k == 1 ? (sc->H ? sc->last_ver : INT64_MIN) : 0);
+        slots[i] = v;
+    }
+}
+
+// step 4: the carry-in of the apply -- the last version of the nearest
+// earlier non-empty shard after the previous compaction, or v0
+__global__ __launch_bounds__(64) void k_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0) {
+    if (threadIdx.x != 0) return;
+    int64_t cur = v0;
+    for (int g = 0; g < rank; g++)
+        if (slots[g * SH_WORDS] > 0) cur = slots[g * SH_WORDS + 1];
+    sc->carry_apply = cur;
+}
+
+// exchange 2's contribution after the merge: (H, g0, last, own begins).  g0 =
+// the first local index >= removalKey: only the owner searches (k_bmax_commit
+// before a compaction); shards below the owner hold only smaller keys (H),
+// shards above only larger ones (0); "" (no owner): 0
+__global__ __launch_bounds__(64) void k_sh_info_out(const Scalars* sc, int64_t* send, int rank) {
+    if (threadIdx.x != 0) return;
+    const int owner = sc->sh_rk_owner;
+    const int64_t H = sc->H;
+    send[0] = H;
+    send[1] = owner == rank ? sc->win_g0 : (owner < 0 ? 0 : (rank < owner ? H : 0));
+    send[2] = H ? sc->last_ver : INT64_MIN;
+    send[3] = sc->n_comb_own;
+}
+
+// steps 6-7 from exchange 2's infos: the carry-in of the next check, and with
+// a compaction the window's part in this shard (as k_win_explicit) and the
+// boundary that becomes removalKey (copied into rk by its owner)
+__global__ __launch_bounds__(64) void k_sh_plan(Pool pool, Dir dir, Scalars* sc, const int64_t* infos, int rank,
+                                                int G, int64_t v0, int compact, RemovalKey rk) {
+    __shared__ int64_t s_part[4];
+    __shared__ int64_t s_owner[2];
+    if (threadIdx.x == 0) {
+        int64_t tot = 0, carry = v0, cur = v0;
+        for (int g = 0; g < G; g++) {
+            if (g == rank) carry = cur;
+            if (infos[g * SH_WORDS] > 0) cur = infos[g * SH_WORDS + 2];
+        }
+        sc->carry_check = carry;
+        int64_t n_comb = 0, G0 = -1, off_me = 0, H_me = infos[rank * SH_WORDS];
+        for (int g = 0; g < G; g++) {
+            const int64_t H = infos[g * SH_WORDS], g0 = infos[g * SH_WORDS + 1];
+            if (g == rank) off_me = tot;
+            if (G0 < 0 && g0 < H) G0 = tot + g0;
+            tot += H;
+            n_comb += infos[g * SH_WORDS + 3];
+        }
+        int64_t a = 0, b = 0, keep = 0, prev = 0, og = -1, oi = 0;
+        if (G0 >= 0) {
+            const int64_t G1 = min(tot, G0 + 3 * n_comb + 10);
+            a = min(max(G0 - off_me, (int64_t)0), H_me);
+            b = min(max(G1 - off_me, (int64_t)0), H_me);
+            keep = off_me <= G0 && G0 < off_me + H_me;
+            if (a == 0 && a < b && !keep) {  // the node before a: the nearest earlier non-empty shard's last
+                int64_t pl = 0;
+                for (int g = 0; g < rank; g++)
+                    if (infos[g * SH_WORDS] > 0) pl = infos[g * SH_WORDS + 2];
+                prev = pl;
+            }
+            if (G1 < tot) {
+                int64_t o = 0;
+                for (int g = 0; g < G; g++) {
+                    const int64_t H = infos[g * SH_WORDS];
+                    if (o <= G1 && G1 < o + H) {
+                        og = g;
+                        oi = G1 - o;
+                        break;
+                    }
+                    o += H;
+                }
+            }
+        }
+        s_part[0] = a; s_part[1] = b; s_part[2] = keep; s_part[3] = prev;
+        s_owner[0] = og; s_owner[1] = oi;
+    }
+    __syncthreads();
+    if (!compact) return;
+    const int64_t a = s_part[0], b = s_part[1];
+    const int D = sc->D;
+    const int pA = a < b ? wave_start_search(dir.start, D, a) : 1;
+    const int pB = a < b ? wave_start_search(dir.start, D, b - 1) : 0;
+    const int og = (int)s_owner[0];
+    if (og == rank) {  // this shard holds the next removalKey: read it before the compaction moves it
+        const int64_t g = s_owner[1];
+        const int q = wave_start_search(dir.start, D, g);
+        const Key k = pool_key(pool, (int64_t)dir.page[q] * PAGE + (g - dir.start[q]));
+        if (threadIdx.x == 0) {
+            rk.hi[0] = k.hi;
+            rk.lo[0] = k.lo;
+            rk.meta[0] = k.meta;
+        }
+        const uint32_t L = key_len(k.meta);
+        if (L > 17)
+            for (uint32_t w = threadIdx.x; w < (L - 17 + 7) / 8; w += 64)
+                reinterpret_cast<uint64_t*>(rk.tail)[w] = reinterpret_cast<const uint64_t*>(k.tail)[w];
+    }
+    if (threadIdx.x == 0) {
+        sc->win_g0 = a;
+        sc->win_r0 = s_part[2] ? a + 1 : a;
+        sc->win_g1 = b;
+        sc->win_prev = s_part[3];
+        sc->win_pA = pA;
+        sc->win_pB = pB;
+        sc->win_np = pB - pA + 1 > 0 ? pB - pA + 1 : 0;
+        sc->sh_rk_owner = og;
+    }
+}
+
+void launch_sh_init(Scalars* sc, int64_t v0, bool reset_owner, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_init, dim3(1), dim3(64), 0, s, sc, v0, (int)reset_owner);
+}
+void launch_sh_slot_out(const Scalars* sc, int64_t* slots, int rank, int G, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_slot_out, dim3(1), dim3(64), 0, s, sc, slots, rank, G);
+}
+void launch_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_carry, dim3(1), dim3(64), 0, s, sc, slots, rank, v0);
+}
+void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_info_out, dim3(1), dim3(64), 0, s, sc, send, rank);
+}
+void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
+                    hipStream_t s) {
+    const RemovalKey rk{h.rk_hi, h.rk_lo, h.rk_meta, h.rk_tail};
+    hipLaunchKernelGGL(k_sh_plan, dim3(1), dim3(64), 0, s, h.pool, h.dir[cur], sc, infos, rank, G, v0, (int)compact,
+                       rk);
 }
 
 // ------------------------------------------------------------------ reset ----

@@ -159,6 +159,9 @@ __global__ __launch_bounds__(RB) void k_roll_scan(uint32_t* blk_cnt, const uint3
 __global__ __launch_bounds__(RB) void k_roll_emit(RollArgs a, const uint32_t* blk_cnt, const uint64_t* blk_boff,
                                                   int64_t* out_amount, uint32_t* out_len, uint64_t* out_off,
                                                   uint8_t* out_bytes, uint64_t cap_n, uint64_t cap_b) {
+    __shared__ const uint8_t* e_src[RB];
+    __shared__ uint64_t e_off[RB];
+    __shared__ uint32_t e_len[RB];
     const int64_t n = (int64_t)a.R + a.W;
     const int64_t pos = (int64_t)blockIdx.x * RB + threadIdx.x;
     uint32_t c = 0, b = 0, slot = 0, len = 0;
@@ -169,15 +172,27 @@ __global__ __launch_bounds__(RB) void k_roll_emit(RollArgs a, const uint32_t* bl
     }
     uint32_t ec, eb, tc, tb;
     block_scan2(c, b, ec, eb, tc, tb);
-    if (!c) return;
-    const uint64_t i = blk_cnt[blockIdx.x] + ec;
-    const uint64_t off = blk_boff[blockIdx.x] + eb;
-    if (i >= cap_n || off + len > cap_b) return;
-    out_amount[i] = x;
-    out_len[i] = len;
-    out_off[i] = off;
-    const uint8_t* src = a.key_bytes + a.key_off[slot];
-    for (uint32_t k = 0; k < len; k++) out_bytes[off + k] = src[k];
+    if (c) {
+        const uint64_t i = blk_cnt[blockIdx.x] + ec;
+        const uint64_t off = blk_boff[blockIdx.x] + eb;
+        const bool fits = i < cap_n && off + len <= cap_b;
+        if (fits) {
+            out_amount[i] = x;
+            out_len[i] = len;
+            out_off[i] = off;
+        }
+        e_src[ec] = a.key_bytes + a.key_off[slot];
+        e_off[ec] = off;
+        e_len[ec] = fits ? len : 0;
+    }
+    __syncthreads();
+    // the block's sampled keys, one after another, each copied by the whole
+    // block (a long key is not one lane's serial byte loop across the link)
+    for (uint32_t j = 0; j < tc; j++) {
+        const uint8_t* src = e_src[j];
+        uint8_t* dst = out_bytes + e_off[j];
+        for (uint32_t k = threadIdx.x; k < e_len[j]; k += RB) dst[k] = src[k];
+    }
 }
 
 template <class T>
@@ -269,6 +284,17 @@ struct FlatSample {
         arena.swap(na);
         garbage = 0;
         used = live;
+    }
+    // the metric of key k (0: not in the sample)
+    int64_t get(const uint8_t* k, uint32_t len, uint64_t h) const {
+        if (t.empty()) return 0;
+        const size_t mask = t.size() - 1;
+        for (size_t i = h & mask; t[i].st; i = (i + 1) & mask) {
+            const E& e = t[i];
+            if (e.st == 1 && e.h == h && e.len == len && (len == 0 || !memcmp(arena.data() + e.off, k, len)))
+                return e.m;
+        }
+        return 0;
     }
     // IndexedSet::addMetric (flow/IndexedSet.h:587-598) followed by the
     // erase-at-zero of StorageMetrics.actor.h:136-137 / :177-178
@@ -471,10 +497,13 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
         if (r) return r;
     }
     if (dv.txn_count < 0 || dv.read_count < 0 || dv.write_count < 0) return FDBCS_E_ARG;
-    const uint64_t seq = s->seq++;
+    const uint64_t seq = s->seq;  // (advanced once the batch is in the sample)
     const int64_t n = (int64_t)dv.read_count + dv.write_count;
     if (out_sampled) *out_sampled = 0;
-    if (n == 0 || dv.txn_count == 0) return FDBCS_OK;
+    if (n == 0 || dv.txn_count == 0) {
+        s->seq++;
+        return FDBCS_OK;
+    }
     hipStream_t st = (hipStream_t)fdbcs_stream(cs);
     const int64_t nblk = (n + RB - 1) / RB;
     if (nblk > INT32_MAX) return FDBCS_E_CAPACITY;
@@ -522,11 +551,15 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
     }
     s->queued += m;
     s->queue.push_back(std::move(g));
+    s->seq++;
     return FDBCS_OK;
 }
 
 int fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric) {
     if (!s || (len && !key)) return FDBCS_E_ARG;
+    // an entry's metric stays >= 0 (a negative one would break the prefix-sum
+    // index; the Resolver's amounts are positive and expire back to 0)
+    if (metric < 0 && s->sample.get(key, len, FlatSample::hash(key, len)) + metric < 0) return FDBCS_E_ARG;
     s->add_metric(key, len, metric);
     return FDBCS_OK;
 }

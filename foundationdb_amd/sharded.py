@@ -557,3 +557,147 @@ class DistShardedConflictSet:
 
     def close(self):
         self.shard.close()
+
+
+class _LocalEngine(ConflictSet):
+    """A non-owning view of the engine inside an fdbcs_sharded (its shard's history)."""
+
+    def __init__(self, lib, handle):
+        self._lib = lib
+        self._h = C.c_void_p(handle)
+
+    def close(self):
+        self._h = None  # (owned by the sharded set)
+
+
+class ShardedResolver:
+    """``fdbcs_sharded`` (include/fdbcs.h): one exact Resolver over G GPUs
+    behind the C ABI, one instance per rank (SURVEY.md §8e protocol A).
+
+    The per-batch protocol of this module's docstring runs inside libfdbcs on
+    the engine's stream; carry-ins, the compaction plan and removalKey's owner
+    are computed on the device, and the host waits once per batch, for the
+    verdicts.  Exchanges: RCCL (``comm_id`` from ``unique_id()`` on rank 0,
+    shared by the caller; one GPU per rank), or host collectives over a
+    torch.distributed ``group`` (gloo) -- the multi-process tests on one GPU.
+    """
+
+    def __init__(self, bounds, rank, world, device=0, v0=0, max_history=0, comm_id=None, group=None):
+        assert len(bounds) + 1 == world
+        self._lib = _abi.lib()
+        self.rank, self.world = rank, world
+        kb = b"".join(bounds)
+        offs = np.cumsum([0] + [len(b) for b in bounds])[:-1].astype(np.uint64) if bounds else np.zeros(1, np.uint64)
+        lens = np.array([len(b) for b in bounds] or [0], np.uint32)
+        kb_arr = np.frombuffer(kb + b"\0", np.uint8).copy()
+        cfg = _abi.Config(device=device, max_history=max_history)
+        h = C.c_void_p()
+        ops_p = None
+        cid = None
+        if comm_id is None:
+            self._ops = self._host_ops(group)
+            ops_p = C.byref(self._ops)
+        else:
+            cid = (C.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
+        check(self._lib.fdbcs_sharded_create(C.byref(h), rank, world, kb_arr.ctypes.data, offs.ctypes.data,
+                                             lens.ctypes.data, v0, C.byref(cfg), cid, ops_p), "fdbcs_sharded_create")
+        self._h = h
+        self.local = _LocalEngine(self._lib, self._lib.fdbcs_sharded_local(h))
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * _abi.COMM_ID_BYTES)()
+        check(_abi.lib().fdbcs_comm_unique_id(buf), "fdbcs_comm_unique_id")
+        return bytes(buf)
+
+    def _host_ops(self, group):
+        import torch
+        import torch.distributed as dist
+
+        world = self.world
+
+        def allreduce(_ctx, buf, n):
+            try:
+                t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,)))  # (in place)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+                return 0
+            except Exception:  # (an exception must not cross the C frame)
+                return 1
+
+        def allgather(_ctx, send, recv, n):
+            try:
+                s = torch.from_numpy(np.ctypeslib.as_array(send, shape=(n,)).copy())
+                out = [torch.empty(n, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(out, s, group=group)
+                np.ctypeslib.as_array(recv, shape=(n * world,))[:] = torch.cat(out).numpy()
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = (_abi.ALLREDUCE_FN(allreduce), _abi.ALLGATHER_FN(allgather))
+        return _abi.CommOps(None, self._cb[0], self._cb[1])
+
+    @property
+    def handle(self):
+        return self._h
+
+    def detect_device(self, view, now, new_oldest):
+        """view: the whole batch in device memory (every rank); returns the T verdicts."""
+        out = np.zeros(max(1, view.txn_count), np.uint8)
+        check(self._lib.fdbcs_sharded_detect_device(self._h, C.byref(view), now, new_oldest, out.ctypes.data),
+              "fdbcs_sharded_detect_device")
+        return out[:view.txn_count]
+
+    def detect_packed(self, batch, now, new_oldest):
+        import torch
+        from .batch import DeviceBatch
+
+        db = DeviceBatch(batch, torch.device("cuda", torch.cuda.current_device()))
+        return self.detect_device(db.view, now, new_oldest)
+
+    def detect_txns(self, txns, now, new_oldest):
+        """The Resolver's per-transaction calls: begin, add per (snapshot, reads, writes), detect."""
+        keep = []
+
+        def ranges(rs):
+            arr = (_abi.Range * max(1, len(rs)))()
+            for i, (b, e) in enumerate(rs):
+                bb, eb = C.create_string_buffer(bytes(b), max(1, len(b))), C.create_string_buffer(bytes(e),
+                                                                                                   max(1, len(e)))
+                keep.append((bb, eb))
+                arr[i].begin, arr[i].begin_len = C.cast(bb, C.c_void_p), len(b)
+                arr[i].end, arr[i].end_len = C.cast(eb, C.c_void_p), len(e)
+            return arr
+
+        check(self._lib.fdbcs_sharded_batch_begin(self._h), "ConflictBatch")
+        for snap, reads, writes in txns:
+            check(self._lib.fdbcs_sharded_batch_add(self._h, snap, ranges(reads), len(reads), ranges(writes),
+                                                    len(writes)), "addTransaction")
+        out = np.zeros(max(1, len(txns)), np.uint8)
+        check(self._lib.fdbcs_sharded_batch_detect(self._h, now, new_oldest, out.ctypes.data), "detectConflicts")
+        return out[:len(txns)]
+
+    def clear(self, v):
+        check(self._lib.fdbcs_sharded_clear(self._h, v), "clearConflictSet")
+
+    def removal_key_owner(self):
+        r = self._lib.fdbcs_sharded_removal_key_owner(self._h)
+        if r < -1:
+            check(int(r), "fdbcs_sharded_removal_key_owner")
+        return int(r)
+
+    def history(self):
+        """This rank's part of the history [(key, version)]."""
+        return self.local.history()
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            self.local = None
+            self._lib.fdbcs_sharded_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

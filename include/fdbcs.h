@@ -356,7 +356,10 @@ int  fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* 
 
 /* IndexedSet::addMetric on the sample without the roll or the queue
  * (flow/IndexedSet.h:587-598; StorageMetrics.actor.h's own test inserts this
- * way, :81-93).  An entry whose metric reaches 0 is erased. */
+ * way, :81-93).  An entry whose metric reaches 0 is erased.  A delta that
+ * would leave the entry's metric below 0 is refused (FDBCS_E_ARG): the
+ * Resolver's amounts are positive and expire back to 0, and the sample's
+ * prefix-sum index assumes nondecreasing prefixes. */
 int  fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric);
 
 /* TransientStorageMetricSample::poll() (StorageMetrics.actor.h:150-164):
@@ -386,6 +389,59 @@ const char* fdbcs_strerror(int status);
 
 /* Library build identification (git-independent): "fdbcs gfx950 <version>". */
 const char* fdbcs_version(void);
+
+/* ---- One Resolver over G GPUs (SURVEY.md §8e protocol A) ----------------
+ * Replaces the proxy's split over G resolvers (MasterProxyServer.actor.cpp:
+ * 242-320) with one exact resolver: the verdicts, the concatenated history,
+ * removalKey and oldestVersion equal one ConflictSet's
+ * (ConflictSet.h:27-60) bit for bit.  One process (rank) per GPU; rank g
+ * holds the keys [bound[g-1], bound[g]) and receives every transaction.
+ * Per batch two exchanges run on the engine's stream (RCCL all-reduce MAX of
+ * the abort flags + per-shard slots, all-gather of per-shard counts); the
+ * carry-ins, the compaction plan and removalKey's owner are computed on the
+ * device; the host waits once, for the verdicts. */
+typedef struct fdbcs_sharded fdbcs_sharded;
+
+#define FDBCS_COMM_ID_BYTES 128
+
+/* Host-memory collectives over the ranks (tests: torch.distributed gloo).
+ * Each returns 0 on success. */
+typedef struct fdbcs_comm_ops {
+    void* ctx;
+    /* element-wise MAX over ranks of n bytes, in place */
+    int (*allreduce_max_u8)(void* ctx, uint8_t* buf, uint64_t n);
+    /* rank r's n bytes land at recv[r * n .. (r + 1) * n) on every rank */
+    int (*allgather_u8)(void* ctx, const uint8_t* send, uint8_t* recv, uint64_t n);
+} fdbcs_comm_ops;
+
+/* An RCCL unique id (rank 0 makes it; the caller hands it to every rank). */
+int  fdbcs_comm_unique_id(uint8_t* id /* FDBCS_COMM_ID_BYTES */);
+
+/* newConflictSet() for rank `rank` of `world` (SkipList.cpp:956).  bounds:
+ * world - 1 increasing split keys (key i at bound_bytes + bound_off[i],
+ * bound_len[i] bytes).  Exactly one of comm_id (RCCL, one GPU per rank, the
+ * device from cfg) or ops (host collectives) is given. */
+int  fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const uint8_t* bound_bytes,
+                          const uint64_t* bound_off, const uint32_t* bound_len, int64_t v0,
+                          const fdbcs_config* cfg, const uint8_t* comm_id, const fdbcs_comm_ops* ops);
+void fdbcs_sharded_destroy(fdbcs_sharded* sh);
+/* clearConflictSet (SkipList.cpp:957-959), on every rank. */
+int  fdbcs_sharded_clear(fdbcs_sharded* sh, int64_t v);
+/* ConflictBatch on the sharded set: the same calls as fdbcs_batch_*, on every
+ * rank with the same transactions; every rank receives all T verdicts. */
+int  fdbcs_sharded_batch_begin(fdbcs_sharded* sh);
+int  fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
+                             const fdbcs_range* writes, int32_t nwrites);
+int  fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict);
+/* A device-resident batch view (every rank the whole batch); host verdicts. */
+int  fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_batch, int64_t now,
+                                 int64_t new_oldest, uint8_t* verdict);
+/* This rank's engine: its part of the history (fdbcs_dump_history,
+ * fdbcs_history_size); the owner's fdbcs_removal_key is removalKey. */
+fdbcs* fdbcs_sharded_local(fdbcs_sharded* sh);
+/* The rank holding removalKey (-1: removalKey is ""). */
+int32_t fdbcs_sharded_removal_key_owner(fdbcs_sharded* sh);
+int64_t fdbcs_sharded_header_version(const fdbcs_sharded* sh);
 
 #ifdef __cplusplus
 }

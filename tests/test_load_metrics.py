@@ -295,3 +295,15 @@ def test_device_roll_explicit_device_batch(gpu):
     with pytest.raises(_abi.FdbcsError):
         g.add_batch(cs, 9.0)
     cs.close()
+
+
+def test_add_metric_refuses_a_negative_total():
+    """An entry's metric never goes below 0 (the prefix-sum index)."""
+    s = IopsSample(1000)
+    s.add_metric(b"a", 5)
+    s.add_metric(b"a", -5)  # back to 0: erased
+    with pytest.raises(Exception):
+        s.add_metric(b"b", -1)
+    with pytest.raises(Exception):
+        s.add_metric(b"a", -1)
+    s.close()

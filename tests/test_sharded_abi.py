@@ -1,0 +1,121 @@
+"""fdbcs_sharded (include/fdbcs.h): one exact Resolver over G GPUs behind the
+C ABI -- the HIP engine, the protocol's exchanges and device-side carry-ins /
+compaction plan inside libfdbcs (SURVEY.md §8e protocol A).
+
+On the one-GPU test box the ranks share GPU 0 and exchange through host
+collectives over torch.distributed gloo (fdbcs_comm_ops); the RCCL path is
+the same code with the exchanges on the stream (bench.py --gpus N).  After
+every batch, every rank's verdicts, the concatenation of the ranks'
+histories, removalKey (read from the rank that owns it) and oldestVersion
+must equal one conflict set's (oracle/cpu_spec.cpp).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from gen import mixed_stream, rand_key, tiny_stream
+from oracle import CpuSpec
+
+
+def _streams(kind, seed):
+    if kind == "tiny":
+        return list(tiny_stream(seed, n_batches=25, maxlen=3))
+    if kind == "long":
+        return list(tiny_stream(seed, n_batches=20, maxlen=40))
+    return list(mixed_stream(seed, n_batches=8, max_txns=400, keyspace=3000))
+
+
+def _rank(rank, world, port, bounds, kind, seed, q):
+    import torch
+    import torch.distributed as dist
+
+    from foundationdb_amd.sharded import ShardedResolver
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        sh = ShardedResolver(bounds, rank, world, device=0)
+        out = []
+        for i, (batch, now, nold) in enumerate(_streams(kind, seed)):
+            if kind == "tiny" and i == 12:
+                sh.clear(now - 5)  # clearConflictSet mid-stream (SkipList.cpp:957-959)
+            if i % 3 == 1:  # the Resolver's per-transaction calls
+                v = sh.detect_txns(batch.txns(), now, nold)
+            else:
+                v = sh.detect_packed(batch, now, nold)
+            owner = sh.removal_key_owner()
+            rk = sh.local.removal_key() if owner == rank else None
+            out.append((v.tolist(), sh.history(), owner, rk, sh.local.oldest_version))
+        sh.close()
+        q.put((rank, out))
+    except Exception as e:  # (report, so the parent does not wait for the timeout)
+        q.put((rank, repr(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,kind", [(2, "tiny"), (3, "tiny"), (2, "long"), (2, "mixed"), (3, "mixed")])
+def test_sharded_abi_equals_one_conflict_set(gpu, world, kind):
+    rng = random.Random(world * 31 + len(kind))
+    if kind == "mixed":
+        bounds = sorted({b"k%06d" % rng.randrange(1, 3000) for _ in range(world - 1)})
+    else:
+        alpha = b"ab\x00c"
+        ks = set()
+        while len(ks) < world - 1:
+            ks.add(rand_key(rng, 3, alpha))
+        bounds = sorted(ks)
+    assert len(bounds) == world - 1
+    seed = 4321 + world + len(kind)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + random.Random(os.getpid() * 13 + world + len(kind)).randint(0, 3000)
+    procs = [ctx.Process(target=_rank, args=(r, world, port, bounds, kind, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(got[r], str), f"rank {r}: {got[r]}"
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(_streams(kind, seed)):
+        if kind == "tiny" and i == 12:
+            c.clear(now - 5)
+        vc = c.detect_packed(batch, now, nold).tolist()
+        hist = []
+        owners = set()
+        for r in range(world):
+            v, h, owner, rk, old = got[r][i]
+            assert v == vc, (i, r, np.nonzero(np.array(v) != np.array(vc))[0][:10])
+            assert old == c.oldest_version(), (i, r)
+            owners.add(owner)
+            if rk is not None:
+                assert rk == c.removal_key(), (i, r)
+            hist += h
+        assert len(owners) == 1, (i, owners)  # every rank agrees on removalKey's owner
+        if owners == {-1}:
+            assert c.removal_key() == b"", i
+        assert hist == c.history(), i
+    c.close()
+
+
+@pytest.mark.gpu
+def test_sharded_abi_rccl_one_rank(gpu):
+    """The RCCL path (exchanges on the engine's stream) with one rank: the same
+    stream as one conflict set, through both the packed and per-txn calls."""
+    from foundationdb_amd.sharded import ShardedResolver
+    sh = ShardedResolver([], 0, 1, device=0, comm_id=ShardedResolver.unique_id())
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(_streams("mixed", 99)):
+        v = sh.detect_txns(batch.txns(), now, nold) if i % 2 else sh.detect_packed(batch, now, nold)
+        assert np.array_equal(v, c.detect_packed(batch, now, nold)), i
+        assert sh.history() == c.history(), i
+        assert sh.local.removal_key() == c.removal_key(), i
+    sh.close()
+    c.close()
