@@ -207,8 +207,21 @@ struct Scalars {
     int32_t sh_rk_owner;    // shard holding removalKey (-1: "")
     int64_t carry_check;    // after the previous merge (step 7)
     int64_t carry_apply;    // after the previous compaction (from exchange 1)
+    // tail arena GC (kernels_hist.hip): the arena's two halves; new tails go to
+    // half tail_half (tail_used bytes of it), the compaction window copies the
+    // survivors' tails out of the other half, and a sweep that covered the
+    // whole history frees it
+    int32_t tail_half;
+    int32_t tail_flags;     // TF_* below
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
+
+constexpr int32_t TF_NOGC = 1;        // a survivor's tail could not be moved this sweep: no swap
+constexpr int32_t TF_FROM_START = 2;  // this sweep's first window started at boundary 0
+constexpr int32_t TF_WRAP = 4;        // this batch's window reached the end (removalKey -> "")
+
+// bytes of one half of a tail arena of `cap` bytes
+__host__ __device__ inline uint64_t tail_half_bytes(uint64_t cap) { return (cap / 2) & ~7ull; }
 
 // Intra-kernel phase timestamps for profiling builds (-DFDBCS_PHASES): block 0
 // thread 0 records the 100 MHz wall clock into Scalars::ph[i].

@@ -346,16 +346,20 @@ int grow_pool(fdbcs* cs, int64_t pages) {
     return FDBCS_OK;
 }
 
-int grow_tail(fdbcs* cs, uint64_t need) {
+// Grow the tail arena so that each half holds at least need_half bytes; each
+// old half lands at the start of the same new half (pointers relocated).
+int grow_tail(fdbcs* cs, uint64_t need_half) {
     int r;
     if ((r = sync_state(cs))) return r;
     HistBufs& h = cs->h;
-    uint64_t ncap = std::max<uint64_t>(need, h.tail_cap * 2);
+    const uint64_t ncap = std::max<uint64_t>(2 * need_half + 16, h.tail_cap * 2);
     GROWLOG("tail arena %llu -> %llu bytes\n", (unsigned long long)h.tail_cap, (unsigned long long)ncap);
     uint8_t* na = nullptr;
     if ((r = dalloc(na, (int64_t)ncap))) return r;
-    HIPOK(hipMemcpyAsync(na, h.tail_arena, cs->known_tail, hipMemcpyDeviceToDevice, cs->stream));
-    launch_relocate_tails(h, h.tail_arena, h.tail_cap, na, cs->stream);
+    const uint64_t oh = tail_half_bytes(h.tail_cap), nh = tail_half_bytes(ncap);
+    HIPOK(hipMemcpyAsync(na, h.tail_arena, oh, hipMemcpyDeviceToDevice, cs->stream));
+    HIPOK(hipMemcpyAsync(na + nh, h.tail_arena + oh, oh, hipMemcpyDeviceToDevice, cs->stream));
+    launch_relocate_tails(h, h.tail_arena, h.tail_cap, na, ncap, cs->stream);
     HIPOK(hipStreamSynchronize(cs->stream));
     dfree(h.tail_arena);
     h.tail_arena = na;
@@ -595,10 +599,15 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
         }
     }
     const uint64_t tneed = write_tail_bytes + 8 * 2 * (uint64_t)W + 64;
-    if (cs->known_tail + cs->pending_tail + tneed > cs->h.tail_cap) {
+    // merges allocate in the current half; the compaction's GC moves never
+    // take it past its middle, so since the last sync the used part is at
+    // most max(known, half / 2) plus the merges
+    const uint64_t half = tail_half_bytes(cs->h.tail_cap);
+    auto fits = [&](uint64_t pend) { return std::max(cs->known_tail, half / 2) + pend + tneed <= half; };
+    if (!fits(cs->pending_tail)) {
         if (cs->pending_tail && (r = sync_state(cs))) return r;
-        if (cs->known_tail + tneed > cs->h.tail_cap) {
-            if ((r = grow_tail(cs, cs->known_tail + 2 * tneed + (1 << 20)))) return r;
+        if (!fits(0)) {
+            if ((r = grow_tail(cs, 2 * (cs->known_tail + 2 * tneed + (1 << 20))))) return r;
         }
     }
     cs->pending_pages += need;
@@ -1155,14 +1164,13 @@ int64_t fdbcs_dump_history(fdbcs* cs, int64_t cap, int64_t* versions, uint32_t* 
     launch_gather(cs->h, cs->cur, cs->sc, out, cs->stream);
     std::vector<uint64_t> hi(H), lo(H), tail(H);
     std::vector<uint32_t> meta(H);
-    std::vector<uint8_t> arena(cs->known_tail);
+    std::vector<uint8_t> arena(cs->h.tail_cap);  // (both halves: survivors may still be in the old one)
     hipMemcpyAsync(hi.data(), out.hi, H * 8, hipMemcpyDeviceToHost, cs->stream);
     hipMemcpyAsync(lo.data(), out.lo, H * 8, hipMemcpyDeviceToHost, cs->stream);
     hipMemcpyAsync(meta.data(), out.meta, H * 4, hipMemcpyDeviceToHost, cs->stream);
     hipMemcpyAsync(versions, out.ver, H * 8, hipMemcpyDeviceToHost, cs->stream);
     hipMemcpyAsync(tail.data(), out.tail, H * 8, hipMemcpyDeviceToHost, cs->stream);
-    if (cs->known_tail)
-        hipMemcpyAsync(arena.data(), cs->h.tail_arena, cs->known_tail, hipMemcpyDeviceToHost, cs->stream);
+    hipMemcpyAsync(arena.data(), cs->h.tail_arena, cs->h.tail_cap, hipMemcpyDeviceToHost, cs->stream);
     hipError_t e = hipStreamSynchronize(cs->stream);
     dfree(out.hi); dfree(out.lo); dfree(out.meta); dfree(out.ver); dfree(out.tail);
     if (e != hipSuccess) return FDBCS_E_HIP;
@@ -1206,7 +1214,7 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     if (np + 64 > cs->h.cap_pages) {
         if ((r = grow_pool(cs, 2 * np + 1024))) return r;
     }
-    if (tail_bytes + 64 > cs->h.tail_cap) {
+    if (tail_bytes + 64 > tail_half_bytes(cs->h.tail_cap) / 2) {  // (loaded into half 0)
         if ((r = grow_tail(cs, 2 * tail_bytes + (1 << 20)))) return r;
     }
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return r;
@@ -1323,7 +1331,8 @@ int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
     if ((r = sync_state(cs))) return r;  // (detect returns before the history update ends)
     const Scalars& h = *cs->sc_host;
     const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
-                                    h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc};
+                                    h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc,
+                                    (int64_t)cs->h.tail_cap, (int64_t)h.tail_used, h.tail_half};
     const int n = std::min(cap, (int)FDBCS_STATS);
     for (int i = 0; i < n; i++) out[i] = v[i];
     return n;
@@ -1685,7 +1694,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     // 6: exchange 2, the plan, the compaction
     int64_t* send = sh->x2;
     int64_t* infos = sh->x2 + SH_WORDS;
-    launch_sh_info_out(sc, send, sh->rank, s);
+    launch_sh_info_out(sc, send, sh->rank, (h.shard.has_lo | h.shard.has_hi) != 0, s);
     if ((r = sh_allgather(sh, send, infos))) return r;
     launch_sh_plan(h, cs->cur, sc, infos, sh->rank, sh->world, sh->v0, compact, s);
     if (compact) {

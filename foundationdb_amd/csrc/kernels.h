@@ -241,14 +241,14 @@ void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s);
 void launch_gather(HistBufs& h, int cur, Scalars* sc, Pool out, hipStream_t s);
 void launch_push_free(HistBufs& h, int32_t from_top, int32_t first_id, int32_t count, hipStream_t s);
 void launch_relocate_tails(HistBufs& h, const uint8_t* old_base, uint64_t old_cap, const uint8_t* new_base,
-                           hipStream_t s);
+                           uint64_t new_cap, hipStream_t s);
 
 // fdbcs_sharded: the protocol's exchange-side steps on the device (kernels_hist.hip)
 constexpr int SH_WORDS = 4;  // int64 words per shard in exchange 1 (slots) and 2 (infos)
 void launch_sh_init(Scalars* sc, int64_t v0, bool reset_owner, hipStream_t s);
 void launch_sh_slot_out(const Scalars* sc, int64_t* slots, int rank, int G, hipStream_t s);
 void launch_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0, hipStream_t s);
-void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, hipStream_t s);
+void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, bool bounded, hipStream_t s);
 void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
                     hipStream_t s);
 

@@ -420,17 +420,42 @@ __device__ inline void copy_tail(const Key& k, uint8_t* arena, uint64_t cap, Sca
         *out = nullptr;
         return;
     }
+    const uint64_t half = tail_half_bytes(cap);
     const uint64_t padded = ((uint64_t)(L - 17) + 7) & ~7ull;
     const uint64_t o = atomicAdd((unsigned long long*)&sc->tail_used, (unsigned long long)padded);
-    if (o + padded > cap) {
+    if (o + padded > half) {
         atomicCAS(&sc->err, 0, FDBCS_E_CAPACITY);
         *out = nullptr;
         return;
     }
     const uint64_t* src = reinterpret_cast<const uint64_t*>(k.tail);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(arena + o);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(arena + (sc->tail_half ? half : 0) + o);
     for (uint64_t w = 0; w < padded / 8; w++) dst[w] = src[w];
-    *out = arena + o;
+    *out = reinterpret_cast<const uint8_t*>(dst);
+}
+
+// The compaction window's survivors move their tails out of the half being
+// freed (tail arena GC).  The moves fill the new half to at most its middle
+// (the merges' room is kept by ensure_history); past that, or with nothing to
+// move, the old pointer stays and this sweep frees nothing (TF_NOGC).
+__device__ inline const uint8_t* move_tail(const uint8_t* tail, uint32_t meta, uint8_t* arena, uint64_t cap,
+                                           Scalars* sc) {
+    const uint32_t L = key_len(meta);
+    if (L <= 17 || !tail) return tail;
+    const uint64_t half = tail_half_bytes(cap);
+    const uint8_t* from = arena + (sc->tail_half ? 0 : half);
+    if (tail < from || tail >= from + half) return tail;
+    const uint64_t padded = ((uint64_t)(L - 17) + 7) & ~7ull;
+    const uint64_t o = atomicAdd((unsigned long long*)&sc->tail_used, (unsigned long long)padded);
+    if (o + padded > half / 2) {
+        atomicAdd((unsigned long long*)&sc->tail_used, (unsigned long long)(0ull - padded));
+        atomicOr(&sc->tail_flags, TF_NOGC);
+        return tail;
+    }
+    uint64_t* dst = reinterpret_cast<uint64_t*>(arena + (sc->tail_half ? half : 0) + o);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(tail);
+    for (uint64_t w = 0; w < padded / 8; w++) dst[w] = src[w];
+    return reinterpret_cast<const uint8_t*>(dst);
 }
 
 struct DescArrays {
@@ -891,6 +916,12 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
             g0 = g1 = H;
         }
     }
+    if (lane == 0 && update_rk && !sc->err && g0 < g1) {  // tail arena GC: where this sweep stands
+        int tf = sc->tail_flags;
+        if (g0 == 0) tf = TF_FROM_START;  // a sweep from the first boundary starts here (it can move everything)
+        if (g1 >= H) tf |= TF_WRAP;
+        sc->tail_flags = tf;
+    }
     if (lane == 0) {
         sc->win_g0 = g0;
         sc->win_r0 = g0 + 1;  // the first scanned node is never removed
@@ -1077,7 +1108,8 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
 // global atomic per part
 __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars* sc,
                                                     const uint8_t* __restrict__ keep, const int32_t* __restrict__ cnt,
-                                                    const int32_t* __restrict__ free_stack, DescArrays desc) {
+                                                    const int32_t* __restrict__ free_stack, DescArrays desc,
+                                                    uint8_t* arena, uint64_t arena_cap, int gc) {
     __shared__ int32_t tmp[256 / 64 + 1];
     __shared__ long long lmax[4];
     const int np = sc->win_np;
@@ -1116,6 +1148,7 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
             const uint32_t meta = pool.meta[sidx];
             const int64_t ver = pool.ver[sidx];
             const uint8_t* tail = pool.tail[sidx];
+            if (gc) tail = move_tail(tail, meta, arena, arena_cap, sc);
             put_entry(pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
             atomicMax(&lmax[min(3, part - part0)], (long long)ver);
             if (slot == 0) put_desc(desc, part, dp, min(per, S - part * per), hi, lo, meta, tail);
@@ -1204,6 +1237,14 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
             sc->last_ver = lp >= 0 && lc > 0 ? pool_ver[(int64_t)lp * PAGE + lc - 1] : INT64_MIN;
         }
         sc->win_newpages = k;
+        const int tf = sc->tail_flags;
+        if (tf & TF_WRAP) {  // a sweep ended: if it covered everything and moved every tail, free the old half
+            if ((tf & TF_FROM_START) && !(tf & TF_NOGC)) {
+                sc->tail_half ^= 1;
+                sc->tail_used = 0;
+            }
+            sc->tail_flags = 0;
+        }
         sc->last_err = sc->err;  // end of batch: the next batch's encoder allocates from these
         sc->err = 0;
         sc->btail_used = 0;
@@ -1266,7 +1307,8 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        b.win_keep, b.win_cnt, b.desc_max);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
-                       b.win_keep, b.win_cnt, h.free_stack, da);
+                       b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap,
+                       (int)!(h.shard.has_lo | h.shard.has_hi));
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
 }
@@ -1313,14 +1355,14 @@ __global__ __launch_bounds__(64) void k_sh_carry(Scalars* sc, const int64_t* slo
 // the first local index >= removalKey: only the owner searches (k_bmax_commit
 // before a compaction); shards below the owner hold only smaller keys (H),
 // shards above only larger ones (0); "" (no owner): 0
-__global__ __launch_bounds__(64) void k_sh_info_out(const Scalars* sc, int64_t* send, int rank) {
+__global__ __launch_bounds__(64) void k_sh_info_out(const Scalars* sc, int64_t* send, int rank, int bounded) {
     if (threadIdx.x != 0) return;
     const int owner = sc->sh_rk_owner;
     const int64_t H = sc->H;
     send[0] = H;
     send[1] = owner == rank ? sc->win_g0 : (owner < 0 ? 0 : (rank < owner ? H : 0));
     send[2] = H ? sc->last_ver : INT64_MIN;
-    send[3] = sc->n_comb_own;
+    send[3] = bounded ? sc->n_comb_own : sc->n_comb;  // (one unbounded shard: every range begins in it)
 }
 
 // steps 6-7 from exchange 2's infos: the carry-in of the next check, and with
@@ -1415,8 +1457,8 @@ void launch_sh_slot_out(const Scalars* sc, int64_t* slots, int rank, int G, hipS
 void launch_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0, hipStream_t s) {
     hipLaunchKernelGGL(k_sh_carry, dim3(1), dim3(64), 0, s, sc, slots, rank, v0);
 }
-void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, hipStream_t s) {
-    hipLaunchKernelGGL(k_sh_info_out, dim3(1), dim3(64), 0, s, sc, send, rank);
+void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, bool bounded, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_info_out, dim3(1), dim3(64), 0, s, sc, send, rank, (int)bounded);
 }
 void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
                     hipStream_t s) {
@@ -1436,6 +1478,8 @@ __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int c
         sc->free_top = cap_pages - 1;
         sc->H = 0;
         sc->tail_used = 0;
+        sc->tail_half = 0;
+        sc->tail_flags = 0;
         sc->err = 0;
     }
 }
@@ -1480,20 +1524,22 @@ void launch_push_free(HistBufs& h, int32_t from_top, int32_t first_id, int32_t c
 }
 
 __global__ __launch_bounds__(256) void k_relocate(const uint8_t** p, int64_t n, const uint8_t* old_base,
-                                                  uint64_t old_cap, const uint8_t* new_base) {
+                                                  uint64_t old_half, const uint8_t* new_base, uint64_t new_half) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* t = p[i];
-    if (t >= old_base && t < old_base + old_cap) p[i] = new_base + (t - old_base);
+    if (t >= old_base && t < old_base + old_half) p[i] = new_base + (t - old_base);
+    else if (t >= old_base + old_half && t < old_base + 2 * old_half) p[i] = new_base + new_half + (t - old_base - old_half);
 }
-
+// tail pointers into an arena of old_cap bytes -> one of new_cap bytes (each half to its half)
 void launch_relocate_tails(HistBufs& h, const uint8_t* old_base, uint64_t old_cap, const uint8_t* new_base,
-                           hipStream_t s) {
+                           uint64_t new_cap, hipStream_t s) {
     const int64_t n = (int64_t)h.cap_pages * PAGE;
-    hipLaunchKernelGGL(k_relocate, dim3(cdiv(n, 256)), dim3(256), 0, s, h.pool.tail, n, old_base, old_cap, new_base);
+    const uint64_t oh = tail_half_bytes(old_cap), nh = tail_half_bytes(new_cap);
+    hipLaunchKernelGGL(k_relocate, dim3(cdiv(n, 256)), dim3(256), 0, s, h.pool.tail, n, old_base, oh, new_base, nh);
     for (int d = 0; d < 2; d++)
         hipLaunchKernelGGL(k_relocate, dim3(cdiv(h.cap_dir, 256)), dim3(256), 0, s, h.dir[d].ftail,
-                           (int64_t)h.cap_dir, old_base, old_cap, new_base);
+                           (int64_t)h.cap_dir, old_base, oh, new_base, nh);
 }
 
 }  // namespace fdbcs_dev

@@ -313,9 +313,11 @@ int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
  * window pages  [8] boundaries surviving in them  [9] transactions with
  * intra-batch sources  [10] decision rounds  [11] 1: a sort bucket
  * overflowed and the batch's endpoints were bucketed again by splitters from
- * its own sample  [12] largest sort bucket above 128 records (0: none).
+ * its own sample  [12] largest sort bucket above 128 records (0: none)
+ * [13] tail arena bytes (both halves)  [14] bytes used in its current half
+ * [15] current half (flips when a compaction sweep freed the other).
  * Returns the count written. */
-#define FDBCS_STATS 13
+#define FDBCS_STATS 16
 int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
 
 /* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the

@@ -93,7 +93,7 @@ def test_sharded_abi_equals_one_conflict_set(gpu, world, kind):
         for r in range(world):
             v, h, owner, rk, old = got[r][i]
             assert v == vc, (i, r, np.nonzero(np.array(v) != np.array(vc))[0][:10])
-            assert old == c.oldest_version(), (i, r)
+            assert old == c.oldest_version, (i, r)
             owners.add(owner)
             if rk is not None:
                 assert rk == c.removal_key(), (i, r)
