@@ -1,6 +1,6 @@
 """Aggregate rocprofv3 --pmc counter CSVs per kernel over the last N batches.
 
-usage: python scripts/pmc_summary.py gpurun_out/pmc [batches=50] [marker=k_ingest]
+usage: python scripts/pmc_summary.py gpurun_out/pmc [batches=50] [marker=k_ingest] [out.json] [history_pre]
 Each pN/ directory holds one pass.  FETCH_SIZE is doubled (gfx950 reports half
 of the bytes of wide coalesced reads: MI355X_MICROARCH.md §HBM); both
 FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KB.
@@ -57,6 +57,7 @@ def main():
         with open(sys.argv[4], "w") as f:
             json.dump({"bytes_per_batch": round(tot_f + tot_w), "fetch_bytes": round(tot_f), "write_bytes": round(tot_w),
                        "batches": batches,
+                       "history_pre": int(sys.argv[5]) if len(sys.argv) > 5 else None,
                        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over the bench workload; "
                                  "FETCH_SIZE x2 (gfx950 correction), KB->bytes; summed over all kernels of a batch",
                        "per_kernel_bytes": {k: round(2 * per_kernel[k].get("FETCH_SIZE", 0) * 1024 / batches
