@@ -99,7 +99,8 @@ CONFIG_SHAPE = {
     1: "skiplisttest keys (12 x '.' + BE32), 1R+1W",
     2: "5R+2W, uniform 16-byte keys",
     3: "5R+2W, Zipf(0.99) hot 16-byte keys over 10^6 ranks (long intra-batch chains)",
-    4: "4 point reads + 1 wide read (10^3-10^5 boundaries) + 2W, 68-100-byte keys (tail compares)",
+    4: "4 point reads + 1 wide read to the S-th boundary after its begin, S ~ logU[10^3, 10^5] (fdbcs_nth_after on "
+       "the history before the batch) + 2W, 68-100-byte keys (tail compares)",
     5: "5R+2W, uniform 16-byte keys, history preloaded to 10^8 boundaries (50 blind-write batches of 10^6)",
 }
 
@@ -165,7 +166,7 @@ def key_prefix_u64(lens, offs, kb):
     return out
 
 
-def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts):
+def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None):
     """oracle/cpu_spec.cpp (the build's CPU restatement) on the GPU box's host
     cores, on the timed batches, starting from the GPU's own steady-state
     history: 1 core (one ConflictSet, verdicts compared
@@ -181,7 +182,8 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts):
     c = CpuSpec()
     c.load_history_arrays(len(vers), vers, lens, offs, kb, v0=v0, oldest=oldest, removal_key=rk)
     t_load = time.perf_counter() - t_load
-    batches = [wl.batch(first + i) for i in range(n_max)]
+    if batches is None:
+        batches = [wl.batch(first + i) for i in range(n_max)]
     n, mism, tc = 0, 0, 0.0
     while n < n_max and tc < args.cpu_seconds:
         b, now, nold = batches[n]
@@ -286,9 +288,17 @@ def run_single(args):
     if args.prefill:
         wl.prefill(cs, 0, args.prefill)
     first = args.prefill
-    run_w = wl.prepare_run(first, args.warmup)
-    run_w.run(cs, verdicts=False)  # warmup through the Resolver's loop
-    del run_w
+    seq = cfg == 4  # config 4: each batch's wide reads are drawn from the history before it
+    if seq:
+        wl.set_successor(cs)  # (the prefill used the key-space-fraction wide reads: reads do not change the history)
+        for i in range(first, first + args.warmup):
+            r1 = wl.prepare_run(i, 1)
+            r1.run(cs, verdicts=False)
+            del r1
+    else:
+        run_w = wl.prepare_run(first, args.warmup)
+        run_w.run(cs, verdicts=False)  # warmup through the Resolver's loop
+        del run_w
     first += args.warmup
     H_pre = cs.history_size()
     print(f"# steady state: {args.prefill} prefill + {args.warmup} warmup batches, H={H_pre}, "
@@ -296,19 +306,35 @@ def run_single(args):
     snap = None
     if not args.no_cpu:  # the CPU baseline starts from the GPU's own steady-state history
         snap = cs.dump_arrays() + (cs.header_version, cs.oldest_version, cs.removal_key())
-    run = wl.prepare_run(first, args.steps)
-    T = run.T
     key_bytes = None
-    # ---- timed region: K batches through the Resolver's window ----------------
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    us, add_us, verdicts = run.run(cs)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    seq_batches = None
+    if seq:
+        # ---- timed: K windows, each batch generated (untimed) from the history before it ----
+        us, add_us, verdicts, seq_batches = [], [], [], []
+        for i in range(first, first + args.steps):
+            seq_batches.append(wl.batch(i))  # (the same input the run draws: the CPU baseline replays it)
+            r1 = wl.prepare_run(i, 1)
+            T = r1.T
+            u, a, v = r1.run(cs)
+            us.append(u[0])
+            add_us.append(a[0])
+            verdicts.append(v[0])
+            del r1
+        us, add_us = np.array(us), np.array(add_us)
+        elapsed = float(us.sum()) * 1e-6  # the windows only (generation excluded)
+    else:
+        run = wl.prepare_run(first, args.steps)
+        T = run.T
+        # ---- timed region: K batches through the Resolver's window ----------------
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        us, add_us, verdicts = run.run(cs)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        del run
     H_post = cs.history_size()
     value = T * args.steps / elapsed
     lat_ms = us / 1e3
-    del run
     next_i = first + args.steps
 
     # ---- packed path (secondary): whole host batch views through fdbcs_batch_detect_packed ----
@@ -421,7 +447,7 @@ def run_single(args):
 
     cpu = None
     if snap is not None:
-        cpu = cpu_baselines(args, snap, wl, first, args.steps, verdicts)
+        cpu = cpu_baselines(args, snap, wl, first, args.steps, verdicts, batches=seq_batches)
     shim = shim_skiplisttest() if cfg == 2 and not args.no_shim else None
     workload = f"config{cfg}: {T}-txn batches, {CONFIG_SHAPE.get(cfg, '')}, 5M-version window"
     out = {

@@ -120,6 +120,8 @@ FDBCS_FUNCS = [
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
     ("fdbcs_comm_unique_id", C.c_int, [C.c_void_p]),
+    ("fdbcs_nth_after", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_uint32, C.c_void_p]),
     ("fdbcs_sharded_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_int64, C.POINTER(Config), C.c_void_p, C.POINTER(CommOps)]),
     ("fdbcs_sharded_destroy", None, [C.c_void_p]),
@@ -143,6 +145,8 @@ WL_FUNCS = [
     ("fdbwl_run_txns", C.c_int32, [C.c_void_p]),
     ("fdbwl_run_resolver", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fdbwl_prefill", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
+    ("fdbwl_set_successor", None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fdbwl_run_adds", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 ]
 
 _lib = None

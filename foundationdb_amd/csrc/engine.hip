@@ -1836,3 +1836,87 @@ int32_t fdbcs_sharded_removal_key_owner(fdbcs_sharded* sh) {
 int64_t fdbcs_sharded_header_version(const fdbcs_sharded* sh) { return sh ? sh->v0 : 0; }
 
 }  // extern "C"
+
+// ================================================== history queries ====
+extern "C" int fdbcs_nth_after(fdbcs* cs, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off,
+                               const uint32_t* key_len, const int64_t* steps, uint8_t* out, uint32_t out_stride,
+                               int32_t* out_len) {
+    if (!cs || n < 0 || (n && (!key_bytes || !key_off || !key_len || !steps || !out || !out_len))) return FDBCS_E_ARG;
+    if (n == 0) return FDBCS_OK;
+    hipStream_t s = cs->stream;
+    // the queries, encoded; tails 8-byte aligned and zero padded (tail_cmp reads whole words)
+    std::vector<uint64_t> hi(n), lo(n);
+    std::vector<uint32_t> meta(n);
+    std::vector<uint64_t> toff(n, ~0ull);
+    uint64_t tbytes = 0;
+    for (int32_t i = 0; i < n; i++) {
+        if (key_len[i] > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+        encode_host(key_bytes + key_off[i], key_len[i], hi[i], lo[i], meta[i]);
+        if (key_len[i] > 17) {
+            toff[i] = tbytes;
+            tbytes += ((uint64_t)key_len[i] - 17 + 7) & ~7ull;
+        }
+    }
+    std::vector<uint8_t> tails(tbytes + 8, 0);
+    for (int32_t i = 0; i < n; i++)
+        if (key_len[i] > 17) memcpy(tails.data() + toff[i], key_bytes + key_off[i] + 17, key_len[i] - 17);
+    const uint32_t tstride = out_stride > 17 ? ((out_stride - 17 + 7) & ~7u) : 8;
+    uint64_t *dhi = nullptr, *dlo = nullptr, *dout = nullptr;
+    uint32_t* dmeta = nullptr;
+    const uint8_t** dtp = nullptr;
+    uint8_t *dtails = nullptr, *douttail = nullptr;
+    int64_t* dsteps = nullptr;
+    int r = FDBCS_OK;
+    auto cleanup = [&]() {
+        dfree(dhi); dfree(dlo); dfree(dmeta); dfree(dtp); dfree(dtails); dfree(dsteps); dfree(dout); dfree(douttail);
+    };
+    if ((r = dalloc(dhi, n)) || (r = dalloc(dlo, n)) || (r = dalloc(dmeta, n)) || (r = dalloc(dtp, n)) ||
+        (r = dalloc(dtails, (int64_t)tbytes + 8)) || (r = dalloc(dsteps, n)) || (r = dalloc(dout, 3 * (int64_t)n)) ||
+        (r = dalloc(douttail, (int64_t)n * tstride))) {
+        cleanup();
+        return r;
+    }
+    std::vector<const uint8_t*> tp(n, nullptr);
+    for (int32_t i = 0; i < n; i++)
+        if (key_len[i] > 17) tp[i] = dtails + toff[i];
+    hipError_t e = hipSuccess;
+    auto cp = [&](void* d, const void* h, size_t b) {
+        if (e == hipSuccess) e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, s);
+    };
+    cp(dhi, hi.data(), (size_t)n * 8);
+    cp(dlo, lo.data(), (size_t)n * 8);
+    cp(dmeta, meta.data(), (size_t)n * 4);
+    cp(dtp, tp.data(), (size_t)n * 8);
+    cp(dtails, tails.data(), tails.size());
+    cp(dsteps, steps, (size_t)n * 8);
+    NthArgs a{};
+    a.n = n; a.qhi = dhi; a.qlo = dlo; a.qmeta = dmeta; a.qtail = dtp; a.steps = dsteps;
+    a.out = dout; a.out_tail = douttail; a.tail_stride = tstride;
+    launch_nth_after(cs->h, cs->cur, cs->sc, a, s);  // (after every batch already on the stream)
+    std::vector<uint64_t> res(3 * (size_t)n);
+    std::vector<uint8_t> rtail((size_t)n * tstride);
+    if (e == hipSuccess) e = hipMemcpyAsync(res.data(), dout, res.size() * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(rtail.data(), douttail, rtail.size(), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    cleanup();
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        return FDBCS_E_HIP;
+    }
+    for (int32_t i = 0; i < n; i++) {
+        const uint64_t m = res[3 * (size_t)i + 2];
+        if (m == ~0ull) {
+            out_len[i] = -1;
+            continue;
+        }
+        const std::vector<uint8_t> k = decode_key(res[3 * (size_t)i], res[3 * (size_t)i + 1], (uint32_t)m,
+                                                  rtail.data() + (size_t)i * tstride);
+        if (k.size() > out_stride) {
+            out_len[i] = (int32_t)k.size();  // (too long for out_stride: not copied)
+            continue;
+        }
+        memcpy(out + (size_t)i * out_stride, k.data(), k.size());
+        out_len[i] = (int32_t)k.size();
+    }
+    return FDBCS_OK;
+}

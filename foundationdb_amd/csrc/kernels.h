@@ -252,4 +252,23 @@ void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, bool bounded
 void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
                     hipStream_t s);
 
+// fdbcs_nth_after (kernels_hist.hip): query keys (encoded; tails 8-byte
+// aligned, zero padded, in device memory) -> out[3q] = hi, lo, meta (~0: past
+// the end) and the tail words at out_tail + q * tail_stride
+struct NthArgs {
+    Pool pool;
+    Dir dir;
+    const Scalars* sc;
+    int n;
+    const uint64_t* qhi;
+    const uint64_t* qlo;
+    const uint32_t* qmeta;
+    const uint8_t* const* qtail;
+    const int64_t* steps;
+    uint64_t* out;
+    uint8_t* out_tail;
+    uint32_t tail_stride;
+};
+void launch_nth_after(HistBufs& h, int cur, const Scalars* sc, const NthArgs& a, hipStream_t s);
+
 }  // namespace fdbcs_dev

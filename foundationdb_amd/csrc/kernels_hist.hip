@@ -1313,6 +1313,45 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
 }
 
+// --------------------------------------------------------- nth after ----
+// fdbcs_nth_after: per query (a wavefront each) the key of the boundary
+// `step` positions after the first boundary >= key, or "none" past the end.
+__global__ __launch_bounds__(64) void k_nth_after(NthArgs A) {
+    const int q = blockIdx.x;
+    if (q >= A.n) return;
+    const int lane = threadIdx.x;
+    const Key k{A.qhi[q], A.qlo[q], A.qmeta[q], A.qtail[q]};
+    const int D = A.sc->D;
+    const int64_t H = A.dir.start[D];
+    const int p0 = wave_dir_search(A.dir, D, k);
+    const int i0 = wave_page_lb(A.pool, A.dir.page[p0], A.dir.cnt[p0], k);
+    const int64_t j = A.dir.start[p0] + i0 + A.steps[q];
+    if (j < 0 || j >= H) {
+        if (lane == 0) A.out[3 * (int64_t)q + 2] = ~0ull;
+        return;
+    }
+    const int qq = wave_start_search(A.dir.start, D, j);
+    const Key r = pool_key(A.pool, (int64_t)A.dir.page[qq] * PAGE + (j - A.dir.start[qq]));
+    if (lane == 0) {
+        A.out[3 * (int64_t)q] = r.hi;
+        A.out[3 * (int64_t)q + 1] = r.lo;
+        A.out[3 * (int64_t)q + 2] = r.meta;
+    }
+    const uint32_t L = key_len(r.meta);
+    if (L > 17)
+        for (uint32_t w = lane; w < (L - 17 + 7) / 8 && 8 * (w + 1) <= A.tail_stride; w += 64)
+            reinterpret_cast<uint64_t*>(A.out_tail + (int64_t)q * A.tail_stride)[w] =
+                reinterpret_cast<const uint64_t*>(r.tail)[w];
+}
+
+void launch_nth_after(HistBufs& h, int cur, const Scalars* sc, const NthArgs& a0, hipStream_t s) {
+    NthArgs a = a0;
+    a.pool = h.pool;
+    a.dir = h.dir[cur];
+    a.sc = sc;
+    if (a.n > 0) hipLaunchKernelGGL(k_nth_after, dim3(a.n), dim3(64), 0, s, a);
+}
+
 // ------------------------------------------------ fdbcs_sharded (device) ----
 // SURVEY.md §8e protocol A with its exchanges and host-side arithmetic moved
 // onto the device (foundationdb_amd/sharded.py holds the same steps in

@@ -63,6 +63,13 @@ struct fdbwl {
     std::vector<uint64_t> koff;
     std::vector<uint32_t> klen;
     std::vector<uint8_t> bytes;
+    // config 4: the wide read ends at the S-th boundary after its begin in the
+    // current history, answered by `succ` (the engine's
+    // fdbcs_nth_after, or the oracle's); without it, a log-uniform fraction
+    // of the tenant's key space
+    fdbwl_succ_fn succ = nullptr;
+    void* succ_ctx = nullptr;
+    std::vector<int64_t> wide_step;  // per txn: S (0: no query)
 };
 
 namespace {
@@ -125,6 +132,15 @@ void gen_chunk(fdbwl* g, int64_t index, int c0, int c1) {
                 const uint64_t tenant = rng.uniform(16);
                 put_be64(b, tenant);
                 memcpy(b + 8, kPath, 56);
+                if (is_read && k == g->shape.reads - 1 && g->succ) {
+                    // wide read [b, the S-th boundary after b), S ~ logU[1e3, 1e5]:
+                    // the begin here, the end from g->succ once the batch is generated
+                    const uint32_t n = (uint32_t)rng.range(4, 36);
+                    for (uint32_t i = 0; i < n; i++) b[64 + i] = (uint8_t)rng.next();
+                    w.set(sb, 64 + n);
+                    g->wide_step[t] = (int64_t)std::exp(std::log(1e3) + rng.u01() * (std::log(1e5) - std::log(1e3)));
+                    continue;
+                }
                 if (is_read && k == g->shape.reads - 1) {
                     // wide read over a log-uniform fraction of the tenant's space
                     const double f = std::exp(std::log(1e-3) + rng.u01() * (std::log(1e-1) - std::log(1e-3)));
@@ -244,6 +260,36 @@ int fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* v, int64_t* now, i
         for (auto& x : th) x.join();
     }
     const int cfg = g->config;
+    if (cfg == 4 && g->succ) {  // the wide reads' ends: one batched query of the history
+        const int nr = g->shape.reads;
+        std::vector<uint64_t> qoff(T);
+        std::vector<uint32_t> qlen(T);
+        std::vector<int32_t> olen(T);
+        const uint32_t stride = g->shape.stride;
+        std::vector<uint8_t> out((size_t)T * stride);
+        for (int t = 0; t < T; t++) {
+            const int64_t sb = 2 * ((int64_t)t * nr + nr - 1);
+            qoff[t] = g->koff[sb];
+            qlen[t] = g->klen[sb];
+        }
+        const int r = g->succ(g->succ_ctx, T, g->bytes.data(), qoff.data(), qlen.data(), g->wide_step.data(),
+                              out.data(), stride, olen.data());
+        if (r) return r;
+        for (int t = 0; t < T; t++) {
+            const int64_t se = 2 * ((int64_t)t * nr + nr - 1) + 1;
+            uint8_t* e = g->bytes.data() + (uint64_t)se * stride;
+            if (olen[t] < 0 || (uint32_t)olen[t] > stride) {  // past the last boundary: to the end of the key space
+                e[0] = 0xFF;
+                e[1] = 0xFF;
+                g->koff[se] = (uint64_t)se * stride;
+                g->klen[se] = 2;
+            } else {
+                memcpy(e, out.data() + (size_t)t * stride, (size_t)olen[t]);
+                g->koff[se] = (uint64_t)se * stride;
+                g->klen[se] = (uint32_t)olen[t];
+            }
+        }
+    }
     const int64_t nw = cfg == 1 ? index + 50 : (cfg == 50 ? 100000 * (index + 1) : 10000000 + index * 10000);
     if (now) *now = nw;
     if (new_oldest) *new_oldest = cfg == 1 ? index : (cfg == 50 ? 0 : nw - 5000000);
@@ -278,6 +324,18 @@ struct fdbwl_run {
 };
 
 extern "C" {
+
+void fdbwl_set_successor(fdbwl* g, fdbwl_succ_fn fn, void* ctx) {
+    if (!g) return;
+    g->succ = fn;
+    g->succ_ctx = ctx;
+    g->wide_step.assign(g->T, 0);
+}
+
+int fdbwl_succ_engine(void* cs, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off, const uint32_t* key_len,
+                      const int64_t* steps, uint8_t* out, uint32_t out_stride, int32_t* out_len) {
+    return fdbcs_nth_after((fdbcs*)cs, n, key_bytes, key_off, key_len, steps, out, out_stride, out_len);
+}
 
 fdbwl_run* fdbwl_run_prepare(fdbwl* g, int64_t first, int32_t n) {
     if (!g || n < 0) return nullptr;

@@ -67,6 +67,15 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
 /* Grow a conflict set's history through n generated batches [first, first+n)
  * (fdbcs_batch_submit_packed / fdbcs_batch_wait, generation of batch i+1
  * overlapping batch i): the bench's steady-state prefill. */
+// Config 4's wide reads end at the S-th boundary after their begin in the
+// current history; fn answers a batch of such queries (the signature of
+// fdbcs_nth_after: fdbwl_succ_engine with ctx = an fdbcs*, or the oracle's).
+typedef int (*fdbwl_succ_fn)(void* ctx, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off,
+                             const uint32_t* key_len, const int64_t* steps, uint8_t* out, uint32_t out_stride,
+                             int32_t* out_len);
+void fdbwl_set_successor(fdbwl* g, fdbwl_succ_fn fn, void* ctx);
+int fdbwl_succ_engine(void* cs, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off, const uint32_t* key_len,
+                      const int64_t* steps, uint8_t* out, uint32_t out_stride, int32_t* out_len);
 // (measurement) the adds of fdbwl_run_resolver alone, no detect
 int fdbwl_run_adds(fdbwl_run* r, fdbcs* cs, double* add_us);
 int fdbwl_prefill(fdbwl* g, fdbcs* cs, int64_t first, int32_t n);

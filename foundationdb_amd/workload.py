@@ -26,6 +26,23 @@ class Workload:
         v, now, nold = self.view(index)
         return PackedBatch.from_view(v), now, nold
 
+    def set_successor(self, source):
+        """Config 4: the wide read ends at the S-th boundary after its begin in
+        ``source``'s current history -- a ConflictSet (the
+        engine's fdbcs_nth_after) or an oracle CpuSpec (orc_nth_after); None
+        restores the log-uniform key-space fraction."""
+        if source is None:
+            self._lib.fdbwl_set_successor(self._g, None, None)
+            return
+        if hasattr(source, "_l"):  # oracle.CpuSpec
+            fn = C.cast(source._l.orc_nth_after, C.c_void_p)
+            ctx = source._h
+        else:
+            fn = C.cast(self._lib.fdbwl_succ_engine, C.c_void_p)
+            ctx = source.handle
+        self._succ_keep = source
+        self._lib.fdbwl_set_successor(self._g, fn, ctx)
+
     def prefill(self, cs, first, n):
         """Grow cs's history through batches [first, first + n) (native, pipelined)."""
         _abi.check(self._lib.fdbwl_prefill(self._g, cs.handle, first, n), "prefill")

@@ -386,6 +386,15 @@ int64_t fdbcs_sample_size(const fdbcs_sample* s);
 int64_t fdbcs_sample_queue_size(const fdbcs_sample* s);
 int32_t fdbcs_sample_entry(const fdbcs_sample* s, int64_t i, uint8_t* out, uint32_t cap, int64_t* metric);
 
+/* History query (bench / test support): for each of
+ * n keys, the key of the boundary `steps[i]` positions after the first
+ * boundary >= key i, into out + i * out_stride (out_len[i] = its length, or -1
+ * past the last boundary; a key longer than out_stride is not copied).
+ * Synchronous; sees every batch already resolved. */
+int  fdbcs_nth_after(fdbcs* cs, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off,
+                     const uint32_t* key_len, const int64_t* steps, uint8_t* out, uint32_t out_stride,
+                     int32_t* out_len);
+
 /* Human-readable message for a status code. */
 const char* fdbcs_strerror(int status);
 

@@ -405,4 +405,33 @@ int orc_load(void* p, int64_t n, const int64_t* versions, const uint32_t* key_le
     return FDBCS_OK;
 }
 
+// fdbcs_nth_after's restatement (config 4's generator): the key
+// of the boundary steps[i] positions after the first boundary >= key i.
+int orc_nth_after(void* p, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off, const uint32_t* key_len,
+                  const int64_t* steps, uint8_t* out, uint32_t out_stride, int32_t* out_len) {
+    const History& h = ((Oracle*)p)->h;
+    for (int32_t q = 0; q < n; q++) {
+        Pos pos = h.lower_bound(Key((const char*)key_bytes + key_off[q], key_len[q]));
+        int64_t left = steps[q];
+        while (h.valid(pos) && left > 0) {  // whole chunks, then within one
+            const int64_t room = (int64_t)h.ch[pos.c].k.size() - (int64_t)pos.i;
+            if (left >= room) {
+                left -= room;
+                pos = Pos{pos.c + 1, 0};
+            } else {
+                pos.i += (size_t)left;
+                left = 0;
+            }
+        }
+        if (!h.valid(pos)) {
+            out_len[q] = -1;
+            continue;
+        }
+        const Key& k = h.key(pos);
+        out_len[q] = (int32_t)k.size();
+        if (k.size() <= out_stride) memcpy(out + (size_t)q * out_stride, k.data(), k.size());
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -36,6 +36,8 @@ def make(name):
     spec = STREAMS[name]
     wl = Workload(spec["config"], txns=spec["txns"])
     cs = CpuSpec()
+    if spec["config"] == 4:  # wide reads end at the S-th boundary after their begin
+        wl.set_successor(cs)
     out = []
     t0 = time.time()
     for i in range(spec["first"], spec["first"] + spec["batches"]):

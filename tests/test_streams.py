@@ -31,8 +31,9 @@ def check_record(got, want, name, i):
     assert got["samples"] == want["samples"], f"{name} batch {i}: sampled boundaries differ"
 
 
-@pytest.mark.parametrize("name", list(STREAMS))
+@pytest.mark.parametrize("name", [n for n in STREAMS if STREAMS[n]["config"] != 4])
 def test_generator_inputs_unchanged(name):
+    """(config 4's inputs depend on the history: checked by the replays below)"""
     from foundationdb_amd.workload import Workload
     fx = load(name)
     wl = Workload(fx["config"], txns=fx["txns"])
@@ -50,8 +51,11 @@ def test_cpu_spec_reproduces_stream(name):
     fx = load(name)
     wl = Workload(fx["config"], txns=fx["txns"])
     cs = CpuSpec()
+    if fx["config"] == 4:
+        wl.set_successor(cs)
     for rec in fx["batches_out"][:CPU_PREFIX[name]]:
         b, now, nold = wl.batch(rec["index"])
+        assert batch_sha(b) == rec["input_sha256"], f"{name} batch {rec['index']}: input differs"
         v = cs.detect_packed(b, now, nold)
         assert np.array_equal(v, unpack_verdicts(rec["verdict_b64"], b.T)), f"{name} batch {rec['index']}"
         check_record(history_record(cs), rec, name, rec["index"])
@@ -67,6 +71,8 @@ def test_gpu_replays_stream(name):
     fx = load(name)
     wl = Workload(fx["config"], txns=fx["txns"])
     cs = ConflictSet(device=0, max_history=4_000_000)
+    if fx["config"] == 4:  # the wide reads' ends from the engine's own history (fdbcs_nth_after)
+        wl.set_successor(cs)
     per_txn = name in ("config2", "config3")
     for rec in fx["batches_out"]:
         i = rec["index"]
@@ -77,6 +83,7 @@ def test_gpu_replays_stream(name):
             del run
         else:
             b, now, nold = wl.batch(i)
+            assert batch_sha(b) == rec["input_sha256"], f"{name} batch {i}: input differs"
             v = cs.detect_packed(b, now, nold)
         want = unpack_verdicts(rec["verdict_b64"], len(v))
         assert np.array_equal(np.asarray(v, np.uint8), want), \
