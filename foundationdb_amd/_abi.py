@@ -167,6 +167,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m foundationdb_amd.build`")
+        # torch's ROCm runtime first: it ships its own libamdhip64 / librccl,
+        # whose sonames then satisfy this library's dependencies.  Loaded the
+        # other way round, the process holds two HIP runtimes (heap corruption
+        # at exit).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         # RTLD_GLOBAL: the workload library's bench drivers call the C ABI through it
         _lib = _bind(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL), FDBCS_FUNCS)
     return _lib

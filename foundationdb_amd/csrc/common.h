@@ -20,6 +20,8 @@ namespace fdbcs_dev {
 constexpr int SS_QT = 64;          // tail bytes kept per sort splitter (longer ones are compared as prefixes)
 constexpr int PAGE = 256;          // history page capacity (boundaries)
 constexpr int FILL = 192;          // target fill when a page is split / repacked
+constexpr int SPLIT = 224;         // a merge splits a page whose boundaries would exceed this
+constexpr int HOLE_EVERY = 3;      // a rewritten page holds a hole after every 3rd boundary (at most)
 constexpr uint32_t LEN_MASK = 0xFFFFFFu;
 
 struct Key {
@@ -136,14 +138,49 @@ struct Pool {
     // 16 (16 per page = one 128-byte line), kept by every slot writer
     // (put_entry); the first step of a cooperative page search reads it.
     uint64_t* pidx;
+    // holes: bit i of hmask[4 * page + i / 64] marks slot i of the page as a
+    // hole (below).  Bits at or above the page's slot count are zero.
+    uint64_t* hmask;
 };
 constexpr int PIDX_STRIDE = 16;
+constexpr int HM_WORDS = PAGE / 64;
+
+// Page slack ("holes").  Inserting into a dense sorted page moves every slot
+// after the insertion point; instead a page keeps holes spread through it and
+// an insertion moves only the slots up to the next hole (kernels_hist.hip
+// k_page_merge).  A hole is an exact copy (key, version, tail pointer) of the
+// real boundary before it, so lower bounds, range maxima and valueBefore read
+// through holes unchanged; only global indices (start[], the compaction
+// window, dumps) count real boundaries, and slot 0 of a page is always real.
+// A page written with n real boundaries holds them at slot m + m / g
+// (spread_slot) -- a hole after every g-th -- using spread_used(n) slots.
+__host__ __device__ inline int spread_gap(int n) {
+    if (n >= PAGE) return PAGE + 1;  // dense
+    const int g = (n - 1) / (PAGE - n + 1) + 1;  // smallest g with (n-1)/g <= PAGE-n
+    return g > HOLE_EVERY ? g : HOLE_EVERY;
+}
+__host__ __device__ inline int spread_slot(int m, int g) { return m + m / g; }
+__host__ __device__ inline int spread_used(int n) { return n > 0 ? spread_slot(n - 1, spread_gap(n)) + 1 : 0; }
+// a hole follows real boundary m (< n) of a spread page
+__host__ __device__ inline bool spread_hole_after(int m, int n, int g) { return (m + 1) % g == 0 && m + 1 < n; }
+// word w of the hole mask of a page spread with n boundaries: holes are the
+// used slots s with s % (g + 1) == g
+__host__ __device__ inline uint64_t spread_mask_word(int n, int w) {
+    const int g = spread_gap(n), used = spread_used(n);
+    uint64_t m = 0;
+    if (g > PAGE) return 0;
+    const int lo = 64 * w;
+    int s = lo + ((g - lo % (g + 1)) + (g + 1)) % (g + 1);  // first s >= lo with s % (g+1) == g
+    for (; s < lo + 64 && s < used; s += g + 1) m |= 1ull << (s - lo);
+    return m;
+}
 
 struct Dir {
     int32_t* page;      // pool page id
-    int32_t* cnt;       // boundaries in the page
+    int32_t* cnt;       // slots in use in the page (boundaries and holes)
+    int32_t* nr;        // boundaries in the page (real slots)
     int64_t* maxv;      // max version in the page
-    int64_t* start;     // global index of the page's first boundary; start[D] = H
+    int64_t* start;     // global index of the page's first boundary (prefix of nr); start[D] = H
     uint64_t* fhi;      // first key of the page (copy, for the search)
     uint64_t* flo;
     uint32_t* fmeta;
@@ -178,6 +215,7 @@ struct Scalars {
     int32_t err;            // nonzero: abort history mutation
     int32_t n_comb;         // combined write ranges
     int32_t n_aff;          // affected pages
+    int32_t n_full;         // of them, pages the merge rewrites (not in place)
     int32_t n_dep;          // dependent transactions (intra-batch)
     int32_t edges_total;
     int64_t H;              // boundaries

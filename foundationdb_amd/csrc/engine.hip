@@ -190,12 +190,13 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
     const int64_t slots = (int64_t)pages * PAGE;
     if ((r = dalloc(h.pool.hi, slots)) || (r = dalloc(h.pool.lo, slots)) || (r = dalloc(h.pool.meta, slots)) ||
         (r = dalloc(h.pool.ver, slots)) || (r = dalloc(h.pool.tail, slots)) || (r = dalloc(h.pool.pidx, slots / PIDX_STRIDE)) ||
-        (r = dalloc(h.free_stack, pages)))
+        (r = dalloc(h.pool.hmask, (int64_t)pages * HM_WORDS)) || (r = dalloc(h.free_stack, pages)))
         return r;
     h.cap_dir = pages + 1;
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
-        if ((r = dalloc(x.page, h.cap_dir)) || (r = dalloc(x.cnt, h.cap_dir)) || (r = dalloc(x.maxv, h.cap_dir)) ||
+        if ((r = dalloc(x.page, h.cap_dir)) || (r = dalloc(x.cnt, h.cap_dir)) || (r = dalloc(x.nr, h.cap_dir)) ||
+            (r = dalloc(x.maxv, h.cap_dir)) ||
             (r = dalloc(x.start, h.cap_dir + 1)) || (r = dalloc(x.fhi, h.cap_dir)) || (r = dalloc(x.flo, h.cap_dir)) ||
             (r = dalloc(x.fmeta, h.cap_dir)) || (r = dalloc(x.ftail, h.cap_dir)) ||
             (r = dalloc(x.bmax, h.cap_dir / 64 + 2)) || (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))))
@@ -207,10 +208,10 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
 
 void free_pool(HistBufs& h) {
     dfree(h.pool.hi); dfree(h.pool.lo); dfree(h.pool.meta); dfree(h.pool.ver); dfree(h.pool.tail);
-    dfree(h.pool.pidx); dfree(h.free_stack);
+    dfree(h.pool.pidx); dfree(h.pool.hmask); dfree(h.free_stack);
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
-        dfree(x.page); dfree(x.cnt); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
+        dfree(x.page); dfree(x.cnt); dfree(x.nr); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
         dfree(x.ftail); dfree(x.bmax); dfree(x.sidx);
     }
 }
@@ -320,11 +321,13 @@ int grow_pool(fdbcs* cs, int64_t pages) {
     HIPOK(hipMemcpyAsync(h.pool.ver, old.pool.ver, os * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.tail, old.pool.tail, os * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.pidx, old.pool.pidx, os / PIDX_STRIDE * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.hmask, old.pool.hmask, (size_t)old.cap_pages * HM_WORDS * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.free_stack, old.free_stack, (size_t)old.cap_pages * 4, hipMemcpyDeviceToDevice, s));
     const size_t od = (size_t)old.cap_dir;
     for (int d = 0; d < 2; d++) {
         HIPOK(hipMemcpyAsync(h.dir[d].page, old.dir[d].page, od * 4, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].cnt, old.dir[d].cnt, od * 4, hipMemcpyDeviceToDevice, s));
+        HIPOK(hipMemcpyAsync(h.dir[d].nr, old.dir[d].nr, od * 4, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].maxv, old.dir[d].maxv, od * 8, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].start, old.dir[d].start, (od + 1) * 8, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].fhi, old.dir[d].fhi, od * 8, hipMemcpyDeviceToDevice, s));
@@ -376,12 +379,11 @@ int alloc_keys(KeyArrays& k, int64_t n) {
 void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.tail); }
 
 void free_plan(BatchBufs& b) {
-    dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff); dfree(b.acc.fmin);
-    dfree(b.aff_f);
+    dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff);
     dfree(b.blk_agg); dfree(b.blk_diff);
     dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn); dfree(b.aff_parts);
     dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off); dfree(b.aff_free_off); dfree(b.aff_start);
-    dfree(b.freed_list); dfree(b.aff_page); dfree(b.aff_cnt);
+    dfree(b.freed_list); dfree(b.full_list); dfree(b.aff_page); dfree(b.aff_cnt);
 }
 
 void free_batch(BatchBufs& b) {
@@ -396,10 +398,10 @@ void free_batch(BatchBufs& b) {
     dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
-    dfree(b.wh.vb);
+    dfree(b.wh.vb); dfree(b.wh.rb); dfree(b.wh.re);
     free_plan(b);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-    dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
+    dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_nr); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
     dfree(b.desc_fmeta); dfree(b.desc_ftail);
     dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
     dfree(b.scan_tmp);
@@ -463,7 +465,7 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
-        dfree(b.wh.vb);
+        dfree(b.wh.vb); dfree(b.wh.rb); dfree(b.wh.re);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         dfree(b.wnew); dfree(b.winv);
         if ((r = dalloc(b.wnew, 2 * n + 64)) || (r = dalloc(b.winv, 2 * n))) return r;
@@ -477,7 +479,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||
             (r = dalloc(b.ne_ins, 2 * n)) || (r = dalloc(b.wh.pb, n)) || (r = dalloc(b.wh.ib, n)) ||
             (r = dalloc(b.wh.cb, n)) || (r = dalloc(b.wh.pe, n)) || (r = dalloc(b.wh.ie, n)) ||
-            (r = dalloc(b.wh.feq, n)) || (r = dalloc(b.wh.vb, n)))
+            (r = dalloc(b.wh.feq, n)) || (r = dalloc(b.wh.vb, n)) || (r = dalloc(b.wh.rb, n)) ||
+            (r = dalloc(b.wh.re, n)))
             return r;
         cs->capW = n;
     }
@@ -559,24 +562,23 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
             (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) || (r = dalloc(b.aff_parts, n)) ||
             (r = dalloc(b.aff_nn_off, n)) || (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
             (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)) ||
-            (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)) || (r = dalloc(b.acc.fmin, n)) ||
-            (r = dalloc(b.aff_f, n)))
+            (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)) || (r = dalloc(b.full_list, n)))
             return r;
         HIPOK(hipMemsetAsync(b.acc.er, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.nn, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.diff, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.jlo, 0x7F, n * 4, s));  // "no range yet" (> any range index)
         HIPOK(hipMemsetAsync(b.acc.jhi, 0xFF, n * 4, s));  // -1
-        HIPOK(hipMemsetAsync(b.acc.fmin, 0x7F, n * 4, s));  // no slot changed yet
         cs->capDirB = cd;
     }
     // page descriptors: the merge makes at most cap_dir of them, the compaction
     // window initialises 2 per window page
     const int64_t nd = std::max<int64_t>(cd + 2, 2 * cs->capWinPages + 2);
     if (nd > cs->capDesc) {
-        dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
+        dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_nr); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
         dfree(b.desc_fmeta); dfree(b.desc_ftail);
-        if ((r = dalloc(b.desc_page, nd)) || (r = dalloc(b.desc_cnt, nd)) || (r = dalloc(b.desc_max, nd)) ||
+        if ((r = dalloc(b.desc_page, nd)) || (r = dalloc(b.desc_cnt, nd)) || (r = dalloc(b.desc_nr, nd)) ||
+            (r = dalloc(b.desc_max, nd)) ||
             (r = dalloc(b.desc_fhi, nd)) || (r = dalloc(b.desc_flo, nd)) || (r = dalloc(b.desc_fmeta, nd)) ||
             (r = dalloc(b.desc_ftail, nd)))
             return r;
@@ -1028,6 +1030,7 @@ void fdbcs_destroy(fdbcs* cs) {
         if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
     if (cs->ev_verdict) hipEventDestroy(cs->ev_verdict);
     if (cs->vmap) hipHostFree(cs->vmap);
+    cs->st.release();  // (its destructor would otherwise synchronize a destroyed stream)
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -1225,7 +1228,8 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     std::vector<uint32_t> meta(slots, 0);
     std::vector<int64_t> ver(slots, 0);
     std::vector<uint8_t> arena(tail_bytes + 8, 0);
-    std::vector<int32_t> dpage(np), dcnt(np);
+    std::vector<int32_t> dpage(np), dcnt(np), dnr(np);
+    std::vector<uint64_t> hmask((size_t)np * HM_WORDS, 0);
     std::vector<int64_t> dmax(np);
     std::vector<uint64_t> dfhi(np), dflo(np), dftail(np);
     std::vector<uint32_t> dfmeta(np);
@@ -1233,19 +1237,27 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     uint64_t toff = 0;
     for (int64_t p = 0; p < np; p++) {
         const int64_t a = n * p / np, e = n * (p + 1) / np;
+        const int pn = (int)(e - a), g = spread_gap(pn);  // pages are written with holes (common.h)
         dpage[p] = (int32_t)p;
-        dcnt[p] = (int32_t)(e - a);
+        dcnt[p] = spread_used(pn);
+        dnr[p] = pn;
+        for (int w = 0; w < HM_WORDS; w++) hmask[(size_t)p * HM_WORDS + w] = spread_mask_word(pn, w);
         int64_t mx = INT64_MIN;
         for (int64_t i = a; i < e; i++) {
-            const int64_t sl = p * PAGE + (i - a);
+            const int m = (int)(i - a);
+            const int64_t sl = p * PAGE + spread_slot(m, g);
             encode_host(key_bytes + key_off[i], key_len[i], hi[sl], lo[sl], meta[sl]);
             ver[sl] = versions[i];
             mx = std::max(mx, versions[i]);
             if (key_len[i] > 17) {
-                const uint32_t m = key_len[i] - 17;
-                memcpy(arena.data() + toff, key_bytes + key_off[i] + 17, m);
+                const uint32_t t = key_len[i] - 17;
+                memcpy(arena.data() + toff, key_bytes + key_off[i] + 17, t);
                 tail[sl] = abase + toff;
-                toff += (m + 7) & ~7u;
+                toff += (t + 7) & ~7u;
+            }
+            if (spread_hole_after(m, pn, g)) {  // the hole repeats its predecessor exactly
+                hi[sl + 1] = hi[sl]; lo[sl + 1] = lo[sl]; meta[sl + 1] = meta[sl];
+                ver[sl + 1] = ver[sl]; tail[sl + 1] = tail[sl];
             }
         }
         dmax[p] = mx;
@@ -1265,6 +1277,8 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     Dir& d = h.dir[cs->cur];
     HIPOK(hipMemcpyAsync(d.page, dpage.data(), np * 4, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.cnt, dcnt.data(), np * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d.nr, dnr.data(), np * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.hmask, hmask.data(), hmask.size() * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.maxv, dmax.data(), np * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.fhi, dfhi.data(), np * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.flo, dflo.data(), np * 8, hipMemcpyHostToDevice, s));

@@ -280,6 +280,72 @@ __device__ inline void grp_page_find2(const Group<PIDX_STRIDE>& g, const Pool& p
     i2 = W2.i; eq2 = W2.eq;
 }
 
+// ---------------------------------------------------------------- holes ----
+// Real boundaries before slot i (0 <= i <= PAGE) of a page with hole mask hm.
+__device__ inline int real_before(const uint64_t* hm, int i) {
+    int h = 0;
+#pragma unroll
+    for (int w = 0; w < HM_WORDS; w++) {
+        const int lo = 64 * w;
+        if (i >= lo + 64) h += __popcll(hm[w]);
+        else if (i > lo) h += __popcll(hm[w] & ((1ull << (i - lo)) - 1));
+    }
+    return i - h;
+}
+
+__device__ inline void load_hmask(const Pool& p, int page, uint64_t hm[HM_WORDS]) {
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p.hmask + (int64_t)page * HM_WORDS);
+    const ulonglong2 a = q[0], b = q[1];
+    hm[0] = a.x; hm[1] = a.y; hm[2] = b.x; hm[3] = b.y;
+}
+
+// the same for a page the whole wavefront works on: the mask in scalar registers
+__device__ inline uint64_t sgpr64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ inline void load_hmask_uniform(const Pool& p, int page, uint64_t hm[HM_WORDS]) {
+    load_hmask(p, page, hm);
+#pragma unroll
+    for (int w = 0; w < HM_WORDS; w++) hm[w] = sgpr64(hm[w]);
+}
+
+// The slot of real boundary r (0 <= r < real count) of a page with `used`
+// slots, by one wavefront (every lane gets the answer).
+__device__ inline int wave_select_real(const uint64_t* hm, int used, int r) {
+    const int lane = threadIdx.x & 63;
+    int flags = 0, c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int s = 4 * lane + q;
+        const bool real = s < used && !((hm[s >> 6] >> (s & 63)) & 1);
+        flags |= (int)real << q;
+        c += real;
+    }
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    int res = -1;
+    if (r >= incl - c && r < incl) {
+        int k = r - (incl - c);
+        for (int q = 0; q < 4; q++)
+            if ((flags >> q) & 1) {
+                if (k == 0) {
+                    res = 4 * lane + q;
+                    break;
+                }
+                k--;
+            }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) res = max(res, __shfl_xor(res, d));
+    return res;
+}
+
 // (pa, ia) <= (pb, ib) lexicographically
 __device__ inline bool pos_le(int pa, int ia, int pb, int ib) { return pa < pb || (pa == pb && ia <= ib); }
 __device__ inline bool pos_lt(int pa, int ia, int pb, int ib) { return pa < pb || (pa == pb && ia < ib); }

@@ -10,7 +10,9 @@ namespace fdbcs_dev {
 struct WriteHits {
     int32_t* pb;   // directory entry of b
     int32_t* ib;   // lower bound of b in its page
-    int32_t* cb;   // boundaries in b's page
+    int32_t* cb;   // boundaries (real) in b's page
+    int32_t* rb;   // real boundaries before slot ib (holes, common.h)
+    int32_t* re;   // real boundaries before slot ie
     int32_t* pe;   // directory entry of e
     int32_t* ie;   // lower bound of e in its page
     uint8_t* feq;  // e is a boundary
@@ -23,7 +25,6 @@ struct PageAcc {
     int32_t* jlo;   // first combined range touching the page
     int32_t* jhi;   // last one
     int32_t* diff;  // +1 / -1 marks of pages wholly inside a range
-    int32_t* fmin;  // first old slot a range changes (>= PAGE: none)
 };
 
 // Per-batch device working set (sized by the engine before each batch).
@@ -107,13 +108,13 @@ struct BatchBufs {
     int64_t* aff_start;  // start[] of its first output page
     int32_t* aff_page;   // its pool page and boundary count
     int32_t* aff_cnt;
-    int32_t* aff_f;      // first old slot a range changes
     int32_t* freed_list; // pages the merge frees, pushed after its pops
+    int32_t* full_list;  // affected pages the merge rewrites (not in place)
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order
     int32_t* ne_ins;     // insertion index in the old page
     // page descriptors produced by rebuilds [cap]
-    int32_t* desc_page; int32_t* desc_cnt; int64_t* desc_max;
+    int32_t* desc_page; int32_t* desc_cnt; int32_t* desc_nr; int64_t* desc_max;
     uint64_t* desc_fhi; uint64_t* desc_flo; uint32_t* desc_fmeta; const uint8_t** desc_ftail;
     // compaction window
     uint8_t* win_keep;   // [window pages * PAGE]

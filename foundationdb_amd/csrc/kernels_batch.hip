@@ -1287,6 +1287,10 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     bool eqb, eqe;
     grp_page_find2(g, A.pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
     if (g.lane != 0) return;
+    uint64_t hmb[HM_WORDS], hme[HM_WORDS];  // real positions for the merge plan's counts (holes, common.h)
+    load_hmask(A.pool, hb.page, hmb);
+    load_hmask(A.pool, he.page, hme);
+    const int nrb = A.dir.nr[hb.x];
     int64_t vb;
     bool from_v0 = false;  // no boundary below e: the header version (sharded: the carry-in)
     if (ie > 0) vb = A.pool.ver[(int64_t)he.page * PAGE + ie - 1];
@@ -1295,7 +1299,9 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     else vb = A.v0, from_v0 = true;  // (only entry 0 can be an empty page)
     A.wh.pb[w] = hb.x;
     A.wh.ib[w] = ib;
-    A.wh.cb[w] = hb.cnt;
+    A.wh.cb[w] = nrb;
+    A.wh.rb[w] = real_before(hmb, ib);
+    A.wh.re[w] = real_before(hme, ie);
     A.wh.pe[w] = he.x;
     A.wh.ie[w] = ie;
     A.wh.feq[w] = (uint8_t)(eqe | from_v0 << 1);  // the merge substitutes its own v0 for bit 1

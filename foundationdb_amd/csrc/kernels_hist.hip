@@ -112,8 +112,10 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     const int wb = (int)((sb - wbase) >> 1), we = (int)((se - wbase) >> 1);
     const Key b = cb.k.get(sb), e = ce.k.get(se);
     const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
-    const int p_b = wh.pb[wb], i_b = wh.ib[wb], c_b = wh.cb[wb];
-    const int p_e = wh.pe[we], i_e = wh.ie[we];
+    // erased boundaries are counted as real ones (r_b, r_e: real boundaries
+    // before the slots i_b, i_e; c_b: real boundaries in b's page)
+    const int p_b = wh.pb[wb], i_b = wh.ib[wb], c_b = wh.cb[wb], r_b = wh.rb[wb];
+    const int p_e = wh.pe[we], i_e = wh.ie[we], r_e = wh.re[we];
     const bool found = wh.feq[we] & 1;
     // valueBefore(e) fell back to the header version: the merge's v0 (sharded
     // mode: the exact carry-in, which may differ from the one the search saw)
@@ -137,19 +139,17 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     ie_o[j] = i_e;
     need_o[j] = (uint8_t)(need | has_b << 1);
     vb_o[j] = vb;
-    atomicMin(&acc.fmin[p_b], i_b);
-    if (p_b != p_e) atomicMin(&acc.fmin[p_e], 0);
     if (p_b == p_e) {
-        atomicAdd(&acc.er[p_b], max(0, i_e - i_b));
+        if (r_e > r_b) atomicAdd(&acc.er[p_b], r_e - r_b);
         atomicAdd(&acc.nn[p_b], has_b + need);
         atomicMin(&acc.jlo[p_b], j);
         atomicMax(&acc.jhi[p_b], j);
     } else {
-        atomicAdd(&acc.er[p_b], c_b - i_b);
+        if (c_b > r_b) atomicAdd(&acc.er[p_b], c_b - r_b);
         atomicAdd(&acc.nn[p_b], has_b);
         atomicMin(&acc.jlo[p_b], j);
         atomicMax(&acc.jhi[p_b], j);
-        atomicAdd(&acc.er[p_e], i_e);
+        if (r_e) atomicAdd(&acc.er[p_e], r_e);
         if (need) atomicAdd(&acc.nn[p_e], 1);
         atomicMin(&acc.jlo[p_e], j);
         atomicMax(&acc.jhi[p_e], j);
@@ -180,15 +180,14 @@ static constexpr int PS_BLOCK = PS_THREADS * PS_ITEMS;
 
 struct PlanItem {
     bool affected;
-    int32_t nout, parts, nn, jlo, jhi, f;
+    int32_t nout, parts, nn, jlo, jhi;
 };
 
-__device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, bool covered) {
+// cnt: the entry's real boundaries (Dir::nr)
+__device__ inline PlanItem plan_item(const PageAcc& acc, int cnt, int x, bool covered) {
     PlanItem it;
-    const int cnt = dir.cnt[x];
     it.jlo = acc.jlo[x];
     it.jhi = acc.jhi[x];
-    it.f = acc.fmin[x];
     it.nn = 0;
     if (covered) {
         it.affected = true;
@@ -202,8 +201,9 @@ __device__ inline PlanItem plan_item(const PageAcc& acc, const Dir& dir, int x, 
         it.nout = cnt;
     }
     // an emptied entry 0 stays (as an empty page): the directory never has
-    // zero entries (a shard's whole history can be erased in sharded mode)
-    it.parts = !it.affected ? 1 : (it.nout == 0 ? (x == 0 ? 1 : 0) : (it.nout <= PAGE ? 1 : cdiv(it.nout, FILL)));
+    // zero entries (a shard's whole history can be erased in sharded mode).
+    // Pages split early (SPLIT < PAGE) so that they keep holes.
+    it.parts = !it.affected ? 1 : (it.nout == 0 ? (x == 0 ? 1 : 0) : (it.nout <= SPLIT ? 1 : cdiv(it.nout, FILL)));
     return it;
 }
 
@@ -259,10 +259,10 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_aggr(Dir dir, const Scalars
         cov += dl[k];
         const int x = x0 + k;
         if (x < D) {
-            const int cnt = dir.cnt[x];
+            const int cnt = dir.nr[x];
 #pragma unroll
             for (int s = 0; s < 2; s++) {  // s = state at the block start
-                const PlanItem it = plan_item(acc, dir, x, s + cov > 0);
+                const PlanItem it = plan_item(acc, cnt, x, s + cov > 0);
                 int64_t w[3];
                 pack_item(it, cnt, w);
                 v[3 * s + 0] += w[0];
@@ -286,7 +286,7 @@ struct PlanArgs {
     const int64_t* blk_agg;
     const int32_t* blk_diff;
     int32_t *aff_list, *aff_jlo, *aff_jhi, *aff_nn, *aff_parts, *aff_nn_off, *aff_parts_off, *aff_extra_off,
-        *aff_free_off, *aff_page, *aff_cnt, *aff_f;
+        *aff_free_off, *aff_page, *aff_cnt;
     int64_t* aff_start;
 };
 
@@ -347,8 +347,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         it[k] = PlanItem{false, 0, 0, 0, 0, -1};
         w[k][0] = w[k][1] = w[k][2] = 0;
         if (x < D) {
-            cnt[k] = A.src.cnt[x];
-            it[k] = plan_item(A.acc, A.src, x, cov > 0);
+            cnt[k] = A.src.nr[x];
+            it[k] = plan_item(A.acc, cnt[k], x, cov > 0);
             pack_item(it[k], cnt[k], w[k]);
         }
         tsum[0] += w[k][0];
@@ -369,8 +369,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
                 const int a = (int)(uint32_t)ex[0];
                 A.aff_list[a] = x;
                 A.aff_page[a] = A.src.page[x];
-                A.aff_cnt[a] = cnt[k];
-                A.aff_f[a] = it[k].f;
+                A.aff_cnt[a] = A.src.cnt[x];  // slots in use
                 A.aff_jlo[a] = it[k].jlo;
                 A.aff_jhi[a] = it[k].jhi;
                 A.aff_nn[a] = it[k].nn;
@@ -382,7 +381,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
                 A.aff_start[a] = st;
             } else {
                 A.dst.page[pos] = A.src.page[x];
-                A.dst.cnt[pos] = cnt[k];
+                A.dst.cnt[pos] = A.src.cnt[x];
+                A.dst.nr[pos] = cnt[k];
                 A.dst.maxv[pos] = A.src.maxv[x];
                 A.dst.fhi[pos] = A.src.fhi[x];
                 A.dst.flo[pos] = A.src.flo[x];
@@ -396,7 +396,6 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
             A.acc.jlo[x] = INT32_MAX;
             A.acc.jhi[x] = -1;
             A.acc.diff[x] = 0;
-            A.acc.fmin[x] = INT32_MAX;
 #pragma unroll
             for (int f = 0; f < 3; f++) ex[f] += w[k][f];
         }
@@ -407,6 +406,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         const int Dn = (int)(t0 >> 32);
         const int extra = (int)(uint32_t)t1, freed = (int)(t1 >> 32);
         sc->n_aff = (int)(uint32_t)t0;
+        sc->n_full = 0;
         sc->D_next = Dn;
         sc->extra_total = extra;
         sc->free_next = (int)(top0 - extra + freed);
@@ -460,7 +460,8 @@ __device__ inline const uint8_t* move_tail(const uint8_t* tail, uint32_t meta, u
 
 struct DescArrays {
     int32_t* page;
-    int32_t* cnt;
+    int32_t* cnt;  // slots in use
+    int32_t* nr;   // boundaries
     int64_t* maxv;
     uint64_t* fhi;
     uint64_t* flo;
@@ -475,8 +476,9 @@ struct MergeArgs {
     Scalars* sc;
     const int32_t* free_stack;
     int32_t* freed_list;
+    int32_t* full_list;  // pages the in-place pass left to the rewrite
     const int32_t* aff_list;
-    const int32_t *aff_page, *aff_cnt, *aff_f;
+    const int32_t *aff_page, *aff_cnt;
     const int32_t *jlo, *jhi, *nn, *nn_off, *parts, *parts_off, *extra_off, *free_off;
     const int64_t* aff_start;
     const int32_t *pb, *ib, *pe, *ie;
@@ -496,36 +498,47 @@ __device__ inline void put_entry(const Pool& pool, int64_t d, uint64_t hi, uint6
     if ((d & (PIDX_STRIDE - 1)) == 0) pool.pidx[d / PIDX_STRIDE] = hi;
 }
 
-__device__ inline void put_desc(const DescArrays& D, int x, int page, int cnt, uint64_t hi, uint64_t lo,
+__device__ inline void put_desc(const DescArrays& D, int x, int page, int n, uint64_t hi, uint64_t lo,
                                 uint32_t meta, const uint8_t* tail) {
-    D.page[x] = page; D.cnt[x] = cnt; D.fhi[x] = hi; D.flo[x] = lo; D.fmeta[x] = meta; D.ftail[x] = tail;
+    D.page[x] = page; D.cnt[x] = spread_used(n); D.nr[x] = n;
+    D.fhi[x] = hi; D.flo[x] = lo; D.fmeta[x] = meta; D.ftail[x] = tail;
 }
 
 // K3: one wavefront per affected page (four pages per workgroup, no
 // workgroup barriers), four consecutive old slots per lane.
 //   1. plan lanes (one per combined range touching the page) mark the slots
 //      their range erases (+1 / -1 in a difference array) and count the new
-//      boundaries inserted before each old slot (b_j at ib_j, e_j at ie_j);
-//   2. slot lanes prefix-scan both: an old slot survives if no range covers
-//      it, and lands at (kept before it) + (new entries at or before it);
-//   3. every lane writes its surviving old entries, every plan lane its new
-//      ones at (new entries before it) + (kept before its slot).
-// Output pages: the first in place (the lane's old slots are loaded before any
+//      boundaries inserted before each old slot (b_j at ib_j, e_j at ie_j).
+//   2a. In place (the usual case: the page stays one page and nothing in it
+//      is erased): new boundaries are pushed right into the next hole
+//      (common.h "holes").  A carry of pending entries runs over the slots:
+//      it grows by the insertions at a slot and a hole with carry > 0 absorbs
+//      one, so the carry arriving at slot i is a saturating prefix
+//      c(i) = max(c(i-1) + a(i-1) - h(i-1), 0), scanned across the wavefront
+//      as a composition of x -> max(x + d, L).  Old boundary i moves to
+//      i + c(i) + a(i) (most do not move); the new entries at slot i land at
+//      i + c(i) + t.  Free slots past the used ones count as holes.  Only
+//      moved slots are read and written.
+//   2b. Otherwise (erasures, a split, no room to the right): the page is
+//      rewritten.  An old slot survives if no range covers it and it is not a
+//      hole; survivors and new entries are numbered in key order and spread
+//      over the output parts with fresh holes (spread_slot).
+// Output pages: the first in place (every old slot is loaded before any
 // write), the others from the free stack; a page that disappears goes back on
 // it (k_bmax_commit pushes it after every pop).  Directory entries go to the
-// positions K2 assigned.  Old slots before the first changed one keep their
-// slot when the page stays one page, so they are not rewritten.
+// positions K2 assigned.
 static constexpr int MW_WAVES = 4;  // pages in flight per workgroup
 
 struct WaveMerge {
-    int32_t er[PAGE + 1];   // erase marks (difference array), then kept-before per slot
-    int32_t ins[PAGE + 1];  // new boundaries inserted before each old slot
+    int32_t er[PAGE + 1];   // erase marks (difference array), then kept-before per slot; in place: carry
+    int32_t ins[PAGE + 1];  // new boundaries inserted before each old slot; in place: their exclusive prefix
     long long pmax[MAXP];
     // first key of each output part (its directory entry), written by whichever lane lands it
     uint64_t f_hi[MAXP], f_lo[MAXP];
     const uint8_t* f_tail[MAXP];
     uint32_t f_meta[MAXP];
     int32_t f_dp[MAXP];
+    unsigned long long hm[HM_WORDS];  // in place: the page's hole mask as holes are consumed
 };
 
 // Lanes of one wavefront exchanging data through LDS: LDS operations of a
@@ -536,14 +549,23 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// every global load of this wavefront has returned (the page is read before
+// it is written in place: all lanes' loads precede all lanes' stores)
+__device__ inline void wave_loads_done() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ inline int lane_read(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+__device__ inline bool hm_bit(const uint64_t* hm, int i) { return (hm[i >> 6] >> (i & 63)) & 1; }
 
 // A part's first entry: its directory entry is stashed in LDS (written after
 // the merge by one lane per part); parts beyond MAXP write it directly.
-__device__ inline void part_first_direct(const Dir& D, const MergeArgs& A, int a, int y, int q, int per,
-                                               int nout, int dp, uint64_t h, uint64_t l, uint32_t mt,
-                                               const uint8_t* tl) {
-    D.page[y] = dp; D.cnt[y] = min(per, nout - q * per);
+__device__ inline void part_dir(const Dir& D, const MergeArgs& A, int a, int y, int q, int per, int nout, int dp,
+                                uint64_t h, uint64_t l, uint32_t mt, const uint8_t* tl) {
+    const int n = min(per, nout - q * per);
+    D.page[y] = dp; D.cnt[y] = spread_used(n); D.nr[y] = n;
     D.fhi[y] = h; D.flo[y] = l; D.fmeta[y] = mt; D.ftail[y] = tl;
     D.start[y] = A.aff_start[a] + (int64_t)q * per;
 }
@@ -553,7 +575,7 @@ __device__ inline void part_first(WaveMerge& S, const Dir& D, const MergeArgs& A
     if (q < MAXP) {
         S.f_hi[q] = h; S.f_lo[q] = l; S.f_meta[q] = mt; S.f_tail[q] = tl; S.f_dp[q] = dp;
     } else {
-        part_first_direct(D, A, a, doff + q, q, per, nout, dp, h, l, mt, tl);
+        part_dir(D, A, a, doff + q, q, per, nout, dp, h, l, mt, tl);
     }
 }
 
@@ -575,13 +597,148 @@ __device__ inline RangePlan load_plan(const MergeArgs& A, int j) {
     return r;
 }
 
+// x -> max(x + d, L) packed as (d, L) in one 64-bit lane value; compose(x, e)
+// applies e (an earlier stretch of slots) first, then x
+__device__ inline uint64_t sat_pack(int d, int L) { return (uint64_t)(uint32_t)d | ((uint64_t)(uint32_t)L << 32); }
+__device__ inline int sat_d(uint64_t f) { return (int)(uint32_t)f; }
+__device__ inline int sat_L(uint64_t f) { return (int)(uint32_t)(f >> 32); }
+constexpr int SAT_NONE = -(1 << 28);
+
+// 2a.  Returns false (nothing written) if the new entries do not fit to the
+// right of their insertion points; S.er / S.ins then still hold step 1's marks.
+__device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S, int a, int p, int pg, int C, const uint64_t* hm,
+                               int jlo, int jhi, const RangePlan& r0, bool has0, int doff, int nn) {
+    const int lane = threadIdx.x & 63;
+    const int i0 = 4 * lane;
+    const int64_t pbase = (int64_t)pg * PAGE;
+    const int64_t omax = A.dir.maxv[p];  // no boundary is erased: the maximum only grows
+    int av[4], hv[4];
+    uint64_t f = sat_pack(0, SAT_NONE);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int i = i0 + q;
+        av[q] = S.ins[i];
+        hv[q] = i >= C || hm_bit(hm, i);  // (free slots past the used ones absorb like holes)
+        const int d = av[q] - hv[q];
+        f = sat_pack(sat_d(f) + d, max(sat_L(f) + d, 0));
+    }
+    const uint64_t incl = wave_incl_scan_op(f, sat_pack(0, SAT_NONE), [](uint64_t x, uint64_t e) {
+        return sat_pack(sat_d(e) + sat_d(x), max(sat_L(e) + sat_d(x), sat_L(x)));
+    });
+    const uint64_t ex = __shfl_up(incl, 1);
+    const uint64_t ex_fix = lane == 0 ? sat_pack(0, SAT_NONE) : ex;  // (lane 0: nothing before it)
+    int c = max(sat_d(ex_fix), sat_L(ex_fix));  // carry arriving at slot i0 (none before slot 0)
+    int cb[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        cb[q] = c;
+        c = max(c + av[q] - hv[q], 0);
+    }
+    const int last = lane_read(c, 63);
+    if (last != 0 || S.ins[PAGE] != 0) return false;  // some entries would run past the page
+    // ---- positions
+    const int isum = av[0] + av[1] + av[2] + av[3];
+    int irun = wave_incl_scan(isum) - isum;
+    uint32_t movem = 0, usem = 0;
+    int maxout = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int i = i0 + q;
+        S.ins[i] = irun;  // new entries inserted before slot i
+        S.er[i] = cb[q];  // carry arriving at slot i
+        irun += av[q];
+        if (i < C && !hv[q] && cb[q] + av[q] > 0) movem |= 1u << q;  // old boundary i moves
+        if (i < C && hv[q] && cb[q] > 0) usem |= 1u << q;            // hole i absorbs one
+        if ((movem >> q) & 1) maxout = max(maxout, i + cb[q] + av[q]);
+    }
+    if (lane == 0)
+        for (int w = 0; w < HM_WORDS; w++) S.hm[w] = hm[w];
+    wave_lds_sync();
+    // ---- read the boundaries that move, then write them
+    uint64_t ohi[4], olo[4];
+    uint32_t ometa[4];
+    int64_t over[4];
+    const uint8_t* otail[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (!((movem >> q) & 1)) continue;
+        const int64_t sl = pbase + i0 + q;
+        ohi[q] = A.pool.hi[sl]; olo[q] = A.pool.lo[sl]; ometa[q] = A.pool.meta[sl];
+        over[q] = A.pool.ver[sl]; otail[q] = A.pool.tail[sl];
+    }
+    wave_loads_done();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int i = i0 + q;
+        if ((movem >> q) & 1) put_entry(A.pool, pbase + i + cb[q] + av[q], ohi[q], olo[q], ometa[q], over[q], otail[q]);
+        if ((usem >> q) & 1) atomicAnd(&S.hm[i >> 6], ~(1ull << (i & 63)));
+    }
+    // ---- the new entries, by the plan lanes: b_j (version now), then e_j
+    int64_t vmax = omax;
+    int base = 0;
+    for (int j0 = jlo; j0 <= jhi; j0 += 64) {
+        const int j = j0 + lane;
+        const bool v = j <= jhi;
+        RangePlan r{};
+        if (v) r = j0 == jlo ? r0 : load_plan(A, j);
+        const bool eb = v && r.pb == p && r.has_b;
+        const bool ee = v && r.pe == p && r.need;
+        const int cnt = (int)eb + (int)ee;
+        const int inc = wave_incl_scan(cnt);
+        int k = base + inc - cnt;  // new entries of this page before this lane's
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            if (!(w == 0 ? eb : ee)) continue;
+            const Key kk = w == 0 ? A.rb.get(j) : A.re.get(j);
+            const int at = w == 0 ? r.ib : r.ie;
+            const int64_t ver = w == 0 ? A.now : r.vb;
+            const int out = at + S.er[at] + (k - S.ins[at]);
+            const uint8_t* tl;
+            copy_tail(kk, A.arena, A.arena_cap, A.sc, &tl);
+            put_entry(A.pool, pbase + out, kk.hi, kk.lo, kk.meta, ver, tl);
+            vmax = max(vmax, ver);
+            maxout = max(maxout, out);
+            if (out == 0) part_first(S, A.dst, A, a, doff, 0, 1, 1, pg, kk.hi, kk.lo, kk.meta, tl);
+            k++;
+        }
+        base += lane_read(inc, 63);
+    }
+    vmax = wave_reduce_max(vmax);
+    maxout = wave_reduce_max(maxout);
+    wave_lds_sync();
+    // ---- directory entry and hole mask
+    const Dir& D = A.dst;
+    if (lane < HM_WORDS) A.pool.hmask[(int64_t)pg * HM_WORDS + lane] = S.hm[lane];
+    if (lane == 0) {
+        int holes = 0;
+        for (int w = 0; w < HM_WORDS; w++) holes += __popcll(hm[w]);
+        D.page[doff] = pg;
+        D.cnt[doff] = max(C, maxout + 1);
+        D.nr[doff] = C - holes + nn;
+        D.maxv[doff] = vmax;
+        D.start[doff] = A.aff_start[a];
+        if (S.ins[1] == 0) {  // nothing inserted before slot 0: the pre-batch first key
+            const Key first = dir_first(A.dir, p);
+            D.fhi[doff] = first.hi; D.flo[doff] = first.lo; D.fmeta[doff] = first.meta; D.ftail[doff] = first.tail;
+        } else {
+            D.fhi[doff] = S.f_hi[0]; D.flo[doff] = S.f_lo[0]; D.fmeta[doff] = S.f_meta[0]; D.ftail[doff] = S.f_tail[0];
+        }
+    }
+    return true;
+}
+
+// INPLACE: the first pass over every affected page (k_page_merge); pages it
+// cannot do in place go on a list for the second (k_page_merge_full), which
+// rewrites them -- two kernels, so the short in-place path is compiled apart
+// from the register-heavy rewrite.
+template <bool INPLACE>
 __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
     const int lane = threadIdx.x & 63;
     const int p = A.aff_list[a];
     const int parts = A.parts[a];
-    const int pg = A.aff_page[a], cntp = A.aff_cnt[a];
-    if (parts == 0) {  // wholly erased: returns to the free stack in k_bmax_commit (after every pop)
+    const int pg = A.aff_page[a], cntp = A.aff_cnt[a];  // cntp: slots in use
+    if (INPLACE && parts == 0) {  // wholly erased: returns to the free stack in k_bmax_commit (after every pop)
         if (lane == 0) A.freed_list[A.free_off[a]] = pg;
         return;
     }
@@ -589,42 +746,13 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     const int nn = A.nn[a];
     const int xoff = A.extra_off[a], doff = A.parts_off[a];
     const int64_t pbase = (int64_t)pg * PAGE;
-    // ---- 0. every load the page needs, issued together (one round trip):
-    // old slots before the first changed one (f, from K1) keep their slot
-    // when the page stays one page, so they are neither rewritten nor read,
-    // except for their versions (the page maximum); this lane's old slots
-    // i0 .. i0+3 are loaded before any write (part 0 is rewritten in place);
-    // the first 64 ranges' plans; the page's first key (kept if unchanged).
-    const int64_t c0 = PCLK();
-    const int f = min(A.aff_f[a], PAGE);
-    const int u = parts == 1 ? min(f, cntp) : 0;
     const int i0 = 4 * lane;
-    uint64_t ohi[4] = {}, olo[4] = {};
-    int64_t over[4];
-    uint32_t ometa[4] = {};
-    const uint8_t* otail[4] = {};
-    {
-        const longlong2* v2 = reinterpret_cast<const longlong2*>(A.pool.ver + pbase + i0);
-        const longlong2 va = v2[0], vb = v2[1];
-        over[0] = va.x; over[1] = va.y; over[2] = vb.x; over[3] = vb.y;
-        if (i0 + 3 >= u && i0 < cntp) {
-            const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(A.pool.hi + pbase + i0);
-            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(A.pool.lo + pbase + i0);
-            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(A.pool.tail + pbase + i0);
-            const uint4 m4 = *reinterpret_cast<const uint4*>(A.pool.meta + pbase + i0);
-            const ulonglong2 ha = h2[0], hb = h2[1], la = l2[0], lb = l2[1], ta = t2[0], tb = t2[1];
-            ohi[0] = ha.x; ohi[1] = ha.y; ohi[2] = hb.x; ohi[3] = hb.y;
-            olo[0] = la.x; olo[1] = la.y; olo[2] = lb.x; olo[3] = lb.y;
-            ometa[0] = m4.x; ometa[1] = m4.y; ometa[2] = m4.z; ometa[3] = m4.w;
-            otail[0] = (const uint8_t*)ta.x; otail[1] = (const uint8_t*)ta.y;
-            otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
-        }
-    }
+    // ---- 0. the hole mask and the first 64 ranges' plans
+    uint64_t hm[HM_WORDS];
+    load_hmask_uniform(A.pool, pg, hm);
     const bool has0 = jlo + lane <= jhi;
     RangePlan r0{};
     if (has0) r0 = load_plan(A, jlo + lane);
-    Key first{};
-    if (u > 0 && lane == 0) first = dir_first(A.dir, p);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         S.er[i0 + q] = 0;
@@ -636,8 +764,8 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     }
     S.pmax[lane] = INT64_MIN;
     wave_lds_sync();
-    const int64_t c1 = PCLK();
     // ---- 1. plan lanes: erased intervals and insertion counts
+    bool erases = false;
     for (int j0 = jlo; j0 <= jhi; j0 += 64) {
         const int j = j0 + lane;
         if (j <= jhi) {
@@ -646,14 +774,39 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             if (e0 > s0) {
                 atomicAdd(&S.er[s0], 1);
                 atomicAdd(&S.er[e0], -1);
+                erases = true;
             }
             if (r.pb == p && r.has_b) atomicAdd(&S.ins[r.ib], 1);
             if (r.pe == p && r.need) atomicAdd(&S.ins[r.ie], 1);
         }
     }
     wave_lds_sync();
-    const int64_t c2 = PCLK();
-    // ---- 2. slot lanes: survivors and output positions
+    if (INPLACE) {
+        if (parts == 1 && !__ballot(erases) && merge_in_place(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
+            return;
+        if (lane == 0) A.full_list[atomicAdd(&sc->n_full, 1)] = a;
+        return;
+    }
+    // ---- 2b. rewrite: every old slot, loaded before any write
+    uint64_t ohi[4] = {}, olo[4] = {};
+    int64_t over[4] = {};
+    uint32_t ometa[4] = {};
+    const uint8_t* otail[4] = {};
+    if (i0 < cntp) {
+        const longlong2* v2 = reinterpret_cast<const longlong2*>(A.pool.ver + pbase + i0);
+        const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(A.pool.hi + pbase + i0);
+        const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(A.pool.lo + pbase + i0);
+        const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(A.pool.tail + pbase + i0);
+        const uint4 m4 = *reinterpret_cast<const uint4*>(A.pool.meta + pbase + i0);
+        const longlong2 va = v2[0], vb = v2[1];
+        const ulonglong2 ha = h2[0], hb = h2[1], la = l2[0], lb = l2[1], ta = t2[0], tb = t2[1];
+        over[0] = va.x; over[1] = va.y; over[2] = vb.x; over[3] = vb.y;
+        ohi[0] = ha.x; ohi[1] = ha.y; ohi[2] = hb.x; ohi[3] = hb.y;
+        olo[0] = la.x; olo[1] = la.y; olo[2] = lb.x; olo[3] = lb.y;
+        ometa[0] = m4.x; ometa[1] = m4.y; ometa[2] = m4.z; ometa[3] = m4.w;
+        otail[0] = (const uint8_t*)ta.x; otail[1] = (const uint8_t*)ta.y;
+        otail[2] = (const uint8_t*)tb.x; otail[3] = (const uint8_t*)tb.y;
+    }
     int ec[4], ic[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -670,7 +823,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         erun += ec[q];
         irun += ic[q];
         newb[q] = irun;
-        if (i0 + q < cntp && erun == 0) keepm |= 1u << q;
+        if (i0 + q < cntp && erun == 0 && !hm_bit(hm, i0 + q)) keepm |= 1u << q;
     }
     const int kc = __popc(keepm);
     const int kinc = wave_incl_scan(kc);
@@ -695,26 +848,24 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     }
     const Dir& D = A.dst;
     auto dest = [&](int q) -> int { return q == 0 ? pg : A.free_stack[top0 - 1 - (xoff + q - 1)]; };
+    // output entry m: part m / per, spread inside it (a hole after every g-th)
+    auto place = [&](int m, uint64_t h, uint64_t l, uint32_t mt, int64_t ver, const uint8_t* tl, int64_t& vmax) {
+        const int qq = m / per, r = m - qq * per;
+        const int n = min(per, nout - qq * per), g = spread_gap(n);
+        const int dp = dest(qq);
+        const int64_t sl = (int64_t)dp * PAGE + spread_slot(r, g);
+        put_entry(A.pool, sl, h, l, mt, ver, tl);
+        if (spread_hole_after(r, n, g)) put_entry(A.pool, sl + 1, h, l, mt, ver, tl);
+        if (parts == 1) vmax = max(vmax, ver);
+        else if (qq < MAXP) atomicMax(&S.pmax[qq], (long long)ver);
+        if (r == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, h, l, mt, tl);
+    };
     int64_t vmax = INT64_MIN;  // parts == 1: the page maximum by a wave reduction
-    const int64_t c3 = PCLK();
+    wave_loads_done();
     // ---- 3a. surviving old entries
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        if (!((keepm >> q) & 1)) continue;
-        const int i = i0 + q;
-        const int m = kb[q] + newb[q];
-        const int qq = m / per, slot = m - qq * per;
-        if (parts == 1) vmax = max(vmax, over[q]);
-        else if (qq < MAXP) atomicMax(&S.pmax[qq], (long long)over[q]);
-        if (i >= u) {
-            const int dp = dest(qq);
-            put_entry(A.pool, (int64_t)dp * PAGE + slot, ohi[q], olo[q], ometa[q], over[q], otail[q]);
-            if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, ohi[q], olo[q], ometa[q], otail[q]);
-        } else if (i == 0) {  // unchanged first slot: the pre-batch directory holds its key
-            part_first(S, D, A, a, doff, 0, per, nout, pg, first.hi, first.lo, first.meta, first.tail);
-        }
-    }
-    const int64_t c4 = PCLK();
+    for (int q = 0; q < 4; q++)
+        if ((keepm >> q) & 1) place(kb[q] + newb[q], ohi[q], olo[q], ometa[q], over[q], otail[q], vmax);
     // ---- 3b. new entries, by the plan lanes: b_j (version now), then e_j
     int base = 0;
     for (int j0 = jlo; j0 <= jhi; j0 += 64) {
@@ -733,39 +884,20 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             const Key kk = w == 0 ? A.rb.get(j) : A.re.get(j);
             const int at = w == 0 ? r.ib : r.ie;
             const int64_t ver = w == 0 ? A.now : r.vb;
-            const int m = k + S.er[at];
-            const int qq = m / per, slot = m - qq * per;
-            const int dp = dest(qq);
             const uint8_t* tl;
             copy_tail(kk, A.arena, A.arena_cap, sc, &tl);
-            put_entry(A.pool, (int64_t)dp * PAGE + slot, kk.hi, kk.lo, kk.meta, ver, tl);
-            if (parts == 1) vmax = max(vmax, ver);
-            else if (qq < MAXP) atomicMax(&S.pmax[qq], (long long)ver);
-            if (slot == 0) part_first(S, D, A, a, doff, qq, per, nout, dp, kk.hi, kk.lo, kk.meta, tl);
+            place(k + S.er[at], kk.hi, kk.lo, kk.meta, ver, tl, vmax);
             k++;
         }
         base += lane_read(inc, 63);
     }
-    const int64_t c5 = PCLK();
-    if (lane == 0) {
-        PACC(sc, 16, c1 - c0);
-        PACC(sc, 17, c2 - c1);
-        PACC(sc, 18, c3 - c2);
-        PACC(sc, 19, c4 - c3);
-        PACC(sc, 20, c5 - c4);
-        PACC(sc, 21, 1);
-    }
     if (parts == 1) vmax = wave_reduce_max(vmax);
     wave_lds_sync();  // the LDS stash of part-first entries, written by any lane
-    for (int q = lane; q < min(parts, MAXP); q += 64) {  // directory entries of the parts
-        const int y = doff + q;
-        D.page[y] = S.f_dp[q];
-        D.cnt[y] = min(per, nout - q * per);
-        D.fhi[y] = S.f_hi[q];
-        D.flo[y] = S.f_lo[q];
-        D.fmeta[y] = S.f_meta[q];
-        D.ftail[y] = S.f_tail[q];
-        D.start[y] = A.aff_start[a] + (int64_t)q * per;
+    for (int q = lane; q < min(parts, MAXP); q += 64)  // directory entries of the parts
+        part_dir(D, A, a, doff + q, q, per, nout, S.f_dp[q], S.f_hi[q], S.f_lo[q], S.f_meta[q], S.f_tail[q]);
+    for (int x = lane; x < parts * HM_WORDS; x += 64) {  // the parts' hole masks
+        const int q = x / HM_WORDS;
+        A.pool.hmask[(int64_t)dest(q) * HM_WORDS + x % HM_WORDS] = spread_mask_word(min(per, nout - q * per), x % HM_WORDS);
     }
     if (parts == 1) {
         if (lane == 0) D.maxv[doff] = vmax;
@@ -778,7 +910,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
             mx = S.pmax[q];
         } else {  // very large outputs (e.g. a first batch into an empty history)
             const int64_t bq = (int64_t)dest(q) * PAGE;
-            const int c = min(per, nout - q * per);
+            const int c = spread_used(min(per, nout - q * per));
             mx = INT64_MIN;
             // (these slots were written by this wavefront above)
             for (int i = 0; i < c; i++) mx = max(mx, A.pool.ver[bq + i]);
@@ -788,7 +920,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
 }
 
 #ifndef FDBCS_PM_WAVES
-#define FDBCS_PM_WAVES 4
+#define FDBCS_PM_WAVES 3
 #endif
 __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A) {
     __shared__ WaveMerge S[MW_WAVES];
@@ -797,16 +929,27 @@ __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A)
     const int naff = sc->n_aff;
     const int top0 = sc->free_top;
     const int w = threadIdx.x >> 6;
-    for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES) merge_page_wave(A, S[w], a, top0);
+    for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES) merge_page_wave<true>(A, S[w], a, top0);
+}
+
+__global__ __launch_bounds__(256, 2) void k_page_merge_full(MergeArgs A) {
+    __shared__ WaveMerge S[MW_WAVES];
+    Scalars* sc = A.sc;
+    if (sc->err) return;
+    const int nf = sc->n_full;
+    const int top0 = sc->free_top;
+    const int w = threadIdx.x >> 6;
+    for (int x = blockIdx.x * MW_WAVES + w; x < nf; x += gridDim.x * MW_WAVES)
+        merge_page_wave<false>(A, S[w], A.full_list[x], top0);
 }
 
 __device__ inline void dir_copy(const Dir& s, int x, const Dir& d, int y) {
-    d.page[y] = s.page[x]; d.cnt[y] = s.cnt[x]; d.maxv[y] = s.maxv[x];
+    d.page[y] = s.page[x]; d.cnt[y] = s.cnt[x]; d.nr[y] = s.nr[x]; d.maxv[y] = s.maxv[x];
     d.fhi[y] = s.fhi[x]; d.flo[y] = s.flo[x]; d.fmeta[y] = s.fmeta[x]; d.ftail[y] = s.ftail[x];
 }
 
 __device__ inline void desc_copy(const DescArrays& s, int x, const Dir& d, int y) {
-    d.page[y] = s.page[x]; d.cnt[y] = s.cnt[x]; d.maxv[y] = s.maxv[x];
+    d.page[y] = s.page[x]; d.cnt[y] = s.cnt[x]; d.nr[y] = s.nr[x]; d.maxv[y] = s.maxv[x];
     d.fhi[y] = s.fhi[x]; d.flo[y] = s.flo[x]; d.fmeta[y] = s.fmeta[x]; d.ftail[y] = s.ftail[x];
 }
 
@@ -873,6 +1016,14 @@ __device__ inline int wave_start_search(const int64_t* start, int D, int64_t g) 
     return lo - 1 + __popcll(__ballot(q < hi && start[q] <= g));
 }
 
+// pool slot of real boundary r of directory entry q (by one wavefront)
+__device__ inline int64_t real_slot(const Pool& pool, const Dir& dir, int q, int64_t r) {
+    const int pg = dir.page[q];
+    uint64_t hm[HM_WORDS];
+    load_hmask(pool, pg, hm);
+    return (int64_t)pg * PAGE + wave_select_real(hm, dir.cnt[q], (int)r);
+}
+
 struct RemovalKey {
     uint64_t* hi;
     uint64_t* lo;
@@ -901,7 +1052,9 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
         const Key rk{rk_hi[0], rk_lo[0], rk_meta[0], rk_tail};
         const int p0 = wave_dir_search(dir, D, rk);
         const int i0 = wave_page_lb(pool, dir.page[p0], dir.cnt[p0], rk);
-        g0 = dir.start[p0] + i0;
+        uint64_t hm[HM_WORDS];
+        load_hmask(pool, dir.page[p0], hm);
+        g0 = dir.start[p0] + real_before(hm, i0);
         if (g0 < H) {
             const int64_t budget = 3 * (int64_t)sc->n_comb + 10;
             g1 = min(H, g0 + budget);
@@ -909,7 +1062,7 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
             pB = wave_start_search(dir.start, D, g1 - 1);
             if (g1 < H) {
                 const int q1 = pB + 1 < D && dir.start[pB + 1] <= g1 ? pB + 1 : pB;  // entry holding g1
-                nk = pool_key(pool, (int64_t)dir.page[q1] * PAGE + (g1 - dir.start[q1]));
+                nk = pool_key(pool, real_slot(pool, dir, q1, g1 - dir.start[q1]));
                 has_key = true;
             }
         } else {
@@ -1024,7 +1177,7 @@ static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
     // full recompute of start[] (used after reset / load)
     Dir& d = h.dir[cur];
-    scan_i64_from_i32(d.cnt, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
+    scan_i64_from_i32(d.nr, d.start, &sc->D, 0, &sc->H, b.scan_tmp, s);
     (void)hipMemcpyAsync(&sc->D_next, &sc->D, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
     (void)hipMemcpyAsync(&sc->free_next, &sc->free_top, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
     launch_bmax_commit(h, cur, sc, s, true);
@@ -1047,7 +1200,6 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
                        b.blk_diff);
     PlanArgs P;
     P.src = src; P.dst = dst; P.sc = sc; P.acc = b.acc; P.blk_agg = b.blk_agg; P.blk_diff = b.blk_diff;
-    P.aff_f = b.aff_f;
     P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
     P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
     P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
@@ -1057,15 +1209,17 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
         MergeArgs A;
         A.pool = h.pool; A.dir = src; A.dst = dst; A.sc = sc; A.free_stack = h.free_stack; A.freed_list = b.freed_list;
-        A.aff_list = b.aff_list; A.aff_page = b.aff_page; A.aff_cnt = b.aff_cnt; A.aff_f = b.aff_f;
+        A.aff_list = b.aff_list; A.aff_page = b.aff_page; A.aff_cnt = b.aff_cnt;
         A.jlo = b.aff_jlo; A.jhi = b.aff_jhi; A.nn = b.aff_nn; A.nn_off = b.aff_nn_off; A.parts = b.aff_parts;
         A.parts_off = b.aff_parts_off; A.extra_off = b.aff_extra_off; A.free_off = b.aff_free_off;
         A.aff_start = b.aff_start;
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
         A.rb = b.rkb; A.re = b.rke; A.ne = b.ne; A.ne_ins = b.ne_ins;
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
-        hipLaunchKernelGGL(k_page_merge, dim3(std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)))), dim3(256),
-                           0, s, A);
+        A.full_list = b.full_list;
+        const int grid = std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)));
+        hipLaunchKernelGGL(k_page_merge, dim3(grid), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_page_merge_full, dim3(std::min(grid, 1024)), dim3(256), 0, s, A);
     }
     launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
 }
@@ -1083,10 +1237,16 @@ __global__ __launch_bounds__(256) void k_win_keep(Pool pool, Dir dir, const Scal
         const int pg = dir.page[q], c = dir.cnt[q];
         const int64_t st = dir.start[q];
         const int i = threadIdx.x;
+        // holes are dropped (the repack spreads fresh ones); global indices
+        // count the real boundaries before slot i
+        const bool real = i < c && !((pool.hmask[(int64_t)pg * HM_WORDS + (i >> 6)] >> (i & 63)) & 1);
+        int nreal;
+        const int ri = block_excl_scan((int)real, tmp, nreal);
         int keep = 0;
-        if (i < c) {
+        if (i < c) keep_o[(int64_t)w * PAGE + i] = 0;
+        if (real) {
             keep = 1;
-            const int64_t g = st + i;
+            const int64_t g = st + ri;
             if (g >= r0 && g < g1) {
                 const bool above = pool.ver[(int64_t)pg * PAGE + i] >= oldest;
                 const int64_t pv = i > 0    ? pool.ver[(int64_t)pg * PAGE + i - 1]
@@ -1141,7 +1301,8 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
         const int part0 = offw / per;
         if (kp) {
             const int m = offw + ex;
-            const int part = m / per, slot = m - part * per;
+            const int part = m / per, r = m - part * per;
+            const int n = min(per, S - part * per), g = spread_gap(n);  // spread with fresh holes
             const int dp = free_stack[top0 - 1 - part];
             const int64_t sidx = (int64_t)pg * PAGE + i;
             const uint64_t hi = pool.hi[sidx], lo = pool.lo[sidx];
@@ -1149,9 +1310,14 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
             const int64_t ver = pool.ver[sidx];
             const uint8_t* tail = pool.tail[sidx];
             if (gc) tail = move_tail(tail, meta, arena, arena_cap, sc);
-            put_entry(pool, (int64_t)dp * PAGE + slot, hi, lo, meta, ver, tail);
+            const int64_t d = (int64_t)dp * PAGE + spread_slot(r, g);
+            put_entry(pool, d, hi, lo, meta, ver, tail);
+            if (spread_hole_after(r, n, g)) put_entry(pool, d + 1, hi, lo, meta, ver, tail);
             atomicMax(&lmax[min(3, part - part0)], (long long)ver);
-            if (slot == 0) put_desc(desc, part, dp, min(per, S - part * per), hi, lo, meta, tail);
+            if (r == 0) {
+                put_desc(desc, part, dp, n, hi, lo, meta, tail);
+                for (int w2 = 0; w2 < HM_WORDS; w2++) pool.hmask[(int64_t)dp * HM_WORDS + w2] = spread_mask_word(n, w2);
+            }
         }
         __syncthreads();
         if (i < 4 && lmax[i] != INT64_MIN) atomicMax((long long*)&desc.maxv[part0 + i], lmax[i]);
@@ -1277,7 +1443,7 @@ __global__ __launch_bounds__(64) void k_key_at(Pool pool, Dir dir, const Scalars
                                                uint8_t* out_tail) {
     const int D = sc->D;
     const int q = wave_start_search(dir.start, D, g);
-    const Key k = pool_key(pool, (int64_t)dir.page[q] * PAGE + (g - dir.start[q]));
+    const Key k = pool_key(pool, real_slot(pool, dir, q, g - dir.start[q]));
     if (threadIdx.x == 0) {
         out[0] = k.hi;
         out[1] = k.lo;
@@ -1305,7 +1471,7 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                            win->prev);
     hipLaunchKernelGGL(k_win_keep, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc, oldest,
                        b.win_keep, b.win_cnt, b.desc_max);
-    DescArrays da{b.desc_page, b.desc_cnt, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
+    DescArrays da{b.desc_page, b.desc_cnt, b.desc_nr, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
                        b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap,
                        (int)!(h.shard.has_lo | h.shard.has_hi));
@@ -1325,13 +1491,15 @@ __global__ __launch_bounds__(64) void k_nth_after(NthArgs A) {
     const int64_t H = A.dir.start[D];
     const int p0 = wave_dir_search(A.dir, D, k);
     const int i0 = wave_page_lb(A.pool, A.dir.page[p0], A.dir.cnt[p0], k);
-    const int64_t j = A.dir.start[p0] + i0 + A.steps[q];
+    uint64_t hm[HM_WORDS];
+    load_hmask(A.pool, A.dir.page[p0], hm);
+    const int64_t j = A.dir.start[p0] + real_before(hm, i0) + A.steps[q];
     if (j < 0 || j >= H) {
         if (lane == 0) A.out[3 * (int64_t)q + 2] = ~0ull;
         return;
     }
     const int qq = wave_start_search(A.dir.start, D, j);
-    const Key r = pool_key(A.pool, (int64_t)A.dir.page[qq] * PAGE + (j - A.dir.start[qq]));
+    const Key r = pool_key(A.pool, real_slot(A.pool, A.dir, qq, j - A.dir.start[qq]));
     if (lane == 0) {
         A.out[3 * (int64_t)q] = r.hi;
         A.out[3 * (int64_t)q + 1] = r.lo;
@@ -1464,7 +1632,7 @@ __global__ __launch_bounds__(64) void k_sh_plan(Pool pool, Dir dir, Scalars* sc,
     if (og == rank) {  // this shard holds the next removalKey: read it before the compaction moves it
         const int64_t g = s_owner[1];
         const int q = wave_start_search(dir.start, D, g);
-        const Key k = pool_key(pool, (int64_t)dir.page[q] * PAGE + (g - dir.start[q]));
+        const Key k = pool_key(pool, real_slot(pool, dir, q, g - dir.start[q]));
         if (threadIdx.x == 0) {
             rk.hi[0] = k.hi;
             rk.lo[0] = k.lo;
@@ -1507,11 +1675,13 @@ void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int
 }
 
 // ------------------------------------------------------------------ reset ----
-__global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int cap_pages, Scalars* sc) {
+__global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int cap_pages, Scalars* sc,
+                                              uint64_t* hmask) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < HM_WORDS) hmask[i] = 0;  // page 0: empty
     if (i < cap_pages - 1) free_stack[i] = cap_pages - 1 - i;  // pops yield page 1, 2, ...
     if (i == 0) {
-        d.page[0] = 0; d.cnt[0] = 0; d.maxv[0] = INT64_MIN; d.start[0] = 0; d.start[1] = 0;
+        d.page[0] = 0; d.cnt[0] = 0; d.nr[0] = 0; d.maxv[0] = INT64_MIN; d.start[0] = 0; d.start[1] = 0;
         d.fhi[0] = 0; d.flo[0] = 0; d.fmeta[0] = 0; d.ftail[0] = nullptr; d.bmax[0] = INT64_MIN;
         sc->D = 1;
         sc->free_top = cap_pages - 1;
@@ -1525,7 +1695,7 @@ __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int c
 
 void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s) {
     hipLaunchKernelGGL(k_reset, dim3(cdiv(h.cap_pages, 256)), dim3(256), 0, s, h.dir[cur], h.free_stack,
-                       h.cap_pages, sc);
+                       h.cap_pages, sc, h.pool.hmask);
 }
 
 }  // namespace fdbcs_dev
@@ -1535,15 +1705,20 @@ namespace fdbcs_dev {
 // --------------------------------------------------------- dump / growth ----
 __global__ __launch_bounds__(256) void k_gather(Pool pool, Dir dir, const Scalars* sc, Pool out) {
     const int D = sc->D;
-    for (int x = blockIdx.x; x < D; x += gridDim.x) {
-        const int c = dir.cnt[x];
-        const int64_t b = (int64_t)dir.page[x] * PAGE, o = dir.start[x];
-        for (int i = threadIdx.x; i < c; i += blockDim.x) {
-            out.hi[o + i] = pool.hi[b + i];
-            out.lo[o + i] = pool.lo[b + i];
-            out.meta[o + i] = pool.meta[b + i];
-            out.ver[o + i] = pool.ver[b + i];
-            out.tail[o + i] = pool.tail[b + i];
+    __shared__ int32_t tmp[256 / 64 + 1];
+    for (int x = blockIdx.x; x < D; x += gridDim.x) {  // (a thread per slot: PAGE == blockDim)
+        const int c = dir.cnt[x], pg = dir.page[x];
+        const int64_t b = (int64_t)pg * PAGE;
+        const int i = threadIdx.x;
+        const bool real = i < c && !((pool.hmask[(int64_t)pg * HM_WORDS + (i >> 6)] >> (i & 63)) & 1);
+        int tot;
+        const int64_t o = dir.start[x] + block_excl_scan((int)real, tmp, tot);
+        if (real) {
+            out.hi[o] = pool.hi[b + i];
+            out.lo[o] = pool.lo[b + i];
+            out.meta[o] = pool.meta[b + i];
+            out.ver[o] = pool.ver[b + i];
+            out.tail[o] = pool.tail[b + i];
         }
     }
 }

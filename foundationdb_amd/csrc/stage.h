@@ -28,12 +28,14 @@ namespace fdbcs_dev {
 class TxnStage {
    public:
     TxnStage() = default;
-    ~TxnStage();
+    ~TxnStage() { release(); }
     TxnStage(const TxnStage&) = delete;
     TxnStage& operator=(const TxnStage&) = delete;
 
     // stream: where the H2D copies and k_unpack go; chunk: bytes per streamed copy
     void configure(hipStream_t stream, uint64_t chunk);
+    // free the buffers and forget the stream (before the owner destroys it)
+    void release();
 
     int begin();
     // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md

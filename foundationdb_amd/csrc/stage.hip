@@ -67,13 +67,19 @@ __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int
 
 }  // namespace
 
-TxnStage::~TxnStage() {
+void TxnStage::release() {
     if (stream_) hipStreamSynchronize(stream_);
     if (pin_) hipHostFree(pin_);
     if (toff_) hipHostFree(toff_);
     if (dev_) hipFree(dev_);
     if (dtoff_) hipFree(dtoff_);
     if (view_) hipFree(view_);
+    pin_ = dev_ = view_ = nullptr;
+    toff_ = dtoff_ = nullptr;
+    cap_ = view_cap_ = 0;
+    toff_cap_ = 0;
+    stream_ = nullptr;
+    open_ = false;
 }
 
 void TxnStage::configure(hipStream_t stream, uint64_t chunk) {

@@ -28,7 +28,7 @@ def test_header_declares_expected_surface():
 
 
 def test_library_exports_every_declared_symbol():
-    lib = ctypes.CDLL(_abi.LIB_PATH)
+    lib = _abi.lib()  # (loads torch's ROCm runtime first)
     for name in declared("fdbcs.h"):
         assert hasattr(lib, name), name
     bound = {n for n, _r, _a in _abi.FDBCS_FUNCS}
