@@ -706,8 +706,11 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
         if (++cs->vseq == 0) cs->vseq = 1;
         eo = EarlyOut{cs->vmap_dev + 64, reinterpret_cast<uint32_t*>(cs->vmap_dev), cs->vseq};
     }
+    // (the single-workgroup decision combines in the same launch, after it has
+    // raised the verdict flag; the grid decision's combine follows the copies)
+    const bool split = early && !b.rounds;
     cs->early_mapped =
-        launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, early, eo.flag ? &eo : nullptr);
+        launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, split, eo.flag ? &eo : nullptr);
     if (early) {
         if (!cs->early_mapped) {  // (the grid decision of large batches: copies)
             if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
@@ -715,7 +718,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
         }
         HIPOK(hipEventRecord(cs->ev_verdict, s));
         launch_write_search(v, b, cs->h, cs->cur, sc, cs->v0, s);  // (for the merge: after the verdicts)
-        launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
+        if (split) launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
     }
     record(cs, 4);
     const bool compact = new_oldest > cs->oldest;
@@ -986,10 +989,11 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
     if ((r = reset_history(cs, v0))) return fail(r);
     cs->oldest = 0;
-    if (const char* c = getenv("FDBCS_STAGE_CHUNK"))  // bytes per streamed H2D chunk of the per-transaction path
-        cs->st.configure(cs->stream, strtoull(c, nullptr, 0));
-    else
-        cs->st.configure(cs->stream, 512 << 10);
+    if (hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FDBCS_E_HIP);
+    {
+        const char* c = getenv("FDBCS_STAGE_CHUNK");  // bytes per streamed H2D chunk of the per-transaction path
+        if ((r = cs->st.configure(cs->stream, cs->copy_stream, c ? strtoull(c, nullptr, 0) : 512 << 10))) return fail(r);
+    }
 
     *out = cs;
     return FDBCS_OK;
@@ -1025,12 +1029,12 @@ void fdbcs_destroy(fdbcs* cs) {
         if (S.copied) hipEventDestroy(S.copied);
         if (S.done) hipEventDestroy(S.done);
     }
-    if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
     for (int i = 0; i < 8; i++)
         if (cs->ev[i]) hipEventDestroy(cs->ev[i]);
     if (cs->ev_verdict) hipEventDestroy(cs->ev_verdict);
     if (cs->vmap) hipHostFree(cs->vmap);
     cs->st.release();  // (its destructor would otherwise synchronize a destroyed stream)
+    if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -1040,6 +1044,7 @@ int fdbcs_batch_begin(fdbcs* cs) {
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_STATE;  // (pipelined batches still in flight)
     int r;
     if ((r = cs->st.begin())) return r;
+    cs->have_last_dv = false;  // (the staged bytes of the last batch are overwritten from here on)
     cs->in_batch = true;
     return FDBCS_OK;
 }
@@ -1088,8 +1093,6 @@ int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
     int r;
     if ((r = check_host_view(hv))) return r;
     fdbcs::Slot& S = cs->slot[cs->sub_head & 1];
-    if (!cs->copy_stream && hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess)
-        return FDBCS_E_HIP;
     if (!S.copied && (hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) != hipSuccess ||
                       hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess))
         return FDBCS_E_HIP;

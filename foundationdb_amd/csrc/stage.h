@@ -5,10 +5,16 @@
 // detectConflicts (Resolver.actor.cpp:140-153).  Each call checks its ranges
 // and appends one record -- a StageHdr, the range lengths, the key bytes
 // (kernels.h) -- to a pinned byte stream: the only host copy of the batch.
-// Every `chunk` bytes the new part of the stream starts its H2D copy on the
-// conflict set's stream, so most of the batch is on the device by the time
-// detectConflicts is called; finish() sends the rest plus the record offsets
-// and k_unpack builds the batch view on the device.
+// Every `chunk` bytes the new part of the stream starts its H2D copy on a
+// copy stream of its own, so most of the batch is on the device by the time
+// detectConflicts is called -- while the previous batch's history update is
+// still running on the conflict set's stream (copies queued behind it there
+// held every batch up by ~90 us).  finish() appends the record offsets to the
+// stream, sends the rest in one copy, makes the conflict set's stream wait for
+// it, and k_unpack builds the batch view on the device.  One device buffer
+// suffices: the previous batch's k_unpack (the only reader of the record
+// bytes; the encoder copies key tails into the batch's own buffer) finished
+// before its verdicts came back, i.e. before this batch's first add.
 //
 // (Measured and dropped: handing the record copies to helper threads during
 // the adds -- the calling thread got slower, 185 -> 250-990 us per config-2
@@ -32,8 +38,9 @@ class TxnStage {
     TxnStage(const TxnStage&) = delete;
     TxnStage& operator=(const TxnStage&) = delete;
 
-    // stream: where the H2D copies and k_unpack go; chunk: bytes per streamed copy
-    void configure(hipStream_t stream, uint64_t chunk);
+    // stream: where k_unpack goes; copy: where the H2D copies go (event-joined
+    // into stream); chunk: bytes per streamed copy
+    int configure(hipStream_t stream, hipStream_t copy, uint64_t chunk);
     // free the buffers and forget the stream (before the owner destroys it)
     void release();
 
@@ -50,7 +57,11 @@ class TxnStage {
    private:
     int grow(int64_t need_txns, uint64_t need_bytes);
 
+    void sync();
+
     hipStream_t stream_ = nullptr;
+    hipStream_t copy_ = nullptr;
+    hipEvent_t copied_ = nullptr;
     uint64_t chunk_ = 512 << 10;
     bool open_ = false;
     int64_t T_ = 0, R_ = 0, W_ = 0;
@@ -59,8 +70,7 @@ class TxnStage {
     uint8_t* dev_ = nullptr;
     uint64_t cap_ = 0;
     uint64_t used_ = 0, sent_ = 0;
-    uint64_t* toff_ = nullptr;    // pinned [T]: record offsets
-    uint64_t* dtoff_ = nullptr;   // device copy
+    uint64_t* toff_ = nullptr;    // host [T]: record offsets (appended to the stream at finish)
     int64_t toff_cap_ = 0;
     uint8_t* view_ = nullptr;     // device: the unpacked arrays
     uint64_t view_cap_ = 0;

@@ -67,24 +67,33 @@ __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int
 
 }  // namespace
 
-void TxnStage::release() {
+void TxnStage::sync() {
+    if (copy_) hipStreamSynchronize(copy_);
     if (stream_) hipStreamSynchronize(stream_);
+}
+
+void TxnStage::release() {
+    sync();
     if (pin_) hipHostFree(pin_);
-    if (toff_) hipHostFree(toff_);
     if (dev_) hipFree(dev_);
-    if (dtoff_) hipFree(dtoff_);
     if (view_) hipFree(view_);
+    if (copied_) hipEventDestroy(copied_);
+    free(toff_);
     pin_ = dev_ = view_ = nullptr;
-    toff_ = dtoff_ = nullptr;
+    toff_ = nullptr;
+    copied_ = nullptr;
     cap_ = view_cap_ = 0;
     toff_cap_ = 0;
-    stream_ = nullptr;
+    stream_ = copy_ = nullptr;
     open_ = false;
 }
 
-void TxnStage::configure(hipStream_t stream, uint64_t chunk) {
+int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
     stream_ = stream;
+    copy_ = copy;
     chunk_ = std::max<uint64_t>(4096, chunk);
+    if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
+    return FDBCS_OK;
 }
 
 int TxnStage::begin() {
@@ -101,23 +110,15 @@ int TxnStage::begin() {
 // Grow the offsets and / or the stream.  Chunks already sent went to the old
 // device buffer: the whole stream is sent again (sent_ = 0).
 int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
-    if (stream_) hipStreamSynchronize(stream_);  // copies in flight read the old buffers
     if (need_txns > toff_cap_) {
         const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
-        uint64_t* nt = nullptr;
-        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, hipHostMallocDefault) != hipSuccess) return FDBCS_E_NOMEM;
-        if (toff_) {
-            memcpy(nt, toff_, (size_t)T_ * 8);
-            hipHostFree(toff_);
-        }
+        uint64_t* nt = static_cast<uint64_t*>(realloc(toff_, (size_t)nc * 8));
+        if (!nt) return FDBCS_E_NOMEM;
         toff_ = nt;
-        if (dtoff_) hipFree(dtoff_);
-        dtoff_ = nullptr;
-        toff_cap_ = 0;
-        if (hipMalloc((void**)&dtoff_, (size_t)nc * 8) != hipSuccess) return FDBCS_E_NOMEM;
         toff_cap_ = nc;
     }
     if (need_bytes > cap_) {
+        sync();  // copies in flight read the old buffers
         const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
         uint8_t* np = nullptr;
         if (hipHostMalloc((void**)&np, nc, hipHostMallocDefault) != hipSuccess) return FDBCS_E_NOMEM;
@@ -151,8 +152,10 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     }
     if (longest > FDBCS_MAX_KEY) return FDBCS_E_KEY;
     const uint64_t rec = (sizeof(StageHdr) + 8 * (uint64_t)n + kbytes + 7) & ~uint64_t(7);
-    if (T_ + 1 > toff_cap_ || used_ + rec > cap_) {
-        int r = grow(T_ + 1, used_ + rec);
+    // (room for the record offsets appended at finish)
+    const uint64_t need = used_ + rec + 8 * (uint64_t)(T_ + 1) + 16;
+    if (T_ + 1 > toff_cap_ || need > cap_) {
+        int r = grow(T_ + 1, need);
         if (r) return r;
     }
     // one pass: check begin < end and copy, reads then writes
@@ -170,7 +173,7 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     R_ += nr;
     W_ += nw;
     if (used_ - sent_ >= chunk_) {
-        if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, stream_) != hipSuccess)
+        if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
             return FDBCS_E_HIP;
         sent_ = used_;
     }
@@ -180,11 +183,15 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
 int TxnStage::finish(fdbcs_batch_view& dv) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
-    if (used_ > sent_ &&
-        hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, stream_) != hipSuccess)
+    // the record offsets go after the records (8-byte aligned: records are),
+    // and the rest of the stream in one copy
+    const uint64_t o_toff = used_;
+    if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
+    const uint64_t end = o_toff + 8 * (uint64_t)T_;
+    if (end > sent_ && hipMemcpyAsync(dev_ + sent_, pin_ + sent_, end - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
         return FDBCS_E_HIP;
-    sent_ = used_;
-    if (T_ && hipMemcpyAsync(dtoff_, toff_, (size_t)T_ * 8, hipMemcpyHostToDevice, stream_) != hipSuccess)
+    sent_ = end;
+    if (hipEventRecord(copied_, copy_) != hipSuccess || hipStreamWaitEvent(stream_, copied_, 0) != hipSuccess)
         return FDBCS_E_HIP;
     // the view's arrays: snapshot [T] | read_off [T+1] | write_off [T+1] | key_off [2R+2W] | key_len [2R+2W]
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
@@ -193,7 +200,7 @@ int TxnStage::finish(fdbcs_batch_view& dv) {
                    o_kl = al(o_ko + 8 * slots), total = al(o_kl + 4 * slots) + 16;
     if (total > view_cap_) {
         if (view_) {
-            hipStreamSynchronize(stream_);
+            sync();
             hipFree(view_);
             view_ = nullptr;
         }
@@ -213,7 +220,7 @@ int TxnStage::finish(fdbcs_batch_view& dv) {
     dv.key_len = (const uint32_t*)(view_ + o_kl);
     dv.key_bytes = dev_;
     dv.key_bytes_len = used_;
-    launch_unpack(dev_, dtoff_, (int)T_, (int)R_, (int)W_,
+    launch_unpack(dev_, reinterpret_cast<const uint64_t*>(dev_ + o_toff), (int)T_, (int)R_, (int)W_,
                   UnpackOut{(int64_t*)dv.snapshot, (int32_t*)dv.read_off, (int32_t*)dv.write_off,
                             (uint64_t*)dv.key_off, (uint32_t*)dv.key_len},
                   stream_);
