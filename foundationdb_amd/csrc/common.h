@@ -186,12 +186,15 @@ struct Dir {
     uint32_t* fmeta;
     const uint8_t** ftail;
     int64_t* bmax;      // max of maxv over groups of 64 directory entries
+    int64_t* bmax2;     // max of maxv over groups of 4096 entries (built by each batch's ingest)
     // search index: level l >= 1 holds fhi[i * 16^l]; levels start at
     // 16-entry (128-byte) boundaries, so a 16-wide probe window is one cache
     // line (hist_search.h).  Rebuilt by k_bmax_commit with the directory.
     uint64_t* sidx;
     int32_t cap;        // entries allocated (levels are sized from it)
 };
+
+constexpr int BMAX2_SPAN = 4096;  // directory entries per bmax2 word
 
 constexpr int SIDX_B = 16;      // fan-out
 constexpr int SIDX_LOG = 4;

@@ -199,7 +199,8 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
             (r = dalloc(x.maxv, h.cap_dir)) ||
             (r = dalloc(x.start, h.cap_dir + 1)) || (r = dalloc(x.fhi, h.cap_dir)) || (r = dalloc(x.flo, h.cap_dir)) ||
             (r = dalloc(x.fmeta, h.cap_dir)) || (r = dalloc(x.ftail, h.cap_dir)) ||
-            (r = dalloc(x.bmax, h.cap_dir / 64 + 2)) || (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))))
+            (r = dalloc(x.bmax, h.cap_dir / 64 + 2)) || (r = dalloc(x.bmax2, h.cap_dir / BMAX2_SPAN + 2)) ||
+            (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))))
             return r;
         x.cap = h.cap_dir;
     }
@@ -212,7 +213,7 @@ void free_pool(HistBufs& h) {
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
         dfree(x.page); dfree(x.cnt); dfree(x.nr); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
-        dfree(x.ftail); dfree(x.bmax); dfree(x.sidx);
+        dfree(x.ftail); dfree(x.bmax); dfree(x.bmax2); dfree(x.sidx);
     }
 }
 
@@ -692,7 +693,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
-    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), s);
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
     record(cs, 1);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
@@ -1444,7 +1445,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     const bool scatter = cs->have_quantiles && !b.large;
-    launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), s);
+    launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
     if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;
@@ -1682,7 +1683,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     uint8_t* flags = sh->x1 + slots;
     // 1-2: the check, clipped to this shard (carry-in: sc->carry_check)
     const bool scatter = cs->have_quantiles && !b.large;
-    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), s);
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;

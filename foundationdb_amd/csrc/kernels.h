@@ -177,8 +177,10 @@ void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, in
 // ---- batch stages (kernels_batch.hip) ----
 // scatter: the sort splitters exist (an earlier batch) -- the ingest puts
 // the sort records into their buckets itself (launch_sort_ranges(scattered))
+// hd: the directory the batch's read check will search (its bmax2 level is
+// built here, from the maxima the last history update left)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   hipStream_t s);
+                   const Dir& hd, hipStream_t s);
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s);

@@ -55,7 +55,8 @@ __device__ inline Key encode_key(const uint8_t* p, uint32_t L, uint8_t* btail, u
 }
 
 struct IngestArgs {
-    int T, R, W, prep_blocks;
+    int T, R, W, prep_blocks, bmax2_blocks;
+    Dir hd;  // bmax2 blocks: the history directory of this batch's read check
     const int64_t* snap;
     const int32_t* ro;
     const int32_t* wo;
@@ -152,11 +153,17 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
     } else {
         for (int i = lo + g.lane; i < cb; i += RC_G) c |= pool.ver[baseb + i] > s;
         for (int i = g.lane; i < ie; i += RC_G) c |= pool.ver[basee + i] > s;
+        // entries strictly between: a three-level range maximum (entries,
+        // 64-entry groups, 4096-entry groups), at most 63 words per edge
         const int q0 = pb + 1, q1 = pe;
         const int qa = min(q1, (q0 + 63) & ~63), qz = max(qa, q1 & ~63);
         for (int q = q0 + g.lane; q < qa; q += RC_G) c |= dir.maxv[q] > s;
-        for (int q = (qa >> 6) + g.lane; q < (qz >> 6); q += RC_G) c |= dir.bmax[q] > s;
         for (int q = qz + g.lane; q < q1; q += RC_G) c |= dir.maxv[q] > s;
+        const int g0 = qa >> 6, g1 = qz >> 6;
+        const int ga = min(g1, (g0 + 63) & ~63), gz = max(ga, g1 & ~63);
+        for (int q = g0 + g.lane; q < ga; q += RC_G) c |= dir.bmax[q] > s;
+        for (int q = gz + g.lane; q < g1; q += RC_G) c |= dir.bmax[q] > s;
+        for (int q = (ga >> 6) + g.lane; q < (gz >> 6); q += RC_G) c |= dir.bmax2[q] > s;
     }
     if (g.ballot(c) && g.lane == 0) A.hist[t] = 1;
 }
@@ -505,6 +512,28 @@ __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) 
 #ifndef FDBCS_INGEST_BLOCK
 #define FDBCS_INGEST_BLOCK 256
 #endif
+// The top level of the read check's range maximum: bmax2[k] = max of maxv over
+// directory entries [4096k, 4096k + 4096), from independent loads (16 per
+// thread of a 256-thread block) and one block reduction.
+__device__ inline void bmax2_block(const Dir& d, int D, int k) {
+    __shared__ int64_t red[FDBCS_INGEST_BLOCK / 64];
+    const int base = k * BMAX2_SPAN;
+    if (base >= D) return;
+    constexpr int PER = BMAX2_SPAN / FDBCS_INGEST_BLOCK;
+    int64_t m = INT64_MIN;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int x = base + q * FDBCS_INGEST_BLOCK + (int)threadIdx.x;
+        if (x < D) m = max(m, d.maxv[x]);
+    }
+    m = wave_reduce_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < FDBCS_INGEST_BLOCK / 64; w++) m = max(m, red[w]);
+        d.bmax2[k] = m;
+    }
+}
 template <bool SCATTER>
 __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, SortJobs J) {
     if ((int)blockIdx.x < A.prep_blocks) {
@@ -529,7 +558,11 @@ __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, Sor
         for (int w = A.wo[t], w1 = A.wo[t + 1]; w < w1; w++) A.write_txn[w] = t;
         return;
     }
-    const int64_t i0 = (int64_t)(blockIdx.x - A.prep_blocks) * blockDim.x;
+    if ((int)blockIdx.x < A.prep_blocks + A.bmax2_blocks) {  // bmax2: one word per block
+        bmax2_block(A.hd, A.sc->D, (int)blockIdx.x - A.prep_blocks);
+        return;
+    }
+    const int64_t i0 = (int64_t)(blockIdx.x - A.prep_blocks - A.bmax2_blocks) * blockDim.x;
     const int64_t i = i0 + threadIdx.x;
     [[maybe_unused]] __shared__ uint64_t sp[2][SCATTER ? SS_MAXB : 1];
     if constexpr (SCATTER) {
@@ -1177,7 +1210,7 @@ void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, in
 }
 
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   hipStream_t s) {
+                   const Dir& hd, hipStream_t s) {
     constexpr int IB = FDBCS_INGEST_BLOCK;  // (A/B: scripts/build_variants.sh)
     IngestArgs A;
     A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
@@ -1187,7 +1220,9 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
     A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
-    const int blocks = A.prep_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
+    A.hd = hd;
+    A.bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
+    const int blocks = A.prep_blocks + A.bmax2_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     if (scatter)
         hipLaunchKernelGGL(k_ingest<true>, dim3(blocks), dim3(IB), 0, s, A, J);

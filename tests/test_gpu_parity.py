@@ -218,6 +218,41 @@ def test_steady_state_preloaded_history(cs):
         check_pair(cs, c, batch, now, nold, history=(i in (0, 11)))
 
 
+def test_wide_reads_three_level_range_max(cs):
+    """Reads spanning up to the whole history (> 3 x 4096 directory entries):
+    the read check's entry / 64-group / 4096-group maxima.  Low versions
+    everywhere except a few spikes, so each verdict hinges on whether a spike
+    lies inside the read -- at any level of the range maximum."""
+    rng = np.random.default_rng(11)
+    n = 2_600_000
+    raw = np.unique(rng.integers(0, 2**63, size=n, dtype=np.int64))
+    n = len(raw)
+    keys = raw.astype(">u8").view(np.uint8).reshape(-1, 8)
+    blob = np.concatenate([keys, np.zeros((n, 8), np.uint8)], axis=1).reshape(-1).copy()
+    lens = np.full(n, 16, np.uint32)
+    offs = np.arange(n, dtype=np.uint64) * 16
+    vers = rng.integers(100, 1000, size=n).astype(np.int64)
+    spikes = rng.choice(n, size=4, replace=False)
+    vers[spikes] = 10_000
+    c = CpuSpec()
+    cs.load_history_arrays(n, vers, lens, offs, blob, v0=0, oldest=0, removal_key=b"")
+    c.load_history_arrays(n, vers, lens, offs, blob, v0=0, oldest=0, removal_key=b"")
+    key = lambda i: bytes(blob[16 * i:16 * i + 16])
+    txns = []
+    for t in range(3000):
+        span = int(n * 10 ** rng.uniform(-4, 0))
+        a = int(rng.integers(0, max(1, n - span)))
+        b = min(n - 1, a + max(1, span))
+        if t % 7 == 0:
+            a, b = 0, n - 1
+        txns.append((int(rng.choice([500, 5_000, 20_000])), [(key(a), key(b))], []))
+    batch = PackedBatch.from_txns(txns)
+    vg = cs.detect_packed(batch, 30_000, 0)
+    vc = c.detect_packed(batch, 30_000, 0)
+    assert np.array_equal(vg, vc)
+    assert 0 < int((vg == _abi.CONFLICT).sum()) < len(txns)  # both outcomes occur
+
+
 def test_empty_and_degenerate_batches(cs):
     cs.load_history([], [], v0=7, oldest=0, removal_key=b"")
     c = CpuSpec(v0=7)
