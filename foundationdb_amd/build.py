@@ -106,7 +106,7 @@ def build_shim_check(verbose=False):
     deps = [SHIM, main, os.path.join(stub, "fdbclient", "CommitTransaction.h"), LIB,
             os.path.join(ROOT, "include", "fdbcs.h")]
     if _stale(SHIM_CHECK, deps):
-        _run(["g++", "-std=c++17", "-O2", "-Wall", "-iquote", stub, "-iquote", REF_HEADER_DIR, "-I",
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-iquote", stub, "-iquote", REF_HEADER_DIR, "-I",
               os.path.join(ROOT, "include"), SHIM, main, "-L", PKG, "-lfdbcs",
               "-Wl,-rpath,$ORIGIN/../../foundationdb_amd", "-o", SHIM_CHECK], verbose)
     return SHIM_CHECK

@@ -82,3 +82,49 @@ def test_shim_skiplisttest_entry(gpu):
     assert 380_000 < hist < 480_000, out
     assert rate > 0.155, out  # the reference's "New conflict set" rate here: 0.155 Mtxn/s
     print(f"skipListTest through the shim: {rate} Mtxn/s, {hist} history entries")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,bounds", [(3, "61,62"), (2, None)])
+def test_shim_multi_gpu_one_resolver(gpu, tmp_path, shards, bounds):
+    """FDBCS_SHARDS=G: the drop-in TU presents G exact shards (fdbcs_sharded_*)
+    as ONE conflict set to the Resolver's call sequence.  Here every rank
+    shares the test box's GPU and exchanges through in-process host
+    collectives; nonConflicting / tooOld must equal one oracle conflict
+    set's, split keys included (b"a", b"b": between the tiny alphabet's keys)."""
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    batches = list(tiny_stream(21, n_batches=25, max_txns=40)) + list(mixed_stream(22, n_batches=5))
+    wl = Workload(2, txns=600)
+    batches += [wl.batch(i) for i in range(4)]
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    write_batches(fin, batches)
+    env = dict(os.environ, FDBCS_SHARDS=str(shards), FDBCS_SHARD_COMM="host", FDBCS_SHARD_DEVICES="0")
+    if bounds:
+        env["FDBCS_SHARD_BOUNDS"] = bounds
+    subprocess.run([B.SHIM_CHECK, str(fin), str(fout)], check=True, timeout=120, env=env)
+    got = read_results(fout, len(batches))
+    c = CpuSpec()
+    for (batch, now, nold), (nc, to) in zip(batches, got):
+        v = c.detect_packed(batch, now, nold)
+        assert nc == list(np.nonzero(v == 2)[0])
+        assert to == list(np.nonzero(v == 1)[0])
+
+
+@pytest.mark.gpu
+def test_shim_multi_gpu_skiplisttest(gpu):
+    """skipListTest() through a 2-shard resolver (keys '............' + 4 bytes,
+    split at the middle of that range): the same history size as one shard."""
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    env = dict(os.environ, FDBCS_SHARDS="2", FDBCS_SHARD_COMM="host", FDBCS_SHARD_DEVICES="0",
+               FDBCS_SHARD_BOUNDS="2e2e2e2e2e2e2e2e2e2e2e2e00989680")  # setK(10^7)
+    one = subprocess.run([B.SHIM_CHECK, "skiplisttest"], capture_output=True, text=True, timeout=120, check=True)
+    two = subprocess.run([B.SHIM_CHECK, "skiplisttest"], capture_output=True, text=True, timeout=300, check=True,
+                         env=env)
+    h1 = int(re.search(r"(\d+) entries in version history", one.stdout).group(1))
+    h2 = int(re.search(r"(\d+) entries in version history", two.stdout).group(1))
+    a1 = int(re.search(r"(\d+) transactions accepted", one.stdout).group(1))
+    a2 = int(re.search(r"(\d+) transactions accepted", two.stdout).group(1))
+    assert "(2 GPUs as one resolver)" in two.stdout
+    assert (h1, a1) == (h2, a2)
