@@ -178,6 +178,10 @@ struct fdbcs {
         int64_t T = 0;
     } slot[2];
     hipStream_t copy_stream = nullptr;
+    // end of the last run_batch's history update (its scalars are then in the
+    // host-mapped mirror: ensure_history refreshes its budget without a sync)
+    hipEvent_t ev_end = nullptr;
+    bool end_mirror = false;
     int64_t sub_head = 0, sub_tail = 0;  // batches submitted / waited for
 };
 
@@ -256,6 +260,19 @@ int sync_state(fdbcs* cs) {
     HIPOK(hipStreamSynchronize(cs->stream));
     adopt_scalars(cs);
     return FDBCS_OK;
+}
+
+// The scalars after everything issued: from the host-mapped mirror when the
+// last run_batch (which publishes them at its end) has finished -- usually
+// so by the next detectConflicts, whose adds overlap that batch's history
+// update -- else by a stream sync.
+int refresh_state(fdbcs* cs) {
+    if (cs->end_mirror && hipEventQuery(cs->ev_end) == hipSuccess) {
+        memcpy(cs->sc_host, (const void*)cs->sc_mapped, sizeof(Scalars));
+        adopt_scalars(cs);
+        return FDBCS_OK;
+    }
+    return sync_state(cs);
 }
 
 // Wait for the stream.  FDBCS_SYNC_SPIN=1: poll instead of the runtime's
@@ -595,7 +612,7 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
     const int64_t naff_max = std::min<int64_t>(cs->known_D + cs->pending_pages + 1, 2 * W + 2);
     const int64_t need = 2 * naff_max + 2 * cdiv64(2 * W, FILL) + cdiv64(3 * W + 10 + 2 * PAGE, FILL) + 8;
     if (cs->known_free - cs->pending_pages < need) {
-        if (cs->pending_pages && (r = sync_state(cs))) return r;
+        if (cs->pending_pages && (r = refresh_state(cs))) return r;
         if (cs->known_free < need) {
             const int64_t used = cs->h.cap_pages - cs->known_free;
             if ((r = grow_pool(cs, used + 4 * need + 1024))) return r;  // (slack: fewer syncs behind early verdicts)
@@ -608,7 +625,7 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
     const uint64_t half = tail_half_bytes(cs->h.tail_cap);
     auto fits = [&](uint64_t pend) { return std::max(cs->known_tail, half / 2) + pend + tneed <= half; };
     if (!fits(cs->pending_tail)) {
-        if (cs->pending_tail && (r = sync_state(cs))) return r;
+        if (cs->pending_tail && (r = refresh_state(cs))) return r;
         if (!fits(0)) {
             if ((r = grow_tail(cs, 2 * (cs->known_tail + 2 * tneed + (1 << 20))))) return r;
         }
@@ -710,15 +727,18 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     // (the single-workgroup decision combines in the same launch, after it has
     // raised the verdict flag; the grid decision's combine follows the copies)
     const bool split = early && !b.rounds;
-    cs->early_mapped =
-        launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, split, eo.flag ? &eo : nullptr);
+    // (the deferred write searches run as extra blocks of the decision's
+    // launch: it holds one CU; a side stream cost ~7 us of event latency
+    // before the decision)
+    cs->early_mapped = launch_decide(v, b, sc, dev_verdict ? dev_verdict : b.verdict, s, split,
+                                     eo.flag ? &eo : nullptr, &cs->h, cs->cur, cs->v0);
     if (early) {
         if (!cs->early_mapped) {  // (the grid decision of large batches: copies)
             if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
             HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
         }
         HIPOK(hipEventRecord(cs->ev_verdict, s));
-        launch_write_search(v, b, cs->h, cs->cur, sc, cs->v0, s);  // (for the merge: after the verdicts)
+        launch_write_search(v, b, cs->h, cs->cur, sc, cs->v0, s);  // (grid decision: for the merge, after the verdicts)
         if (split) launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
     }
     record(cs, 4);
@@ -732,6 +752,8 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     }
     record(cs, 6);
     if (compact) cs->oldest = new_oldest;
+    HIPOK(hipEventRecord(cs->ev_end, s));
+    cs->end_mirror = true;
     if (sync) {
         if ((r = sync_batch(cs))) return r;
         read_stage_times(cs);
@@ -990,7 +1012,9 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
     if ((r = reset_history(cs, v0))) return fail(r);
     cs->oldest = 0;
-    if (hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FDBCS_E_HIP);
+    if (hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&cs->ev_end, hipEventDisableTiming) != hipSuccess)
+        return fail(FDBCS_E_HIP);
     {
         const char* c = getenv("FDBCS_STAGE_CHUNK");  // bytes per streamed H2D chunk of the per-transaction path
         if ((r = cs->st.configure(cs->stream, cs->copy_stream, c ? strtoull(c, nullptr, 0) : 512 << 10))) return fail(r);
@@ -1036,6 +1060,7 @@ void fdbcs_destroy(fdbcs* cs) {
     if (cs->vmap) hipHostFree(cs->vmap);
     cs->st.release();  // (its destructor would otherwise synchronize a destroyed stream)
     if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
+    if (cs->ev_end) hipEventDestroy(cs->ev_end);
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -1072,8 +1097,10 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     cs->have_last_dv = false;
     int r;
     fdbcs_batch_view dv;
-    if ((r = cs->st.finish(dv))) return r;
-    if ((r = finish_detect(cs, dv, now, new_oldest, verdict))) return r;
+    if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
+    r = finish_detect(cs, dv, now, new_oldest, verdict);
+    cs->b.staged = StagedBatch{};  // (the ingest that reads it was launched)
+    if (r) return r;
     cs->last_dv = dv;
     cs->have_last_dv = true;
     return FDBCS_OK;
@@ -1429,6 +1456,7 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
 
 int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
                       uint8_t* dev_hist) {
+    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     (void)now;
     (void)new_oldest;
     if (!cs || !db) return FDBCS_E_ARG;
@@ -1463,6 +1491,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
 int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
                       const uint8_t* removal_key, int32_t removal_key_len, const uint8_t* dev_hist,
                       uint8_t* dev_verdict, int64_t* info) {
+    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     if (!cs || !db || !info || removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
     cs->edges_known = false;
     const fdbcs_batch_view& v = *db;
@@ -1540,6 +1569,7 @@ int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_e
 
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
                         int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {
+    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     if (!cs || !info || a < 0 || b < a || key_index >= cs->known_H) return FDBCS_E_ARG;
     hipStream_t s = cs->stream;
     if (key_index >= 0) {  // the boundary that becomes removalKey, read before the compaction moves it
@@ -1639,6 +1669,7 @@ int sh_allgather(fdbcs_sharded* sh, const int64_t* dev_send, int64_t* dev_recv) 
 
 // one batch of the sharded resolver on the device-resident view v
 int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+    sh->cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     fdbcs* cs = sh->cs;
     int r;
     if ((r = check_batch_shape(v))) return r;
@@ -1840,8 +1871,10 @@ int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldes
     cs->in_batch = false;
     fdbcs_batch_view dv;
     int r;
-    if ((r = cs->st.finish(dv))) return r;
-    return sh_run(sh, dv, now, new_oldest, verdict);
+    if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
+    r = sh_run(sh, dv, now, new_oldest, verdict);
+    cs->b.staged = StagedBatch{};
+    return r;
 }
 
 int32_t fdbcs_sharded_removal_key_owner(fdbcs_sharded* sh) {

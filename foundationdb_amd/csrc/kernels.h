@@ -28,7 +28,44 @@ struct PageAcc {
 };
 
 // Per-batch device working set (sized by the engine before each batch).
+// ---- per-transaction staging (ConflictBatch::addTransaction, SkipList.cpp:979-1008) ----
+// fdbcs_batch_add appends one record per transaction to a pinned byte stream:
+// a StageHdr, then (nr + nw) StageRange entries (reads first, in call order),
+// then the key bytes (begin, end of each range), padded to 8 bytes.  ro / wo
+// are the reads / writes added before this transaction.
+struct StageHdr {
+    int64_t snap;
+    int32_t ro, wo, nr, nw;
+};
+static_assert(sizeof(StageHdr) == 24, "stage record header");
+// a range's keys: the begin key at `kofs` bytes from the record's start, the
+// end key right after it (key lengths <= FDBCS_MAX_KEY < 2^16)
+struct StageRange {
+    uint32_t kofs;
+    uint16_t blen, elen;
+};
+static_assert(sizeof(StageRange) == 8, "stage range entry");
+// k_unpack: one lane per transaction turns the stream (device copy) into the
+// arrays of a fdbcs_batch_view (layout below, key_bytes = the stream itself)
+struct UnpackOut {
+    int64_t* snap;     // [T]
+    int32_t* ro;       // [T+1]
+    int32_t* wo;       // [T+1]
+    uint64_t* koff;    // [2R+2W]
+    uint32_t* klen;    // [2R+2W]
+};
+void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s);
+// the staged batch the next launch_ingest reads straight from the record
+// stream (one launch for k_unpack's work and the ingest's; stream == null:
+// the ingest reads a batch view)
+struct StagedBatch {
+    const uint8_t* stream = nullptr;  // device copy of the record stream
+    const uint64_t* toff = nullptr;   // [T] record offsets (device)
+    UnpackOut view{};                 // the batch view's arrays, written on the way
+};
+
 struct BatchBufs {
+    StagedBatch staged;  // per-transaction path: set for one run_batch (stage.h)
     // transaction level [T]
     uint8_t* too_old;
     uint8_t* hist;
@@ -153,27 +190,6 @@ void scan_i32(const int32_t* in, int32_t* out, const int32_t* n_ptr, int32_t n_h
 void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, int32_t n_host, int64_t* total_out,
                        int64_t* tmp, hipStream_t s);
 
-// ---- per-transaction staging (ConflictBatch::addTransaction, SkipList.cpp:979-1008) ----
-// fdbcs_batch_add appends one record per transaction to a pinned byte stream:
-// a StageHdr, then (nr + nw) pairs {begin_len, end_len} (reads first, in call
-// order), then the key bytes (begin, end of each range), padded to 8 bytes.
-// ro / wo are the reads / writes added before this transaction.
-struct StageHdr {
-    int64_t snap;
-    int32_t ro, wo, nr, nw;
-};
-static_assert(sizeof(StageHdr) == 24, "stage record header");
-// k_unpack: one lane per transaction turns the stream (device copy) into the
-// arrays of a fdbcs_batch_view (layout below, key_bytes = the stream itself)
-struct UnpackOut {
-    int64_t* snap;     // [T]
-    int32_t* ro;       // [T+1]
-    int32_t* wo;       // [T+1]
-    uint64_t* koff;    // [2R+2W]
-    uint32_t* klen;    // [2R+2W]
-};
-void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s);
-
 // ---- batch stages (kernels_batch.hip) ----
 // scatter: the sort splitters exist (an earlier batch) -- the ingest puts
 // the sort records into their buckets itself (launch_sort_ranges(scattered))
@@ -212,8 +228,11 @@ struct EarlyOut {
 // split: the combine is left to launch_combine (issued after the verdicts).
 // eo: write the verdicts there (returns true if this batch's decision does;
 // the grid decision of large batches does not).
+// h (single-workgroup decision, write searches deferred by the read check):
+// the write searches run as extra blocks of the decision's launch
 bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
-                   bool split = false, const EarlyOut* eo = nullptr);
+                   bool split = false, const EarlyOut* eo = nullptr, HistBufs* h = nullptr, int cur = 0,
+                   int64_t v0 = 0);
 // k_decide_rounds keeps its state in LDS: batches up to this shape
 bool rounds_fit(int64_t T, int64_t W);
 void launch_combine(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s);

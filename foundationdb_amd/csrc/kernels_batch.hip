@@ -516,21 +516,18 @@ __global__ __launch_bounds__(256) void k_ss_scatter(SortJobs J, KeyArrays keys) 
 // directory entries [4096k, 4096k + 4096), from independent loads (16 per
 // thread of a 256-thread block) and one block reduction.
 __device__ inline void bmax2_block(const Dir& d, int D, int k) {
-    __shared__ int64_t red[FDBCS_INGEST_BLOCK / 64];
+    __shared__ int64_t red[1024 / 64];
     const int base = k * BMAX2_SPAN;
     if (base >= D) return;
-    constexpr int PER = BMAX2_SPAN / FDBCS_INGEST_BLOCK;
+    const int end = min(D, base + BMAX2_SPAN);
     int64_t m = INT64_MIN;
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        const int x = base + q * FDBCS_INGEST_BLOCK + (int)threadIdx.x;
-        if (x < D) m = max(m, d.maxv[x]);
-    }
+#pragma unroll 4
+    for (int x = base + (int)threadIdx.x; x < end; x += blockDim.x) m = max(m, d.maxv[x]);
     m = wave_reduce_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < FDBCS_INGEST_BLOCK / 64; w++) m = max(m, red[w]);
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = max(m, red[w]);
         d.bmax2[k] = m;
     }
 }
@@ -584,6 +581,113 @@ __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, Sor
             const int w = (int)(i - A.R);
             scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
             scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(2 * i + 1), 0}, tails, sp[1]);
+        }
+    }
+}
+
+// The per-transaction path (stage.h): k_unpack's work and the ingest's in one
+// launch, straight from the record stream.  A wavefront takes STG_TPW
+// consecutive transactions: lanes < STG_TPW read their record headers (into
+// LDS), then the wavefront's ranges go one per lane -- range k belongs to the
+// transaction whose range prefix covers it, and its StageRange entry (written
+// by the host's add) gives both keys' places with no prefix sum over the
+// record.  Each lane writes the batch view's entries of its range (later
+// readers: load metrics), the prep arrays (tooOld, range -> txn) and encodes,
+// validates and scatters the range as k_ingest's encode lanes do.
+constexpr int STG_TPW = 8;
+constexpr int STG_BLOCK = 256;
+
+template <bool SCATTER>
+__global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJobs J, StagedBatch S, int stg_blocks) {
+    __shared__ uint64_t s_base[STG_BLOCK / 64][STG_TPW];
+    __shared__ int64_t s_snap[STG_BLOCK / 64][STG_TPW];
+    __shared__ int32_t s_ro[STG_BLOCK / 64][STG_TPW], s_wo[STG_BLOCK / 64][STG_TPW], s_nr[STG_BLOCK / 64][STG_TPW],
+        s_pre[STG_BLOCK / 64][STG_TPW];
+    [[maybe_unused]] __shared__ uint64_t sp[2][SCATTER ? SS_MAXB : 1];
+    if ((int)blockIdx.x >= stg_blocks) {  // bmax2: one word per block
+        bmax2_block(A.hd, A.sc->D, (int)blockIdx.x - stg_blocks);
+        return;
+    }
+    if constexpr (SCATTER) {
+        splitter_fill(J, 0, sp[0]);
+        splitter_fill(J, 1, sp[1]);
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.sc->n_comb = 0;  // stays 0 if the batch has no transactions
+        A.sc->n_comb_own = 0;
+        A.sc->ss_resample = 0;
+        A.sc->ss_maxc = 0;
+        S.view.ro[A.T] = A.R;
+        S.view.wo[A.T] = A.W;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t0 = ((int)blockIdx.x * (STG_BLOCK / 64) + wv) * STG_TPW;
+    if (t0 >= A.T) return;  // (the whole wavefront)
+    // ---- headers: lane q < STG_TPW reads transaction t0 + q
+    const int t = t0 + lane;
+    const bool ht = lane < STG_TPW && t < A.T;
+    int n = 0;
+    if (ht) {
+        const uint64_t base = S.toff[t];
+        const StageHdr h = *reinterpret_cast<const StageHdr*>(S.stream + base);
+        n = h.nr + h.nw;
+        s_base[wv][lane] = base;
+        s_snap[wv][lane] = h.snap < A.oldest && h.nr > 0 ? INT64_MAX : h.snap;  // (tooOld: nothing to check)
+        s_ro[wv][lane] = h.ro;
+        s_wo[wv][lane] = h.wo;
+        s_nr[wv][lane] = h.nr;
+        S.view.snap[t] = h.snap;
+        S.view.ro[t] = h.ro;
+        S.view.wo[t] = h.wo;
+        A.too_old[t] = h.snap < A.oldest && h.nr > 0 ? 1 : 0;  // addTransaction's rule (SkipList.cpp:985)
+        A.hist[t] = 0;
+        A.deg[t] = 0;
+    }
+    const int incl = wave_incl_scan(n);
+    if (lane < STG_TPW) s_pre[wv][lane] = incl;
+    const int ntot = __builtin_amdgcn_readlane(incl, STG_TPW - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wavefront's LDS writes, read below)
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* const* tails = A.keys.tail;
+    // ---- the wavefront's ranges, one per lane
+    for (int k = lane; k < ntot; k += 64) {
+        int j = 0;  // owner: the transactions whose range prefix ends at or before k
+#pragma unroll
+        for (int q = 0; q < STG_TPW - 1; q++) j += s_pre[wv][q] <= k;
+        const int q = k - (j ? s_pre[wv][j - 1] : 0);
+        const uint64_t base = s_base[wv][j];
+        const StageRange e = reinterpret_cast<const StageRange*>(S.stream + base + sizeof(StageHdr))[q];
+        const int nrj = s_nr[wv][j];
+        int64_t i;  // range index: reads first, then writes (the slot layout of fdbcs_batch_view)
+        if (q < nrj) {
+            const int r = s_ro[wv][j] + q;
+            i = r;
+            A.read_txn[r] = t0 + j;
+            A.read_snap[r] = s_snap[wv][j];
+        } else {
+            const int w = s_wo[wv][j] + q - nrj;
+            i = (int64_t)A.R + w;
+            A.write_txn[w] = t0 + j;
+        }
+        const uint64_t ob = base + e.kofs, oe = ob + e.blen;
+        S.view.koff[2 * i] = ob;
+        S.view.klen[2 * i] = e.blen;
+        S.view.koff[2 * i + 1] = oe;
+        S.view.klen[2 * i + 1] = e.elen;
+        const Key b = encode_key(S.stream + ob, e.blen, A.btail, A.btail_cap, A.sc);
+        const Key en = encode_key(S.stream + oe, e.elen, A.btail, A.btail_cap, A.sc);
+        A.keys.put(2 * i, b);
+        A.keys.put(2 * i + 1, en);
+        if (kcmp(b, en) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
+        if constexpr (SCATTER) {
+            if (i < A.R) {
+                scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
+            } else {
+                const int w = (int)(i - A.R);
+                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
+                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(2 * i + 1), 0}, tails, sp[1]);
+            }
         }
     }
 }
@@ -1192,16 +1296,14 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* __restrict__ stre
     o.snap[t] = h.snap;
     o.ro[t] = h.ro;
     o.wo[t] = h.wo;
-    const uint2* lens = reinterpret_cast<const uint2*>(stream + base + sizeof(StageHdr));
-    uint64_t kp = base + sizeof(StageHdr) + 8ull * (uint32_t)(h.nr + h.nw);
+    const StageRange* ent = reinterpret_cast<const StageRange*>(stream + base + sizeof(StageHdr));
     for (int k = 0; k < h.nr + h.nw; k++) {
-        const uint2 l = lens[k];
+        const StageRange e = ent[k];
         const int64_t slot = k < h.nr ? 2ll * (h.ro + k) : 2ll * R + 2ll * (h.wo + k - h.nr);
-        o.koff[slot] = kp;
-        o.klen[slot] = l.x;
-        o.koff[slot + 1] = kp + l.x;
-        o.klen[slot + 1] = l.y;
-        kp += (uint64_t)l.x + l.y;
+        o.koff[slot] = base + e.kofs;
+        o.klen[slot] = e.blen;
+        o.koff[slot + 1] = base + e.kofs + e.blen;
+        o.klen[slot + 1] = e.elen;
     }
 }
 
@@ -1224,6 +1326,14 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
     const int blocks = A.prep_blocks + A.bmax2_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
+    if (b.staged.stream) {  // the per-transaction path: straight from the record stream
+        const int sb = std::max(1, cdiv(cdiv((int64_t)v.txn_count, STG_TPW), STG_BLOCK / 64));
+        if (scatter)
+            hipLaunchKernelGGL(k_ingest_staged<true>, dim3(sb + A.bmax2_blocks), dim3(STG_BLOCK), 0, s, A, J, b.staged, sb);
+        else
+            hipLaunchKernelGGL(k_ingest_staged<false>, dim3(sb + A.bmax2_blocks), dim3(STG_BLOCK), 0, s, A, J, b.staged, sb);
+        return;
+    }
     if (scatter)
         hipLaunchKernelGGL(k_ingest<true>, dim3(blocks), dim3(IB), 0, s, A, J);
     else
@@ -1840,6 +1950,9 @@ struct RoundArgs {
     int32_t* cb_slot;         // combined range begins / ends, as key slots
     int32_t* ce_slot;
     Scalars* sc;
+    // blocks 1.. of the launch: the merge's write searches (deferred by the
+    // read check), beside the decision in block 0, which holds one CU
+    WriteSearchArgs ws;
 };
 
 static constexpr int DC_THREADS = 1024;
@@ -1904,6 +2017,11 @@ __device__ inline void blocks_of(int a, int b, F1 pos, F2 blk1, F3 blk2) {
 __device__ inline bool bit_of(const uint32_t* bits, int t) { return (bits[t >> 5] >> (t & 31)) & 1; }
 
 __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
+    if (blockIdx.x > 0) {  // a write-search block: 64 groups of RC_G lanes
+        const Group<RC_G> g;
+        write_search_group(A.ws, g, (int)(((blockIdx.x - 1) * blockDim.x + threadIdx.x) / RC_G));
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ int32_t red32[DC_THREADS / 64 + 1];
     __shared__ int32_t s_nw, s_nr;
@@ -2437,7 +2555,7 @@ __global__ __launch_bounds__(1024) void k_dec_walk(DecGridArgs A) {
 }
 
 bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t* verdict, hipStream_t s,
-                   bool split, const EarlyOut* eo) {
+                   bool split, const EarlyOut* eo, HistBufs* h, int cur, int64_t v0) {
     const int T = v.txn_count;
     if (T == 0) return false;  // n_comb was zeroed by k_prep
     const int P = 2 * v.write_count;
@@ -2470,7 +2588,13 @@ bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
         A.eo = *eo;
         A.verdict = eo->verdict;
     }
-    hipLaunchKernelGGL(k_decide_rounds, dim3(1), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
+    int wsb = 0;  // the deferred write searches ride in the same launch
+    if (h && b.ws_deferred && v.write_count > 0) {
+        b.ws_deferred = false;
+        A.ws = WriteSearchArgs{v.read_count, v.write_count, b.keys, h->pool, h->dir[cur], sc, v0, b.wh, nullptr};
+        wsb = cdiv((int64_t)v.write_count * RC_G, DC_THREADS);
+    }
+    hipLaunchKernelGGL(k_decide_rounds, dim3(1 + wsb), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
     if (multi && !split) launch_combine_grid(v, b, sc, s);
     return eo != nullptr;
 }

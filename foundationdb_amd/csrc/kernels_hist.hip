@@ -730,8 +730,10 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
 // INPLACE: the first pass over every affected page (k_page_merge); pages it
 // cannot do in place go on a list for the second (k_page_merge_full), which
 // rewrites them -- two kernels, so the short in-place path is compiled apart
-// from the register-heavy rewrite.
-template <bool INPLACE>
+// from the register-heavy rewrite.  UNIFIED (FDBCS_PM_UNIFIED builds): a page
+// the in-place pass cannot do is rewritten by the same wavefront at once (one
+// launch; both paths fit 3 waves per SIMD).
+template <bool INPLACE, bool UNIFIED = false>
 __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
     const int lane = threadIdx.x & 63;
@@ -784,8 +786,10 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     if (INPLACE) {
         if (parts == 1 && !__ballot(erases) && merge_in_place(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
             return;
-        if (lane == 0) A.full_list[atomicAdd(&sc->n_full, 1)] = a;
-        return;
+        if (!UNIFIED) {
+            if (lane == 0) A.full_list[atomicAdd(&sc->n_full, 1)] = a;
+            return;
+        }
     }
     // ---- 2b. rewrite: every old slot, loaded before any write
     uint64_t ohi[4] = {}, olo[4] = {};
@@ -922,6 +926,9 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
 #ifndef FDBCS_PM_WAVES
 #define FDBCS_PM_WAVES 3
 #endif
+#ifndef FDBCS_PM_UNIFIED
+#define FDBCS_PM_UNIFIED 1
+#endif
 __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A) {
     __shared__ WaveMerge S[MW_WAVES];
     Scalars* sc = A.sc;
@@ -929,7 +936,8 @@ __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A)
     const int naff = sc->n_aff;
     const int top0 = sc->free_top;
     const int w = threadIdx.x >> 6;
-    for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES) merge_page_wave<true>(A, S[w], a, top0);
+    for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES)
+        merge_page_wave<true, FDBCS_PM_UNIFIED != 0>(A, S[w], a, top0);
 }
 
 __global__ __launch_bounds__(256, 2) void k_page_merge_full(MergeArgs A) {
@@ -1219,7 +1227,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         A.full_list = b.full_list;
         const int grid = std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)));
         hipLaunchKernelGGL(k_page_merge, dim3(grid), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(k_page_merge_full, dim3(std::min(grid, 1024)), dim3(256), 0, s, A);
+        if (!FDBCS_PM_UNIFIED) hipLaunchKernelGGL(k_page_merge_full, dim3(std::min(grid, 1024)), dim3(256), 0, s, A);
     }
     launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
 }

@@ -48,9 +48,11 @@ class TxnStage {
     // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md
     // §0.6) refuse the transaction, which is then not part of the batch.
     int add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw);
-    // Sends the rest and unpacks on the stream; dv = the device batch view
-    // (valid until the next begin()).
-    int finish(fdbcs_batch_view& dv);
+    // Sends the rest; dv = the device batch view (valid until the next
+    // begin()).  With `staged`, the next ingest builds dv's arrays itself
+    // straight from the stream (*staged: where to find it); else k_unpack
+    // builds them now (FDBCS_SEPARATE_UNPACK: always).
+    int finish(fdbcs_batch_view& dv, StagedBatch* staged = nullptr);
     int64_t txns() const { return T_; }
     bool open() const { return open_; }
 

@@ -2,6 +2,7 @@
 #include "stage.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace fdbcs_dev {
@@ -48,16 +49,17 @@ __attribute__((always_inline)) inline void copy_small(uint8_t* d, const uint8_t*
     }
 }
 
-// check and copy ranges into a record: lens (begin, end lengths) and the key
-// bytes at kp (advanced); true if some range has begin >= end
-__attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int n, uint32_t* lens, uint8_t*& kp) {
+// check and copy ranges into the record at rec: entries (where the keys are,
+// their lengths) and the key bytes at kp (advanced); true if some range has
+// begin >= end
+__attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int n, StageRange* ent,
+                                                      const uint8_t* rec, uint8_t*& kp) {
     bool bad = false;
     for (int i = 0; i < n; i++) {
         const uint8_t *b = rg[i].begin, *e = rg[i].end;
         const uint32_t bl = rg[i].begin_len, el = rg[i].end_len;
         bad |= key_cmp(b, bl, e, el) >= 0;
-        lens[2 * i] = bl;
-        lens[2 * i + 1] = el;
+        ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)el};
         copy_small(kp, b, bl);
         copy_small(kp + bl, e, el);
         kp += bl + el;
@@ -160,10 +162,10 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     }
     // one pass: check begin < end and copy, reads then writes
     uint8_t* p = pin_ + used_;
-    uint32_t* lens = reinterpret_cast<uint32_t*>(p + sizeof(StageHdr));
-    uint8_t* kp = p + sizeof(StageHdr) + 8 * (size_t)n;
-    bool bad = put_ranges(reads, nr, lens, kp);
-    bad |= put_ranges(writes, nw, lens + 2 * nr, kp);
+    StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
+    uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)n;
+    bool bad = put_ranges(reads, nr, ent, p, kp);
+    bad |= put_ranges(writes, nw, ent + nr, p, kp);
     if (bad) return FDBCS_E_RANGE;  // (the record is not committed: used_ stays)
     const StageHdr h{snap, (int32_t)R_, (int32_t)W_, nr, nw};
     memcpy(p, &h, sizeof h);
@@ -180,7 +182,7 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     return FDBCS_OK;
 }
 
-int TxnStage::finish(fdbcs_batch_view& dv) {
+int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
     // the record offsets go after the records (8-byte aligned: records are),
@@ -188,6 +190,8 @@ int TxnStage::finish(fdbcs_batch_view& dv) {
     const uint64_t o_toff = used_;
     if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
     const uint64_t end = o_toff + 8 * (uint64_t)T_;
+    // (measured and kept: the rest on the copy stream too -- sending it on the
+    // conflict set's stream, right before the kernels, was ~12 us slower)
     if (end > sent_ && hipMemcpyAsync(dev_ + sent_, pin_ + sent_, end - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
         return FDBCS_E_HIP;
     sent_ = end;
@@ -220,10 +224,15 @@ int TxnStage::finish(fdbcs_batch_view& dv) {
     dv.key_len = (const uint32_t*)(view_ + o_kl);
     dv.key_bytes = dev_;
     dv.key_bytes_len = used_;
-    launch_unpack(dev_, reinterpret_cast<const uint64_t*>(dev_ + o_toff), (int)T_, (int)R_, (int)W_,
-                  UnpackOut{(int64_t*)dv.snapshot, (int32_t*)dv.read_off, (int32_t*)dv.write_off,
-                            (uint64_t*)dv.key_off, (uint32_t*)dv.key_len},
-                  stream_);
+    const UnpackOut out{(int64_t*)dv.snapshot, (int32_t*)dv.read_off, (int32_t*)dv.write_off, (uint64_t*)dv.key_off,
+                        (uint32_t*)dv.key_len};
+    const uint64_t* dtoff = reinterpret_cast<const uint64_t*>(dev_ + o_toff);
+    static const bool separate = getenv("FDBCS_SEPARATE_UNPACK") != nullptr;  // (A/B measurements)
+    if (staged && !separate) {
+        *staged = StagedBatch{dev_, dtoff, out};
+        return FDBCS_OK;
+    }
+    launch_unpack(dev_, dtoff, (int)T_, (int)R_, (int)W_, out, stream_);
     return FDBCS_OK;
 }
 
