@@ -166,7 +166,7 @@ def key_prefix_u64(lens, offs, kb):
     return out
 
 
-def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None):
+def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm=()):
     """oracle/cpu_spec.cpp (the build's CPU restatement) on the GPU box's host
     cores, on the timed batches, starting from the GPU's own steady-state
     history: 1 core (one ConflictSet, verdicts compared
@@ -182,6 +182,8 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None):
     c = CpuSpec()
     c.load_history_arrays(len(vers), vers, lens, offs, kb, v0=v0, oldest=oldest, removal_key=rk)
     t_load = time.perf_counter() - t_load
+    for b, now, nold in warm:  # the GPU's warmup batches (the snapshot precedes them), untimed
+        c.detect_packed(b, now, nold)
     if batches is None:
         batches = [wl.batch(first + i) for i in range(n_max)]
     n, mism, tc = 0, 0, 0.0
@@ -197,7 +199,8 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None):
     T = batches[0][0].T
     one = {"value": round(n * T / tc, 1), "unit": "txn/s", "cores": 1, "kind": "port",
            "sample": f"config {args.config}: batches {first}..{first + n - 1} ({n} x {T} txns, the timed batches) "
-                     f"from the GPU's steady-state history (H={len(vers)}); verdict mismatches vs GPU: {mism}",
+                     f"from the GPU's steady-state history (H={len(vers)}, then the {len(warm)} warmup batches "
+                     f"replayed untimed); verdict mismatches vs GPU: {mism}",
            "host_cpu": model, "host_cpus_available": avail, "history_load_s": round(t_load, 1)}
     # N cores: N key-range resolvers, each loaded with its slice of the history
     N = max(1, min(args.cpu_threads, avail))
@@ -215,6 +218,8 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None):
             carry = int(vers[a - 1]) if a > 0 else v0
             cs.load_history_arrays(z - a, np.ascontiguousarray(vers[a:z]), np.ascontiguousarray(lens[a:z]),
                                    np.ascontiguousarray(offs[a:z]), kb, v0=carry, oldest=oldest)
+            for b, now, nold in warm:  # (untimed)
+                cs.detect_packed(kr.split(b, g)[0], now, nold)
             subs = [kr.split(b, g)[0] for b, _now, _o in batches[:n]]
             shards.append((cs, subs))
         times = [0.0] * N
@@ -289,9 +294,19 @@ def run_single(args):
         wl.prefill(cs, 0, args.prefill)
     first = args.prefill
     seq = cfg == 4  # config 4: each batch's wide reads are drawn from the history before it
+    # The CPU baseline starts from the GPU's own steady-state history, dumped
+    # here and replaying the warmup batches (untimed) -- so the dump's host
+    # traffic (~0.7 GB at H = 19 M) happens before the warmup, not right
+    # before the timed batches.
+    snap = None
+    if not args.no_cpu:
+        snap = cs.dump_arrays() + (cs.header_version, cs.oldest_version, cs.removal_key())
+    warm_batches = []
     if seq:
         wl.set_successor(cs)  # (the prefill used the key-space-fraction wide reads: reads do not change the history)
         for i in range(first, first + args.warmup):
+            if snap is not None:
+                warm_batches.append(wl.batch(i))  # (the input the run draws, for the CPU replay)
             r1 = wl.prepare_run(i, 1)
             r1.run(cs, verdicts=False)
             del r1
@@ -303,9 +318,6 @@ def run_single(args):
     H_pre = cs.history_size()
     print(f"# steady state: {args.prefill} prefill + {args.warmup} warmup batches, H={H_pre}, "
           f"{time.time() - t_w:.1f}s", file=sys.stderr, flush=True)
-    snap = None
-    if not args.no_cpu:  # the CPU baseline starts from the GPU's own steady-state history
-        snap = cs.dump_arrays() + (cs.header_version, cs.oldest_version, cs.removal_key())
     key_bytes = None
     seq_batches = None
     if seq:
@@ -447,7 +459,9 @@ def run_single(args):
 
     cpu = None
     if snap is not None:
-        cpu = cpu_baselines(args, snap, wl, first, args.steps, verdicts, batches=seq_batches)
+        if not seq:
+            warm_batches = [wl.batch(first - args.warmup + j) for j in range(args.warmup)]
+        cpu = cpu_baselines(args, snap, wl, first, args.steps, verdicts, batches=seq_batches, warm=warm_batches)
     shim = shim_skiplisttest() if cfg == 2 and not args.no_shim else None
     workload = f"config{cfg}: {T}-txn batches, {CONFIG_SHAPE.get(cfg, '')}, 5M-version window"
     out = {
