@@ -40,13 +40,31 @@ __device__ inline uint64_t load_be64(const uint8_t* p) {
 }
 
 // Compare the tails (bytes 17..) of two keys that both have length > 17 and
-// identical first 17 bytes.  Tails are 8-byte aligned and zero padded.
+// identical first 17 bytes.  Tails are 8-byte aligned and zero padded.  Four
+// words of each tail per step, their loads issued together (keys sharing a
+// long prefix -- tenants, paths -- differ only words in; one dependent load
+// per word made every such compare a chain of round trips).
+#ifndef FDBCS_TAIL_CHUNK
+#define FDBCS_TAIL_CHUNK 4
+#endif
 __device__ inline int tail_cmp(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
-    uint32_t m = (la < lb ? la : lb) - 17;
-    uint32_t words = (m + 7) >> 3;
-    for (uint32_t w = 0; w < words; w++) {
-        uint64_t a = load_be64(ta + 8 * w), b = load_be64(tb + 8 * w);
-        if (a != b) return a < b ? -1 : 1;
+    constexpr uint32_t C = FDBCS_TAIL_CHUNK;
+    const uint32_t m = (la < lb ? la : lb) - 17;
+    const uint32_t words = (m + 7) >> 3;
+    const uint64_t* a = reinterpret_cast<const uint64_t*>(ta);
+    const uint64_t* b = reinterpret_cast<const uint64_t*>(tb);
+    for (uint32_t w = 0; w < words; w += C) {
+        uint64_t x[C], y[C];
+#pragma unroll
+        for (uint32_t k = 0; k < C; k++) {
+            const bool ok = w + k < words;  // (never past a tail's last word)
+            x[k] = ok ? a[w + k] : 0;
+            y[k] = ok ? b[w + k] : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < C; k++) {
+            if (x[k] != y[k]) return __builtin_bswap64(x[k]) < __builtin_bswap64(y[k]) ? -1 : 1;
+        }
     }
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
