@@ -250,7 +250,7 @@ struct Scalars {
     int32_t win_newpages;   // pages produced by the repack
     int32_t win_surv;       // survivors in the window pages
     int32_t jac_iters;      // stats: Jacobi iterations in the decision
-    int32_t blocks_done;    // last-block-commits counter (k_win_dir); zero between launches
+    int32_t blocks_done;    // last-block-commits counter (k_bmax_commit, k_win_dir); zero between launches
     int32_t free_next;      // free_top after the rebuild in flight
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)

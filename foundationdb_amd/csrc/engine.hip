@@ -710,7 +710,8 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
-    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
+                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
     record(cs, 1);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
@@ -1473,12 +1474,28 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     BatchBufs& b = cs->b;
     hipStream_t s = cs->stream;
     const bool scatter = cs->have_quantiles && !b.large;
-    launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
+    // FDBCS_DEBUG_SYNC: wait after each stage and name the one that failed (fault hunting)
+    static const bool dbg = getenv("FDBCS_DEBUG_SYNC") != nullptr;
+    auto stage_ok = [&](const char* what) {
+        if (!dbg) return FDBCS_OK;
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            fprintf(stderr, "fdbcs debug: %s failed: %s (T=%d R=%d W=%d D=%d cap=%d)\n", what, hipGetErrorString(e),
+                    v.txn_count, v.read_count, v.write_count, (int)cs->known_D, cs->h.cap_dir);
+            return FDBCS_E_HIP;
+        }
+        return FDBCS_OK;
+    };
+    launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
+                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
+    if ((r = stage_ok("ingest"))) return r;
     if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
+    if ((r = stage_ok("sort"))) return r;
     if ((r = edges_read_check(cs, v, carry_in))) return r;
+    if ((r = stage_ok("read check"))) return r;
     if (dev_hist) launch_flags_out(b, v.txn_count, dev_hist, s);
     // the edge count rides the sync below (fdbcs_shard_edge_count reads it without another round trip)
     HIPOK(hipMemcpyAsync(&cs->sc_host->edges_total, &cs->sc->edges_total, sizeof(int32_t), hipMemcpyDeviceToHost,
@@ -1714,7 +1731,8 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     uint8_t* flags = sh->x1 + slots;
     // 1-2: the check, clipped to this shard (carry-in: sc->carry_check)
     const bool scatter = cs->have_quantiles && !b.large;
-    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s);
+    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
+                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
         cs->have_quantiles = true;

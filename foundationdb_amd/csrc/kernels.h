@@ -196,7 +196,7 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // hd: the directory the batch's read check will search (its bmax2 level is
 // built here, from the maxima the last history update left)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   const Dir& hd, hipStream_t s);
+                   const Dir& hd, hipStream_t s, bool sharded = false);
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s);

@@ -115,7 +115,11 @@ __device__ inline int dir_entry_after(const Group<RC_G>& g, const Dir& dir, int 
     return h1.x;
 }
 
-// read r, checked by the RC_G lanes of its group (g.lane)
+// read r, checked by the RC_G lanes of its group (g.lane).  WIDE: the range
+// maximum between the edge pages has a third level (bmax2, 4096-entry
+// groups), so a read costs at most 63 words per edge of each level at any
+// span; the exact sharded modes keep two levels.
+template <bool WIDE>
 __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G>& g, int r) {
     if (r >= A.R) return;
     const Pool& pool = A.pool;
@@ -153,17 +157,19 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
     } else {
         for (int i = lo + g.lane; i < cb; i += RC_G) c |= pool.ver[baseb + i] > s;
         for (int i = g.lane; i < ie; i += RC_G) c |= pool.ver[basee + i] > s;
-        // entries strictly between: a three-level range maximum (entries,
-        // 64-entry groups, 4096-entry groups), at most 63 words per edge
-        const int q0 = pb + 1, q1 = pe;
+        const int q0 = pb + 1, q1 = pe;  // the entries strictly between
         const int qa = min(q1, (q0 + 63) & ~63), qz = max(qa, q1 & ~63);
         for (int q = q0 + g.lane; q < qa; q += RC_G) c |= dir.maxv[q] > s;
         for (int q = qz + g.lane; q < q1; q += RC_G) c |= dir.maxv[q] > s;
-        const int g0 = qa >> 6, g1 = qz >> 6;
-        const int ga = min(g1, (g0 + 63) & ~63), gz = max(ga, g1 & ~63);
-        for (int q = g0 + g.lane; q < ga; q += RC_G) c |= dir.bmax[q] > s;
-        for (int q = gz + g.lane; q < g1; q += RC_G) c |= dir.bmax[q] > s;
-        for (int q = (ga >> 6) + g.lane; q < (gz >> 6); q += RC_G) c |= dir.bmax2[q] > s;
+        if constexpr (WIDE) {
+            const int g0 = qa >> 6, g1 = qz >> 6;
+            const int ga = min(g1, (g0 + 63) & ~63), gz = max(ga, g1 & ~63);
+            for (int q = g0 + g.lane; q < ga; q += RC_G) c |= dir.bmax[q] > s;
+            for (int q = gz + g.lane; q < g1; q += RC_G) c |= dir.bmax[q] > s;
+            for (int q = (ga >> 6) + g.lane; q < (gz >> 6); q += RC_G) c |= dir.bmax2[q] > s;
+        } else {
+            for (int q = (qa >> 6) + g.lane; q < (qz >> 6); q += RC_G) c |= dir.bmax[q] > s;
+        }
     }
     if (g.ballot(c) && g.lane == 0) A.hist[t] = 1;
 }
@@ -1312,7 +1318,7 @@ void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, in
 }
 
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   const Dir& hd, hipStream_t s) {
+                   const Dir& hd, hipStream_t s, bool sharded) {
     constexpr int IB = FDBCS_INGEST_BLOCK;  // (A/B: scripts/build_variants.sh)
     IngestArgs A;
     A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
@@ -1323,7 +1329,9 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
     A.hd = hd;
-    A.bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
+    // (D <= cap; idle blocks exit.  The exact sharded modes keep a two-level
+    // range maximum: no bmax2.)
+    A.bmax2_blocks = v.read_count > 0 && !sharded ? cdiv(hd.cap, BMAX2_SPAN) : 0;
     const int blocks = A.prep_blocks + A.bmax2_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     if (b.staged.stream) {  // the per-transaction path: straight from the record stream
@@ -1643,12 +1651,13 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
 // One launch, three kinds of blocks: read-check groups and write-search
 // groups (history), then edge lanes (intra-batch) -- all latency-bound
 // searches, so they overlap.
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int rc_blocks, WriteSearchArgs WA,
                                                           int ws_blocks, EdgesArgs EA) {
     __shared__ uint64_t smp_r[EQ], smp_w[EQ];
     if ((int)blockIdx.x < rc_blocks) {
         const Group<RC_G> g;
-        read_check_group(RA, g, (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G));
+        read_check_group<WIDE>(RA, g, (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G));
     } else if ((int)blockIdx.x < rc_blocks + ws_blocks) {
         const Group<RC_G> g;
         write_search_group(WA, g, (int)(((blockIdx.x - rc_blocks) * blockDim.x + threadIdx.x) / RC_G));
@@ -1887,9 +1896,15 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
-    if (rc_blocks + ws_blocks + e_blocks > 0)
-        hipLaunchKernelGGL(k_edges_read_check, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA, rc_blocks,
-                           WA, ws_blocks, EA);
+    const bool wide = !(h.shard.has_lo | h.shard.has_hi);  // (bmax2 is built by the ingest in this mode only)
+    if (rc_blocks + ws_blocks + e_blocks > 0) {
+        if (wide)
+            hipLaunchKernelGGL(k_edges_read_check<true>, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA,
+                               rc_blocks, WA, ws_blocks, EA);
+        else
+            hipLaunchKernelGGL(k_edges_read_check<false>, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA,
+                               rc_blocks, WA, ws_blocks, EA);
+    }
     if (join && R > 0 && W > 0)
         hipLaunchKernelGGL(k_edges_merge, dim3(cdiv((int64_t)R + 2 * (int64_t)W, MS_CHUNK)), dim3(MS_THREADS), 0, s,
                            EA);

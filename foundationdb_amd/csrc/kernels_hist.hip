@@ -1156,7 +1156,19 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         m = wave_reduce_max(m);
         if (lane == 0) d.bmax[g] = m;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // Commit by the LAST block to finish: every block read free_top above
+    // for its part of the free-stack push, and a block that started after an
+    // early commit would push to the wrong slots (seen as free-stack
+    // corruption under contention: two processes sharing the GPU delayed the
+    // late blocks).  No fence: the values were consumed before the barrier
+    // (k_win_dir does the same).
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&sc->blocks_done, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        sc->blocks_done = 0;
         sc->D = Dn;
         sc->free_top = sc->free_next;
         sc->H = d.start[Dn];
@@ -1167,7 +1179,7 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
             sc->btail_used = 0;
         }
     }
-    if (end_of_batch && blockIdx.x == 0) {
+    if (end_of_batch) {
         __syncthreads();
         if (threadIdx.x < 64) publish_scalars(sc, mirror);
     }

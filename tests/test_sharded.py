@@ -231,3 +231,19 @@ def test_gpu_shards_protocol_b_zipf_and_large(gpu):
             check_step(sh, c, batch, now, nold, history=(i == 7))
     finally:
         sh.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [True, False])
+def test_dist_sharded_hip_engines(gpu, sparse):
+    """The bench's N > 1 path -- DistShardedConflictSet, one HIP engine per
+    process, exchanges over torch.distributed (gloo; both ranks on this GPU)
+    -- at the bench's batch size past the point where a 2-process rehearsal
+    once faulted (~50 batches), against one oracle conflict set: verdicts every
+    batch, history sizes at the end."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "dist_hip_verify.py"), "2", "80", "10000",
+                        "1" if sparse else "0"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
