@@ -118,7 +118,7 @@ __device__ inline int dir_entry_after(const Group<RC_G>& g, const Dir& dir, int 
 // read r, checked by the RC_G lanes of its group (g.lane).  WIDE: the range
 // maximum between the edge pages has a third level (bmax2, 4096-entry
 // groups), so a read costs at most 63 words per edge of each level at any
-// span; the exact sharded modes keep two levels.
+// span.
 template <bool WIDE>
 __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G>& g, int r) {
     if (r >= A.R) return;
@@ -1329,9 +1329,8 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
     A.hd = hd;
-    // (D <= cap; idle blocks exit.  The exact sharded modes keep a two-level
-    // range maximum: no bmax2.)
-    A.bmax2_blocks = v.read_count > 0 && !sharded ? cdiv(hd.cap, BMAX2_SPAN) : 0;
+    A.bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
+    (void)sharded;
     const int blocks = A.prep_blocks + A.bmax2_blocks + cdiv((int64_t)v.read_count + v.write_count, IB);
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     if (b.staged.stream) {  // the per-transaction path: straight from the record stream
@@ -1896,7 +1895,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
-    const bool wide = !(h.shard.has_lo | h.shard.has_hi);  // (bmax2 is built by the ingest in this mode only)
+    const bool wide = true;  // (WIDE = false: the two-level range maximum, kept for A/B)
     if (rc_blocks + ws_blocks + e_blocks > 0) {
         if (wide)
             hipLaunchKernelGGL(k_edges_read_check<true>, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA,
