@@ -250,7 +250,7 @@ struct Scalars {
     int32_t win_newpages;   // pages produced by the repack
     int32_t win_surv;       // survivors in the window pages
     int32_t jac_iters;      // stats: Jacobi iterations in the decision
-    int32_t blocks_done;    // last-block-commits counter (k_bmax_commit, k_win_dir); zero between launches
+    int32_t blocks_done;    // last-block-commits counter (k_win_dir); zero between launches
     int32_t free_next;      // free_top after the rebuild in flight
     int32_t win_np;         // directory entries covered by the compaction window
     int32_t last_err;       // err of the last batch (err is reset for the next one)
@@ -272,6 +272,8 @@ struct Scalars {
     // whole history frees it
     int32_t tail_half;
     int32_t tail_flags;     // TF_* below
+    int32_t free_base;      // free-stack slot where the merge's freed pages go (free_top - extra_total before
+                            // k_bmax_commit moves free_top: its blocks read this, not free_top)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 

@@ -410,6 +410,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         sc->D_next = Dn;
         sc->extra_total = extra;
         sc->free_next = (int)(top0 - extra + freed);
+        sc->free_base = (int)(top0 - extra);
         A.dst.start[Dn] = A.src.start[D] + (int64_t)(int32_t)(uint32_t)((uint64_t)t2 >> 32);
     }
 }
@@ -1141,7 +1142,11 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
     // a compaction follows: its window over the new directory (one wavefront)
     if (!end_of_batch && blockIdx.x == 0 && threadIdx.x < 64) win_setup_wave(pool, d, Dn, sc, rkey, !sharded);
     if (freed_list) {
-        const int base = sc->free_top - sc->extra_total;
+        // (free_base, not free_top: block 0 commits free_top below while later
+        // blocks may not have started -- reading it here was a race that
+        // corrupted the free stack under contention, e.g. two processes
+        // sharing the GPU)
+        const int base = sc->free_base;
         const int nf = sc->free_next - base;
         for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x)
             free_stack[base + i] = freed_list[i];
@@ -1156,19 +1161,9 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         m = wave_reduce_max(m);
         if (lane == 0) d.bmax[g] = m;
     }
-    // Commit by the LAST block to finish: every block read free_top above
-    // for its part of the free-stack push, and a block that started after an
-    // early commit would push to the wrong slots (seen as free-stack
-    // corruption under contention: two processes sharing the GPU delayed the
-    // late blocks).  No fence: the values were consumed before the barrier
-    // (k_win_dir does the same).
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&sc->blocks_done, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) {
-        sc->blocks_done = 0;
+    // block 0 commits (no other block reads what it writes: D_next, free_base,
+    // free_next and extra_total stay)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         sc->D = Dn;
         sc->free_top = sc->free_next;
         sc->H = d.start[Dn];
@@ -1179,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
             sc->btail_used = 0;
         }
     }
-    if (end_of_batch) {
+    if (end_of_batch && blockIdx.x == 0) {
         __syncthreads();
         if (threadIdx.x < 64) publish_scalars(sc, mirror);
     }
