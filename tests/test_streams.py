@@ -3,7 +3,7 @@
 CPU: the generator still produces the recorded inputs (every batch's input
 SHA-256) and the CPU restatement reproduces the recorded verdicts and
 post-batch histories on a prefix of each stream.  GPU: the whole stream
-through the engine -- config 2 and 3 through the Resolver's per-transaction
+through the engine -- configs 2, 3 and 4 through the Resolver's per-transaction
 loop (fdbwl_run_resolver: fdbcs_batch_begin / add / detect), the others as
 packed batches -- bit-exact after every batch: verdicts, H, the history's
 SHA-256, 32 sampled boundaries, removalKey, oldestVersion.
@@ -73,7 +73,7 @@ def test_gpu_replays_stream(name):
     cs = ConflictSet(device=0, max_history=4_000_000)
     if fx["config"] == 4:  # the wide reads' ends from the engine's own history (fdbcs_nth_after)
         wl.set_successor(cs)
-    per_txn = name in ("config2", "config3")
+    per_txn = name in ("config2", "config3", "config4")  # (config 4: 68-100-byte keys through the staged ingest)
     for rec in fx["batches_out"]:
         i = rec["index"]
         if per_txn:  # the Resolver's loop: begin, T x add, detect (native)
