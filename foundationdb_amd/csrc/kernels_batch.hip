@@ -600,8 +600,15 @@ __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, Sor
 // record.  Each lane writes the batch view's entries of its range (later
 // readers: load metrics), the prep arrays (tooOld, range -> txn) and encodes,
 // validates and scatters the range as k_ingest's encode lanes do.
-constexpr int STG_TPW = 8;
-constexpr int STG_BLOCK = 256;
+#ifndef FDBCS_STG_TPW
+#define FDBCS_STG_TPW 8
+#endif
+#ifndef FDBCS_STG_BLOCK
+#define FDBCS_STG_BLOCK 256
+#endif
+constexpr int STG_TPW = FDBCS_STG_TPW;
+constexpr int STG_BLOCK = FDBCS_STG_BLOCK;
+static_assert(STG_TPW >= 1 && STG_TPW <= 64 && STG_BLOCK % 64 == 0, "staged ingest shape");
 
 template <bool SCATTER>
 __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJobs J, StagedBatch S, int stg_blocks) {
