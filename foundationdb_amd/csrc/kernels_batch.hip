@@ -1902,7 +1902,10 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
-    const bool wide = true;  // (WIDE = false: the two-level range maximum, kept for A/B)
+#ifndef FDBCS_RC_WIDE
+#define FDBCS_RC_WIDE 1
+#endif
+    const bool wide = FDBCS_RC_WIDE;  // (WIDE = false: the two-level range maximum, kept for A/B)
     if (rc_blocks + ws_blocks + e_blocks > 0) {
         if (wide)
             hipLaunchKernelGGL(k_edges_read_check<true>, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA,
