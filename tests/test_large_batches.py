@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 from foundationdb_amd import ConflictSet
+from foundationdb_amd.conflict_set import COMMITTED
 from foundationdb_amd.batch import PackedBatch
 from foundationdb_amd.workload import Workload
 from gen import mixed_stream, tiny_stream
@@ -153,3 +154,31 @@ def test_real_large_batches(cs, cfg, T, nb):
     for i in range(nb):
         batch, now, nold = wl.batch(i)
         check_pair(cs, c, batch, now, nold, history=(i == nb - 1))
+
+
+def test_config5_one_gpu_share(gpu):
+    """Config 5 at one GPU's share: 10^8 history
+    boundaries over 8 GPUs is 12.5 M per GPU, and in exact mode A every GPU
+    resolves the whole 10^6-txn batch against its part.  Preload 7 blind-write
+    batches of 10^6 point writes (bench.py's config-5 preload, ~14 M
+    boundaries), load the oracle from the GPU's own dump, then three full
+    10^6-txn config-5 batches: verdicts, oldest version and the whole history
+    after the last batch must be identical."""
+    g = ConflictSet(device=0, max_history=30_000_000)
+    c = CpuSpec()
+    try:
+        Workload(50, txns=1_000_000).prefill(g, 0, 7)
+        vers, lens, offs, kb = g.dump_arrays()
+        assert len(vers) > 12_000_000, len(vers)
+        c.load_history_arrays(len(vers), vers, lens, offs, kb, v0=g.header_version, oldest=g.oldest_version,
+                              removal_key=g.removal_key())
+        del vers, lens, offs, kb
+        same_history(g, c)
+        wl = Workload(5, txns=1_000_000)
+        for i in range(3):
+            batch, now, nold = wl.batch(i)
+            vg = check_pair(g, c, batch, now, nold, history=(i == 2))
+            assert (vg == COMMITTED).any()
+    finally:
+        c.close()
+        g.close()
