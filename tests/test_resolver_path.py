@@ -46,9 +46,12 @@ def make_cs(chunk):
 
 
 @pytest.mark.parametrize("cfg,T,nb,chunk", [(2, 2000, 12, None), (2, 2000, 6, 4096), (1, 2500, 10, None),
-                                            (3, 1500, 10, 65536), (4, 400, 8, 8192)])
+                                            (3, 1500, 10, 65536), (4, 400, 8, 8192), (5, 1_000_000, 2, None)])
 def test_resolver_loop_matches_oracle(gpu, cfg, T, nb, chunk):
-    """The bench's timed loop (native: fdbwl_run_resolver) against cpu_spec."""
+    """The bench's timed loop (native: fdbwl_run_resolver) against cpu_spec.
+    (Config 5: 10^6 addTransaction calls per batch -- the staging stream grows
+    to ~300 MB mid-batch and the large-batch pipeline runs on the staged
+    ingest.)"""
     g = make_cs(chunk)
     c = CpuSpec()
     wl = Workload(cfg, txns=T)
