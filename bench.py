@@ -77,6 +77,10 @@ def parse():
     p.add_argument("--lm-batches", type=int, default=None,
                    help="batches whose load-metrics roll (iopsSample, Resolver.actor.cpp:146-151) is timed "
                         "(default 50; config 5: 2)")
+    p.add_argument("--latency-batches", type=int, default=None,
+                   help="after the timed region, this many more batches through the same window for the per-batch "
+                        "latency distribution (p99 over >= 500 batches, SURVEY.md §8d; default 500, config 4: 200, "
+                        "config 5: 0)")
     p.add_argument("--protocol", choices=["a", "b"], default="b",
                    help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
                         "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
@@ -88,6 +92,8 @@ def parse():
             setattr(a, name, large if big else small)
     if a.prefill is None:
         a.prefill = PREFILL.get(a.config, 0)
+    if a.latency_batches is None:
+        a.latency_batches = {4: 200, 5: 0}.get(a.config, 500)
     return a
 
 
@@ -155,17 +161,6 @@ def host_cpu():
     return model, n
 
 
-def key_prefix_u64(lens, offs, kb):
-    """First 8 key bytes of every boundary as a big-endian integer (zero padded)."""
-    n = len(lens)
-    out = np.zeros(n, np.uint64)
-    for i in range(8):
-        has = lens > i
-        idx = np.where(has, offs + i, 0).astype(np.int64)
-        out |= np.where(has, kb[idx].astype(np.uint64), 0) << np.uint64(56 - 8 * i)
-    return out
-
-
 def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm=()):
     """oracle/cpu_spec.cpp (the build's CPU restatement) on the GPU box's host
     cores, on the timed batches, starting from the GPU's own steady-state
@@ -173,7 +168,7 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm
     with the GPU's), and N cores = N independent key-range resolvers (FDB's
     multi-resolver mode: proxy split, MasterProxyServer.actor.cpp:267-307;
     throughput only, its verdicts are the conservative ones)."""
-    from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
+    from foundationdb_amd.resolvers import KeyRangeResolvers
     from oracle import CpuSpec
 
     vers, lens, offs, kb, v0, oldest, rk = snap
@@ -206,11 +201,20 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm
     N = max(1, min(args.cpu_threads, avail))
     multi = None
     if N > 1:
-        bounds = uniform_bounds(N)
+        # splitters = history quantiles: boundary k*H/N's key,
+        # so every resolver holds ~H/N boundaries whatever the key
+        # distribution (config 4's keys share their first 64 bytes)
+        H = len(vers)
+        edges, bounds = [0], []
+        for g in range(1, N):
+            i = (g * H) // N
+            k = bytes(kb[int(offs[i]):int(offs[i]) + int(lens[i])])
+            if i > edges[-1] and (not bounds or k > bounds[-1]):
+                edges.append(i)
+                bounds.append(k)
+        edges.append(H)
+        N = len(edges) - 1
         kr = KeyRangeResolvers(bounds)
-        pre = key_prefix_u64(lens, offs, kb)
-        cut = np.searchsorted(pre, np.array([int.from_bytes(x, "big") for x in bounds], np.uint64), side="left")
-        edges = [0] + [int(x) for x in cut] + [len(vers)]
         shards = []
         for g in range(N):
             a, z = edges[g], edges[g + 1]
@@ -241,9 +245,10 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm
         for cs, _s in shards:
             cs.close()
         multi = {"value": round(n * T / wall, 1), "unit": "txn/s", "cores": N, "kind": "port",
-                 "sample": f"the same {n} batches split over {N} key-range resolvers (equal slices of the first 8 "
-                           f"key bytes; each one thread, its slice of the history) -- FDB's multi-resolver mode, "
-                           f"throughput only", "slowest_shard_s": round(max(times), 3)}
+                 "sample": f"the same {n} batches split over {N} key-range resolvers (splitters at the history's "
+                           f"quantiles; each one thread, its slice of the history) -- FDB's multi-resolver mode, "
+                           f"throughput only", "slowest_shard_s": round(max(times), 3),
+                 "fastest_shard_s": round(min(times), 3)}
     one["n_cores"] = multi
     return one
 
@@ -348,6 +353,32 @@ def run_single(args):
     value = T * args.steps / elapsed
     lat_ms = us / 1e3
     next_i = first + args.steps
+    # key bytes of the timed batches (SURVEY.md §8d's input term), regenerated after the clock
+    kbytes = [int(np.asarray(wl.batch(first + j)[0].key_len, np.int64).sum()) for j in range(min(args.steps, 20))] \
+        if seq_batches is None else [int(np.asarray(b.key_len, np.int64).sum()) for b, _n, _o in seq_batches]
+    key_bytes_timed = float(np.mean(kbytes)) if kbytes else 0.0
+
+    # ---- latency leg (secondary): >= 500 more batches through the same window, for a real p99 ----
+    latency = None
+    if args.latency_batches > 0:
+        lus, ladd = [], []
+        done = 0
+        while done < args.latency_batches:
+            n1 = 1 if seq else min(100, args.latency_batches - done)
+            r1 = wl.prepare_run(next_i + done, n1)  # (generated outside the windows)
+            u, a_, _v = r1.run(cs, verdicts=False)
+            lus.extend(u.tolist())
+            ladd.extend(a_.tolist())
+            del r1
+            done += n1
+        next_i += done
+        la = np.array(lus) / 1e3
+        latency = {"batches": done, "mean_ms": round(float(la.mean()), 4),
+                   "p50_ms": round(float(np.percentile(la, 50)), 4), "p99_ms": round(float(np.percentile(la, 99)), 4),
+                   "p999_ms": round(float(np.percentile(la, 99.9)), 4), "max_ms": round(float(la.max()), 4),
+                   "add_us_mean": round(float(np.mean(ladd)), 2), "history_post": cs.history_size(),
+                   "window": "the timed region's window (fdbcs_batch_begin + T x fdbcs_batch_add + fdbcs_batch_detect), "
+                             "per batch, right after the timed region"}
 
     # ---- packed path (secondary): whole host batch views through fdbcs_batch_detect_packed ----
     packed = None
@@ -396,20 +427,34 @@ def run_single(args):
                    "batches": half, "path": "fdbcs_detect_device on batches staged in HBM (no host ingest, no PCIe)"}
         mean = np.array(st_us).mean(axis=0)  # [6 stages..., whole batch] us
         batch_us = float(mean[6])
-        algo = float(np.mean([pipeline_bytes(nb, t, a, b, cfg) for a, b, nb, t in hp]))
+        algo_hbm = float(np.mean([pipeline_bytes(nb, t, a, b, cfg) for a, b, nb, t in hp]))
         dom = int(np.argmax(mean[:6]))
         dom_bytes = float(np.mean([stage_bytes(STAGES[dom], s, nb) for s, (_a, _b, nb, _T) in zip(stats, hp)]))
-        achieved = algo / (batch_us * 1e-6) / 1e9
         key_bytes = float(np.mean([x[2] for x in hp]))
+        # the headline roofline: SURVEY.md §8d bytes of a timed batch over the
+        # timed region's ms_per_step (the driver's clock), not over the
+        # HBM-resident batches' device time (kept below as a secondary)
+        algo = pipeline_bytes(key_bytes_timed, T, H_pre, H_post, cfg)
+        step_s = elapsed / args.steps
+        achieved = algo / step_s / 1e9
+        ach_hbm = algo_hbm / (batch_us * 1e-6) / 1e9
         roofline = {
             "bound": "hbm",
-            "kernel": "detectConflicts device pipeline (one batch, all kernels; SURVEY §8d bytes per batch)",
+            "kernel": "one Resolver window (T x addTransaction + detectConflicts): SURVEY §8d bytes per batch over "
+                      "the timed ms_per_step",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
             "algo_bytes_per_batch": round(algo),
+            "algo_bytes_terms": {"key_bytes": round(key_bytes_timed), "txn_bytes": 9 * T,
+                                 "history_bytes": round((32.0 if cfg == 4 else E_HIST) * (H_pre + H_post))},
+            "ms_per_step": round(step_s * 1e3, 4),
+            "hbm_resident": {"batch_us": round(batch_us, 2), "achieved": round(ach_hbm, 1),
+                             "frac": round(ach_hbm / HBM_PEAK_GBS, 4), "algo_bytes_per_batch": round(algo_hbm),
+                             "path": "the device pipeline alone: fdbcs_detect_device on batches already in HBM, "
+                                     "HIP events around the whole batch (no host adds, no PCIe)"},
             "batch_us": round(batch_us, 2),
             "history_pre": int(np.mean([a for a, _b, _n, _t in hp])),
             "stage_us": {n: round(float(mean[i]), 2) for i, n in enumerate(STAGES)},
@@ -430,7 +475,8 @@ def run_single(args):
                 pm = json.load(f)
             if pm.get("history_pre", 0) >= 0.5 * roofline["history_pre"]:  # (only a profile of the same H)
                 roofline["traffic"] = pm.get("bytes_per_batch")
-                roofline["traffic_source"] = pm.get("source")
+                roofline["traffic_source"] = ("committed profile (not this run): " + str(pm.get("source")) +
+                                              f" -- profiles/pmc_traffic_config{cfg}.json")
                 roofline["physical_GBps"] = round(pm["bytes_per_batch"] / (batch_us * 1e-6) / 1e9, 1)
                 roofline["physical_frac"] = round(roofline["physical_GBps"] / HBM_PEAK_GBS, 4)
         del staged
@@ -475,6 +521,7 @@ def run_single(args):
         "p99_batch_ms": round(float(np.percentile(lat_ms, 99)), 4),
         "p50_batch_ms": round(float(np.percentile(lat_ms, 50)), 4),
         "add_us_mean": round(float(np.mean(add_us)), 2),
+        "latency": latency,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

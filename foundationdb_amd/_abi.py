@@ -176,8 +176,36 @@ def lib():
         except ImportError:
             pass
         # RTLD_GLOBAL: the workload library's bench drivers call the C ABI through it
-        _lib = _bind(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL), FDBCS_FUNCS)
+        h = _bind(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL), FDBCS_FUNCS)
+        check_single_hip_runtime()
+        _lib = h
     return _lib
+
+
+def hip_runtimes():
+    """Distinct HIP runtime images (libamdhip64, by device + inode) mapped into
+    this process, as paths."""
+    seen = {}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and os.path.basename(parts[5].strip()).startswith("libamdhip64"):
+                    seen[(parts[3], parts[4])] = parts[5].strip()
+    except OSError:
+        return []
+    return sorted(set(seen.values()))
+
+
+def check_single_hip_runtime():
+    """Raise if more than one HIP runtime is mapped.  That happens when
+    libfdbcs.so (which resolves libamdhip64 by soname) is loaded before torch
+    and torch then maps its own copy: two runtimes, two heaps, two device
+    contexts -- the heap corruption at exit round 2 traced to import order."""
+    rt = hip_runtimes()
+    if len(rt) > 1:
+        raise RuntimeError("two HIP runtimes are mapped into this process (" + ", ".join(rt) + "): load torch "
+                           "before libfdbcs.so (foundationdb_amd._abi.lib() does), or run without torch")
 
 
 def workload_lib():

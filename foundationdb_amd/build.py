@@ -77,7 +77,7 @@ def build_workload(verbose=False):
     s = os.path.join(CSRC, "workload.cpp")
     deps = [s, os.path.join(CSRC, "workload.h"), os.path.join(ROOT, "include", "fdbcs.h")]
     if _stale(WL_LIB, deps):
-        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", WL_LIB, s], verbose)
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", WL_LIB, s, "-ldl"], verbose)
     return WL_LIB
 
 

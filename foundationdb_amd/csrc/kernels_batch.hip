@@ -2227,16 +2227,53 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     }
 decided:
     PHASE(sc, 5);
-    for (int t = tid; t < T; t += nthr) {
-        const bool c = (cbits[t >> 5] >> (t & 31)) & 1;
-        A.committed[t] = c;
-        A.verdict[t] = c ? FDBCS_COMMITTED : (A.too_old[t] ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+    {
+        // 16 transactions per lane, one 16-byte store each of verdicts and
+        // committed flags: into host-mapped memory that is one PCIe write per
+        // 16 verdicts instead of one per verdict (byte stores made the flag
+        // ~20 us late at T = 5,000)
+        const bool al16 = ((reinterpret_cast<uintptr_t>(A.verdict) | reinterpret_cast<uintptr_t>(A.committed)) & 15) == 0;
+        for (int t0 = 16 * tid; t0 < T; t0 += 16 * nthr) {
+            const uint32_t cw = cbits[t0 >> 5] >> (t0 & 31);  // (t0 % 32 is 0 or 16; bits past T are 0)
+            const uint4 to4 = *reinterpret_cast<const uint4*>(A.too_old + t0);  // (too_old is padded by 64 bytes)
+            const uint32_t tw[4] = {to4.x, to4.y, to4.z, to4.w};
+            uint32_t vw[4] = {0, 0, 0, 0}, cm[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t c = (cw >> k) & 1;
+                const uint32_t v = c ? FDBCS_COMMITTED : (((tw[k >> 2] >> (8 * (k & 3))) & 0xFF) ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+                vw[k >> 2] |= v << (8 * (k & 3));
+                cm[k >> 2] |= c << (8 * (k & 3));
+            }
+            if (al16 && t0 + 16 <= T) {
+                *reinterpret_cast<uint4*>(A.verdict + t0) = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+                *reinterpret_cast<uint4*>(A.committed + t0) = make_uint4(cm[0], cm[1], cm[2], cm[3]);
+            } else {
+                for (int k = 0; k < 16 && t0 + k < T; k++) {
+                    A.verdict[t0 + k] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
+                    A.committed[t0 + k] = (uint8_t)(cm[k >> 2] >> (8 * (k & 3)));
+                }
+            }
+        }
     }
-    if (A.eo.flag) {  // host-mapped verdicts: every lane's stores, then flag + error words in one 16-byte store
+    if (A.eo.flag) {
+        // host-mapped verdicts: every lane's stores and the error words, a
+        // system-scope fence, then the flag -- itself pushed out with a second
+        // fence: a plain store after the first fence stayed in L2 until the
+        // workgroup ended (the host saw the flag ~19 us late, after the
+        // combine below)
+        if (tid == 0) {
+            A.eo.flag[1] = (uint32_t)sc->err;
+            A.eo.flag[2] = (uint32_t)sc->last_err;
+        }
         __threadfence_system();
         __syncthreads();
-        if (tid == 0) *reinterpret_cast<int4*>(A.eo.flag) = make_int4((int)A.eo.seq, sc->err, sc->last_err, 0);
+        if (tid == 0) {
+            __hip_atomic_store(A.eo.flag, A.eo.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+        }
     }
+    PHASE(sc, 1);
     if (tid == 0) {
         sc->n_dep = ncand;  // candidate reads of U (stats)
         if (ncand == 0) sc->jac_iters = 0;

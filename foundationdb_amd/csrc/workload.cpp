@@ -1,9 +1,11 @@
-#include <cstdlib>
 // workload.cpp -- deterministic synthetic batch generators (see workload.h).
 #include "workload.h"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -366,6 +368,17 @@ void fdbwl_run_destroy(fdbwl_run* r) { delete r; }
 
 int32_t fdbwl_run_txns(const fdbwl_run* r) { return r ? r->T : 0; }
 
+// FDBWL_MARK=1 (measurement): a no-op HIP API call at the window's start, at
+// the end of the adds and at detectConflicts' return, so that a rocprofv3
+// --hip-runtime-trace aligns the host phases with the device timeline
+// (scripts/api_timeline.py).  Resolved at run time: this library does not
+// link the HIP runtime.
+static void trace_mark() {
+    using fn = int (*)();
+    static const fn f = getenv("FDBWL_MARK") ? (fn)dlsym(RTLD_DEFAULT, "hipPeekAtLastError") : nullptr;
+    if (f) f();
+}
+
 int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts) {
     if (!r || !cs) return FDBCS_E_ARG;
     std::vector<uint8_t> scratch(std::max<int32_t>(r->T, 1));
@@ -379,6 +392,7 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
             for (size_t k = 0; k < B.reads.size(); k += 2) acc += B.reads[k].begin_len;
             for (size_t k = 0; k < B.writes.size(); k += 2) acc += B.writes[k].begin_len;
         }
+        trace_mark();
         const auto t0 = std::chrono::steady_clock::now();
         int st = fdbcs_batch_begin(cs);  // ConflictBatch conflictBatch(self->conflictSet)
         const int T = (int)B.snap.size();
@@ -386,8 +400,10 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
             st = fdbcs_batch_add(cs, B.snap[t], B.reads.data() + B.roff[t], B.roff[t + 1] - B.roff[t],
                                  B.writes.data() + B.woff[t], B.woff[t + 1] - B.woff[t]);
         const auto ta = std::chrono::steady_clock::now();
+        trace_mark();
         if (st == FDBCS_OK) st = fdbcs_batch_detect(cs, B.now, B.nold, out);  // detectConflicts(...)
         const auto t1 = std::chrono::steady_clock::now();
+        trace_mark();
         if (st != FDBCS_OK) return st;
         if (batch_us) batch_us[i] = std::chrono::duration<double, std::micro>(t1 - t0).count();
         if (add_us) add_us[i] = std::chrono::duration<double, std::micro>(ta - t0).count();

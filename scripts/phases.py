@@ -23,7 +23,7 @@ def main():
     for i in range(warm):
         v, now, nold = wl.view(i)
         out = cs.detect_view(v, now, nold, out)
-    acc = []
+    acc, stats = [], []
     buf = (C.c_int64 * 32)()
     for i in range(warm, warm + nb):
         v, now, nold = wl.view(i)
@@ -33,6 +33,8 @@ def main():
             print("not a FDBCS_PHASES build")
             return
         acc.append(np.array(buf[:n], dtype=np.int64))
+        st = cs.batch_stats()
+        stats.append((st.get("dependents", 0), st.get("decision_rounds", 0)))
     a = np.array(acc)
     base = a[:, 0:1]
     d = (a - base) * 0.01  # 100 MHz ticks -> us
@@ -41,6 +43,9 @@ def main():
     for i in range(min(16, a.shape[1])):
         if a[:, i].any():
             print(f"  ph[{i:2d}] {m[i]:9.2f}  (+{m[i] - (m[i - 1] if i else 0):8.2f})")
+    sd = np.array(stats)
+    print(f"  decision: candidate reads mean {sd[:, 0].mean():.1f} (batches with any: {(sd[:, 0] > 0).sum()}), "
+          f"rounds mean {sd[:, 1].mean():.2f}")
     if a.shape[1] > 16:  # cumulative per-wave cycle accumulators: per-batch deltas
         dd = np.diff(a[:, 16:], axis=0).mean(axis=0)
         print("  accumulators per batch:", " ".join(f"[{16 + i}]={v:.0f}" for i, v in enumerate(dd) if v))

@@ -82,3 +82,36 @@ def test_packed_batch_roundtrip():
     pb = PackedBatch.from_txns(txns)
     assert pb.T == 3 and pb.R == 2 and pb.W == 2
     assert pb.txns() == [(s, r, w) for s, r, w in txns]
+
+
+def test_single_hip_runtime_in_the_usual_order():
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from foundationdb_amd import _abi\n"
+            "_abi.lib()\n"
+            "print('RUNTIMES', len(_abi.hip_runtimes()))\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "RUNTIMES 1" in r.stdout
+
+
+def test_two_hip_runtimes_are_refused():
+    """libfdbcs.so mapped before torch: torch then maps its own libamdhip64.
+    The loader's guard must name it (or the process must hold one runtime)."""
+    import subprocess
+    import sys
+    code = ("import ctypes, sys; sys.path.insert(0, %r)\n"
+            "ctypes.CDLL(%r, mode=ctypes.RTLD_GLOBAL)\n"
+            "import torch\n"
+            "from foundationdb_amd import _abi\n"
+            "n = len(_abi.hip_runtimes())\n"
+            "try:\n"
+            "    _abi.lib()\n"
+            "    print('LOADED', n, flush=True)\n"
+            "except RuntimeError as e:\n"
+            "    print('GUARD', n, e, flush=True)\n"
+            "import os; os._exit(0)\n") % (ROOT, _abi.LIB_PATH)  # (_exit: skip the two runtimes' teardown)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert ("GUARD 2" in r.stdout and "two HIP runtimes" in r.stdout) or "LOADED 1" in r.stdout, r.stdout
