@@ -24,11 +24,32 @@ def short(n):
     return n.split("(")[0].replace("void ", "").replace("fdbcs_dev::", "")[:34]
 
 
+def load_db(path):
+    """The same three record lists from a rocpd SQLite output (rocprofv3's
+    default output format on this image)."""
+    import sqlite3
+    c = sqlite3.connect(path)
+    api = [{"Function": n, "Thread_Id": str(t), "Start_Timestamp": s, "End_Timestamp": e}
+           for n, t, s, e in c.execute("select name, tid, start, end from regions")]
+    ker = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+           for n, s, e in c.execute("select name, start, end from kernels")]
+    cp = [{"Direction": n, "Bytes": b, "Start_Timestamp": s, "End_Timestamp": e}
+          for n, b, s, e in c.execute("select name, size, start, end from memory_copies")]
+    return api, ker, cp
+
+
 def main():
     d = sys.argv[1]
     last = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     show = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-    api = list(csv.DictReader(open(find(d, "hip_api_trace.csv"))))
+    db = find(d, "_results.db")
+    if db:
+        api, ker, cps = load_db(db)
+    else:
+        api = list(csv.DictReader(open(find(d, "hip_api_trace.csv"))))
+        ker = list(csv.DictReader(open(find(d, "kernel_trace.csv"))))
+        mp = find(d, "memory_copy_trace.csv")
+        cps = list(csv.DictReader(open(mp))) if mp else []
     marks = sorted(int(r["Start_Timestamp"]) for r in api if r["Function"] == "hipPeekAtLastError")
     tid = defaultdict(int)
     for r in api:
@@ -38,13 +59,11 @@ def main():
     calls = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "api " + r["Function"]) for r in api
                    if r["Thread_Id"] == main_tid and r["Function"] != "hipPeekAtLastError")
     dev = []
-    for r in csv.DictReader(open(find(d, "kernel_trace.csv"))):
+    for r in ker:
         dev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K " + short(r["Kernel_Name"])))
-    mp = find(d, "memory_copy_trace.csv")
-    if mp:
-        for r in csv.DictReader(open(mp)):
-            dev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
-                        "C " + r["Direction"].replace("MEMORY_COPY_", "") + f" {int(r.get('Bytes', 0) or 0) // 1024}K"))
+    for r in cps:
+        dev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                    "C " + r["Direction"].replace("MEMORY_COPY_", "") + f" {int(r.get('Bytes', 0) or 0) // 1024}K"))
     dev.sort()
     n = len(marks) // 3
     wins = [(marks[3 * i], marks[3 * i + 1], marks[3 * i + 2]) for i in range(n)][-last:]
