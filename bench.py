@@ -136,6 +136,37 @@ def stage_bytes(name, st, key_bytes):
     return key_bytes + 2 * (R + W) * 24.0  # encode
 
 
+def pin_host(dev_index):
+    """Keep this (the Resolver's) thread on the CPUs of the GPU's NUMA node,
+    as a GPU resolver is deployed (taskset / numactl on the fdbserver process).
+    Unpinned, the one host thread of the window migrated across the box's
+    sockets: p50 0.31 ms with 0.5-1.2 ms windows every few batches, against
+    p50 0.28 ms and no such outliers pinned (scripts/diag_window.py,
+    profiles/r03_diag_window_affinity.txt).  Returns a description."""
+    if os.environ.get("FDBCS_BENCH_NO_PIN"):
+        return "not pinned (FDBCS_BENCH_NO_PIN)"
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(dev_index)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return f"not pinned (GPU {bdf} reports no NUMA node)"
+        cpus = set()
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        mine = sorted(cpus & os.sched_getaffinity(0))
+        if not mine:
+            return f"not pinned (no allowed CPU on NUMA node {node})"
+        os.sched_setaffinity(0, mine)
+        return f"the calling thread on NUMA node {node}'s {len(mine)} CPUs (GPU {bdf})"
+    except (OSError, ValueError, AttributeError, RuntimeError) as e:
+        return f"not pinned ({e})"
+
+
 def host_cpu():
     """(model name, CPUs this process may use: affinity, capped by a cgroup quota)."""
     model = "unknown"
@@ -284,6 +315,7 @@ def run_single(args):
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    affinity = pin_host(0)
     from foundationdb_amd import ConflictSet
     from foundationdb_amd.batch import DeviceBatch
     from foundationdb_amd.workload import Workload
@@ -528,7 +560,7 @@ def run_single(args):
         "dtype": "int64",
         "data": "synthetic (deterministic generator, SURVEY.md §8d)",
         "config": {"workload": workload, "txns_per_batch": T, "prefill_batches": args.prefill,
-                   "history_pre": H_pre, "history_post": H_post, "parallelism": "single",
+                   "history_pre": H_pre, "history_post": H_post, "parallelism": "single", "host_affinity": affinity,
                    "window": "Resolver.actor.cpp:139-154: fdbcs_batch_begin + T x fdbcs_batch_add (pinned append, "
                              "chunked H2D) + fdbcs_batch_detect (device pipeline, verdict D2H), native loop"},
         "hbm_resident": hbm,
@@ -578,6 +610,7 @@ def run_multi(args, rank, world):
     local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    affinity = pin_host(local)
     # RCCL over xGMI; FDBCS_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs
     backend = os.environ.get("FDBCS_BENCH_BACKEND", "nccl")
     if backend == "nccl":
@@ -713,6 +746,7 @@ def run_multi(args, rank, world):
             "dtype": "int64",
             "data": "synthetic (deterministic generator, SURVEY.md §8d)",
             "config": {"workload": workload, "txns_per_batch": Tg, "history_pre": H_pre, "history_post": H_post,
+                       "host_affinity": f"rank 0: {affinity}",
                        "parallelism": {"exact": f"sharded{world}", "resolvers": f"keyrange{world}"}[mode],
                        "window": "batches staged in HBM (device path; the RCCL exchanges inside the step)"},
             "roofline": None,

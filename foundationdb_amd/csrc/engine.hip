@@ -127,6 +127,7 @@ struct fdbcs {
     // stage.h (pinned record stream, chunked H2D, k_unpack at detect)
     bool in_batch = false;
     TxnStage st;
+    uint64_t stage_key_total = 0;  // the staged batch's key bytes while it runs (TxnStage::key_total)
     // pinned host staging + device input staging
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
@@ -684,8 +685,11 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
     cs->edges_known = false;
     cs->have_last_dv = false;  // (the host paths set it again once this batch succeeded)
-    if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
-    if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    // (a staged batch's keys can outnumber its stream's bytes: point ranges
+    // share theirs, stage.hip)
+    const uint64_t kb = std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total);
+    if ((r = ensure_batch(cs, T, R, W, kb))) return r;
+    if ((r = ensure_history(cs, W, kb))) return r;
     if (early && (r = ensure_pinned(cs->vpin, cs->vpin_cap, vpin_scalars_off(T) + sizeof(Scalars)))) return r;
     if (early && (size_t)T + 64 > cs->vmap_cap) {
         if (cs->vmap) hipHostFree(cs->vmap);
@@ -1099,7 +1103,9 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     int r;
     fdbcs_batch_view dv;
     if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
+    cs->stage_key_total = cs->st.key_total();
     r = finish_detect(cs, dv, now, new_oldest, verdict);
+    cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};  // (the ingest that reads it was launched)
     if (r) return r;
     cs->last_dv = dv;
@@ -1465,8 +1471,8 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     int r;
     if ((r = check_batch_shape(v))) return r;
     cs->have_last_dv = false;
-    if ((r = ensure_batch(cs, v.txn_count, v.read_count, v.write_count, v.key_bytes_len))) return r;
-    if ((r = ensure_history(cs, v.write_count, v.key_bytes_len))) return r;
+    if ((r = ensure_batch(cs, v.txn_count, v.read_count, v.write_count, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
+    if ((r = ensure_history(cs, v.write_count, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
     cs->last_T = v.txn_count;
     cs->last_R = v.read_count;
     cs->last_W = v.write_count;
@@ -1587,18 +1593,33 @@ int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_e
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
                         int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {
     if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
-    if (!cs || !info || a < 0 || b < a || key_index >= cs->known_H) return FDBCS_E_ARG;
+    // (the window lies in the history the last apply left: known_H, synchronized there)
+    if (!cs || !info || a < 0 || b < a || b > cs->known_H || key_index >= cs->known_H) return FDBCS_E_ARG;
     hipStream_t s = cs->stream;
+    static const bool dbg = getenv("FDBCS_DEBUG_SYNC") != nullptr;  // (fault hunting: name the failing step)
+    auto step_ok = [&](const char* what) {
+        if (!dbg) return FDBCS_OK;
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            fprintf(stderr, "fdbcs debug: shard_compact %s failed: %s (a=%lld b=%lld H=%lld D=%d key=%lld win_cap=%d)\n",
+                    what, hipGetErrorString(e), (long long)a, (long long)b, (long long)cs->known_H, (int)cs->known_D,
+                    (long long)key_index, (int)cs->b.win_cap_pages);
+            return FDBCS_E_HIP;
+        }
+        return FDBCS_OK;
+    };
+    int r;
     if (key_index >= 0) {  // the boundary that becomes removalKey, read before the compaction moves it
         launch_key_at(cs->h, cs->cur, cs->sc, key_index, cs->key_out, cs->key_out_tail, s);
+        if ((r = step_ok("key_at"))) return r;
         HIPOK(hipMemcpyAsync(cs->rk_stage, cs->key_out, 24, hipMemcpyDeviceToHost, s));
         HIPOK(hipMemcpyAsync(cs->rk_stage + 24, cs->key_out_tail, RK_TAIL_FAST, hipMemcpyDeviceToHost, s));
     }
     const WinExplicit w{a, b, keep_first, prev_version};
     launch_compact(cs->b, cs->h, cs->cur, cs->sc, new_oldest, s, &w);
+    if ((r = step_ok("window"))) return r;
     cs->cur ^= 1;
     if (new_oldest > cs->oldest) cs->oldest = new_oldest;
-    int r;
     if ((r = sync_batch(cs))) return r;
     info[0] = cs->sc_host->H;
     info[1] = cs->sc_host->last_ver;
@@ -1694,8 +1715,8 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     if (T && !verdict) return FDBCS_E_ARG;
     cs->have_last_dv = false;
     cs->edges_known = false;
-    if ((r = ensure_batch(cs, T, R, W, v.key_bytes_len))) return r;
-    if ((r = ensure_history(cs, W, v.key_bytes_len))) return r;
+    if ((r = ensure_batch(cs, T, R, W, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
+    if ((r = ensure_history(cs, W, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
     const size_t slots = sh_slot_bytes(sh), nx = slots + (size_t)std::max<int64_t>(T, 1);
     if ((int64_t)nx > sh->x1_cap) {  // (the slots written after the last batch are kept)
         uint8_t* nb = nullptr;
@@ -1890,7 +1911,9 @@ int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldes
     fdbcs_batch_view dv;
     int r;
     if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
+    cs->stage_key_total = cs->st.key_total();
     r = sh_run(sh, dv, now, new_oldest, verdict);
+    cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};
     return r;
 }

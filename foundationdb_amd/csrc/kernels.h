@@ -39,12 +39,39 @@ struct StageHdr {
 };
 static_assert(sizeof(StageHdr) == 24, "stage record header");
 // a range's keys: the begin key at `kofs` bytes from the record's start, the
-// end key right after it (key lengths <= FDBCS_MAX_KEY < 2^16)
+// end key right after it (key lengths <= FDBCS_MAX_KEY < 2^15).  A point range
+// [k, k\x00) -- the Resolver's usual read and write -- is stored as k and one
+// 0 byte: the end key is then the same bytes one longer, at the begin's
+// offset, marked by STAGE_SHARED in elen (16 of a 16-byte key's 33 bytes not
+// written by the add nor sent over PCIe).
 struct StageRange {
     uint32_t kofs;
     uint16_t blen, elen;
 };
 static_assert(sizeof(StageRange) == 8, "stage range entry");
+constexpr uint16_t STAGE_SHARED = 0x8000;
+static_assert(FDBCS_MAX_KEY < STAGE_SHARED, "the shared-end flag sits above every key length");
+// A transaction with no ranges (always committed: tooOld needs a read,
+// SkipList.cpp:985) has no record: its offset entry is STAGE_EMPTY | wo << 32
+// | ro, the reads and writes added before it -- one 8-byte store per add.
+// Protocol B shards see many (the transactions with no range on the shard).
+constexpr uint64_t STAGE_EMPTY = 1ull << 63;
+struct StageTxn {
+    int64_t snap;
+    int32_t ro, wo, nr, nw;
+    uint64_t base;  // record offset (nr + nw > 0)
+};
+__host__ __device__ inline StageTxn stage_txn(const uint8_t* stream, uint64_t toff) {
+    if (toff & STAGE_EMPTY)
+        return StageTxn{0, (int32_t)(uint32_t)toff, (int32_t)((toff >> 32) & 0x7fffffffu), 0, 0, 0};
+    const StageHdr h = *reinterpret_cast<const StageHdr*>(stream + toff);  // (records are 8-byte aligned)
+    return StageTxn{h.snap, h.ro, h.wo, h.nr, h.nw, toff};
+}
+// (end offset from the record, end length) of a StageRange
+__host__ __device__ inline uint32_t stage_end_ofs(const StageRange& e) {
+    return e.kofs + ((e.elen & STAGE_SHARED) ? 0u : (uint32_t)e.blen);
+}
+__host__ __device__ inline uint32_t stage_end_len(const StageRange& e) { return e.elen & (STAGE_SHARED - 1); }
 // k_unpack: one lane per transaction turns the stream (device copy) into the
 // arrays of a fdbcs_batch_view (layout below, key_bytes = the stream itself)
 struct UnpackOut {

@@ -44,7 +44,10 @@ __device__ inline Key encode_key(const uint8_t* p, uint32_t L, uint8_t* btail, u
         const uint64_t m = L - 17, padded = (m + 7) & ~7ull;
         const uint64_t o = atomicAdd((unsigned long long*)&sc->btail_used, (unsigned long long)padded);
         if (o + padded > btail_cap) {
+            // the batch fails; later kernels still compare this key, so it
+            // points at readable bytes (the buffer holds >= 64 KB > any tail)
             atomicCAS(&sc->err, 0, FDBCS_E_CAPACITY);
+            tail = btail;
         } else {
             uint8_t* d = btail + o;
             for (uint64_t i = 0; i < padded; i++) d[i] = i < m ? p[17 + i] : 0;
@@ -642,10 +645,9 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
     const bool ht = lane < STG_TPW && t < A.T;
     int n = 0;
     if (ht) {
-        const uint64_t base = S.toff[t];
-        const StageHdr h = *reinterpret_cast<const StageHdr*>(S.stream + base);
+        const StageTxn h = stage_txn(S.stream, S.toff[t]);
         n = h.nr + h.nw;
-        s_base[wv][lane] = base;
+        s_base[wv][lane] = h.base;
         s_snap[wv][lane] = h.snap < A.oldest && h.nr > 0 ? INT64_MAX : h.snap;  // (tooOld: nothing to check)
         s_ro[wv][lane] = h.ro;
         s_wo[wv][lane] = h.wo;
@@ -683,13 +685,14 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
             i = (int64_t)A.R + w;
             A.write_txn[w] = t0 + j;
         }
-        const uint64_t ob = base + e.kofs, oe = ob + e.blen;
+        const uint64_t ob = base + e.kofs, oe = base + stage_end_ofs(e);
+        const uint32_t el = stage_end_len(e);
         S.view.koff[2 * i] = ob;
         S.view.klen[2 * i] = e.blen;
         S.view.koff[2 * i + 1] = oe;
-        S.view.klen[2 * i + 1] = e.elen;
+        S.view.klen[2 * i + 1] = el;
         const Key b = encode_key(S.stream + ob, e.blen, A.btail, A.btail_cap, A.sc);
-        const Key en = encode_key(S.stream + oe, e.elen, A.btail, A.btail_cap, A.sc);
+        const Key en = encode_key(S.stream + oe, el, A.btail, A.btail_cap, A.sc);
         A.keys.put(2 * i, b);
         A.keys.put(2 * i + 1, en);
         if (kcmp(b, en) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
@@ -1304,8 +1307,8 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* __restrict__ stre
         o.wo[T] = W;
         return;
     }
-    const uint64_t base = toff[t];
-    const StageHdr h = *reinterpret_cast<const StageHdr*>(stream + base);
+    const StageTxn h = stage_txn(stream, toff[t]);
+    const uint64_t base = h.base;
     o.snap[t] = h.snap;
     o.ro[t] = h.ro;
     o.wo[t] = h.wo;
@@ -1315,8 +1318,8 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* __restrict__ stre
         const int64_t slot = k < h.nr ? 2ll * (h.ro + k) : 2ll * R + 2ll * (h.wo + k - h.nr);
         o.koff[slot] = base + e.kofs;
         o.klen[slot] = e.blen;
-        o.koff[slot + 1] = base + e.kofs + e.blen;
-        o.klen[slot + 1] = e.elen;
+        o.koff[slot + 1] = base + stage_end_ofs(e);
+        o.klen[slot + 1] = stage_end_len(e);
     }
 }
 

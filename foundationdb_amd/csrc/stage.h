@@ -54,6 +54,9 @@ class TxnStage {
     // builds them now (FDBCS_SEPARATE_UNPACK: always).
     int finish(fdbcs_batch_view& dv, StagedBatch* staged = nullptr);
     int64_t txns() const { return T_; }
+    // the batch's key bytes (every begin and end key): more than the stream
+    // holds when point ranges share their bytes; sizes the tail buffers
+    uint64_t key_total() const { return K_; }
     bool open() const { return open_; }
 
    private:
@@ -67,6 +70,7 @@ class TxnStage {
     uint64_t chunk_ = 512 << 10;
     bool open_ = false;
     int64_t T_ = 0, R_ = 0, W_ = 0;
+    uint64_t K_ = 0;
     // the record stream: pinned + device copy, same capacity
     uint8_t* pin_ = nullptr;
     uint8_t* dev_ = nullptr;

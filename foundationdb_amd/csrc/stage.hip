@@ -17,7 +17,8 @@ inline uint64_t ld64(const uint8_t* p) {
     return x;
 }
 
-// the reference's key order (SkipList.cpp:113-120), eight bytes at a time
+// the reference's key order (SkipList.cpp:113-120), eight bytes at a time;
+// -2: a is a proper prefix of b (so a < b)
 __attribute__((always_inline)) inline int key_cmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
     const uint32_t n = std::min(al, bl);
     uint32_t i = 0;
@@ -27,7 +28,7 @@ __attribute__((always_inline)) inline int key_cmp(const uint8_t* a, uint32_t al,
     }
     for (; i < n; i++)
         if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-    return al < bl ? -1 : (al > bl ? 1 : 0);
+    return al < bl ? -2 : (al > bl ? 1 : 0);
 }
 
 // copy n bytes; reads and writes stay inside the n bytes
@@ -51,18 +52,26 @@ __attribute__((always_inline)) inline void copy_small(uint8_t* d, const uint8_t*
 
 // check and copy ranges into the record at rec: entries (where the keys are,
 // their lengths) and the key bytes at kp (advanced); true if some range has
-// begin >= end
+// begin >= end.  A point range [k, k\x00) is written as k\x00 once
+// (kernels.h STAGE_SHARED): the begin < end compare already tells it.
 __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int n, StageRange* ent,
                                                       const uint8_t* rec, uint8_t*& kp) {
     bool bad = false;
     for (int i = 0; i < n; i++) {
         const uint8_t *b = rg[i].begin, *e = rg[i].end;
         const uint32_t bl = rg[i].begin_len, el = rg[i].end_len;
-        bad |= key_cmp(b, bl, e, el) >= 0;
-        ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)el};
+        const int c = key_cmp(b, bl, e, el);
+        bad |= c >= 0;
         copy_small(kp, b, bl);
-        copy_small(kp + bl, e, el);
-        kp += bl + el;
+        if (c == -2 && el == bl + 1 && e[bl] == 0) {  // point range: k then one 0 byte
+            ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)(el | STAGE_SHARED)};
+            kp[bl] = 0;
+            kp += bl + 1;
+        } else {
+            ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)el};
+            copy_small(kp + bl, e, el);
+            kp += bl + el;
+        }
     }
     return bad;
 }
@@ -100,6 +109,7 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
 
 int TxnStage::begin() {
     T_ = R_ = W_ = 0;
+    K_ = 0;
     used_ = sent_ = 0;
     if (!pin_) {
         int r = grow(8192, 4 << 20);
@@ -142,15 +152,28 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     if (nr < 0 || nw < 0 || (nr && !reads) || (nw && !writes)) return FDBCS_E_ARG;
     if (T_ >= MAX_T || R_ + nr > INT32_MAX / 2 || W_ + nw > INT32_MAX / 2) return FDBCS_E_CAPACITY;
     const int n = nr + nw;
+    if (n == 0) {  // no record: the offset entry says so (kernels.h STAGE_EMPTY)
+        if (T_ + 1 > toff_cap_ || used_ + 8 * (uint64_t)(T_ + 1) + 16 > cap_) {
+            int r = grow(T_ + 1, used_ + 8 * (uint64_t)(T_ + 1) + 16);
+            if (r) return r;
+        }
+        toff_[T_++] = STAGE_EMPTY | ((uint64_t)W_ << 32) | (uint64_t)R_;
+        return FDBCS_OK;
+    }
     uint64_t kbytes = 0;
     uint32_t longest = 0;
+    // (the keys are requested here, all at once, and read in the copy pass)
     for (int i = 0; i < nr; i++) {
         kbytes += (uint64_t)reads[i].begin_len + reads[i].end_len;
         longest = std::max({longest, reads[i].begin_len, reads[i].end_len});
+        __builtin_prefetch(reads[i].begin);
+        __builtin_prefetch(reads[i].end);
     }
     for (int i = 0; i < nw; i++) {
         kbytes += (uint64_t)writes[i].begin_len + writes[i].end_len;
         longest = std::max({longest, writes[i].begin_len, writes[i].end_len});
+        __builtin_prefetch(writes[i].begin);
+        __builtin_prefetch(writes[i].end);
     }
     if (longest > FDBCS_MAX_KEY) return FDBCS_E_KEY;
     const uint64_t rec = (sizeof(StageHdr) + 8 * (uint64_t)n + kbytes + 7) & ~uint64_t(7);
@@ -167,11 +190,13 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     bool bad = put_ranges(reads, nr, ent, p, kp);
     bad |= put_ranges(writes, nw, ent + nr, p, kp);
     if (bad) return FDBCS_E_RANGE;  // (the record is not committed: used_ stays)
+    const uint64_t rec_used = ((uint64_t)(kp - p) + 7) & ~uint64_t(7);  // (<= rec: point ranges share bytes)
     const StageHdr h{snap, (int32_t)R_, (int32_t)W_, nr, nw};
     memcpy(p, &h, sizeof h);
     toff_[T_] = used_;
-    used_ += rec;
+    used_ += rec_used;
     T_++;
+    K_ += kbytes;
     R_ += nr;
     W_ += nw;
     if (used_ - sent_ >= chunk_) {
