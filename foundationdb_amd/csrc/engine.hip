@@ -1666,6 +1666,18 @@ struct fdbcs_sharded {
     uint8_t* hx = nullptr;      // pinned staging of the host-callback exchanges
     size_t hx_cap = 0;
     bool in_batch = false;
+    // protocol B (fdbcs_sharded_set_protocol)
+    int proto = FDBCS_PROTOCOL_A;
+    bool presplit = false;                 // the caller's adds carry only this rank's ranges
+    std::vector<uint8_t> lo, hi;           // this rank's keys [lo, hi) (host copies, for the add filter)
+    bool has_lo = false, has_hi = false;
+    std::vector<fdbcs_range> keep;         // the add filter's output
+    int32_t* ebuf = nullptr;               // device: [send 2M | recv G x 2M | readers E | writers E]
+    int64_t ebuf_cap = 0;                  // (int32 elements)
+    uint64_t* emap = nullptr;              // host-mapped: k_sh_edges_plan's {seq, max, total, overflow, own}
+    uint64_t* emap_dev = nullptr;
+    uint64_t eseq = 0;
+    hipEvent_t ev_edges = nullptr;
 };
 
 namespace {
@@ -1688,9 +1700,8 @@ int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
     return FDBCS_OK;
 }
 
-int sh_allgather(fdbcs_sharded* sh, const int64_t* dev_send, int64_t* dev_recv) {
+int sh_allgather(fdbcs_sharded* sh, const void* dev_send, void* dev_recv, size_t n = SH_WORDS * 8) {
     hipStream_t s = sh->cs->stream;
-    const size_t n = SH_WORDS * 8;
     if (!sh->host_ops) {
         if (ncclAllGather(dev_send, dev_recv, n, ncclUint8, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
         return FDBCS_OK;
@@ -1700,9 +1711,73 @@ int sh_allgather(fdbcs_sharded* sh, const int64_t* dev_send, int64_t* dev_recv) 
     HIPOK(hipMemcpyAsync(sh->hx, dev_send, n, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
     if (sh->ops.allgather_u8(sh->ops.ctx, sh->hx, sh->hx + n, n)) return FDBCS_E_HIP;
-    HIPOK(hipMemcpyAsync(dev_recv, sh->hx + n, n * sh->world, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(dev_recv, sh->hx + n, n * (size_t)sh->world, hipMemcpyHostToDevice, s));
     HIPOK(hipStreamSynchronize(s));
     return FDBCS_OK;
+}
+
+// Protocol B, after the check: exchange 1 (the abort flags and slots, which
+// carry every shard's edge count) and then the union of the shards' overlap
+// edges as this shard's list.  The host reads the counts once (mapped
+// memory, ~2 ms of polling before it blocks on an event) to size the edge
+// all-gather; when any shard's list overflowed, every shard searches again
+// into a larger one and exchange 1 repeats (the read check is idempotent).
+int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, uint8_t* flags) {
+    fdbcs* cs = sh->cs;
+    BatchBufs& b = cs->b;
+    hipStream_t s = cs->stream;
+    const int64_t T = v.txn_count;
+    int64_t* sl = reinterpret_cast<int64_t*>(sh->x1);
+    int r;
+    for (int attempt = 0;; attempt++) {
+        launch_sh_edges_count(cs->sc, sl, sh->rank, sh->world, b.edge_cap, s);
+        if (T) launch_flags_out(b, (int)T, flags, s);
+        if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
+        if (++sh->eseq == 0) sh->eseq = 1;
+        launch_sh_edges_plan(sl, sh->world, sh->rank, sh->emap_dev, sh->eseq, s);
+        HIPOK(hipEventRecord(sh->ev_edges, s));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int it = 1; __atomic_load_n(sh->emap, __ATOMIC_ACQUIRE) != sh->eseq; it++) {
+            _mm_pause();
+            if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                if ((r = wait_event(sh->ev_edges))) return r;
+                if (__atomic_load_n(sh->emap, __ATOMIC_ACQUIRE) != sh->eseq) return FDBCS_E_HIP;
+                break;
+            }
+        }
+        const int64_t mx = (int64_t)sh->emap[1], tot = (int64_t)sh->emap[2], own = (int64_t)sh->emap[4];
+        if (!sh->emap[3]) {
+            if (mx == 0) return FDBCS_OK;  // no overlap anywhere: this shard's empty list is the union
+            if (tot > INT32_MAX) return FDBCS_E_CAPACITY;
+            const int64_t need = 2 * mx * (sh->world + 1) + 2 * tot;
+            if (need > sh->ebuf_cap) {
+                HIPOK(hipStreamSynchronize(s));  // (the previous batch's exchange may still read it)
+                if (sh->ebuf) hipFree(sh->ebuf);
+                sh->ebuf = nullptr;
+                sh->ebuf_cap = 0;
+                const int64_t n = need + need / 2 + 4096;
+                if ((r = dalloc(sh->ebuf, n))) return r;
+                sh->ebuf_cap = n;
+            }
+            int32_t* send = sh->ebuf;
+            int32_t* recv = send + 2 * mx;
+            int32_t* cat = recv + 2 * mx * sh->world;
+            launch_sh_edges_pack(b, cs->sc, mx, send, s);
+            if ((r = sh_allgather(sh, send, recv, (size_t)(2 * mx) * 4))) return r;
+            if (tot > b.edge_cap && (r = grow_edges(b, tot + tot / 4 + 1024))) return r;
+            launch_sh_edges_cat(recv, sl, sh->world, mx, cat, cat + tot, s);
+            launch_set_edges(b, cs->sc, (int)T, cat, cat + tot, tot, s);
+            return FDBCS_OK;
+        }
+        // some shard's list overflowed: every shard searches again (into a
+        // larger list where its own overflowed)
+        if (attempt >= 3) return FDBCS_E_CAPACITY;
+        GROWLOG("sharded edges: own %lld cap %lld\n", (long long)own, (long long)b.edge_cap);
+        if (own > b.edge_cap && (r = grow_edges(b, own + own / 4 + 1024))) return r;
+        if (T) HIPOK(hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s));
+        HIPOK(hipMemsetAsync(&cs->sc->edges_total, 0, sizeof(int32_t), s));
+        launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, sh->v0, s);
+    }
 }
 
 // one batch of the sharded resolver on the device-resident view v
@@ -1758,10 +1833,16 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
         cs->sorts++;
         cs->have_quantiles = true;
     }
-    if ((r = edges_read_check(cs, v, sh->v0))) return r;
-    if (T) launch_flags_out(b, (int)T, flags, s);
-    // 3: exchange 1
-    if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
+    if (sh->proto == FDBCS_PROTOCOL_B) {
+        // 3 (protocol B): exchange 1 with the edge counts, then the edges
+        launch_edges_read_check(v, b, cs->h, cs->cur, sc, sh->v0, s);
+        if ((r = sh_exchange_b(sh, v, slots, flags))) return r;
+    } else {
+        if ((r = edges_read_check(cs, v, sh->v0))) return r;
+        if (T) launch_flags_out(b, (int)T, flags, s);
+        // 3: exchange 1
+        if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
+    }
     launch_sh_carry(sc, reinterpret_cast<const int64_t*>(sh->x1), sh->rank, sh->v0, s);
     if (T) launch_flags_in(b, (int)T, flags, s);
     // 4: the decision, verdicts to host-mapped memory
@@ -1834,9 +1915,21 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     // this rank's keys: [bound[rank-1], bound[rank])
     const uint8_t* lo = rank > 0 ? bound_bytes + bound_off[rank - 1] : nullptr;
     const uint8_t* hi = rank < world - 1 ? bound_bytes + bound_off[rank] : nullptr;
+    for (int g = 1; g + 1 < world; g++)  // (the header asks for strictly increasing split keys)
+        if (keycmp(bound_bytes + bound_off[g - 1], bound_len[g - 1], bound_bytes + bound_off[g], bound_len[g]) >= 0)
+            return fail(FDBCS_E_ARG);
     if ((r = fdbcs_set_shard(cs, lo, rank > 0 ? bound_len[rank - 1] : 0, rank > 0, hi,
                              rank < world - 1 ? bound_len[rank] : 0, rank < world - 1)))
         return fail(r);
+    sh->has_lo = rank > 0;
+    sh->has_hi = rank < world - 1;
+    if (sh->has_lo) sh->lo.assign(lo, lo + bound_len[rank - 1]);
+    if (sh->has_hi) sh->hi.assign(hi, hi + bound_len[rank]);
+    if (hipHostMalloc((void**)&sh->emap, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(FDBCS_E_NOMEM);
+    memset(sh->emap, 0, 64);
+    HIPOK(hipHostGetDevicePointer((void**)&sh->emap_dev, sh->emap, 0));
+    HIPOK(hipEventCreateWithFlags(&sh->ev_edges, hipEventDisableTiming));
     if (hipMalloc((void**)&sh->x2, (size_t)(world + 1) * SH_WORDS * 8) != hipSuccess) return fail(FDBCS_E_NOMEM);
     launch_sh_init(cs->sc, v0, true, cs->stream);
     if (ops) {
@@ -1865,6 +1958,9 @@ void fdbcs_sharded_destroy(fdbcs_sharded* sh) {
     if (sh->x1) hipFree(sh->x1);
     if (sh->x2) hipFree(sh->x2);
     if (sh->hx) hipHostFree(sh->hx);
+    if (sh->ebuf) hipFree(sh->ebuf);
+    if (sh->emap) hipHostFree(sh->emap);
+    if (sh->ev_edges) hipEventDestroy(sh->ev_edges);
     if (sh->cs) fdbcs_destroy(sh->cs);
     delete sh;
 }
@@ -1895,11 +1991,56 @@ int fdbcs_sharded_batch_begin(fdbcs_sharded* sh) {
     return FDBCS_OK;
 }
 
+int fdbcs_sharded_set_protocol(fdbcs_sharded* sh, int protocol, int flags) {
+    if (!sh || sh->in_batch || (protocol != FDBCS_PROTOCOL_A && protocol != FDBCS_PROTOCOL_B) ||
+        (flags & ~FDBCS_SHARD_PRESPLIT))
+        return FDBCS_E_ARG;
+    sh->proto = protocol;
+    sh->presplit = (flags & FDBCS_SHARD_PRESPLIT) != 0;
+    sh->cs->sparse_edges = protocol == FDBCS_PROTOCOL_B;  // (the overlap edges are exported, no rounds)
+    return FDBCS_OK;
+}
+
 int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
                             const fdbcs_range* writes, int32_t nwrites) {
     if (!sh) return FDBCS_E_ARG;
     if (!sh->in_batch) return FDBCS_E_STATE;
-    return fdbcs_batch_add(sh->cs, read_snapshot, reads, nreads, writes, nwrites);
+    if (sh->proto == FDBCS_PROTOCOL_A || sh->presplit || sh->world == 1)
+        return fdbcs_batch_add(sh->cs, read_snapshot, reads, nreads, writes, nwrites);
+    // protocol B: only the ranges that intersect this rank's keys, and the
+    // writes ending exactly at its first key (their end node is created here)
+    // -- fdbcs_split_batch_keep_all's rule, as the proxy splits for resolvers
+    // (MasterProxyServer.actor.cpp:267-307).  The transaction stays (its
+    // index is global) even with nothing left.
+    if (nreads < 0 || nwrites < 0 || (nreads && !reads) || (nwrites && !writes)) return FDBCS_E_ARG;
+    // every rank refuses the same transactions: the checks run on all of its
+    // ranges, not just the ones kept here (include/fdbcs.h fdbcs_batch_add)
+    for (int32_t i = 0; i < nreads + nwrites; i++) {
+        const fdbcs_range& x = i < nreads ? reads[i] : writes[i - nreads];
+        if (x.begin_len > FDBCS_MAX_KEY || x.end_len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+    }
+    for (int32_t i = 0; i < nreads + nwrites; i++) {
+        const fdbcs_range& x = i < nreads ? reads[i] : writes[i - nreads];
+        if (keycmp(x.begin, x.begin_len, x.end, x.end_len) >= 0) return FDBCS_E_RANGE;
+    }
+    const uint8_t* lo = sh->lo.data();
+    const uint8_t* hi = sh->hi.data();
+    const uint32_t ll = (uint32_t)sh->lo.size(), hl = (uint32_t)sh->hi.size();
+    auto hits = [&](const fdbcs_range& x) {
+        return (!sh->has_lo || keycmp(x.end, x.end_len, lo, ll) > 0) &&
+               (!sh->has_hi || keycmp(x.begin, x.begin_len, hi, hl) < 0);
+    };
+    std::vector<fdbcs_range>& k = sh->keep;
+    k.clear();
+    for (int32_t i = 0; i < nreads; i++)
+        if (hits(reads[i])) k.push_back(reads[i]);
+    const int32_t kr = (int32_t)k.size();
+    for (int32_t i = 0; i < nwrites; i++)
+        if (hits(writes[i]) || (sh->has_lo && keycmp(writes[i].end, writes[i].end_len, lo, ll) == 0))
+            k.push_back(writes[i]);
+    // (a read dropped here still makes the transaction tooOld-capable: the
+    // shard holding it reports the flag, and the MAX picks it)
+    return fdbcs_batch_add(sh->cs, read_snapshot, k.data(), kr, k.data() + kr, (int32_t)k.size() - kr);
 }
 
 int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict) {

@@ -582,10 +582,19 @@ class ShardedResolver:
     torch.distributed ``group`` (gloo) -- the multi-process tests on one GPU.
     """
 
-    def __init__(self, bounds, rank, world, device=0, v0=0, max_history=0, comm_id=None, group=None):
+    PROTOCOLS = {"a": 0, "b": 1}  # FDBCS_PROTOCOL_A / _B
+    PRESPLIT = 1                  # FDBCS_SHARD_PRESPLIT
+
+    def __init__(self, bounds, rank, world, device=0, v0=0, max_history=0, comm_id=None, group=None, protocol="a",
+                 presplit=False):
+        """protocol "b": this rank takes only the ranges intersecting its keys
+        (fdbcs_sharded_batch_add filters them unless ``presplit``; the packed
+        and device paths take the rank's fdbcs_split_batch_keep_all share)."""
         assert len(bounds) + 1 == world
         self._lib = _abi.lib()
         self.rank, self.world = rank, world
+        self.bounds = list(bounds)
+        self.protocol = protocol
         kb = b"".join(bounds)
         offs = np.cumsum([0] + [len(b) for b in bounds])[:-1].astype(np.uint64) if bounds else np.zeros(1, np.uint64)
         lens = np.array([len(b) for b in bounds] or [0], np.uint32)
@@ -603,6 +612,8 @@ class ShardedResolver:
                                              lens.ctypes.data, v0, C.byref(cfg), cid, ops_p), "fdbcs_sharded_create")
         self._h = h
         self.local = _LocalEngine(self._lib, self._lib.fdbcs_sharded_local(h))
+        check(self._lib.fdbcs_sharded_set_protocol(h, self.PROTOCOLS[protocol], self.PRESPLIT if presplit else 0),
+              "fdbcs_sharded_set_protocol")
 
     @staticmethod
     def unique_id():
@@ -641,8 +652,16 @@ class ShardedResolver:
     def handle(self):
         return self._h
 
+    def split(self, batch):
+        """This rank's input: the whole batch (protocol A) or its keep-all share (B)."""
+        if self.protocol == "a" or self.world == 1:
+            return batch
+        from .resolvers import KeyRangeResolvers
+
+        return KeyRangeResolvers(self.bounds).split(batch, self.rank, keep_all=True)[0]
+
     def detect_device(self, view, now, new_oldest):
-        """view: the whole batch in device memory (every rank); returns the T verdicts."""
+        """view: this rank's batch in device memory (see split); returns the T verdicts."""
         out = np.zeros(max(1, view.txn_count), np.uint8)
         check(self._lib.fdbcs_sharded_detect_device(self._h, C.byref(view), now, new_oldest, out.ctypes.data),
               "fdbcs_sharded_detect_device")
@@ -652,7 +671,7 @@ class ShardedResolver:
         import torch
         from .batch import DeviceBatch
 
-        db = DeviceBatch(batch, torch.device("cuda", torch.cuda.current_device()))
+        db = DeviceBatch(self.split(batch), torch.device("cuda", torch.cuda.current_device()))
         return self.detect_device(db.view, now, new_oldest)
 
     def detect_txns(self, txns, now, new_oldest):

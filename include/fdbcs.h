@@ -401,7 +401,7 @@ const char* fdbcs_strerror(int status);
 /* Library build identification (git-independent): "fdbcs gfx950 <version>". */
 const char* fdbcs_version(void);
 
-/* ---- One Resolver over G GPUs (SURVEY.md §8e protocol A) ----------------
+/* ---- One Resolver over G GPUs (SURVEY.md §8e protocols A and B) ---------
  * Replaces the proxy's split over G resolvers (MasterProxyServer.actor.cpp:
  * 242-320) with one exact resolver: the verdicts, the concatenated history,
  * removalKey and oldestVersion equal one ConflictSet's
@@ -444,9 +444,28 @@ int  fdbcs_sharded_batch_begin(fdbcs_sharded* sh);
 int  fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
                              const fdbcs_range* writes, int32_t nwrites);
 int  fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict);
-/* A device-resident batch view (every rank the whole batch); host verdicts. */
+/* A device-resident batch view (protocol A: every rank the whole batch;
+ * protocol B: this rank's fdbcs_split_batch_keep_all share); host verdicts. */
 int  fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_batch, int64_t now,
                                  int64_t new_oldest, uint8_t* verdict);
+
+/* Protocol B (the bench's N > 1 default): each rank takes
+ * only the ranges that intersect its keys (and the writes ending exactly at
+ * its first key), so ingest, endpoint sort and overlap search stay
+ * shard-local instead of growing with the whole batch.  Transactions keep
+ * their global batch indices (a rank with none of a transaction's ranges
+ * still counts it).  Exchange 1 also carries each rank's overlap-edge count;
+ * the host reads the counts (mapped memory) to size one all-gather of the
+ * edge lists, skipped when no rank has any, and every rank runs the
+ * identical ordered decision over their union.  Flags: FDBCS_SHARD_PRESPLIT
+ * = the caller's adds already carry only this rank's ranges (the proxy's
+ * per-resolver split, fdbcs_split_batch_keep_all); without it
+ * fdbcs_sharded_batch_add drops the others itself (after checking every
+ * range, so all ranks refuse the same transactions).  Between batches. */
+#define FDBCS_PROTOCOL_A     0
+#define FDBCS_PROTOCOL_B     1
+#define FDBCS_SHARD_PRESPLIT 1
+int  fdbcs_sharded_set_protocol(fdbcs_sharded* sh, int protocol, int flags);
 /* This rank's engine: its part of the history (fdbcs_dump_history,
  * fdbcs_history_size); the owner's fdbcs_removal_key is removalKey. */
 fdbcs* fdbcs_sharded_local(fdbcs_sharded* sh);

@@ -1,6 +1,9 @@
 """fdbcs_sharded (include/fdbcs.h): one exact Resolver over G GPUs behind the
 C ABI -- the HIP engine, the protocol's exchanges and device-side carry-ins /
-compaction plan inside libfdbcs (SURVEY.md §8e protocol A).
+compaction plan inside libfdbcs (SURVEY.md §8e protocols A and B).  Under B
+each rank's per-transaction adds drop the ranges outside its keys inside
+libfdbcs, its packed batches are the keep-all split, and the overlap edges
+travel in exchange 1's counts + one all-gather.
 
 On the one-GPU test box the ranks share GPU 0 and exchange through host
 collectives over torch.distributed gloo (fdbcs_comm_ops); the RCCL path is
@@ -28,7 +31,9 @@ def _streams(kind, seed):
     return list(mixed_stream(seed, n_batches=8, max_txns=400, keyspace=3000))
 
 
-def _rank(rank, world, port, bounds, kind, seed, q):
+def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None):
+    if edge_cap:  # (a tiny first edge list: every shard searches again into a larger one)
+        os.environ["FDBCS_TEST_EDGE_CAP"] = str(edge_cap)
     import torch
     import torch.distributed as dist
 
@@ -39,7 +44,7 @@ def _rank(rank, world, port, bounds, kind, seed, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:
-        sh = ShardedResolver(bounds, rank, world, device=0)
+        sh = ShardedResolver(bounds, rank, world, device=0, protocol=protocol)
         out = []
         for i, (batch, now, nold) in enumerate(_streams(kind, seed)):
             if kind == "tiny" and i == 12:
@@ -59,8 +64,9 @@ def _rank(rank, world, port, bounds, kind, seed, q):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("protocol", ["a", "b"])
 @pytest.mark.parametrize("world,kind", [(2, "tiny"), (3, "tiny"), (2, "long"), (2, "mixed"), (3, "mixed")])
-def test_sharded_abi_equals_one_conflict_set(gpu, world, kind):
+def test_sharded_abi_equals_one_conflict_set(gpu, world, kind, protocol, edge_cap=None):
     rng = random.Random(world * 31 + len(kind))
     if kind == "mixed":
         bounds = sorted({b"k%06d" % rng.randrange(1, 3000) for _ in range(world - 1)})
@@ -74,8 +80,9 @@ def test_sharded_abi_equals_one_conflict_set(gpu, world, kind):
     seed = 4321 + world + len(kind)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + random.Random(os.getpid() * 13 + world + len(kind)).randint(0, 3000)
-    procs = [ctx.Process(target=_rank, args=(r, world, port, bounds, kind, seed, q)) for r in range(world)]
+    port = 29500 + random.Random(os.getpid() * 13 + world + len(kind) + 7 * ord(protocol[0])).randint(0, 3000)
+    procs = [ctx.Process(target=_rank, args=(r, world, port, bounds, kind, seed, q, protocol, edge_cap))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=240) for _ in range(world))
@@ -103,6 +110,14 @@ def test_sharded_abi_equals_one_conflict_set(gpu, world, kind):
             assert c.removal_key() == b"", i
         assert hist == c.history(), i
     c.close()
+
+
+@pytest.mark.gpu
+def test_sharded_abi_protocol_b_edge_overflow(gpu):
+    """Protocol B with a 3-pair first edge list: the overlapping mixed stream
+    overflows it on some rank, every rank searches again (exchange 1
+    repeats) and the edges travel in the all-gather."""
+    test_sharded_abi_equals_one_conflict_set(gpu, 3, "mixed", "b", edge_cap=3)
 
 
 @pytest.mark.gpu
