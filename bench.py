@@ -192,7 +192,7 @@ def host_cpu():
     return model, n
 
 
-def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm=()):
+def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm=(), label=None):
     """oracle/cpu_spec.cpp (the build's CPU restatement) on the GPU box's host
     cores, on the timed batches, starting from the GPU's own steady-state
     history: 1 core (one ConflictSet, verdicts compared
@@ -223,10 +223,11 @@ def cpu_baselines(args, snap, wl, first, n_max, gpu_verdicts, batches=None, warm
         n += 1
     c.close()
     T = batches[0][0].T
-    one = {"value": round(n * T / tc, 1), "unit": "txn/s", "cores": 1, "kind": "port",
-           "sample": f"config {args.config}: batches {first}..{first + n - 1} ({n} x {T} txns, the timed batches) "
-                     f"from the GPU's steady-state history (H={len(vers)}, then the {len(warm)} warmup batches "
-                     f"replayed untimed); verdict mismatches vs GPU: {mism}",
+    sample = (f"config {args.config}: batches {first}..{first + n - 1} ({n} x {T} txns, the timed batches) "
+              f"from the GPU's steady-state history (H={len(vers)}, then the {len(warm)} warmup batches "
+              f"replayed untimed); verdict mismatches vs GPU: {mism}") if label is None else label.format(
+        n=n, T=T, H=len(vers), first=first)
+    one = {"value": round(n * T / tc, 1), "unit": "txn/s", "cores": 1, "kind": "port", "sample": sample,
            "host_cpu": model, "host_cpus_available": avail, "history_load_s": round(t_load, 1)}
     # N cores: N key-range resolvers, each loaded with its slice of the history
     N = max(1, min(args.cpu_threads, avail))
@@ -604,6 +605,186 @@ class Source:
 
 
 def run_multi(args, rank, world):
+    """N > 1, --mode exact: one exact resolver sharded by key range over N
+    GPUs behind the C ABI (fdbcs_sharded, protocol B by default), each rank
+    timing the SAME window as N = 1 -- the Resolver's loop in native code
+    (fdbcs_sharded_batch_begin + T x _add + _detect, verdicts to the host) --
+    over its input: under protocol B the proxy's keep-all split of each global
+    batch (every transaction, only the ranges on the rank's keys; generated
+    and split before the clock), under A the whole batch."""
+    if args.mode != "exact" or args.impl != "abi":
+        return run_multi_resolvers(args, rank, world)
+    import torch
+    import torch.distributed as dist
+
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    affinity = pin_host(local)
+    backend = os.environ.get("FDBCS_BENCH_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+    from foundationdb_amd.resolvers import KeyRangeResolvers, uniform_bounds
+    from foundationdb_amd.sharded import ShardedResolver
+    from foundationdb_amd.workload import Workload
+
+    cfg = args.config
+    proto = args.protocol
+    bounds = uniform_bounds(world)
+    if backend == "nccl":  # RCCL inside libfdbcs, on the engine's stream
+        obj = [ShardedResolver.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        eng = ShardedResolver(bounds, rank, world, device=local, max_history=max_history(cfg), comm_id=obj[0],
+                              protocol=proto, presplit=(proto == "b"))
+    else:  # host collectives over the gloo group (rehearsals)
+        eng = ShardedResolver(bounds, rank, world, device=local, max_history=max_history(cfg), group=None,
+                              protocol=proto, presplit=(proto == "b"))
+    split = (bounds, rank) if proto == "b" else None
+    wl = Workload(cfg, txns=args.txns * world)  # weak scaling: T = txns x N per global batch
+
+    def global_sum(x):
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    def run_batches(first, n, chunk=10, verdicts=False):
+        us, add, vs = [], [], []
+        for j in range(first, first + n, chunk):
+            run = wl.prepare_run(j, min(chunk, first + n - j), split)
+            u, a, v = run.run(eng, verdicts=verdicts)
+            us.append(u)
+            add.append(a)
+            if verdicts:
+                vs.append(v)
+            del run
+        return (np.concatenate(us) if us else np.zeros(0), np.concatenate(add) if add else np.zeros(0),
+                np.concatenate(vs) if vs else None)
+
+    t_w = time.time()
+    if cfg == 5:  # preload: 50 blind-write global batches, no compaction
+        pre = Workload(50, txns=args.txns * world)
+        for j in range(PRELOAD_BATCHES):
+            run = pre.prepare_run(j, 1, split)
+            run.run(eng, verdicts=False)
+            del run
+        pre.close()
+    # steady state: the prefill (its global batches carry N x the transactions,
+    # so N x fewer of them reach the same history), then the warmup, all
+    # through the same loop (untimed)
+    n_pre = args.prefill // max(1, world)
+    run_batches(0, n_pre + args.warmup, chunk=1 if cfg == 5 else 10)
+    first = n_pre + args.warmup
+    H_loc_pre = eng.local.history_size()
+    H_pre = global_sum(H_loc_pre)
+    if rank == 0:
+        print(f"# steady state: {n_pre} prefill + {args.warmup} warmup global batches, H={H_pre} "
+              f"({time.time() - t_w:.1f}s)", file=sys.stderr, flush=True)
+    # ---- timed region: K batches through the Resolver's window on every rank ----
+    run = wl.prepare_run(first, args.steps, split)
+    T = run.T
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    us, add_us, verdicts = run.run(eng, verdicts=True)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    del run
+    H_loc_post = eng.local.history_size()
+    H_post = global_sum(H_loc_post)
+    next_i = first + args.steps
+    value = T * args.steps / elapsed
+    lat_ms = us / 1e3
+    # this rank's share: key bytes of the timed batches (regenerated after the clock)
+    probe = wl.prepare_run(first, 1, split)
+    share_key_bytes = probe.key_bytes()
+    del probe
+    # ---- latency leg (secondary) ----
+    latency = None
+    if args.latency_batches > 0:
+        n_lat = min(args.latency_batches, 200)
+        lus, ladd, _v = run_batches(next_i, n_lat)
+        next_i += n_lat
+        la = lus / 1e3
+        latency = {"batches": n_lat, "mean_ms": round(float(la.mean()), 4),
+                   "p50_ms": round(float(np.percentile(la, 50)), 4), "p99_ms": round(float(np.percentile(la, 99)), 4),
+                   "max_ms": round(float(la.max()), 4), "add_us_mean": round(float(np.mean(ladd)), 2),
+                   "window": "rank 0's Resolver window per batch, right after the timed region"}
+    # ---- roofline: SURVEY.md §8d bytes of one GPU's share over the timed ms_per_step ----
+    step_s = elapsed / args.steps
+    kb = share_key_bytes
+    algo = pipeline_bytes(kb, T, H_loc_pre, H_loc_post, cfg)
+    achieved = algo / step_s / 1e9
+    roofline = {"bound": "hbm", "kernel": "one Resolver window per GPU (its share of the global batch): SURVEY §8d "
+                                          "bytes of rank 0's share over the timed ms_per_step (max over ranks)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "algo_bytes_per_batch": round(algo),
+                "algo_bytes_terms": {"key_bytes": kb, "txn_bytes": 9 * T,
+                                     "history_bytes": round((32.0 if cfg == 4 else E_HIST) * (H_loc_pre + H_loc_post))},
+                "history_pre_rank0": H_loc_pre, "ms_per_step": round(step_s * 1e3, 4)}
+    # ---- CPU baseline (rank 0): the oracle on rank 0's share -------------------
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        snap = eng.local.dump_arrays() + (eng.local.header_version, eng.local.oldest_version, b"")
+        kr = KeyRangeResolvers(bounds) if proto == "b" else None
+        sub = []
+        for i in range(next_i, next_i + min(args.steps, 20)):
+            b, now, nold = wl.batch(i)
+            sub.append((kr.split(b, 0, keep_all=True)[0] if kr else b, now, nold))
+        what = "its keep-all split for rank 0's keys" if kr else "the whole batch"
+        cpu = cpu_baselines(args, snap, wl, next_i, len(sub), None, batches=sub,
+                            label="config %d: rank 0's share of global batches {first}..{first}+{n} ({n} x {T} txns, "
+                                  "%s) from rank 0's history slice after the timed region (H={H}): one GPU's share "
+                                  "of the work on the host (throughput only)" % (cfg, what))
+    dist.barrier()
+    if rank == 0:
+        how = ("protocol B: each GPU takes only the ranges on its keys (the proxy's keep-all split, before the clock); "
+               "RCCL MAX all-reduce of abort flags + slots carrying every shard's edge count, one all-gather of the "
+               "overlap edges when any shard has some, all-gather for the compaction window; carry-ins, compaction "
+               "plan and removalKey owner on the device" if proto == "b" else
+               "protocol A: every GPU takes the whole batch; RCCL MAX all-reduce of abort flags + all-gather for the "
+               "compaction window")
+        workload = (f"config{cfg}: {T}-txn global batches ({args.txns}/GPU), {CONFIG_SHAPE.get(cfg, '')}, "
+                    f"5M-version window; one exact resolver sharded by key range over {world} GPUs ({how})")
+        out = {
+            "metric": "resolved txns/sec (whole node) at 5k-txn batches; p99 detectConflicts latency",
+            "value": round(value, 1),
+            "unit": "txn/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "p99_batch_ms": round(float(np.percentile(lat_ms, 99)), 4),
+            "p50_batch_ms": round(float(np.percentile(lat_ms, 50)), 4),
+            "add_us_mean": round(float(np.mean(add_us)), 2),
+            "latency": latency,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (deterministic generator, SURVEY.md §8d)",
+            "config": {"workload": workload, "txns_per_batch": T, "history_pre": H_pre, "history_post": H_post,
+                       "host_affinity": f"rank 0: {affinity}", "parallelism": f"sharded{world}",
+                       "collectives": "RCCL" if backend == "nccl" else f"host ({backend})",
+                       "window": "Resolver.actor.cpp:139-154 on every rank: fdbcs_sharded_batch_begin + T x "
+                                 "fdbcs_sharded_batch_add + fdbcs_sharded_batch_detect (native loop), max over ranks"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    dist.destroy_process_group()
+
+
+def run_multi_resolvers(args, rank, world):
+    """--mode resolvers (and the Python protocol orchestration, --impl py):
+    batches staged in HBM, the RCCL exchanges inside the step."""
     import torch
     import torch.distributed as dist
 

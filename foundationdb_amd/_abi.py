@@ -142,6 +142,10 @@ WL_FUNCS = [
     ("fdbwl_generate", C.c_int, [C.c_void_p, C.c_int64, C.POINTER(BatchView), C.POINTER(C.c_int64),
                                  C.POINTER(C.c_int64)]),
     ("fdbwl_run_prepare", C.c_void_p, [C.c_void_p, C.c_int64, C.c_int32]),
+    ("fdbwl_run_prepare_split", C.c_void_p, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_int32]),
+    ("fdbwl_run_key_bytes", C.c_uint64, [C.c_void_p, C.c_int32]),
+    ("fdbwl_run_resolver_sharded", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fdbwl_run_destroy", None, [C.c_void_p]),
     ("fdbwl_run_txns", C.c_int32, [C.c_void_p]),
     ("fdbwl_run_resolver", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -364,9 +364,72 @@ fdbwl_run* fdbwl_run_prepare(fdbwl* g, int64_t first, int32_t n) {
     return r;
 }
 
+// As fdbwl_run_prepare, each batch reduced to one rank's protocol-B input:
+// every transaction (global indices) with only the ranges intersecting the
+// rank's keys and the writes ending at its first key -- the proxy's
+// per-resolver split (fdbcs_split_batch_keep_all, MasterProxyServer.actor.cpp:
+// 267-307), done here before the clock as the proxy does it before the
+// request reaches the resolver.
+fdbwl_run* fdbwl_run_prepare_split(fdbwl* g, int64_t first, int32_t n, int32_t nres, const uint8_t* bound_bytes,
+                                   const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver) {
+    if (!g || n < 0 || nres < 1 || resolver < 0 || resolver >= nres) return nullptr;
+    fdbwl_run* r = new fdbwl_run();
+    r->b.resize(n);
+    r->T = g->T;
+    std::vector<int64_t> snap;
+    std::vector<int32_t> ro, wo, idx;
+    std::vector<uint64_t> ko;
+    std::vector<uint32_t> kl;
+    for (int32_t i = 0; i < n; i++) {
+        fdbcs_batch_view v, sv;
+        fdbwl_run::Batch& B = r->b[i];
+        fdbwl_generate(g, first + i, &v, &B.now, &B.nold);
+        snap.resize(v.txn_count);
+        ro.resize(v.txn_count + 1);
+        wo.resize(v.txn_count + 1);
+        idx.resize(v.txn_count);
+        ko.resize(2 * ((size_t)v.read_count + v.write_count));
+        kl.resize(ko.size());
+        if (fdbcs_split_batch_keep_all(&v, nres, bound_bytes, bound_off, bound_len, resolver, &sv, snap.data(),
+                                       ro.data(), wo.data(), ko.data(), kl.data(), idx.data()) != FDBCS_OK) {
+            delete r;
+            return nullptr;
+        }
+        // the share's keys only, in one arena (the request this resolver receives)
+        std::vector<uint64_t> nk(2 * ((size_t)sv.read_count + sv.write_count));
+        uint64_t nb = 0;
+        for (size_t s = 0; s < nk.size(); s++) nb += sv.key_len[s];
+        B.bytes.resize(nb);
+        nb = 0;
+        for (size_t s = 0; s < nk.size(); s++) {
+            memcpy(B.bytes.data() + nb, sv.key_bytes + sv.key_off[s], sv.key_len[s]);
+            nk[s] = nb;
+            nb += sv.key_len[s];
+        }
+        B.snap.assign(sv.snapshot, sv.snapshot + sv.txn_count);
+        B.roff.assign(sv.read_off, sv.read_off + sv.txn_count + 1);
+        B.woff.assign(sv.write_off, sv.write_off + sv.txn_count + 1);
+        const uint8_t* base = B.bytes.data();
+        auto rng = [&](int64_t s) { return fdbcs_range{base + nk[s], sv.key_len[s], base + nk[s + 1], sv.key_len[s + 1]}; };
+        B.reads.resize(sv.read_count);
+        B.writes.resize(sv.write_count);
+        for (int64_t k = 0; k < sv.read_count; k++) B.reads[k] = rng(2 * k);
+        for (int64_t k = 0; k < sv.write_count; k++) B.writes[k] = rng(2 * ((int64_t)sv.read_count + k));
+    }
+    return r;
+}
+
 void fdbwl_run_destroy(fdbwl_run* r) { delete r; }
 
 int32_t fdbwl_run_txns(const fdbwl_run* r) { return r ? r->T : 0; }
+
+uint64_t fdbwl_run_key_bytes(const fdbwl_run* r, int32_t i) {
+    if (!r || i < 0 || (size_t)i >= r->b.size()) return 0;
+    uint64_t n = 0;
+    for (const fdbcs_range& x : r->b[i].reads) n += (uint64_t)x.begin_len + x.end_len;
+    for (const fdbcs_range& x : r->b[i].writes) n += (uint64_t)x.begin_len + x.end_len;
+    return n;
+}
 
 // FDBWL_MARK=1 (measurement): a no-op HIP API call at the window's start, at
 // the end of the adds and at detectConflicts' return, so that a rocprofv3
@@ -402,6 +465,33 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
         const auto ta = std::chrono::steady_clock::now();
         trace_mark();
         if (st == FDBCS_OK) st = fdbcs_batch_detect(cs, B.now, B.nold, out);  // detectConflicts(...)
+        const auto t1 = std::chrono::steady_clock::now();
+        trace_mark();
+        if (st != FDBCS_OK) return st;
+        if (batch_us) batch_us[i] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+        if (add_us) add_us[i] = std::chrono::duration<double, std::micro>(ta - t0).count();
+    }
+    return FDBCS_OK;
+}
+
+// The same loop over one rank of an exact sharded resolver (fdbcs_sharded_*).
+int fdbwl_run_resolver_sharded(fdbwl_run* r, fdbcs_sharded* sh, double* batch_us, double* add_us,
+                               uint8_t* verdicts) {
+    if (!r || !sh) return FDBCS_E_ARG;
+    std::vector<uint8_t> scratch(std::max<int32_t>(r->T, 1));
+    for (size_t i = 0; i < r->b.size(); i++) {
+        const fdbwl_run::Batch& B = r->b[i];
+        uint8_t* out = verdicts ? verdicts + i * (size_t)r->T : scratch.data();
+        trace_mark();
+        const auto t0 = std::chrono::steady_clock::now();
+        int st = fdbcs_sharded_batch_begin(sh);
+        const int T = (int)B.snap.size();
+        for (int t = 0; st == FDBCS_OK && t < T; t++)
+            st = fdbcs_sharded_batch_add(sh, B.snap[t], B.reads.data() + B.roff[t], B.roff[t + 1] - B.roff[t],
+                                         B.writes.data() + B.woff[t], B.woff[t + 1] - B.woff[t]);
+        const auto ta = std::chrono::steady_clock::now();
+        trace_mark();
+        if (st == FDBCS_OK) st = fdbcs_sharded_batch_detect(sh, B.now, B.nold, out);
         const auto t1 = std::chrono::steady_clock::now();
         trace_mark();
         if (st != FDBCS_OK) return st;

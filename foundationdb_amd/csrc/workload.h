@@ -54,8 +54,16 @@ int    fdbwl_generate(fdbwl* g, int64_t index, fdbcs_batch_view* view, int64_t* 
 typedef struct fdbwl_run fdbwl_run;
 fdbwl_run* fdbwl_run_prepare(fdbwl* g, int64_t first, int32_t n);
 void       fdbwl_run_destroy(fdbwl_run* r);
+/* As fdbwl_run_prepare, each batch reduced to rank `resolver`'s input under
+ * the exact sharded protocol B (fdbcs_split_batch_keep_all: every
+ * transaction, only the ranges on the rank's keys), generated and split
+ * before the clock as the proxy splits before the resolver receives. */
+fdbwl_run* fdbwl_run_prepare_split(fdbwl* g, int64_t first, int32_t n, int32_t nres, const uint8_t* bound_bytes,
+                                   const uint64_t* bound_off, const uint32_t* bound_len, int32_t resolver);
 /* Transactions per batch (every prepared batch has the same count). */
 int32_t    fdbwl_run_txns(const fdbwl_run* r);
+/* Key bytes of prepared batch i (every begin and end key of its ranges). */
+uint64_t   fdbwl_run_key_bytes(const fdbwl_run* r, int32_t i);
 
 /* The Resolver's loop (Resolver.actor.cpp:140-153) over the prepared batches:
  * per batch ConflictBatch (fdbcs_batch_begin), T x addTransaction
@@ -63,6 +71,10 @@ int32_t    fdbwl_run_txns(const fdbwl_run* r);
  * wall time of batch i's window, add_us[i] its addTransaction part (both
  * optional); verdicts (optional) = n x T bytes. */
 int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts);
+/* The same loop on one rank of an exact sharded resolver
+ * (fdbcs_sharded_batch_begin / _add / _detect). */
+int fdbwl_run_resolver_sharded(fdbwl_run* r, fdbcs_sharded* sh, double* batch_us, double* add_us,
+                               uint8_t* verdicts);
 
 /* Grow a conflict set's history through n generated batches [first, first+n)
  * (fdbcs_batch_submit_packed / fdbcs_batch_wait, generation of batch i+1

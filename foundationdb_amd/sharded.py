@@ -583,6 +583,7 @@ class ShardedResolver:
     """
 
     PROTOCOLS = {"a": 0, "b": 1}  # FDBCS_PROTOCOL_A / _B
+    sharded = True  # (workload.ResolverRun: the fdbcs_sharded loop)
     PRESPLIT = 1                  # FDBCS_SHARD_PRESPLIT
 
     def __init__(self, bounds, rank, world, device=0, v0=0, max_history=0, comm_id=None, group=None, protocol="a",

@@ -47,9 +47,11 @@ class Workload:
         """Grow cs's history through batches [first, first + n) (native, pipelined)."""
         _abi.check(self._lib.fdbwl_prefill(self._g, cs.handle, first, n), "prefill")
 
-    def prepare_run(self, first, n):
-        """Batches [first, first + n) pre-generated in the Resolver's per-transaction form."""
-        return ResolverRun(self, first, n)
+    def prepare_run(self, first, n, split=None):
+        """Batches [first, first + n) pre-generated in the Resolver's per-transaction form.
+        split = (bounds, rank): each batch reduced to that rank's protocol-B
+        share (fdbwl_run_prepare_split)."""
+        return ResolverRun(self, first, n, split)
 
     def close(self):
         if getattr(self, "_g", None):
@@ -68,9 +70,17 @@ class ResolverRun:
     (Resolver.actor.cpp:140-153: ConflictBatch, T x addTransaction,
     detectConflicts), so the timed window holds no Python."""
 
-    def __init__(self, wl, first, n):
+    def __init__(self, wl, first, n, split=None):
         self._lib = wl._lib
-        self._r = self._lib.fdbwl_run_prepare(wl._g, first, n)
+        if split is None:
+            self._r = self._lib.fdbwl_run_prepare(wl._g, first, n)
+        else:
+            bounds, rank = split
+            kb = np.frombuffer(b"".join(bounds) + b"\0", np.uint8).copy()
+            offs = np.array(np.cumsum([0] + [len(b) for b in bounds])[:-1] if bounds else [0], np.uint64)
+            lens = np.array([len(b) for b in bounds] or [0], np.uint32)
+            self._r = self._lib.fdbwl_run_prepare_split(wl._g, first, n, len(bounds) + 1, kb.ctypes.data,
+                                                        offs.ctypes.data, lens.ctypes.data, rank)
         if not self._r:
             raise RuntimeError("fdbwl_run_prepare failed")
         self.n = n
@@ -78,13 +88,19 @@ class ResolverRun:
 
     def run(self, cs, verdicts=True):
         """Runs every batch; returns (per-batch window in us, its addTransaction
-        part in us, verdicts n x T or None)."""
+        part in us, verdicts n x T or None).  cs: a ConflictSet, or a
+        sharded.ShardedResolver (this rank's fdbcs_sharded calls)."""
         us = np.zeros(max(self.n, 1), np.float64)
         add = np.zeros(max(self.n, 1), np.float64)
         out = np.zeros((max(self.n, 1), max(self.T, 1)), np.uint8) if verdicts else None
-        _abi.check(self._lib.fdbwl_run_resolver(self._r, cs.handle, us.ctypes.data, add.ctypes.data,
-                                                out.ctypes.data if verdicts else None), "resolver loop")
+        fn = self._lib.fdbwl_run_resolver_sharded if getattr(cs, "sharded", False) else self._lib.fdbwl_run_resolver
+        _abi.check(fn(self._r, cs.handle, us.ctypes.data, add.ctypes.data, out.ctypes.data if verdicts else None),
+                   "resolver loop")
         return us[:self.n], add[:self.n], (out[:self.n, :self.T] if verdicts else None)
+
+    def key_bytes(self, i=0):
+        """Key bytes of prepared batch i (SURVEY.md §8d's input term)."""
+        return int(self._lib.fdbwl_run_key_bytes(self._r, i))
 
     def close(self):
         if getattr(self, "_r", None):
