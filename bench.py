@@ -300,14 +300,18 @@ def shim_skiplisttest():
     out = r.stdout
     m = re.search(r"New conflict set:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
     d = re.search(r"Detect only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
+    sk = re.search(r"Skiplist only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
     h = re.search(r"(\d+) entries in version history", out)
     if r.returncode != 0 or not m:
         return {"error": f"rc={r.returncode}", "tail": out[-300:] + r.stderr[-300:]}
     return {"new_conflict_set_mtxn_s": float(m.group(2)), "detect_only_mtxn_s": float(d.group(2)) if d else None,
+            "skiplist_only_mtxn_s": float(sk.group(2)) if sk else None,
             "history_entries": int(h.group(1)) if h else None,
             "reference_here_mtxn_s": 0.155,
             "path": "tests/shim/shim_smoke skiplisttest: ConflictSetShim.cpp skipListTest() (config 1: 500 x 2,500 "
-                    "txns) -> addTransaction / detectConflicts -> libfdbcs"}
+                    "txns) -> addTransaction / detectConflicts -> libfdbcs; 'New conflict set' includes building the "
+                    "transactions (g_buildTest) as SkipList.cpp:1456-1489 does; 'Skiplist only' = device D.CheckRead + "
+                    "D.MergeWrite from a stage-timed second run"}
 
 
 def run_single(args):

@@ -65,6 +65,7 @@ FDBCS_FUNCS = [
     ("fdbcs_set_version", C.c_int, [C.c_void_p, C.c_int64]),
     ("fdbcs_destroy", None, [C.c_void_p]),
     ("fdbcs_batch_begin", C.c_int, [C.c_void_p]),
+    ("fdbcs_batch_skip", C.c_int, [C.c_void_p, C.c_int32]),
     ("fdbcs_batch_add", C.c_int, [C.c_void_p, C.c_int64, C.POINTER(Range), C.c_int32, C.POINTER(Range), C.c_int32]),
     ("fdbcs_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_batch_txn_count", C.c_int32, [C.c_void_p]),
@@ -124,10 +125,13 @@ FDBCS_FUNCS = [
                                   C.c_uint32, C.c_void_p]),
     ("fdbcs_sharded_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_int64, C.POINTER(Config), C.c_void_p, C.POINTER(CommOps)]),
+    ("fdbcs_sharded_comm_init", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("fdbcs_sharded_abort", C.c_int, [C.c_void_p]),
     ("fdbcs_sharded_destroy", None, [C.c_void_p]),
     ("fdbcs_sharded_clear", C.c_int, [C.c_void_p, C.c_int64]),
     ("fdbcs_sharded_batch_begin", C.c_int, [C.c_void_p]),
     ("fdbcs_sharded_batch_add", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
+    ("fdbcs_sharded_batch_skip", C.c_int, [C.c_void_p, C.c_int32]),
     ("fdbcs_sharded_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_sharded_detect_device", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_sharded_set_protocol", C.c_int, [C.c_void_p, C.c_int, C.c_int]),

@@ -211,6 +211,11 @@ class ConflictBatch:
         self._keep.append(keep)
         self._count += 1
 
+    def skip(self, n):
+        """n transactions without ranges in one call (fdbcs_batch_skip)."""
+        check(self._lib.fdbcs_batch_skip(self.cs.handle, n), "fdbcs_batch_skip")
+        self._count += n
+
     def detect_conflicts(self, now, new_oldest_version, non_conflicting=None, too_old=None):
         """Appends committed indices to ``non_conflicting`` and tooOld indices to
         ``too_old`` (if given); returns the verdict byte array."""

@@ -12,6 +12,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -959,6 +960,10 @@ int check_batch_shape(const fdbcs_batch_view& v) {
 
 }  // namespace
 
+namespace fdbcs_dev {
+int engine_device(const fdbcs* cs) { return cs->device; }
+}  // namespace fdbcs_dev
+
 // ============================================================== C ABI ====
 
 extern "C" {
@@ -1089,6 +1094,12 @@ int fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot, const fdbcs_range* reads, 
 }
 
 int32_t fdbcs_batch_txn_count(const fdbcs* cs) { return cs ? (int32_t)cs->st.txns() : 0; }
+
+int fdbcs_batch_skip(fdbcs* cs, int32_t n) {
+    if (!cs) return FDBCS_E_ARG;
+    if (!cs->in_batch) return FDBCS_E_STATE;
+    return cs->st.skip(n);
+}
 
 // ConflictBatch::detectConflicts (SkipList.cpp:1163-1208) on the staged batch:
 // the staging finishes (last chunk, record offsets, k_unpack builds the batch
@@ -1678,6 +1689,7 @@ struct fdbcs_sharded {
     uint64_t* emap_dev = nullptr;
     uint64_t eseq = 0;
     hipEvent_t ev_edges = nullptr;
+    std::atomic<bool> aborted{false};      // fdbcs_sharded_abort (any thread)
 };
 
 namespace {
@@ -1686,6 +1698,7 @@ size_t sh_slot_bytes(const fdbcs_sharded* sh) { return (size_t)sh->world * SH_WO
 
 int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
     hipStream_t s = sh->cs->stream;
+    if (sh->aborted || (!sh->host_ops && !sh->comm)) return FDBCS_E_STATE;
     if (!sh->host_ops) {
         if (ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
         return FDBCS_OK;
@@ -1702,6 +1715,7 @@ int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
 
 int sh_allgather(fdbcs_sharded* sh, const void* dev_send, void* dev_recv, size_t n = SH_WORDS * 8) {
     hipStream_t s = sh->cs->stream;
+    if (sh->aborted || (!sh->host_ops && !sh->comm)) return FDBCS_E_STATE;
     if (!sh->host_ops) {
         if (ncclAllGather(dev_send, dev_recv, n, ncclUint8, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
         return FDBCS_OK;
@@ -1897,7 +1911,8 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
                          const uint8_t* comm_id, const fdbcs_comm_ops* ops) {
     if (!out) return FDBCS_E_ARG;
     *out = nullptr;
-    if (world < 1 || world > 64 || rank < 0 || rank >= world || (!comm_id) == (!ops)) return FDBCS_E_ARG;
+    // (neither comm_id nor ops: the communicator comes later, fdbcs_sharded_comm_init)
+    if (world < 1 || world > 64 || rank < 0 || rank >= world || (comm_id && ops)) return FDBCS_E_ARG;
     if (world > 1 && (!bound_bytes || !bound_off || !bound_len)) return FDBCS_E_ARG;
     if (ops && (!ops->allreduce_max_u8 || !ops->allgather_u8)) return FDBCS_E_ARG;
     fdbcs_sharded* sh = new (std::nothrow) fdbcs_sharded();
@@ -1935,7 +1950,7 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     if (ops) {
         sh->ops = *ops;
         sh->host_ops = true;
-    } else {
+    } else if (comm_id) {
         ncclUniqueId u;
         memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
         if (ncclCommInitRank(&sh->comm, world, u, rank) != ncclSuccess) return fail(FDBCS_E_HIP);
@@ -1951,9 +1966,33 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     return FDBCS_OK;
 }
 
+int fdbcs_sharded_comm_init(fdbcs_sharded* sh, const uint8_t* comm_id) {
+    if (!sh || !comm_id || sh->host_ops || sh->comm || sh->aborted) return FDBCS_E_ARG;
+    ncclUniqueId u;
+    memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
+    HIPOK(hipSetDevice(sh->cs->device));
+    if (ncclCommInitRank(&sh->comm, sh->world, u, sh->rank) != ncclSuccess) {
+        sh->comm = nullptr;
+        return FDBCS_E_HIP;
+    }
+    return FDBCS_OK;
+}
+
+// Another thread's way out of a batch whose peer will never join: RCCL's
+// in-flight collectives end (ncclCommAbort), every later call fails.
+int fdbcs_sharded_abort(fdbcs_sharded* sh) {
+    if (!sh) return FDBCS_E_ARG;
+    sh->aborted = true;
+    if (sh->comm) {
+        ncclCommAbort(sh->comm);
+        sh->comm = nullptr;
+    }
+    return FDBCS_OK;
+}
+
 void fdbcs_sharded_destroy(fdbcs_sharded* sh) {
     if (!sh) return;
-    if (sh->cs) hipStreamSynchronize(sh->cs->stream);
+    if (sh->cs && !sh->aborted) hipStreamSynchronize(sh->cs->stream);
     if (sh->comm) ncclCommDestroy(sh->comm);
     if (sh->x1) hipFree(sh->x1);
     if (sh->x2) hipFree(sh->x2);
@@ -2041,6 +2080,12 @@ int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbc
     // (a read dropped here still makes the transaction tooOld-capable: the
     // shard holding it reports the flag, and the MAX picks it)
     return fdbcs_batch_add(sh->cs, read_snapshot, k.data(), kr, k.data() + kr, (int32_t)k.size() - kr);
+}
+
+int fdbcs_sharded_batch_skip(fdbcs_sharded* sh, int32_t n) {
+    if (!sh) return FDBCS_E_ARG;
+    if (!sh->in_batch) return FDBCS_E_STATE;
+    return fdbcs_batch_skip(sh->cs, n);
 }
 
 int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict) {

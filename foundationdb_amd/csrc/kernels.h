@@ -300,6 +300,8 @@ void launch_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0, hi
 void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, bool bounded, hipStream_t s);
 void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
                     hipStream_t s);
+// the HIP device an engine lives on (engine.hip)
+int engine_device(const fdbcs* cs);
 // protocol B's edge exchange (kernels_hist.hip)
 void launch_sh_edges_count(const Scalars* sc, int64_t* slots, int rank, int G, int64_t edge_cap, hipStream_t s);
 void launch_sh_edges_plan(const int64_t* slots, int G, int rank, uint64_t* map, uint64_t seq, hipStream_t s);

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "../../include/fdbcs.h"
+#include "kernels.h"
 
 namespace {
 
@@ -490,6 +491,19 @@ void fdbcs_sample_destroy(fdbcs_sample* s) { delete s; }
 int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t offset_per_key,
                            double expiration, int64_t* out_sampled) {
     if (!s || !cs || offset_per_key < 0) return FDBCS_E_ARG;
+    // the buffers and launches belong on the engine's device, whatever the
+    // calling thread's current one (the shim's G-GPU mode hands rank 0's
+    // engine to the Resolver's thread); restored on every return
+    struct DeviceScope {
+        int prev = -1;
+        explicit DeviceScope(int d) {
+            if (hipGetDevice(&prev) != hipSuccess || prev == d) prev = -1;
+            else if (hipSetDevice(d) != hipSuccess) prev = -1;
+        }
+        ~DeviceScope() {
+            if (prev >= 0) hipSetDevice(prev);
+        }
+    } scope(fdbcs_dev::engine_device(cs));
     fdbcs_batch_view dv;
     if (dev_batch) dv = *dev_batch;
     else {

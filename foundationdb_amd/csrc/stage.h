@@ -48,6 +48,8 @@ class TxnStage {
     // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md
     // §0.6) refuse the transaction, which is then not part of the batch.
     int add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw);
+    // n transactions without ranges (add(_, _, 0, _, 0) n times, one offset entry each)
+    int skip(int32_t n);
     // Sends the rest; dv = the device batch view (valid until the next
     // begin()).  With `staged`, the next ingest builds dv's arrays itself
     // straight from the stream (*staged: where to find it); else k_unpack

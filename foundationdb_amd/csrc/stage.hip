@@ -207,6 +207,21 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     return FDBCS_OK;
 }
 
+int TxnStage::skip(int32_t n) {
+    if (!open_) return FDBCS_E_STATE;
+    if (n < 0) return FDBCS_E_ARG;
+    if (T_ + n > MAX_T) return FDBCS_E_CAPACITY;
+    const uint64_t need = used_ + 8 * (uint64_t)(T_ + n) + 16;
+    if (T_ + n > toff_cap_ || need > cap_) {
+        int r = grow(T_ + n, need);
+        if (r) return r;
+    }
+    const uint64_t e = STAGE_EMPTY | ((uint64_t)W_ << 32) | (uint64_t)R_;
+    std::fill(toff_ + T_, toff_ + T_ + n, e);
+    T_ += n;
+    return FDBCS_OK;
+}
+
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;

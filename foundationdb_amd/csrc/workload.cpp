@@ -319,6 +319,7 @@ struct fdbwl_run {
         std::vector<fdbcs_range> reads, writes;
         std::vector<int64_t> snap;
         std::vector<int32_t> roff, woff;   // per transaction: its first read / write
+        std::vector<int32_t> gidx;         // split runs: the batch index of each transaction kept
         int64_t now = 0, nold = 0;
     };
     std::vector<Batch> b;
@@ -406,9 +407,17 @@ fdbwl_run* fdbwl_run_prepare_split(fdbwl* g, int64_t first, int32_t n, int32_t n
             nk[s] = nb;
             nb += sv.key_len[s];
         }
-        B.snap.assign(sv.snapshot, sv.snapshot + sv.txn_count);
-        B.roff.assign(sv.read_off, sv.read_off + sv.txn_count + 1);
-        B.woff.assign(sv.write_off, sv.write_off + sv.txn_count + 1);
+        // the transactions with a range here, at their batch indices (the
+        // others reach the rank as runs of fdbcs_sharded_batch_skip)
+        B.roff.assign(1, 0);
+        B.woff.assign(1, 0);
+        for (int32_t t = 0; t < sv.txn_count; t++) {
+            if (sv.read_off[t + 1] == sv.read_off[t] && sv.write_off[t + 1] == sv.write_off[t]) continue;
+            B.gidx.push_back(t);
+            B.snap.push_back(sv.snapshot[t]);
+            B.roff.push_back(sv.read_off[t + 1]);
+            B.woff.push_back(sv.write_off[t + 1]);
+        }
         const uint8_t* base = B.bytes.data();
         auto rng = [&](int64_t s) { return fdbcs_range{base + nk[s], sv.key_len[s], base + nk[s + 1], sv.key_len[s + 1]}; };
         B.reads.resize(sv.read_count);
@@ -485,10 +494,17 @@ int fdbwl_run_resolver_sharded(fdbwl_run* r, fdbcs_sharded* sh, double* batch_us
         trace_mark();
         const auto t0 = std::chrono::steady_clock::now();
         int st = fdbcs_sharded_batch_begin(sh);
-        const int T = (int)B.snap.size();
-        for (int t = 0; st == FDBCS_OK && t < T; t++)
-            st = fdbcs_sharded_batch_add(sh, B.snap[t], B.reads.data() + B.roff[t], B.roff[t + 1] - B.roff[t],
-                                         B.writes.data() + B.woff[t], B.woff[t + 1] - B.woff[t]);
+        const int n = (int)B.snap.size();
+        int32_t next = 0;  // batch index of the next transaction
+        for (int k = 0; st == FDBCS_OK && k < n; k++) {
+            const int32_t t = B.gidx.empty() ? k : B.gidx[k];
+            if (t > next) st = fdbcs_sharded_batch_skip(sh, t - next);
+            if (st == FDBCS_OK)
+                st = fdbcs_sharded_batch_add(sh, B.snap[k], B.reads.data() + B.roff[k], B.roff[k + 1] - B.roff[k],
+                                             B.writes.data() + B.woff[k], B.woff[k + 1] - B.woff[k]);
+            next = t + 1;
+        }
+        if (st == FDBCS_OK && r->T > next) st = fdbcs_sharded_batch_skip(sh, r->T - next);
         const auto ta = std::chrono::steady_clock::now();
         trace_mark();
         if (st == FDBCS_OK) st = fdbcs_sharded_batch_detect(sh, B.now, B.nold, out);

@@ -133,6 +133,13 @@ int  fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot,
                      const fdbcs_range* reads, int32_t nreads,
                      const fdbcs_range* writes, int32_t nwrites);
 
+/* n transactions with no ranges, as n addTransaction calls with empty read
+ * and write lists (such a transaction always commits: tooOld needs a read,
+ * SkipList.cpp:985) -- one call for a run of them.  A protocol-B shard
+ * (fdbcs_sharded_set_protocol) skips the transactions the proxy did not send
+ * it, keeping the others at their global batch indices. */
+int  fdbcs_batch_skip(fdbcs* cs, int32_t n);
+
 /* ConflictBatch::detectConflicts(now, newOldestVersion, nonConflicting,
  * tooOld) (ConflictSet.h:43, SkipList.cpp:1163-1208), synchronous.
  * verdict[t] receives FDBCS_CONFLICT / FDBCS_TOO_OLD / FDBCS_COMMITTED for
@@ -435,6 +442,15 @@ int  fdbcs_comm_unique_id(uint8_t* id /* FDBCS_COMM_ID_BYTES */);
 int  fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const uint8_t* bound_bytes,
                           const uint64_t* bound_off, const uint32_t* bound_len, int64_t v0,
                           const fdbcs_config* cfg, const uint8_t* comm_id, const fdbcs_comm_ops* ops);
+/* comm_id and ops both NULL: the communicator is joined later, once every
+ * rank's create has succeeded (a rank that fails here then never leaves the
+ * others waiting inside ncclCommInitRank). */
+int  fdbcs_sharded_comm_init(fdbcs_sharded* sh, const uint8_t* comm_id);
+/* From any thread: ends this rank's in-flight RCCL collectives
+ * (ncclCommAbort) so a batch whose peer failed returns an error instead of
+ * waiting forever; every later call on sh fails.  Host collectives
+ * (fdbcs_comm_ops) must be released by their owner. */
+int  fdbcs_sharded_abort(fdbcs_sharded* sh);
 void fdbcs_sharded_destroy(fdbcs_sharded* sh);
 /* clearConflictSet (SkipList.cpp:957-959), on every rank. */
 int  fdbcs_sharded_clear(fdbcs_sharded* sh, int64_t v);
@@ -443,6 +459,7 @@ int  fdbcs_sharded_clear(fdbcs_sharded* sh, int64_t v);
 int  fdbcs_sharded_batch_begin(fdbcs_sharded* sh);
 int  fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbcs_range* reads, int32_t nreads,
                              const fdbcs_range* writes, int32_t nwrites);
+int  fdbcs_sharded_batch_skip(fdbcs_sharded* sh, int32_t n);
 int  fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldest, uint8_t* verdict);
 /* A device-resident batch view (protocol A: every rank the whole batch;
  * protocol B: this rank's fdbcs_split_batch_keep_all share); host verdicts. */

@@ -8,6 +8,7 @@
 //   out: per batch: i32 n, n x i32 (nonConflicting); i32 m, m x i32 (tooOld)
 #include <cstdio>
 #include <cstdlib>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -22,11 +23,88 @@ static T rd(FILE* f) {
     return x;
 }
 
+static KeyRangeRef kr(const std::string& b, const std::string& e) {
+    return KeyRangeRef(KeyRef((const uint8_t*)b.data(), (int)b.size()), KeyRef((const uint8_t*)e.data(), (int)e.size()));
+}
+
+// "errors": a batch whose middle transaction has begin >= end, then one with
+// a key over FDBCS_MAX_KEY: addTransaction throws for it (with one GPU and
+// with G), the others resolve
+static int errors_mode() {
+    ConflictSet* cs = newConflictSet();
+    static const std::string a = "a", b = "b", c = "c", d = "d", e = "e", f = "f", big(30002, 'x');
+    for (int round = 0; round < 2; round++) {
+        CommitTransactionRef t0, bad, t2;
+        t0.read_conflict_ranges.push_back(kr(a, b));
+        t0.write_conflict_ranges.push_back(kr(c, d));
+        t0.read_snapshot = 5;
+        if (round == 0) bad.read_conflict_ranges.push_back(kr(b, b));
+        else bad.write_conflict_ranges.push_back(kr(a, big));
+        t2.write_conflict_ranges.push_back(kr(e, f));
+        std::vector<int> nc;
+        ConflictBatch batch(cs);
+        batch.addTransaction(t0);
+        try {
+            batch.addTransaction(bad);
+            printf("accepted\n");
+        } catch (const std::exception& x) {
+            printf("refused: %s\n", x.what());
+        }
+        batch.addTransaction(t2);
+        batch.detectConflicts(10 + round, 0, nc);
+        printf("committed:");
+        for (int i : nc) printf(" %d", i);
+        printf("\n");
+    }
+    destroyConflictSet(cs);
+    return 0;
+}
+
+// "rankfail": batches until detectConflicts throws (a shard made to fail by
+// FDBCS_TEST_FAIL_RANK / _BATCH), then the set must refuse further batches
+static int rankfail_mode() {
+    ConflictSet* cs = newConflictSet();
+    std::vector<std::string> keys, ends;  // (alive while the batches borrow them)
+    for (int i = 0; i < 400; i++) {
+        keys.push_back(std::string(1, (char)('a' + i % 26)) + std::to_string(i));
+        ends.push_back(keys.back() + "~");
+    }
+    for (int i = 0; i < 5; i++) {
+        try {
+            std::vector<CommitTransactionRef> trs(100);
+            for (int t = 0; t < 100; t++) {
+                trs[t].read_conflict_ranges.push_back(kr(keys[4 * t], ends[4 * t]));
+                trs[t].write_conflict_ranges.push_back(kr(keys[4 * t + 1], ends[4 * t + 1]));
+                trs[t].read_snapshot = 100 * i;
+            }
+            std::vector<int> nc;
+            ConflictBatch batch(cs);
+            for (auto& t : trs) batch.addTransaction(t);
+            batch.detectConflicts(100 * i + 50, 0, nc);
+            printf("batch %d ok (%zu committed)\n", i, nc.size());
+        } catch (const std::exception& x) {
+            printf("threw at batch %d: %s\n", i, x.what());
+            break;
+        }
+    }
+    try {
+        ConflictBatch again(cs);
+        printf("usable\n");
+    } catch (const std::exception& x) {
+        printf("unusable: %s\n", x.what());
+    }
+    fflush(stdout);
+    destroyConflictSet(cs);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc == 2 && std::string(argv[1]) == "skiplisttest") {
         skipListTest();
         return 0;
     }
+    if (argc == 2 && std::string(argv[1]) == "errors") return errors_mode();
+    if (argc == 2 && std::string(argv[1]) == "rankfail") return rankfail_mode();
     if (argc != 3) return 2;
     FILE* in = fopen(argv[1], "rb");
     FILE* out = fopen(argv[2], "wb");

@@ -111,6 +111,43 @@ def test_per_transaction_api_appends(cs):
     assert cs.history() == spec.history()
 
 
+def test_per_transaction_skip_runs(cs):
+    """fdbcs_batch_skip: runs of range-less transactions in one call (how a
+    protocol-B shard receives the transactions the proxy did not send it)
+    give the verdicts and history of adding them one by one."""
+    import random
+    for seed in range(3):
+        cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        rng = random.Random(seed)
+        for batch, now, nold in mixed_stream(seed, n_batches=8, max_txns=400, keyspace=3000):
+            txns = []
+            for t in batch.txns():
+                if rng.random() < 0.3:
+                    txns += [(rng.randrange(0, now), [], [])] * rng.randint(1, 5)
+                txns.append(t)
+            txns += [(0, [], [])] * rng.randint(0, 3)
+            vc = c.detect_packed(PackedBatch.from_txns(txns), now, nold)
+            b = ConflictBatch(cs)
+            pending = 0
+            for snap, r, w in txns:
+                if not r and not w:
+                    pending += 1
+                    continue
+                if pending:
+                    b.skip(pending)
+                    pending = 0
+                b.add_transaction(r, w, snap)
+            if pending:
+                b.skip(pending)
+            v = b.detect_conflicts(now, nold)
+            assert np.array_equal(v, vc)
+        assert cs.history() == c.history()
+    b = ConflictBatch(cs)  # a batch of nothing but skipped transactions
+    b.skip(7)
+    assert b.detect_conflicts(10 ** 9, 0).tolist() == [2] * 7
+
+
 @pytest.mark.parametrize("cfg,T,nb", [(1, 2500, 20), (2, 800, 25), (3, 800, 25), (4, 400, 12)])
 def test_workload_configs_small(cs, cfg, T, nb):
     cs.load_history([], [], v0=0, oldest=0, removal_key=b"")

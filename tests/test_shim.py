@@ -128,3 +128,35 @@ def test_shim_multi_gpu_skiplisttest(gpu):
     a2 = int(re.search(r"(\d+) transactions accepted", two.stdout).group(1))
     assert "(2 GPUs as one resolver)" in two.stdout
     assert (h1, a1) == (h2, a2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", ["1", "2"])
+def test_shim_bad_range_same_behaviour(gpu, shards):
+    """A transaction with begin >= end, or a key over FDBCS_MAX_KEY: addTransaction
+    throws for it and the batch goes on without it -- with one GPU and with G
+    GPUs as one resolver alike (the G-GPU mode checks on the caller's thread)."""
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    env = dict(os.environ, FDBCS_SHARDS=shards, FDBCS_SHARD_COMM="host", FDBCS_SHARD_DEVICES="0")
+    r = subprocess.run([B.SHIM_CHECK, "errors"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split("\n")
+    assert [x.split(":")[0] for x in lines if x.startswith(("refused", "accepted"))] == ["refused", "refused"], r.stdout
+    assert lines.count("committed: 0 1") == 2, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", ["a", "b"])
+def test_shim_rank_failure_throws_not_hangs(gpu, protocol):
+    """One of three ranks fails its second detectConflicts before the
+    exchanges (as a failed allocation would); the others are waiting for it
+    in a collective.  The Resolver's call must throw within seconds, and the
+    set refuse later batches, instead of hanging."""
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    env = dict(os.environ, FDBCS_SHARDS="3", FDBCS_SHARD_COMM="host", FDBCS_SHARD_DEVICES="0",
+               FDBCS_SHARD_PROTOCOL=protocol, FDBCS_TEST_FAIL_RANK="1", FDBCS_TEST_FAIL_BATCH="1")
+    r = subprocess.run([B.SHIM_CHECK, "rankfail"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "batch 0 ok" in r.stdout and "threw at batch 1" in r.stdout and "unusable" in r.stdout, r.stdout
