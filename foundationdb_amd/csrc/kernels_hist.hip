@@ -1437,12 +1437,26 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
 // Sharded mode: the host hands this shard its part [a, b) of the global
 // compaction window (local indices), whether a is the window's first node
 // (never removed), and the version of the node before a when a == 0.
+// Tail arena GC in a shard: the global sweep visits the shard's boundaries
+// in key order, entering at its first (a == 0) and leaving at its last
+// (b == H), so a shard's run of window parts from a == 0 to b == H has moved
+// every tail alive when it entered -- the unsharded sweep's rule
+// (k_bmax_commit) restricted to the shard's keys.
+__device__ inline void shard_sweep_flags(Scalars* sc, int64_t a, int64_t b, int64_t H) {
+    if (a >= b) return;
+    int tf = sc->tail_flags;
+    if (a == 0) tf = TF_FROM_START;
+    if (b >= H) tf |= TF_WRAP;
+    sc->tail_flags = tf;
+}
+
 __global__ __launch_bounds__(64) void k_win_explicit(Dir dir, Scalars* sc, int64_t a, int64_t b, int keep_first,
                                                      int64_t prev) {
     const int D = sc->D;
     const int pA = a < b ? wave_start_search(dir.start, D, a) : 1;
     const int pB = a < b ? wave_start_search(dir.start, D, b - 1) : 0;
     if (threadIdx.x == 0) {
+        shard_sweep_flags(sc, a, b, dir.start[D]);
         sc->win_g0 = a;
         sc->win_r0 = keep_first ? a + 1 : a;
         sc->win_g1 = b;
@@ -1488,8 +1502,7 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        b.win_keep, b.win_cnt, b.desc_max);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_nr, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
-                       b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap,
-                       (int)!(h.shard.has_lo | h.shard.has_hi));
+                       b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap, 1);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
 }
@@ -1659,6 +1672,7 @@ __global__ __launch_bounds__(64) void k_sh_plan(Pool pool, Dir dir, Scalars* sc,
                 reinterpret_cast<uint64_t*>(rk.tail)[w] = reinterpret_cast<const uint64_t*>(k.tail)[w];
     }
     if (threadIdx.x == 0) {
+        shard_sweep_flags(sc, a, b, dir.start[D]);
         sc->win_g0 = a;
         sc->win_r0 = s_part[2] ? a + 1 : a;
         sc->win_g1 = b;

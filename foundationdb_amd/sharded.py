@@ -135,8 +135,8 @@ def carry_ins(v0, hl):
 class Shard:
     """One engine holding the keys [lo, hi) (None: unbounded)."""
 
-    def __init__(self, lo, hi, device=-1, v0=0, max_history=0, sparse=False):
-        self.cs = ConflictSet(v0=v0, device=device, max_history=max_history)
+    def __init__(self, lo, hi, device=-1, v0=0, max_history=0, sparse=False, tail_arena_bytes=0):
+        self.cs = ConflictSet(v0=v0, device=device, max_history=max_history, tail_arena_bytes=tail_arena_bytes)
         self._lib = self.cs._lib
         lo_b, hi_b = lo or b"", hi or b""
         check(self._lib.fdbcs_set_shard(self.cs.handle, lo_b, len(lo_b), int(lo is not None), hi_b, len(hi_b),
@@ -264,7 +264,7 @@ class ShardedConflictSet:
     are a device reduction and host lists.  ``shard_factory`` builds a shard
     (tests pass a CPU model of the same interface)."""
 
-    def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard, sparse=False):
+    def __init__(self, bounds, devices=None, v0=0, max_history=0, shard_factory=Shard, sparse=False, **shard_kw):
         import torch
 
         self.torch = torch
@@ -276,7 +276,8 @@ class ShardedConflictSet:
             devices = [d] * len(ranges)
         assert len(devices) == len(ranges)
         self.devices = [_device(torch, d) for d in devices]
-        self.protos = [_Proto(shard_factory(lo, hi, device=d, v0=v0, max_history=max_history, sparse=sparse), g, v0)
+        self.protos = [_Proto(shard_factory(lo, hi, device=d, v0=v0, max_history=max_history, sparse=sparse,
+                                            **shard_kw), g, v0)
                        for g, ((lo, hi), d) in enumerate(zip(ranges, devices))]
         self.shards = [p.shard for p in self.protos]
 
@@ -587,7 +588,7 @@ class ShardedResolver:
     PRESPLIT = 1                  # FDBCS_SHARD_PRESPLIT
 
     def __init__(self, bounds, rank, world, device=0, v0=0, max_history=0, comm_id=None, group=None, protocol="a",
-                 presplit=False):
+                 presplit=False, tail_arena_bytes=0):
         """protocol "b": this rank takes only the ranges intersecting its keys
         (fdbcs_sharded_batch_add filters them unless ``presplit``; the packed
         and device paths take the rank's fdbcs_split_batch_keep_all share)."""
@@ -600,7 +601,7 @@ class ShardedResolver:
         offs = np.cumsum([0] + [len(b) for b in bounds])[:-1].astype(np.uint64) if bounds else np.zeros(1, np.uint64)
         lens = np.array([len(b) for b in bounds] or [0], np.uint32)
         kb_arr = np.frombuffer(kb + b"\0", np.uint8).copy()
-        cfg = _abi.Config(device=device, max_history=max_history)
+        cfg = _abi.Config(device=device, max_history=max_history, tail_arena_bytes=tail_arena_bytes)
         h = C.c_void_p()
         ops_p = None
         cid = None

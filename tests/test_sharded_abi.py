@@ -24,6 +24,9 @@ from oracle import CpuSpec
 
 
 def _streams(kind, seed):
+    if kind == "tailgc":  # long keys, many times the tail arena over the stream (tests/test_tail_gc.py)
+        from test_tail_gc import long_key_stream
+        return list(long_key_stream(seed, 240))
     if kind == "tiny":
         return list(tiny_stream(seed, n_batches=25, maxlen=3))
     if kind == "long":
@@ -44,8 +47,10 @@ def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:
-        sh = ShardedResolver(bounds, rank, world, device=0, protocol=protocol)
+        arena = (4 << 20) if kind == "tailgc" else 0
+        sh = ShardedResolver(bounds, rank, world, device=0, protocol=protocol, tail_arena_bytes=arena)
         out = []
+        halves = set()
         for i, (batch, now, nold) in enumerate(_streams(kind, seed)):
             if kind == "tiny" and i == 12:
                 sh.clear(now - 5)  # clearConflictSet mid-stream (SkipList.cpp:957-959)
@@ -55,7 +60,16 @@ def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None)
                 v = sh.detect_packed(batch, now, nold)
             owner = sh.removal_key_owner()
             rk = sh.local.removal_key() if owner == rank else None
+            if kind == "tailgc":  # the arena stays at its initial size; both halves get used
+                st = sh.local.batch_stats()
+                assert st["tail_arena_bytes"] == arena, (i, st)
+                halves.add(st["tail_half"])
+                if i % 40 != 39:  # (histories compared every 40th batch)
+                    out.append((v.tolist(), None, owner, rk, sh.local.oldest_version))
+                    continue
             out.append((v.tolist(), sh.history(), owner, rk, sh.local.oldest_version))
+        if kind == "tailgc":
+            assert halves == {0, 1}, f"rank {rank} never freed a half"
         sh.close()
         q.put((rank, out))
     except Exception as e:  # (report, so the parent does not wait for the timeout)
@@ -104,11 +118,45 @@ def test_sharded_abi_equals_one_conflict_set(gpu, world, kind, protocol, edge_ca
             owners.add(owner)
             if rk is not None:
                 assert rk == c.removal_key(), (i, r)
-            hist += h
+            hist = None if h is None or hist is None else hist + h
         assert len(owners) == 1, (i, owners)  # every rank agrees on removalKey's owner
         if owners == {-1}:
             assert c.removal_key() == b"", i
-        assert hist == c.history(), i
+        if hist is not None:
+            assert hist == c.history(), i
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", ["a", "b"])
+def test_sharded_abi_tail_arena_gc(gpu, protocol):
+    """Long keys (43-100 B) many times the 4 MB tail arena over the stream,
+    split across two ranks in the middle of their random suffixes: every
+    rank's arena stays at its initial size and both halves get used."""
+    import test_tail_gc
+    bounds = [test_tail_gc.PREFIX + b"\x80"]
+    seed = 77
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + random.Random(os.getpid() * 17 + ord(protocol)).randint(0, 3000)
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, bounds, "tailgc", seed, q, protocol)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert not isinstance(got[r], str), f"rank {r}: {got[r]}"
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(_streams("tailgc", seed)):
+        vc = c.detect_packed(batch, now, nold).tolist()
+        hist = []
+        for r in range(2):
+            v, h, _owner, _rk, _old = got[r][i]
+            assert v == vc, (i, r)
+            hist = None if h is None or hist is None else hist + h
+        if hist is not None:
+            assert hist == c.history(), i
     c.close()
 
 

@@ -1,7 +1,8 @@
 """Tail-arena GC (kernels_hist.hip move_tail / k_win_dir): keys longer than 17
 bytes keep their bytes 17.. in an arena of two halves; the compaction window
 moves the survivors' tails out of the old half, and a sweep that covered the
-whole history frees it.  A long-key stream whose total tail bytes are many
+whole history frees it -- in the exact sharded modes too, where a shard frees
+its old half once the global sweep has passed over all of its keys.  A long-key stream whose total tail bytes are many
 times the arena must then run in the initial arena, bit-exact against the
 oracle."""
 import random
@@ -59,4 +60,32 @@ def test_long_key_stream_stays_in_the_initial_arena(gpu):
     assert halves == {0, 1}, "no sweep freed a half"
     assert g.history() == c.history()
     g.close()
+    c.close()
+
+
+def check_shards_in_arena(stats_per_shard, arena, halves, i):
+    for g, st in enumerate(stats_per_shard):
+        halves[g].add(st["tail_half"])
+        assert st["tail_arena_bytes"] == arena, f"batch {i} shard {g}: the tail arena grew: {st}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+def test_sharded_long_key_stream_stays_in_the_initial_arena(gpu, sparse):
+    """Two shards split in the middle of the random suffixes (the Python
+    protocol, fdbcs_shard_compact's explicit windows; protocol A and B)."""
+    from foundationdb_amd.sharded import ShardedConflictSet
+    arena = 4 << 20
+    sh = ShardedConflictSet([PREFIX + b"\x80"], max_history=1 << 20, sparse=sparse, tail_arena_bytes=arena)
+    c = CpuSpec()
+    halves = [set(), set()]
+    for i, (b, now, nold) in enumerate(long_key_stream(6, 300)):
+        v = sh.detect_packed(b, now, nold)
+        assert np.array_equal(v, c.detect_packed(b, now, nold)), i
+        check_shards_in_arena([x.cs.batch_stats() for x in sh.shards], arena, halves, i)
+        if i % 25 == 24:
+            assert sh.history() == c.history(), i
+            assert sh.removal_key() == c.removal_key(), i
+    assert all(h == {0, 1} for h in halves), f"a shard never freed a half: {halves}"
+    assert sh.history() == c.history()
     c.close()
