@@ -1009,12 +1009,12 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         return fail(r);
     if (hipMemset(cs->h.rk_hi, 0, 8) || hipMemset(cs->h.rk_lo, 0, 8) || hipMemset(cs->h.rk_meta, 0, 4))
         return fail(FDBCS_E_HIP);
-    if ((r = dalloc(cs->h.shard_tails, 2 * (FDBCS_MAX_KEY + 16))) || (r = dalloc(cs->key_out, 3)) ||
+    if ((r = dalloc(cs->h.shard_tails, 2 * (int64_t)SHARD_TAIL_STRIDE)) || (r = dalloc(cs->key_out, 3)) ||
         (r = dalloc(cs->key_out_tail, FDBCS_MAX_KEY + 16)))
         return fail(r);
     if (hipHostMalloc((void**)&cs->rk_stage, 24 + FDBCS_MAX_KEY + 64, hipHostMallocDefault) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
-    if (hipMemset(cs->h.shard_tails, 0, 2 * (FDBCS_MAX_KEY + 16)) != hipSuccess) return fail(FDBCS_E_HIP);
+    if (hipMemset(cs->h.shard_tails, 0, 2 * SHARD_TAIL_STRIDE) != hipSuccess) return fail(FDBCS_E_HIP);
     cs->h.shard = ShardBounds{};
     for (int i = 0; i < 8; i++)
         if (hipEventCreate(&cs->ev[i]) != hipSuccess) return fail(FDBCS_E_HIP);
@@ -1460,7 +1460,7 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
         uint32_t m;
         encode_host(src[k], len[k], dst[k]->hi, dst[k]->lo, m);
         dst[k]->meta = m;
-        uint8_t* t = cs->h.shard_tails + (size_t)k * (FDBCS_MAX_KEY + 16);
+        uint8_t* t = cs->h.shard_tails + (size_t)k * SHARD_TAIL_STRIDE;
         dst[k]->tail = len[k] > 17 ? t : nullptr;
         if (len[k] > 17) {
             std::vector<uint8_t> buf(((len[k] - 17 + 7) & ~7u), 0);

@@ -203,7 +203,7 @@ struct HistBufs {
     uint64_t* rk_hi; uint64_t* rk_lo; uint32_t* rk_meta; uint8_t* rk_tail;  // rk_tail: 30008 bytes
     // exact sharded mode: this engine's key range (unbounded by default)
     ShardBounds shard;
-    uint8_t* shard_tails;  // device copies of the bounds' tails [2][FDBCS_MAX_KEY + 16]
+    uint8_t* shard_tails;  // device copies of the bounds' tails [2][SHARD_TAIL_STRIDE]
     // host-mapped copy of the scalars, written by the kernel that ends a batch
     // (the host reads it after a stream sync instead of issuing a copy)
     Scalars* mirror;
@@ -300,6 +300,11 @@ void launch_sh_carry(Scalars* sc, const int64_t* slots, int rank, int64_t v0, hi
 void launch_sh_info_out(const Scalars* sc, int64_t* send, int rank, bool bounded, hipStream_t s);
 void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int rank, int G, int64_t v0, bool compact,
                     hipStream_t s);
+// bytes per shard-bound tail copy: a multiple of 8, since tails are read a
+// word at a time (tail_cmp) and a misaligned word load returns the aligned
+// word's bytes (a 30,017-byte stride put the upper bound's tail off by one
+// byte and made every compare against a bound longer than 17 bytes wrong)
+constexpr size_t SHARD_TAIL_STRIDE = ((size_t)FDBCS_MAX_KEY + 16 + 7) & ~(size_t)7;
 // the HIP device an engine lives on (engine.hip)
 int engine_device(const fdbcs* cs);
 // protocol B's edge exchange (kernels_hist.hip)

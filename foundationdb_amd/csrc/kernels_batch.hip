@@ -25,33 +25,54 @@ namespace fdbcs_dev {
 //                            begin < end precondition.
 // The per-batch scalars the encoder allocates from (err, btail_used) were
 // reset by the previous batch's last kernel (k_bmax_commit, end of batch).
+// 8 bytes at p (any alignment) as a little-endian word, from the aligned
+// words that hold them: w0 = the word at p & ~7, w1 the next one
+__device__ inline uint64_t funnel8(uint64_t w0, uint64_t w1, uint32_t sh) {
+    return sh ? (w0 >> (8 * sh)) | (w1 << (64 - 8 * sh)) : w0;
+}
+
+// The fixed part of a key at p (any alignment) from up to three aligned
+// 8-byte loads instead of 17 byte loads, and its tail (bytes 17..) copied a
+// word at a time into the batch's tail buffer (8-byte aligned, zero padded).
+// Only the aligned words that hold key bytes are read (a key can end a
+// buffer), and bytes past L are masked to zero.
 __device__ inline Key encode_key(const uint8_t* p, uint32_t L, uint8_t* btail, uint64_t btail_cap, Scalars* sc) {
     if (L > FDBCS_MAX_KEY) {
         atomicCAS(&sc->err, 0, FDBCS_E_KEY);
         L = FDBCS_MAX_KEY;
     }
-    uint64_t hi = 0, lo = 0;
-    uint32_t b16 = 0;
     const uint32_t n = L < 17 ? L : 17;
-    for (uint32_t i = 0; i < n; i++) {
-        uint64_t c = p[i];
-        if (i < 8) hi |= c << (56 - 8 * i);
-        else if (i < 16) lo |= c << (56 - 8 * (i - 8));
-        else b16 = (uint32_t)c;
-    }
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 7);
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(7));
+    const uint64_t w0 = n ? w[0] : 0, w1 = sh + n > 8 ? w[1] : 0, w2 = sh + n > 16 ? w[2] : 0;
+    uint64_t hi = __builtin_bswap64(funnel8(w0, w1, sh)), lo = __builtin_bswap64(funnel8(w1, w2, sh));
+    uint32_t b16 = n == 17 ? (uint32_t)((w2 >> (8 * sh)) & 0xFF) : 0;
+    if (n < 8) hi = n ? hi & (~0ull << (64 - 8 * n)) : 0;  // (big-endian: byte i at bits 56-8i)
+    if (n < 16) lo = n > 8 ? lo & (~0ull << (64 - 8 * (n - 8))) : 0;
     const uint8_t* tail = nullptr;
     if (L > 17) {
-        const uint64_t m = L - 17, padded = (m + 7) & ~7ull;
-        const uint64_t o = atomicAdd((unsigned long long*)&sc->btail_used, (unsigned long long)padded);
-        if (o + padded > btail_cap) {
+        const uint64_t m = L - 17, words = (m + 7) >> 3;
+        const uint64_t o = atomicAdd((unsigned long long*)&sc->btail_used, (unsigned long long)(8 * words));
+        if (o + 8 * words > btail_cap) {
             // the batch fails; later kernels still compare this key, so it
             // points at readable bytes (the buffer holds >= 64 KB > any tail)
             atomicCAS(&sc->err, 0, FDBCS_E_CAPACITY);
             tail = btail;
         } else {
-            uint8_t* d = btail + o;
-            for (uint64_t i = 0; i < padded; i++) d[i] = i < m ? p[17 + i] : 0;
-            tail = d;
+            uint64_t* d = reinterpret_cast<uint64_t*>(btail + o);
+            const uint8_t* q = p + 17;
+            const uint32_t qs = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 7);
+            const uint64_t* qw = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(7));
+            const uint64_t qwords = (qs + m + 7) >> 3;  // aligned words holding the tail's bytes
+            uint64_t cur = qw[0];
+            for (uint64_t i = 0; i < words; i++) {
+                const uint64_t nxt = i + 1 < qwords ? qw[i + 1] : 0;
+                uint64_t x = funnel8(cur, nxt, qs);
+                if (i + 1 == words && (m & 7)) x &= ~0ull >> (64 - 8 * (m & 7));  // zero padding past L
+                d[i] = x;
+                cur = nxt;
+            }
+            tail = reinterpret_cast<const uint8_t*>(d);
         }
     }
     return Key{hi, lo, (b16 << 24) | L, tail};

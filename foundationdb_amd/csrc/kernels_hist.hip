@@ -16,6 +16,7 @@
 // `start[]` (global index of a page's first boundary) is carried forward
 // incrementally, never rescanned.
 #include <algorithm>
+#include <cstdlib>
 #include "kernels.h"
 #include "devutil.h"
 #include "hist_search.h"
@@ -1295,7 +1296,10 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
     int all = 0;
     for (int v = threadIdx.x; v < np; v += blockDim.x) all += cnt[v];
     const int S = block_reduce_sum(all, tmp);
-    if (blockIdx.x == 0 && threadIdx.x == 0) sc->win_surv = S;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sc->win_surv = S;
+        if (!gc) atomicOr(&sc->tail_flags, TF_NOGC);  // (nothing moved: this sweep frees nothing)
+    }
     const int k = S > 0 ? cdiv(S, FILL) : 0;
     const int per = k > 0 ? cdiv(S, k) : 1;
     int before = 0;  // survivors in pages [0, w), advanced by the grid stride
@@ -1501,8 +1505,11 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
     hipLaunchKernelGGL(k_win_keep, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc, oldest,
                        b.win_keep, b.win_cnt, b.desc_max);
     DescArrays da{b.desc_page, b.desc_cnt, b.desc_nr, b.desc_max, b.desc_fhi, b.desc_flo, b.desc_fmeta, b.desc_ftail};
+    // (FDBCS_NO_SHARD_GC: a shard's windows move no tails and free no half -- A/B and fault hunting)
+    static const bool no_shard_gc = getenv("FDBCS_NO_SHARD_GC") != nullptr;
+    const int gc = (h.shard.has_lo | h.shard.has_hi) && no_shard_gc ? 0 : 1;
     hipLaunchKernelGGL(k_win_repack, dim3(std::min(GRID_PAGES, win_cap)), dim3(256), 0, s, h.pool, src, sc,
-                       b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap, 1);
+                       b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap, gc);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
 }
