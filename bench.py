@@ -81,6 +81,8 @@ def parse():
                    help="after the timed region, this many more batches through the same window for the per-batch "
                         "latency distribution (p99 over >= 500 batches, SURVEY.md §8d; default 500, config 4: 200, "
                         "config 5: 0)")
+    p.add_argument("--window-prefill", type=int, default=200,
+                   help="of the prefill batches, the last this many run through the Resolver's window (untimed)")
     p.add_argument("--protocol", choices=["a", "b"], default="b",
                    help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
                         "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
@@ -161,8 +163,23 @@ def pin_host(dev_index):
         mine = sorted(cpus & os.sched_getaffinity(0))
         if not mine:
             return f"not pinned (no allowed CPU on NUMA node {node})"
+        mode = os.environ.get("FDBCS_BENCH_PIN", "numa")
+        what = f"NUMA node {node}'s {len(mine)} CPUs"
+        if mode in ("l3", "core"):  # (A/B: the CPUs sharing the first one's L3, or that CPU alone)
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{mine[0]}/cache/index3/shared_cpu_list") as f:
+                    l3 = set()
+                    for part in f.read().strip().split(","):
+                        a, _, b = part.partition("-")
+                        l3.update(range(int(a), int(b or a) + 1))
+                sub = sorted(l3 & set(mine)) if mode == "l3" else mine[:1]
+                if sub:
+                    mine = sub
+                    what = f"{len(mine)} CPU(s) of NUMA node {node} ({mode})"
+            except OSError:
+                pass
         os.sched_setaffinity(0, mine)
-        return f"the calling thread on NUMA node {node}'s {len(mine)} CPUs (GPU {bdf})"
+        return f"the calling thread on {what} (GPU {bdf})"
     except (OSError, ValueError, AttributeError, RuntimeError) as e:
         return f"not pinned ({e})"
 
@@ -333,7 +350,15 @@ def run_single(args):
     if cfg == 5:  # preload: 50 blind-write batches of 10^6 point writes, no compaction
         Workload(50, txns=args.txns).prefill(cs, 0, PRELOAD_BATCHES)
     if args.prefill:
-        wl.prefill(cs, 0, args.prefill)
+        # the prefill's last batches go through the Resolver's window itself
+        # (untimed): the host path's buffers, caches and pages are warm when
+        # the driver's few warmup batches start
+        nw = min(args.window_prefill, args.prefill) if cfg in (2, 3) else 0
+        wl.prefill(cs, 0, args.prefill - nw)
+        for j in range(args.prefill - nw, args.prefill, 50):
+            r1 = wl.prepare_run(j, min(50, args.prefill - j))
+            r1.run(cs, verdicts=False)
+            del r1
     first = args.prefill
     seq = cfg == 4  # config 4: each batch's wide reads are drawn from the history before it
     # The CPU baseline starts from the GPU's own steady-state history, dumped

@@ -82,6 +82,8 @@ struct UnpackOut {
     uint32_t* klen;    // [2R+2W]
 };
 void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s);
+// bytes from host-mapped memory (a device pointer to it) into dst, on s
+void launch_pull(const uint8_t* host_src, uint8_t* dst, uint64_t bytes, hipStream_t s);
 // the staged batch the next launch_ingest reads straight from the record
 // stream (one launch for k_unpack's work and the ingest's; stream == null:
 // the ingest reads a batch view)

@@ -1344,6 +1344,22 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* __restrict__ stre
     }
 }
 
+// The stream's rest (after the last chunk copy) read by the engine's own
+// queue from the host-mapped pinned buffer: 8-byte words, one per lane
+// (FDBCS_PULL_REST; stage.hip)
+__global__ __launch_bounds__(256) void k_pull(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+void launch_pull(const uint8_t* host_src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
+    const int64_t n = (int64_t)((bytes + 7) / 8);
+    if (n <= 0) return;
+    const int nb = (int)std::min<int64_t>(256, (n + 255) / 256);
+    hipLaunchKernelGGL(k_pull, dim3(nb), dim3(256), 0, s, reinterpret_cast<const uint64_t*>(host_src),
+                       reinterpret_cast<uint64_t*>(dst), n);
+}
+
 void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, int W, UnpackOut o, hipStream_t s) {
     hipLaunchKernelGGL(k_unpack, dim3(cdiv((int64_t)T + 1, 256)), dim3(256), 0, s, stream, toff, T, R, W, o);
 }

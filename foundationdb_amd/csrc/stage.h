@@ -65,6 +65,7 @@ class TxnStage {
     int grow(int64_t need_txns, uint64_t need_bytes);
 
     void sync();
+    static bool pull_rest();
 
     hipStream_t stream_ = nullptr;
     hipStream_t copy_ = nullptr;
@@ -75,7 +76,9 @@ class TxnStage {
     uint64_t K_ = 0;
     // the record stream: pinned + device copy, same capacity
     uint8_t* pin_ = nullptr;
+    uint8_t* pin_dev_ = nullptr;  // pin_ as the device sees it (mapped)
     uint8_t* dev_ = nullptr;
+    bool chunk_sent_ = false;     // a chunk copy (and its event) since begin()
     uint64_t cap_ = 0;
     uint64_t used_ = 0, sent_ = 0;
     uint64_t* toff_ = nullptr;    // host [T]: record offsets (appended to the stream at finish)
