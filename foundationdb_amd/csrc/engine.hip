@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -830,16 +831,55 @@ StageLayout stage_layout(const fdbcs_batch_view& hv) {
     return L;
 }
 
+// Host work over a whole (large) batch split across threads: f(lo, hi) on
+// [0, n) in `parts` pieces, the calling thread taking the first.  One thread
+// below `serial` items.  FDBCS_HOST_THREADS caps the count (default: 16, the
+// GPU box's CPU share, or fewer cores).
+template <class F>
+void parallel_for(int64_t n, int64_t serial, F f) {
+    static const int cap = [] {
+        const char* e = getenv("FDBCS_HOST_THREADS");
+        const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+        return std::max(1, e ? atoi(e) : std::min(16, hw));
+    }();
+    const int parts = n < serial ? 1 : (int)std::min<int64_t>(cap, (n + serial - 1) / serial);
+    if (parts <= 1) {
+        f((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(parts - 1);
+    for (int k = 1; k < parts; k++) th.emplace_back([&, k] { f(n * k / parts, n * (k + 1) / parts); });
+    f((int64_t)0, n / parts);
+    for (auto& t : th) t.join();
+}
+
+// (a config-5 batch -- 10^6 transactions, ~0.4 GB laid out -- packs on
+// several threads: one memcpy thread moves ~10 GB/s)
 void stage_fill(const fdbcs_batch_view& hv, const StageLayout& L, uint8_t* p) {
     const int64_t T = hv.txn_count, slots = 2 * ((int64_t)hv.read_count + hv.write_count);
-    if (T) memcpy(p + L.o_snap, hv.snapshot, 8 * T);
-    memcpy(p + L.o_ro, hv.read_off, 4 * (T + 1));
-    memcpy(p + L.o_wo, hv.write_off, 4 * (T + 1));
-    if (slots) {
-        memcpy(p + L.o_ko, hv.key_off, 8 * slots);
-        memcpy(p + L.o_kl, hv.key_len, 4 * slots);
-    }
-    if (hv.key_bytes_len) memcpy(p + L.o_kb, hv.key_bytes, hv.key_bytes_len);
+    struct Piece {
+        uint8_t* d;
+        const void* s;
+        size_t n;
+    };
+    const Piece pc[6] = {{p + L.o_snap, hv.snapshot, T ? 8 * (size_t)T : 0},
+                         {p + L.o_ro, hv.read_off, 4 * (size_t)(T + 1)},
+                         {p + L.o_wo, hv.write_off, 4 * (size_t)(T + 1)},
+                         {p + L.o_ko, hv.key_off, slots ? 8 * (size_t)slots : 0},
+                         {p + L.o_kl, hv.key_len, slots ? 4 * (size_t)slots : 0},
+                         {p + L.o_kb, hv.key_bytes, (size_t)hv.key_bytes_len}};
+    size_t total = 0;
+    for (const Piece& x : pc) total += x.n;
+    // the pieces as one byte range [0, total), cut into equal shares
+    parallel_for((int64_t)total, 16 << 20, [&](int64_t lo, int64_t hi) {
+        size_t o = 0;
+        for (const Piece& x : pc) {
+            const int64_t a = std::max<int64_t>(lo, (int64_t)o), b = std::min<int64_t>(hi, (int64_t)(o + x.n));
+            if (a < b) memcpy(x.d + (a - o), static_cast<const uint8_t*>(x.s) + (a - o), (size_t)(b - a));
+            o += x.n;
+        }
+    });
 }
 
 fdbcs_batch_view stage_view(const fdbcs_batch_view& hv, const StageLayout& L, uint8_t* din) {
@@ -881,13 +921,20 @@ int stage_batch(fdbcs* cs, const fdbcs_batch_view& hv, fdbcs_batch_view& dv) {
 int check_host_view(const fdbcs_batch_view& hv) {
     if (hv.txn_count < 0 || hv.read_count < 0 || hv.write_count < 0) return FDBCS_E_ARG;
     const int64_t nr = (int64_t)hv.read_count + hv.write_count;
-    for (int64_t i = 0; i < 2 * nr; i++)
-        if (hv.key_len[i] > FDBCS_MAX_KEY) return FDBCS_E_KEY;
-    for (int64_t i = 0; i < nr; i++)
-        if (keycmp(hv.key_bytes + hv.key_off[2 * i], hv.key_len[2 * i], hv.key_bytes + hv.key_off[2 * i + 1],
-                   hv.key_len[2 * i + 1]) >= 0)
-            return FDBCS_E_RANGE;
-    return FDBCS_OK;
+    std::atomic<int> key_err{0}, range_err{0};
+    parallel_for(nr, 1 << 18, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            if (hv.key_len[2 * i] > FDBCS_MAX_KEY || hv.key_len[2 * i + 1] > FDBCS_MAX_KEY) {
+                key_err.store(1, std::memory_order_relaxed);
+                continue;
+            }
+            if (keycmp(hv.key_bytes + hv.key_off[2 * i], hv.key_len[2 * i], hv.key_bytes + hv.key_off[2 * i + 1],
+                       hv.key_len[2 * i + 1]) >= 0)
+                range_err.store(1, std::memory_order_relaxed);
+        }
+    });
+    if (key_err.load()) return FDBCS_E_KEY;  // (the key check first, as before)
+    return range_err.load() ? FDBCS_E_RANGE : FDBCS_OK;
 }
 
 // detectConflicts on a staged device view, verdicts to the host.  The call

@@ -111,6 +111,7 @@ int TxnStage::begin() {
     T_ = R_ = W_ = 0;
     K_ = 0;
     used_ = sent_ = 0;
+    chunk_sent_ = false;
     if (!pin_) {
         int r = grow(8192, 4 << 20);
         if (r) return r;
@@ -133,10 +134,11 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         sync();  // copies in flight read the old buffers
         const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
         uint8_t* np = nullptr;
-        if (hipHostMalloc((void**)&np, nc, hipHostMallocDefault) != hipSuccess) return FDBCS_E_NOMEM;
+        if (hipHostMalloc((void**)&np, nc, hipHostMallocMapped) != hipSuccess) return FDBCS_E_NOMEM;
         if (used_) memcpy(np, pin_, used_);
         if (pin_) hipHostFree(pin_);
         pin_ = np;
+        if (hipHostGetDevicePointer((void**)&pin_dev_, pin_, 0) != hipSuccess) return FDBCS_E_HIP;
         if (dev_) hipFree(dev_);
         dev_ = nullptr;
         cap_ = 0;
@@ -203,8 +205,19 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
         if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
             return FDBCS_E_HIP;
         sent_ = used_;
+        chunk_sent_ = true;
+        if (pull_rest() && hipEventRecord(copied_, copy_) != hipSuccess) return FDBCS_E_HIP;
     }
     return FDBCS_OK;
+}
+
+// FDBCS_PULL_REST=1: finish() has the engine's queue read the stream's rest
+// from the mapped pinned buffer (launch_pull) instead of a last SDMA copy and
+// a cross-queue event behind it (A/B knob: ~5 us per batch, within the
+// run-to-run spread; off by default)
+bool TxnStage::pull_rest() {
+    static const bool on = getenv("FDBCS_PULL_REST") && atoi(getenv("FDBCS_PULL_REST"));
+    return on;
 }
 
 int TxnStage::skip(int32_t n) {
@@ -230,13 +243,22 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     const uint64_t o_toff = used_;
     if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
     const uint64_t end = o_toff + 8 * (uint64_t)T_;
-    // (measured and kept: the rest on the copy stream too -- sending it on the
-    // conflict set's stream, right before the kernels, was ~12 us slower)
-    if (end > sent_ && hipMemcpyAsync(dev_ + sent_, pin_ + sent_, end - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
-        return FDBCS_E_HIP;
-    sent_ = end;
-    if (hipEventRecord(copied_, copy_) != hipSuccess || hipStreamWaitEvent(stream_, copied_, 0) != hipSuccess)
-        return FDBCS_E_HIP;
+    if (pull_rest()) {
+        // the chunks already sent: their last copy's event (recorded at the
+        // copy, long complete by now); the rest: read by the engine's queue
+        if (chunk_sent_ && hipStreamWaitEvent(stream_, copied_, 0) != hipSuccess) return FDBCS_E_HIP;
+        if (end > sent_) launch_pull(pin_dev_ + sent_, dev_ + sent_, end - sent_, stream_);
+        sent_ = end;
+    } else {
+        // (measured and kept: the rest on the copy stream too -- sending it on the
+        // conflict set's stream, right before the kernels, was ~12 us slower)
+        if (end > sent_ &&
+            hipMemcpyAsync(dev_ + sent_, pin_ + sent_, end - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
+            return FDBCS_E_HIP;
+        sent_ = end;
+        if (hipEventRecord(copied_, copy_) != hipSuccess || hipStreamWaitEvent(stream_, copied_, 0) != hipSuccess)
+            return FDBCS_E_HIP;
+    }
     // the view's arrays: snapshot [T] | read_off [T+1] | write_off [T+1] | key_off [2R+2W] | key_len [2R+2W]
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
     const int64_t slots = 2 * (R_ + W_);
