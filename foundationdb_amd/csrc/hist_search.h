@@ -319,7 +319,9 @@ __device__ inline int wave_select_real(const uint64_t* hm, int used, int r) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int s = 4 * lane + q;
-        const bool real = s < used && !((hm[s >> 6] >> (s & 63)) & 1);
+        const int w = s >> 6;  // (selects, not a dynamic index: see hm_word)
+        const uint64_t hw = w < 2 ? (w == 0 ? hm[0] : hm[1]) : (w == 2 ? hm[2] : hm[3]);
+        const bool real = s < used && !((hw >> (s & 63)) & 1);
         flags |= (int)real << q;
         c += real;
     }

@@ -560,7 +560,26 @@ __device__ inline void wave_loads_done() {
 
 __device__ inline int lane_read(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
-__device__ inline bool hm_bit(const uint64_t* hm, int i) { return (hm[i >> 6] >> (i & 63)) & 1; }
+// A page's hole mask in four named words: a dynamically indexed private
+// array lives in scratch memory (k_page_merge stored and reloaded its mask
+// there for every slot test)
+struct HoleMask {
+    uint64_t w0, w1, w2, w3;
+    // (masks, not selects: a select chain over the four words is turned back
+    // into an indexed private array)
+    __device__ uint64_t word(int w) const {
+        return (w0 & (0ull - (uint64_t)(w == 0))) | (w1 & (0ull - (uint64_t)(w == 1))) |
+               (w2 & (0ull - (uint64_t)(w == 2))) | (w3 & (0ull - (uint64_t)(w == 3)));
+    }
+    __device__ bool bit(int i) const { return (word(i >> 6) >> (i & 63)) & 1; }
+    __device__ int popc() const { return __popcll(w0) + __popcll(w1) + __popcll(w2) + __popcll(w3); }
+};
+static_assert(HM_WORDS == 4, "hole mask words");
+__device__ inline HoleMask load_hole_mask_uniform(const Pool& p, int page) {
+    uint64_t hm[HM_WORDS];
+    load_hmask_uniform(p, page, hm);
+    return HoleMask{hm[0], hm[1], hm[2], hm[3]};
+}
 
 // A part's first entry: its directory entry is stashed in LDS (written after
 // the merge by one lane per part); parts beyond MAXP write it directly.
@@ -608,7 +627,7 @@ constexpr int SAT_NONE = -(1 << 28);
 
 // 2a.  Returns false (nothing written) if the new entries do not fit to the
 // right of their insertion points; S.er / S.ins then still hold step 1's marks.
-__device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S, int a, int p, int pg, int C, const uint64_t* hm,
+__device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S, int a, int p, int pg, int C, const HoleMask& hm,
                                int jlo, int jhi, const RangePlan& r0, bool has0, int doff, int nn) {
     const int lane = threadIdx.x & 63;
     const int i0 = 4 * lane;
@@ -620,7 +639,7 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
     for (int q = 0; q < 4; q++) {
         const int i = i0 + q;
         av[q] = S.ins[i];
-        hv[q] = i >= C || hm_bit(hm, i);  // (free slots past the used ones absorb like holes)
+        hv[q] = i >= C || hm.bit(i);  // (free slots past the used ones absorb like holes)
         const int d = av[q] - hv[q];
         f = sat_pack(sat_d(f) + d, max(sat_L(f) + d, 0));
     }
@@ -653,8 +672,9 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
         if (i < C && hv[q] && cb[q] > 0) usem |= 1u << q;            // hole i absorbs one
         if ((movem >> q) & 1) maxout = max(maxout, i + cb[q] + av[q]);
     }
-    if (lane == 0)
-        for (int w = 0; w < HM_WORDS; w++) S.hm[w] = hm[w];
+    if (lane == 0) {
+        S.hm[0] = hm.w0; S.hm[1] = hm.w1; S.hm[2] = hm.w2; S.hm[3] = hm.w3;
+    }
     wave_lds_sync();
     // ---- read the boundaries that move, then write them
     uint64_t ohi[4], olo[4];
@@ -712,8 +732,7 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
     const Dir& D = A.dst;
     if (lane < HM_WORDS) A.pool.hmask[(int64_t)pg * HM_WORDS + lane] = S.hm[lane];
     if (lane == 0) {
-        int holes = 0;
-        for (int w = 0; w < HM_WORDS; w++) holes += __popcll(hm[w]);
+        const int holes = hm.popc();
         D.page[doff] = pg;
         D.cnt[doff] = max(C, maxout + 1);
         D.nr[doff] = C - holes + nn;
@@ -752,8 +771,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     const int64_t pbase = (int64_t)pg * PAGE;
     const int i0 = 4 * lane;
     // ---- 0. the hole mask and the first 64 ranges' plans
-    uint64_t hm[HM_WORDS];
-    load_hmask_uniform(A.pool, pg, hm);
+    const HoleMask hm = load_hole_mask_uniform(A.pool, pg);
     const bool has0 = jlo + lane <= jhi;
     RangePlan r0{};
     if (has0) r0 = load_plan(A, jlo + lane);
@@ -829,7 +847,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         erun += ec[q];
         irun += ic[q];
         newb[q] = irun;
-        if (i0 + q < cntp && erun == 0 && !hm_bit(hm, i0 + q)) keepm |= 1u << q;
+        if (i0 + q < cntp && erun == 0 && !hm.bit(i0 + q)) keepm |= 1u << q;
     }
     const int kc = __popc(keepm);
     const int kinc = wave_incl_scan(kc);

@@ -20,4 +20,5 @@ for r in csv.DictReader(open(f)):
     if re.search(pat, r["Name"]):
         print(v, r["Name"][11:60], r["Calls"], "avg_us=%.2f" % (float(r["AverageNs"]) / 1e3))
 EOF
+  rm -rf gpurun_out/abp_$v  # (the traces are large; the summary lines above are what is kept)
 done
