@@ -126,8 +126,6 @@ struct KeyArrays {           // one key per slot
     }
 };
 
-// Key slots addressed through an index (combined write ranges point at the
-// batch's key slots instead of copying keys).
 // Key range [lo, hi) of a shard in the exact sharded mode (SURVEY.md §8e
 // protocol A); has_lo / has_hi == 0: unbounded.  Keys live in device memory.
 struct ShardBounds {
@@ -137,11 +135,6 @@ struct ShardBounds {
     __device__ bool at_or_above(const Key& k) const;  // k >= hi
 };
 
-struct IndirectKeys {
-    KeyArrays k;
-    const int32_t* slot;
-    __device__ Key get(int64_t j) const { return k.get(slot[j]); }
-};
 
 // The history: a pool of pages (PAGE slots each) plus a directory that lists
 // live pages in key order.  Page 0 of the directory may be empty only when it

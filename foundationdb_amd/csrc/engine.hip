@@ -56,6 +56,14 @@ int dalloc(T*& p, int64_t n) {
         last_hip_error() = e;
         return FDBCS_E_NOMEM;
     }
+    // (FDBCS_POISON=<byte>, debugging: fresh device memory holds that pattern,
+    // so a kernel that reads a buffer before anything wrote it misbehaves the
+    // same way on every run instead of on whatever a freed buffer left)
+    static const int poison = getenv("FDBCS_POISON") ? (int)strtol(getenv("FDBCS_POISON"), nullptr, 0) : -1;
+    if (poison >= 0) {  // (the null stream does not order the engine's non-blocking streams: wait for it)
+        hipMemset(q, poison & 0xFF, (size_t)n * sizeof(T));
+        hipDeviceSynchronize();
+    }
     p = static_cast<T*>(q);
     return FDBCS_OK;
 }
@@ -416,10 +424,9 @@ void free_batch(BatchBufs& b) {
     dfree(b.ss_cnt); dfree(b.ss_gsamp); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
     dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv);
-    dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
+    dfree(b.cb_pos); dfree(b.ce_pos); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
-    dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
-    dfree(b.wh.vb); dfree(b.wh.rb); dfree(b.wh.re);
+    dfree(b.wh.b); dfree(b.wh.e);
     free_plan(b);
     dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
     dfree(b.desc_page); dfree(b.desc_cnt); dfree(b.desc_nr); dfree(b.desc_max); dfree(b.desc_fhi); dfree(b.desc_flo);
@@ -483,25 +490,21 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         GROWLOG("W %lld\n", (long long)W);
         int64_t n = std::max<int64_t>(W, 1024);
         dfree(b.write_txn); dfree(b.rec_w0); dfree(b.sw_slot);
-        dfree(b.cb_slot); dfree(b.ce_slot); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
+        dfree(b.cb_pos); dfree(b.ce_pos); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
-        dfree(b.wh.pb); dfree(b.wh.ib); dfree(b.wh.cb); dfree(b.wh.pe); dfree(b.wh.ie); dfree(b.wh.feq);
-        dfree(b.wh.vb); dfree(b.wh.rb); dfree(b.wh.re);
+        dfree(b.wh.b); dfree(b.wh.e);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
         dfree(b.wnew); dfree(b.winv);
         if ((r = dalloc(b.wnew, 2 * n + 64)) || (r = dalloc(b.winv, 2 * n))) return r;
         if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_rounds
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
-            (r = dalloc(b.cb_slot, n)) || (r = dalloc(b.ce_slot, n)) || (r = dalloc(b.comb_blk, 2 * (n / 2048 + 2))) ||
+            (r = dalloc(b.cb_pos, n)) || (r = dalloc(b.ce_pos, n)) || (r = dalloc(b.comb_blk, 2 * (n / 2048 + 2))) ||
             (r = alloc_keys(b.rkb, n)) ||
             (r = alloc_keys(b.rke, n)) || (r = dalloc(b.pb, n)) ||
             (r = dalloc(b.ib, n)) || (r = dalloc(b.pe, n)) || (r = dalloc(b.ie, n)) || (r = dalloc(b.need_e, n)) ||
             (r = dalloc(b.vb, n)) || (r = dalloc(b.ne.hi, 2 * n)) || (r = dalloc(b.ne.lo, 2 * n)) ||
             (r = dalloc(b.ne.meta, 2 * n)) || (r = dalloc(b.ne.ver, 2 * n)) || (r = dalloc(b.ne.tail, 2 * n)) ||
-            (r = dalloc(b.ne_ins, 2 * n)) || (r = dalloc(b.wh.pb, n)) || (r = dalloc(b.wh.ib, n)) ||
-            (r = dalloc(b.wh.cb, n)) || (r = dalloc(b.wh.pe, n)) || (r = dalloc(b.wh.ie, n)) ||
-            (r = dalloc(b.wh.feq, n)) || (r = dalloc(b.wh.vb, n)) || (r = dalloc(b.wh.rb, n)) ||
-            (r = dalloc(b.wh.re, n)))
+            (r = dalloc(b.ne_ins, 2 * n)) || (r = dalloc(b.wh.b, n)) || (r = dalloc(b.wh.e, n)))
             return r;
         cs->capW = n;
     }
@@ -680,6 +683,8 @@ void read_stage_times(fdbcs* cs) {
 // The whole detectConflicts pipeline on a device-resident batch.
 // early: copy the verdicts and a scalar snapshot to cs->vpin right after the
 // decision and record ev_verdict (finish with verdict_wait).
+int debug_check_dir(fdbcs* cs, const char* where);
+
 int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
               bool sync, bool early = false) {
     int r;
@@ -752,10 +757,12 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     const bool compact = new_oldest > cs->oldest;
     launch_merge(v, b, h, cs->cur, sc, now, cs->v0, !compact, s);
     cs->cur ^= 1;
+    if ((r = debug_check_dir(cs, "merge"))) return r;
     record(cs, 5);
     if (compact) {
         launch_compact(b, h, cs->cur, sc, new_oldest, s);
         cs->cur ^= 1;
+        if ((r = debug_check_dir(cs, "compaction"))) return r;
     }
     record(cs, 6);
     if (compact) cs->oldest = new_oldest;
@@ -802,12 +809,69 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
     return FDBCS_OK;
 }
 
+// FDBCS_DEBUG_DIR (debugging): after each history stage, wait and check the
+// current directory against its pages -- start[] the prefix of nr[], nr[] the
+// real slots of cnt[] under the hole mask, the copied first key the page's
+// first slot, start[D] = H -- and name the stage and entry that broke it.
+int debug_check_dir(fdbcs* cs, const char* where) {
+    static const bool on = getenv("FDBCS_DEBUG_DIR") != nullptr;
+    if (!on) return FDBCS_OK;
+    int r;
+    if ((r = sync_state(cs))) return r;
+    const HistBufs& h = cs->h;
+    const Dir& d = h.dir[cs->cur];
+    const int64_t D = cs->sc_host->D, H = cs->sc_host->H;
+    if (D < 1 || D > d.cap) {
+        fprintf(stderr, "FDBCS_DEBUG_DIR %s: D=%lld out of [1, %d]\n", where, (long long)D, d.cap);
+        return FDBCS_E_STATE;
+    }
+    std::vector<int32_t> page(D), cnt(D), nr(D);
+    std::vector<int64_t> start(D + 1);
+    std::vector<uint64_t> fhi(D);
+    HIPOK(hipMemcpy(page.data(), d.page, D * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(cnt.data(), d.cnt, D * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(nr.data(), d.nr, D * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(start.data(), d.start, (D + 1) * 8, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(fhi.data(), d.fhi, D * 8, hipMemcpyDeviceToHost));
+    int64_t acc = 0;
+    for (int64_t x = 0; x < D; x++) {
+        const char* bad = nullptr;
+        uint64_t hm[HM_WORDS] = {0, 0, 0, 0}, hi0 = 0;
+        if (page[x] < 0 || page[x] >= h.cap_pages) bad = "page id";
+        else if (cnt[x] < 0 || cnt[x] > PAGE) bad = "cnt";
+        else if (start[x] != acc) bad = "start";
+        if (!bad) {
+            HIPOK(hipMemcpy(hm, h.pool.hmask + (int64_t)page[x] * HM_WORDS, sizeof hm, hipMemcpyDeviceToHost));
+            int holes = 0;
+            for (int i = 0; i < cnt[x]; i++) holes += (int)((hm[i >> 6] >> (i & 63)) & 1);
+            if (cnt[x] - holes != nr[x]) bad = "nr vs hole mask";
+            if (cnt[x] > 0) {
+                HIPOK(hipMemcpy(&hi0, h.pool.hi + (int64_t)page[x] * PAGE, 8, hipMemcpyDeviceToHost));
+                if (hi0 != fhi[x]) bad = "first key";
+            }
+        }
+        if (bad) {
+            fprintf(stderr, "FDBCS_DEBUG_DIR %s: entry %lld of %lld: %s (page %d cnt %d nr %d start %lld expected %lld)\n",
+                    where, (long long)x, (long long)D, bad, page[x], cnt[x], nr[x], (long long)start[x], (long long)acc);
+            return FDBCS_E_STATE;
+        }
+        acc += nr[x];
+    }
+    if (start[D] != acc || H != acc) {
+        fprintf(stderr, "FDBCS_DEBUG_DIR %s: start[D]=%lld H=%lld boundaries %lld\n", where, (long long)start[D],
+                (long long)H, (long long)acc);
+        return FDBCS_E_STATE;
+    }
+    return FDBCS_OK;
+}
+
 int reset_history(fdbcs* cs, int64_t v) {
     cs->v0 = v;
     cs->cur = 0;
     launch_reset_history(cs->h, cs->cur, cs->sc, cs->stream);
     launch_dir_finish(cs->h, cs->cur, cs->sc, cs->b, cs->stream);
-    return sync_state(cs);
+    int r = sync_state(cs);
+    return r ? r : debug_check_dir(cs, "reset");
 }
 
 
@@ -1396,7 +1460,8 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     if ((r = set_removal_key(cs, removal_key, removal_key_len))) return r;
     cs->v0 = v0;
     cs->oldest = oldest;
-    return sync_state(cs);
+    if ((r = sync_state(cs))) return r;
+    return debug_check_dir(cs, "load_history");
 }
 
 int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap) {

@@ -7,16 +7,28 @@
 namespace fdbcs_dev {
 
 // Merge-plan accumulators, indexed by directory entry.
+// where write w's ends fall in the pre-batch history (write_search_group),
+// one record per end: the merge plan reads the opening write's begin record and
+// the closing write's end record of every combined range (k_plan_ranges), two
+// random lines per range instead of one per field
+struct alignas(16) WHitB {
+    int32_t pb;   // directory entry of b
+    int32_t ib;   // lower bound of b in its page
+    int32_t cb;   // boundaries (real) in b's page
+    int32_t rb;   // real boundaries before slot ib (holes, common.h)
+};
+struct alignas(16) WHitE {
+    int64_t vb;   // version of the boundary before e (valueBefore(e))
+    int32_t pe;   // directory entry of e
+    int32_t ie;   // lower bound of e in its page
+    int32_t re;   // real boundaries before slot ie
+    int32_t feq;  // bit 0: e is a boundary; bit 1: valueBefore(e) is the header version
+    int64_t pad;
+};
+static_assert(sizeof(WHitB) == 16 && sizeof(WHitE) == 32, "write hit records");
 struct WriteHits {
-    int32_t* pb;   // directory entry of b
-    int32_t* ib;   // lower bound of b in its page
-    int32_t* cb;   // boundaries (real) in b's page
-    int32_t* rb;   // real boundaries before slot ib (holes, common.h)
-    int32_t* re;   // real boundaries before slot ie
-    int32_t* pe;   // directory entry of e
-    int32_t* ie;   // lower bound of e in its page
-    uint8_t* feq;  // e is a boundary
-    int64_t* vb;   // version of the boundary before e (valueBefore(e))
+    WHitB* b;
+    WHitE* e;
 };
 
 struct PageAcc {
@@ -149,9 +161,10 @@ struct BatchBufs {
     int32_t* comb_blk;   // [2 * (combine blocks + 1)] multi-block combine: per-block sums, opens
     int32_t* dec_blk;    // [2 * (T / 256 + 2)] grid decision: dependents and their sources per block
     int64_t edge_cap;
-    // combined write ranges [W], as key slots of their begin / end
-    int32_t* cb_slot;
-    int32_t* ce_slot;
+    // combined write ranges [W], as positions of their begin / end among the
+    // sorted write endpoints (sw: the records hold the keys, in key order)
+    int32_t* cb_pos;
+    int32_t* ce_pos;
     KeyArrays rkb, rke;  // [W] their keys, compact (written by k_plan_ranges)
     // where each write's begin / end fall in the pre-batch history [W]
     // (searched speculatively beside the read check, before the decision)

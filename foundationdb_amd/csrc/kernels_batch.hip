@@ -1496,15 +1496,9 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     else if (he.x > 0 && A.dir.cnt[he.x - 1] > 0)
         vb = A.pool.ver[(int64_t)A.dir.page[he.x - 1] * PAGE + A.dir.cnt[he.x - 1] - 1];
     else vb = A.v0, from_v0 = true;  // (only entry 0 can be an empty page)
-    A.wh.pb[w] = hb.x;
-    A.wh.ib[w] = ib;
-    A.wh.cb[w] = nrb;
-    A.wh.rb[w] = real_before(hmb, ib);
-    A.wh.re[w] = real_before(hme, ie);
-    A.wh.pe[w] = he.x;
-    A.wh.ie[w] = ie;
-    A.wh.feq[w] = (uint8_t)(eqe | from_v0 << 1);  // the merge substitutes its own v0 for bit 1
-    A.wh.vb[w] = vb;
+    A.wh.b[w] = WHitB{hb.x, ib, nrb, real_before(hmb, ib)};
+    // (feq bit 1: the merge substitutes its own v0)
+    A.wh.e[w] = WHitE{vb, he.x, ie, real_before(hme, ie), (int32_t)(eqe | from_v0 << 1), 0};
 }
 
 // Edges need not skip transactions that already conflict with the history:
@@ -2011,8 +2005,8 @@ struct RoundArgs {
     uint2* items;             // [2 * lcap_list] global fallback of the item list
     uint8_t* committed;
     uint8_t* verdict;
-    int32_t* cb_slot;         // combined range begins / ends, as key slots
-    int32_t* ce_slot;
+    int32_t* cb_pos;          // combined range begins / ends, as positions among the sorted write endpoints
+    int32_t* ce_pos;
     Scalars* sc;
     // blocks 1.. of the launch: the merge's write searches (deferred by the
     // read check), beside the decision in block 0, which holds one CU
@@ -2375,8 +2369,8 @@ decided:
     c2 = cnt0;
 #pragma unroll
     for (int k = 0; k < CPMAX; k++) {
-        if (dd[k] == 1 && c2 == 0) A.cb_slot[g++] = (int32_t)slot[k];
-        if (dd[k] == -1 && c2 == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // counter 1 -> 0: it closes
+        if (dd[k] == 1 && c2 == 0) A.cb_pos[g++] = q0 + k;
+        if (dd[k] == -1 && c2 == 1) A.ce_pos[g - 1] = q0 + k;  // counter 1 -> 0: it closes
         c2 += dd[k];
     }
     PHASE(sc, 9);
@@ -2404,8 +2398,8 @@ struct CombArgs {
     const uint8_t* committed;
     int32_t* bsum;   // [blocks]
     int32_t* bopen;  // [blocks]
-    int32_t* cb_slot;
-    int32_t* ce_slot;
+    int32_t* cb_pos;
+    int32_t* ce_pos;
     Scalars* sc;
 };
 
@@ -2488,8 +2482,8 @@ __global__ __launch_bounds__(CB_THREADS) void k_comb_emit(CombArgs A) {
     c = cs;
 #pragma unroll
     for (int k = 0; k < CB_ITEMS; k++) {
-        if (d[k] == 1 && c == 0) A.cb_slot[g++] = (int32_t)slot[k];
-        if (d[k] == -1 && c == 1) A.ce_slot[g - 1] = (int32_t)slot[k];  // (the open may lie in an earlier block)
+        if (d[k] == 1 && c == 0) A.cb_pos[g++] = blockIdx.x * CB_BLOCK + threadIdx.x * CB_ITEMS + k;
+        if (d[k] == -1 && c == 1) A.ce_pos[g - 1] = blockIdx.x * CB_BLOCK + threadIdx.x * CB_ITEMS + k;  // (the open may lie in an earlier block)
         c += d[k];
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) A.sc->n_comb = g0 + gtot;
@@ -2499,7 +2493,7 @@ static void launch_combine_grid(const fdbcs_batch_view& v, BatchBufs& b, Scalars
     const int P = 2 * v.write_count;
     const int nblk = cdiv(P, CB_BLOCK);
     CombArgs C{P, 2 * (int64_t)v.read_count, b.sw_slot, b.write_txn, b.committed, b.comb_blk,
-               b.comb_blk + nblk + 1, b.cb_slot, b.ce_slot, sc};
+               b.comb_blk + nblk + 1, b.cb_pos, b.ce_pos, sc};
     hipLaunchKernelGGL(k_comb_sum, dim3(nblk), dim3(CB_THREADS), 0, s, C);
     hipLaunchKernelGGL(k_comb_open, dim3(nblk), dim3(CB_THREADS), 0, s, C);
     hipLaunchKernelGGL(k_comb_emit, dim3(nblk), dim3(CB_THREADS), 0, s, C);
@@ -2683,7 +2677,7 @@ bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     if (const char* c = getenv("FDBCS_TEST_ROUNDS_LCAP")) A.lcap = std::min(A.lcap, atoi(c));  // (tests: global items)
     A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.write_txn = b.write_txn;
     A.rq = b.rq; A.plist = b.plist; A.wnew = b.wnew; A.winv = b.winv; A.sw_slot = b.sw_slot; A.items = b.items; A.lcap_list = b.list_cap;
-    A.committed = b.committed; A.verdict = verdict; A.cb_slot = b.cb_slot; A.ce_slot = b.ce_slot; A.sc = sc;
+    A.committed = b.committed; A.verdict = verdict; A.cb_pos = b.cb_pos; A.ce_pos = b.ce_pos; A.sc = sc;
     A.eo = EarlyOut{};
     if (eo) {
         A.eo = *eo;

@@ -99,7 +99,13 @@ __global__ __launch_bounds__(1024) void k_scan_small(ScanArgs<NA> a, const int32
 // last range touching the page, first old slot changed.  Pages strictly
 // inside [pb, pe] are wholly erased; they are marked in a difference array
 // (+1 at pb+1, -1 at pe) and resolved by the scan.
-__global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKeys ce, WriteHits wh, int64_t wbase,
+__device__ inline Key srec_key(const SRec& x, const uint8_t* const* tails) {
+    return Key{x.hi, x.lo, x.meta, key_len(x.meta) > 17 ? tails[x.idx] : nullptr};  // (short keys: null, as encoded)
+}
+
+__global__ __launch_bounds__(256) void k_plan_ranges(const int32_t* __restrict__ cb_pos,
+                                                     const int32_t* __restrict__ ce_pos, const SRec* __restrict__ sw,
+                                                     const uint8_t* const* tails, WriteHits wh, int64_t wbase,
                                                      int64_t v0, ShardBounds shard, Scalars* sc, int32_t* __restrict__ pb_o,
                                                      int32_t* __restrict__ ib_o, int32_t* __restrict__ pe_o,
                                                      int32_t* __restrict__ ie_o, uint8_t* __restrict__ need_o,
@@ -109,18 +115,22 @@ __global__ __launch_bounds__(256) void k_plan_ranges(IndirectKeys cb, IndirectKe
     const int nC = sc->n_comb;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nC) return;
-    const int sb = cb.slot[j], se = ce.slot[j];
-    const int wb = (int)((sb - wbase) >> 1), we = (int)((se - wbase) >> 1);
-    const Key b = cb.k.get(sb), e = ce.k.get(se);
-    const bool touch = j + 1 < nC && kcmp(cb.get(j + 1), e) == 0;
+    // (combined ranges are in key order: their sorted records are read nearly
+    // in sequence, the keys' slots only for long keys' tails)
+    const SRec xb = sw[cb_pos[j]], xe = sw[ce_pos[j]];
+    const int wb = (int)(((int64_t)xb.idx - wbase) >> 1), we = (int)(((int64_t)xe.idx - wbase) >> 1);
+    const Key b = srec_key(xb, tails), e = srec_key(xe, tails);
+    const bool touch = j + 1 < nC && kcmp(srec_key(sw[cb_pos[j + 1]], tails), e) == 0;
     // erased boundaries are counted as real ones (r_b, r_e: real boundaries
     // before the slots i_b, i_e; c_b: real boundaries in b's page)
-    const int p_b = wh.pb[wb], i_b = wh.ib[wb], c_b = wh.cb[wb], r_b = wh.rb[wb];
-    const int p_e = wh.pe[we], i_e = wh.ie[we], r_e = wh.re[we];
-    const bool found = wh.feq[we] & 1;
+    const WHitB hb = wh.b[wb];
+    const WHitE he = wh.e[we];
+    const int p_b = hb.pb, i_b = hb.ib, c_b = hb.cb, r_b = hb.rb;
+    const int p_e = he.pe, i_e = he.ie, r_e = he.re;
+    const bool found = he.feq & 1;
     // valueBefore(e) fell back to the header version: the merge's v0 (sharded
     // mode: the exact carry-in, which may differ from the one the search saw)
-    const int64_t vb = (wh.feq[we] & 2) ? (sc->carry_dev ? sc->carry_apply : v0) : wh.vb[we];
+    const int64_t vb = (he.feq & 2) ? (sc->carry_dev ? sc->carry_apply : v0) : he.vb;
     // sharded mode (protocol A step 5): a range acts on this shard iff b < hi
     // and e >= lo; its begin node only if b >= lo, its end node only if e < hi
     // (the positions of keys outside the shard clamp to the shard's ends)
@@ -1225,8 +1235,8 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     Dir& src = h.dir[cur];
     Dir& dst = h.dir[cur ^ 1];
     if (W > 0) {
-        const IndirectKeys cbk{b.keys, b.cb_slot}, cek{b.keys, b.ce_slot};
-        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, cbk, cek, b.wh,
+        hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, (const int32_t*)b.cb_pos,
+                           (const int32_t*)b.ce_pos, (const SRec*)b.sw, (const uint8_t* const*)b.keys.tail, b.wh,
                            2 * (int64_t)v.read_count, v0, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);

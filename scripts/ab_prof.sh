@@ -11,7 +11,7 @@ for v in "$@"; do
   rm -rf gpurun_out/abp_$v
   export FDBCS_LIB_PATH=$PWD/scripts/micro/var/libfdbcs_$v.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/abp_$v -o run -- python3 -u bench.py --config $cfg \
-    --no-cpu --no-shim --lm-batches 0 --steps 30 --warmup 5 > gpurun_out/abp_${cfg}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/abp_${cfg}_$v.log; exit 1; }
+    --no-cpu --no-shim --lm-batches 0 --steps ${STEPS:-30} --warmup ${WARMUP:-5} > gpurun_out/abp_${cfg}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/abp_${cfg}_$v.log; exit 1; }
   f=$(ls gpurun_out/abp_$v/*/run_kernel_stats.csv gpurun_out/abp_$v/run_kernel_stats.csv 2>/dev/null | head -n1)
   python3 - "$f" "$pat" "$v" <<'EOF'
 import csv, re, sys
