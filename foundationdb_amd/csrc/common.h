@@ -19,9 +19,19 @@ namespace fdbcs_dev {
 
 constexpr int SS_QT = 64;          // tail bytes kept per sort splitter (longer ones are compared as prefixes)
 constexpr int PAGE = 256;          // history page capacity (boundaries)
-constexpr int FILL = 192;          // target fill when a page is split / repacked
-constexpr int SPLIT = 224;         // a merge splits a page whose boundaries would exceed this
-constexpr int HOLE_EVERY = 3;      // a rewritten page holds a hole after every 3rd boundary (at most)
+#ifndef FDBCS_FILL  // (page shape knobs: scripts/build_variants.sh A/B)
+#define FDBCS_FILL 192
+#endif
+#ifndef FDBCS_SPLIT
+#define FDBCS_SPLIT 224
+#endif
+#ifndef FDBCS_HOLE_EVERY
+#define FDBCS_HOLE_EVERY 3
+#endif
+constexpr int FILL = FDBCS_FILL;   // target fill when a page is split / repacked
+constexpr int SPLIT = FDBCS_SPLIT; // a merge splits a page whose boundaries would exceed this
+constexpr int HOLE_EVERY = FDBCS_HOLE_EVERY;  // a rewritten page holds a hole after every 3rd boundary (at most)
+static_assert(FILL <= SPLIT && SPLIT <= PAGE && HOLE_EVERY >= 1, "page shape");
 constexpr uint32_t LEN_MASK = 0xFFFFFFu;
 
 struct Key {

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 cfg=$1; shift
 for v in "$@"; do
   FDBCS_LIB_PATH=$PWD/scripts/micro/var/libfdbcs_$v.so timeout -k 10 200 python -u bench.py --config $cfg --no-cpu \
-    --no-shim --lm-batches 0 --steps 30 --warmup 5 > gpurun_out/ab_${cfg}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_${cfg}_$v.log; exit 1; }
+    --no-shim --lm-batches 0 --steps ${STEPS:-30} --warmup ${WARMUP:-5} > gpurun_out/ab_${cfg}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_${cfg}_$v.log; exit 1; }
   python -c "
 import json
 d=json.loads([l for l in open('gpurun_out/ab_${cfg}_$v.log') if l.startswith('{')][-1])
