@@ -71,6 +71,8 @@ class TxnStage {
     hipStream_t copy_ = nullptr;
     hipEvent_t copied_ = nullptr;
     uint64_t chunk_ = 512 << 10;
+    uint64_t early_ = 128 << 10;       // FDBCS_STAGE_EARLY: bytes before the predicted end (0: off)
+    uint64_t early_at_ = ~0ull;        // where this batch's extra chunk goes
     bool open_ = false;
     int64_t T_ = 0, R_ = 0, W_ = 0;
     uint64_t K_ = 0;

@@ -103,6 +103,7 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
     stream_ = stream;
     copy_ = copy;
     chunk_ = std::max<uint64_t>(4096, chunk);
+    if (const char* e = getenv("FDBCS_STAGE_EARLY")) early_ = strtoull(e, nullptr, 0);
     if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
     return FDBCS_OK;
 }
@@ -201,7 +202,10 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     K_ += kbytes;
     R_ += nr;
     W_ += nw;
-    if (used_ - sent_ >= chunk_) {
+    // a chunk every chunk_ bytes, and one more `early_` bytes before where the
+    // previous batch ended (batches are alike): detectConflicts then sends
+    // only that much and the record offsets
+    if (used_ - sent_ >= chunk_ || (used_ >= early_at_ && sent_ < early_at_)) {
         if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
             return FDBCS_E_HIP;
         sent_ = used_;
@@ -241,6 +245,7 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     // the record offsets go after the records (8-byte aligned: records are),
     // and the rest of the stream in one copy
     const uint64_t o_toff = used_;
+    early_at_ = early_ && used_ > early_ ? used_ - early_ : ~0ull;  // (the next batch's extra chunk)
     if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
     const uint64_t end = o_toff + 8 * (uint64_t)T_;
     if (pull_rest()) {
