@@ -142,6 +142,8 @@ struct BatchBufs {
     int64_t lb_hist_cap;
     int64_t ss_tmp_cap;
     bool large;          // large-batch mode (large_batch_mode): merge sort, overlap edges
+    bool dir_join;       // directory entries of the sorted keys by merge-join (large batches; long keys over a
+                         // small directory, engine.hip edges_read_check)
     bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
     // rounds mode (kernels_batch.hip k_decide_rounds)
     int32_t* rq;         // [2R] sorted write endpoints <= each read's begin / < its end

@@ -1915,9 +1915,9 @@ void launch_write_search(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, i
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s, bool defer_ws) {
     const int R = v.read_count, W = v.write_count;
-    // large unsharded batches: directory entries by merge-join (ss_bkt is free once the sort is done)
+    // unsharded batches with b.dir_join: directory entries by merge-join (ss_bkt is free once the sort is done)
     static const bool dir_search = getenv("FDBCS_LARGE_DIR_SEARCH") != nullptr;  // (A/B measurements)
-    const bool dj = b.large && !(h.shard.has_lo | h.shard.has_hi) && !dir_search && R + W > 0;
+    const bool dj = b.dir_join && !(h.shard.has_lo | h.shard.has_hi) && !dir_search && R + W > 0;
     if (dj) {
         DirJoinArgs J{{b.sr, b.sw}, {R, 2 * W}, 0, h.dir[cur], sc, b.keys, R, b.ss_bkt};
         const int64_t cap_f = h.cap_dir;  // (an upper bound on D: blocks past the merged length exit)

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}
-  env $envs timeout -k 10 200 python -u bench.py --no-cpu --no-shim --lm-batches 0 --steps ${STEPS:-30} --warmup 5 \
+  env $envs timeout -k 10 200 python -u bench.py --config ${CONFIG:-2} --no-cpu --no-shim --lm-batches 0 --steps ${STEPS:-30} --warmup 5 \
     > gpurun_out/ab_$name.log 2>&1 || { echo "$name failed"; tail -3 gpurun_out/ab_$name.log; exit 1; }
   python -c "
 import json
