@@ -50,12 +50,15 @@ __device__ inline uint64_t load_be64(const uint8_t* p) {
 }
 
 // Compare the tails (bytes 17..) of two keys that both have length > 17 and
-// identical first 17 bytes.  Tails are 8-byte aligned and zero padded.  Four
+// identical first 17 bytes.  Tails are 8-byte aligned and zero padded.  Six
 // words of each tail per step, their loads issued together (keys sharing a
 // long prefix -- tenants, paths -- differ only words in; one dependent load
-// per word made every such compare a chain of round trips).
+// per word made every such compare a chain of round trips).  Config 4 (keys
+// sharing 64 bytes, so the first difference sits in tail word 5): read check
+// 274 us with 4 words per step, 252 with 6, 256 with 8
+// (profiles/r03_ab_tail_chunk.txt).
 #ifndef FDBCS_TAIL_CHUNK
-#define FDBCS_TAIL_CHUNK 4
+#define FDBCS_TAIL_CHUNK 6
 #endif
 __device__ inline int tail_cmp(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
     constexpr uint32_t C = FDBCS_TAIL_CHUNK;
