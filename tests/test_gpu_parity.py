@@ -148,6 +148,37 @@ def test_per_transaction_skip_runs(cs):
     assert b.detect_conflicts(10 ** 9, 0).tolist() == [2] * 7
 
 
+def test_per_transaction_chunk_edges(gpu, monkeypatch):
+    """The staging's chunk copies at every position: 4 KiB chunks and an early
+    last chunk 4 KiB before where the previous batch's stream ended
+    (FDBCS_STAGE_CHUNK / FDBCS_STAGE_EARLY, read when the conflict set is
+    made), over batches whose sizes jump up and down -- so the early chunk
+    falls inside, at the end of and past the next batch's stream."""
+    import random
+    monkeypatch.setenv("FDBCS_STAGE_CHUNK", "4096")
+    monkeypatch.setenv("FDBCS_STAGE_EARLY", "4096")
+    g = ConflictSet()
+    try:
+        rng = random.Random(5)
+        c = CpuSpec()
+        sizes = [300, 20, 0, 500, 450, 5, 260, 1, 600]
+        now = 1000
+        for i, T in enumerate(sizes):
+            now += rng.randint(50, 200)
+            nold = max(0, now - 600)
+            batch = next(mixed_stream(i, n_batches=1, max_txns=max(T, 1), keyspace=2000))[0]
+            txns = [(min(snap, now - 1), r, w) for snap, r, w in list(batch.txns())[:T]]
+            vc = c.detect_packed(PackedBatch.from_txns(txns), now, nold)
+            b = ConflictBatch(g)
+            for snap, r, w in txns:
+                b.add_transaction(r, w, snap)
+            v = b.detect_conflicts(now, nold)
+            assert np.array_equal(v, vc), i
+            assert g.history() == c.history(), i
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("cfg,T,nb", [(1, 2500, 20), (2, 800, 25), (3, 800, 25), (4, 400, 12)])
 def test_workload_configs_small(cs, cfg, T, nb):
     cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
