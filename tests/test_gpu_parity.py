@@ -286,6 +286,32 @@ def test_steady_state_preloaded_history(cs):
         check_pair(cs, c, batch, now, nold, history=(i in (0, 11)))
 
 
+def test_config2_steady_state_independent(cs):
+    """Config 2 past its 5 M-version window: 540 batches of 5,000 transactions
+    (compaction from batch ~500 on, H ~ 10 M boundaries; ~80 s of oracle).  The GPU builds its
+    history through the pipelined whole-batch prefill (the bench's), the CPU
+    oracle independently from the same generated batches -- not from the GPU's
+    dump -- and the two histories must be identical; then 8 more batches
+    through the checked path compare verdicts and history."""
+    import ctypes as C
+    cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
+    c = CpuSpec()
+    wl = Workload(2)
+    n = 540
+    wl.prefill(cs, 0, n)
+    out = np.zeros(8192, np.uint8)
+    for i in range(n):
+        v, now, nold = wl.view(i)
+        assert v.txn_count <= len(out)
+        assert c._l.orc_detect(c._h, C.byref(v), now, nold, out.ctypes.data) == 0
+    assert cs.history_size() > 5_000_000
+    same_history(cs, c)
+    assert cs.removal_key() == c.removal_key()
+    for i in range(n, n + 8):
+        batch, now, nold = wl.batch(i)
+        check_pair(cs, c, batch, now, nold, history=(i == n + 7))
+
+
 def test_wide_reads_three_level_range_max(cs):
     """Reads spanning up to the whole history (> 3 x 4096 directory entries):
     the read check's entry / 64-group / 4096-group maxima.  Low versions
