@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -1121,7 +1122,10 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         hipHostGetDevicePointer((void**)&cs->h.mirror, cs->sc_mapped, 0) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
     memset(cs->sc_mapped, 0, sizeof(Scalars));
-    if (hipMemset(cs->sc, 0, sizeof(Scalars)) != hipSuccess) return fail(FDBCS_E_HIP);
+    // Every initialisation goes on the engine's own stream: it is
+    // non-blocking, so the legacy null stream (hipMemset, hipMemcpy) does not
+    // order against the kernels that follow on it.
+    if (hipMemsetAsync(cs->sc, 0, sizeof(Scalars), cs->stream) != hipSuccess) return fail(FDBCS_E_HIP);
     int64_t max_hist = cfg && cfg->max_history > 0 ? cfg->max_history : (1 << 20);
     int64_t pages = std::max<int64_t>(1024, cdiv64(max_hist, FILL) * 2);
     if ((r = alloc_pool(cs, (int32_t)pages))) return fail(r);
@@ -1131,14 +1135,16 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = dalloc(cs->h.rk_hi, 1)) || (r = dalloc(cs->h.rk_lo, 1)) || (r = dalloc(cs->h.rk_meta, 1)) ||
         (r = dalloc(cs->h.rk_tail, FDBCS_MAX_KEY + 16)))
         return fail(r);
-    if (hipMemset(cs->h.rk_hi, 0, 8) || hipMemset(cs->h.rk_lo, 0, 8) || hipMemset(cs->h.rk_meta, 0, 4))
+    if (hipMemsetAsync(cs->h.rk_hi, 0, 8, cs->stream) || hipMemsetAsync(cs->h.rk_lo, 0, 8, cs->stream) ||
+        hipMemsetAsync(cs->h.rk_meta, 0, 4, cs->stream))
         return fail(FDBCS_E_HIP);
     if ((r = dalloc(cs->h.shard_tails, 2 * (int64_t)SHARD_TAIL_STRIDE)) || (r = dalloc(cs->key_out, 3)) ||
         (r = dalloc(cs->key_out_tail, FDBCS_MAX_KEY + 16)))
         return fail(r);
     if (hipHostMalloc((void**)&cs->rk_stage, 24 + FDBCS_MAX_KEY + 64, hipHostMallocDefault) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
-    if (hipMemset(cs->h.shard_tails, 0, 2 * SHARD_TAIL_STRIDE) != hipSuccess) return fail(FDBCS_E_HIP);
+    if (hipMemsetAsync(cs->h.shard_tails, 0, 2 * SHARD_TAIL_STRIDE, cs->stream) != hipSuccess)
+        return fail(FDBCS_E_HIP);
     cs->h.shard = ShardBounds{};
     for (int i = 0; i < 8; i++)
         if (hipEventCreate(&cs->ev[i]) != hipSuccess) return fail(FDBCS_E_HIP);
@@ -1590,7 +1596,8 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
         if (len[k] > 17) {
             std::vector<uint8_t> buf(((len[k] - 17 + 7) & ~7u), 0);
             memcpy(buf.data(), src[k] + 17, len[k] - 17);
-            HIPOK(hipMemcpy(t, buf.data(), buf.size(), hipMemcpyHostToDevice));
+            HIPOK(hipMemcpyAsync(t, buf.data(), buf.size(), hipMemcpyHostToDevice, cs->stream));  // (engine stream)
+            HIPOK(hipStreamSynchronize(cs->stream));
         }
     }
     cs->h.shard = sb;
@@ -1815,19 +1822,68 @@ struct fdbcs_sharded {
     uint64_t eseq = 0;
     hipEvent_t ev_edges = nullptr;
     std::atomic<bool> aborted{false};      // fdbcs_sharded_abort (any thread)
+    // The communicator is touched by the rank's own thread (init, enqueues,
+    // progress polls) and by fdbcs_sharded_abort from another one: every use
+    // holds comm_mu, and an aborted communicator (freed by ncclCommAbort) is
+    // marked dead instead of being cleared under the owner's feet.
+    std::mutex comm_mu;
+    bool comm_dead = false;                // (guarded by comm_mu)
 };
 
 namespace {
 
 size_t sh_slot_bytes(const fdbcs_sharded* sh) { return (size_t)sh->world * SH_WORDS * 8; }
 
+// One RCCL call on the rank's communicator.  Communicators are created
+// non-blocking (fdbcs_sharded_comm_init), so a call may return ncclInProgress
+// (the initialisation, a lazy connection); the rank then polls the
+// communicator -- under comm_mu, re-checking `aborted` -- so that
+// fdbcs_sharded_abort can end a wait for a peer that never joins.
+template <class F>
+int sh_nccl(fdbcs_sharded* sh, F call) {
+    ncclResult_t res;
+    {
+        std::lock_guard<std::mutex> lk(sh->comm_mu);
+        if (sh->aborted.load(std::memory_order_acquire) || !sh->comm || sh->comm_dead) return FDBCS_E_STATE;
+        res = call(sh->comm);
+    }
+    for (int it = 0; res == ncclInProgress; it++) {
+        if (it < 4096) _mm_pause();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        std::lock_guard<std::mutex> lk(sh->comm_mu);
+        if (sh->aborted.load(std::memory_order_acquire) || sh->comm_dead) return FDBCS_E_STATE;
+        if (ncclCommGetAsyncError(sh->comm, &res) != ncclSuccess) return FDBCS_E_HIP;
+    }
+    return res == ncclSuccess ? FDBCS_OK : FDBCS_E_HIP;
+}
+
+// a non-blocking communicator of `world` ranks (polled to completion by sh_nccl)
+int sh_comm_init(fdbcs_sharded* sh, const uint8_t* comm_id) {
+    ncclUniqueId u;
+    memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    {
+        std::lock_guard<std::mutex> lk(sh->comm_mu);
+        if (sh->aborted.load(std::memory_order_acquire) || sh->comm) return FDBCS_E_STATE;
+        const ncclResult_t res = ncclCommInitRankConfig(&sh->comm, sh->world, u, sh->rank, &cfg);
+        if (res != ncclSuccess && res != ncclInProgress) {
+            sh->comm = nullptr;
+            return FDBCS_E_HIP;
+        }
+    }
+    ncclResult_t st = ncclInProgress;
+    return sh_nccl(sh, [&](ncclComm_t c) {
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return ncclInternalError;
+        return st;
+    });
+}
+
 int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
     hipStream_t s = sh->cs->stream;
     if (sh->aborted || (!sh->host_ops && !sh->comm)) return FDBCS_E_STATE;
-    if (!sh->host_ops) {
-        if (ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
-        return FDBCS_OK;
-    }
+    if (!sh->host_ops)
+        return sh_nccl(sh, [&](ncclComm_t c) { return ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, c, s); });
     int r;
     if ((r = ensure_pinned(sh->hx, sh->hx_cap, n))) return r;
     HIPOK(hipMemcpyAsync(sh->hx, dev, n, hipMemcpyDeviceToHost, s));
@@ -1841,10 +1897,8 @@ int sh_allreduce_max(fdbcs_sharded* sh, uint8_t* dev, size_t n) {
 int sh_allgather(fdbcs_sharded* sh, const void* dev_send, void* dev_recv, size_t n = SH_WORDS * 8) {
     hipStream_t s = sh->cs->stream;
     if (sh->aborted || (!sh->host_ops && !sh->comm)) return FDBCS_E_STATE;
-    if (!sh->host_ops) {
-        if (ncclAllGather(dev_send, dev_recv, n, ncclUint8, sh->comm, s) != ncclSuccess) return FDBCS_E_HIP;
-        return FDBCS_OK;
-    }
+    if (!sh->host_ops)
+        return sh_nccl(sh, [&](ncclComm_t c) { return ncclAllGather(dev_send, dev_recv, n, ncclUint8, c, s); });
     int r;
     if ((r = ensure_pinned(sh->hx, sh->hx_cap, n * (sh->world + 1)))) return r;
     HIPOK(hipMemcpyAsync(sh->hx, dev_send, n, hipMemcpyDeviceToHost, s));
@@ -2076,9 +2130,7 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
         sh->ops = *ops;
         sh->host_ops = true;
     } else if (comm_id) {
-        ncclUniqueId u;
-        memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
-        if (ncclCommInitRank(&sh->comm, world, u, rank) != ncclSuccess) return fail(FDBCS_E_HIP);
+        if ((r = sh_comm_init(sh, comm_id))) return fail(r);
     }
     // the first exchange 1: this shard's (empty) slot
     const size_t slots = sh_slot_bytes(sh);
@@ -2093,24 +2145,22 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
 
 int fdbcs_sharded_comm_init(fdbcs_sharded* sh, const uint8_t* comm_id) {
     if (!sh || !comm_id || sh->host_ops || sh->comm || sh->aborted) return FDBCS_E_ARG;
-    ncclUniqueId u;
-    memcpy(u.internal, comm_id, FDBCS_COMM_ID_BYTES);
     HIPOK(hipSetDevice(sh->cs->device));
-    if (ncclCommInitRank(&sh->comm, sh->world, u, sh->rank) != ncclSuccess) {
-        sh->comm = nullptr;
-        return FDBCS_E_HIP;
-    }
-    return FDBCS_OK;
+    return sh_comm_init(sh, comm_id);  // (non-blocking: fdbcs_sharded_abort ends a wait for a missing peer)
 }
 
 // Another thread's way out of a batch whose peer will never join: RCCL's
-// in-flight collectives end (ncclCommAbort), every later call fails.
+// in-flight collectives end (ncclCommAbort), every later call fails.  Only
+// `aborted` and, under comm_mu, the communicator are touched here: the rank's
+// thread is either inside an RCCL call (abort waits for it to return) or
+// polls between calls and sees the flag.
 int fdbcs_sharded_abort(fdbcs_sharded* sh) {
     if (!sh) return FDBCS_E_ARG;
-    sh->aborted = true;
-    if (sh->comm) {
-        ncclCommAbort(sh->comm);
-        sh->comm = nullptr;
+    sh->aborted.store(true, std::memory_order_release);
+    std::lock_guard<std::mutex> lk(sh->comm_mu);
+    if (sh->comm && !sh->comm_dead) {
+        ncclCommAbort(sh->comm);  // (frees the communicator; a pending initialisation ends too)
+        sh->comm_dead = true;
     }
     return FDBCS_OK;
 }
@@ -2118,7 +2168,7 @@ int fdbcs_sharded_abort(fdbcs_sharded* sh) {
 void fdbcs_sharded_destroy(fdbcs_sharded* sh) {
     if (!sh) return;
     if (sh->cs && !sh->aborted) hipStreamSynchronize(sh->cs->stream);
-    if (sh->comm) ncclCommDestroy(sh->comm);
+    if (sh->comm && !sh->comm_dead) ncclCommDestroy(sh->comm);
     if (sh->x1) hipFree(sh->x1);
     if (sh->x2) hipFree(sh->x2);
     if (sh->hx) hipHostFree(sh->hx);

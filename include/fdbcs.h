@@ -478,7 +478,12 @@ int  fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_
  * = the caller's adds already carry only this rank's ranges (the proxy's
  * per-resolver split, fdbcs_split_batch_keep_all); without it
  * fdbcs_sharded_batch_add drops the others itself (after checking every
- * range, so all ranks refuse the same transactions).  Between batches. */
+ * range, so all ranks refuse the same transactions).  A PRESPLIT caller must
+ * have validated every range of each global transaction (begin < end, key
+ * lengths) before splitting it: a rank sees only its share, so a
+ * transaction refused on one rank and accepted on another would give the
+ * ranks different transaction counts, and exchange 1 (sized by T) would
+ * mismatch across ranks.  Between batches. */
 #define FDBCS_PROTOCOL_A     0
 #define FDBCS_PROTOCOL_B     1
 #define FDBCS_SHARD_PRESPLIT 1

@@ -167,6 +167,44 @@ def test_gpu_shards_tiny_streams(gpu, maxlen, sparse):
             sh.close()
 
 
+def first_batch_cases():
+    """Shard 0 empty, and a committed write beginning at "" in its first batch
+    (SkipList.cpp:511-522): the state of round
+    3's one-off failure of test_gpu_shards_tiny_streams[11-False] (seed 0:
+    bounds [cbac, ccbb], batch 0 at now=14 -- the oracle's history
+    [("", 14), ("ccab\\0\\0", 0)], the GPU's without the begin at "").  Its
+    batch, plus hand-built writes from "" ending inside shard 0, exactly at the
+    split key and beyond it."""
+    batch, now, nold = next(tiny_stream(11, n_batches=1, maxlen=11))
+    yield [b"cbac", b"ccbb"], batch, now, nold
+    from foundationdb_amd.batch import PackedBatch
+    for end in (b"a", b"m", b"m\x00", b"zz"):
+        txns = [(5, [], [(b"", end)]), (5, [(b"", b"\x00")], [(b"\x00", b"b")])]
+        yield [b"m"], PackedBatch.from_txns(txns), 14, 0
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_model_shards_first_batch_from_empty_key(sparse):
+    for bounds, batch, now, nold in first_batch_cases():
+        sh = ShardedConflictSet(bounds, devices=[-1] * (len(bounds) + 1), shard_factory=ModelShard, sparse=sparse)
+        check_step(sh, CpuSpec(), batch, now, nold)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_shards_first_batch_from_empty_key(gpu, sparse):
+    """Regression: fresh shard engines -- one set per round,
+    so every round starts from freshly allocated device memory -- take a
+    first batch whose committed write begins at "" while shard 0 is empty."""
+    for rnd in range(12):
+        for bounds, batch, now, nold in first_batch_cases():
+            sh = ShardedConflictSet(bounds, max_history=1 << 14, sparse=sparse)
+            try:
+                check_step(sh, CpuSpec(), batch, now, nold)
+            finally:
+                sh.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("sparse", [False, True])
 def test_gpu_shards_bounds_at_keys_and_clear(gpu, sparse):

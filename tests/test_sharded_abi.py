@@ -182,3 +182,59 @@ def test_sharded_abi_rccl_one_rank(gpu):
         assert sh.local.removal_key() == c.removal_key(), i
     sh.close()
     c.close()
+
+
+def _abort_init_child():
+    """Rank 0 of a 2-rank RCCL communicator whose rank 1 never joins: its
+    fdbcs_sharded_comm_init waits (non-blocking init, polled) until another
+    thread calls fdbcs_sharded_abort; then it fails, the handle is destroyed
+    cleanly, and a later call on it is refused."""
+    import ctypes as C
+    import threading
+    import time
+
+    import torch
+
+    from foundationdb_amd import _abi
+    from foundationdb_amd.sharded import ShardedResolver
+
+    torch.cuda.set_device(0)
+    lib = _abi.lib()
+    kb = np.frombuffer(b"m\0", np.uint8).copy()
+    offs = np.zeros(1, np.uint64)
+    lens = np.ones(1, np.uint32)
+    cfg = _abi.Config(device=0, max_history=1 << 12, tail_arena_bytes=0)
+    h = C.c_void_p()
+    assert lib.fdbcs_sharded_create(C.byref(h), 0, 2, kb.ctypes.data, offs.ctypes.data, lens.ctypes.data, 0,
+                                    C.byref(cfg), None, None) == 0
+    cid = (C.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(ShardedResolver.unique_id())
+    res = {}
+
+    def init():
+        res["rc"] = lib.fdbcs_sharded_comm_init(h, cid)
+
+    t = threading.Thread(target=init)
+    t.start()
+    time.sleep(1.0)
+    assert t.is_alive(), f"init returned without its peer: {res}"
+    assert lib.fdbcs_sharded_abort(h) == 0
+    t.join(timeout=30)
+    assert not t.is_alive(), "fdbcs_sharded_abort did not end the pending initialisation"
+    assert res["rc"] != 0
+    assert lib.fdbcs_sharded_batch_begin(h) == 0  # (local state only)
+    out = np.zeros(1, np.uint8)
+    assert lib.fdbcs_sharded_batch_detect(h, 10, 0, out.ctypes.data) != 0  # exchanges refused after the abort
+    lib.fdbcs_sharded_destroy(h)
+    print("ABORT_OK", flush=True)
+
+
+@pytest.mark.gpu
+def test_sharded_abi_rccl_abort_during_init(gpu):
+    """fdbcs_sharded_abort from another thread while the rank waits
+    in RCCL for a peer that never joins (a rank whose own init failed)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_sharded_abi as t; t._abort_init_child()"
+            % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ABORT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
