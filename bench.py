@@ -561,11 +561,43 @@ def run_single(args):
                 roofline["physical_frac"] = round(roofline["physical_GBps"] / HBM_PEAK_GBS, 4)
         del staged
 
-    # ---- Resolver load metrics (not `value`): iopsSample roll of whole batches on the device ----
+    # ---- Resolver load metrics (not `value`): resolverCount > 1 ---------------------------
+    # (a) the Resolver's window with the batch's iopsSample adds inside it
+    #     (Resolver.actor.cpp:146-151) against the same window without, in
+    #     alternating runs: the sample attached to the conflict set, so the
+    #     per-transaction ingest rolls every range on the device and
+    #     fdbcs_sample_add_batch only inserts the entries that came back with
+    #     the verdicts;  (b) the synchronous roll of a batch resident in HBM
+    #     (fdbcs_sample_add_batch on a packed batch, no attachment).
     lm = None
     if args.lm_batches > 0:
         from foundationdb_amd.load_metrics import KEY_BYTES_PER_SAMPLE, SAMPLE_EXPIRATION_TIME, IopsSample
         smp = IopsSample(KEY_BYTES_PER_SAMPLE, seed=1)
+        win = None
+        if not seq:
+            w_with, w_without, a_with, a_without = [], [], [], []
+            per = max(1, args.lm_batches // 5)
+            for rnd in range(10):
+                arm = rnd % 2 == 0
+                smp.attach(cs if arm else None)  # (without: no roll in the ingest either)
+                r1 = wl.prepare_run(next_i, per)  # (generated outside the windows)
+                u, a_, _v = r1.run(cs, verdicts=False, sample=smp if arm else None,
+                                   expire0=next_i * 0.01 + SAMPLE_EXPIRATION_TIME, expire_step=0.01)
+                (w_with if arm else w_without).extend(u.tolist())
+                (a_with if arm else a_without).extend(a_.tolist())
+                next_i += per
+                del r1
+            smp.attach(None)
+            mw, mo = float(np.mean(w_with)), float(np.mean(w_without))
+            win = {"window_us_with_roll": round(mw, 2), "window_us_without": round(mo, 2),
+                   "delta_us_per_batch": round(mw - mo, 2),
+                   "add_us_with": round(float(np.mean(a_with)), 2), "add_us_without": round(float(np.mean(a_without)), 2),
+                   "p50_us_with": round(float(np.percentile(w_with, 50)), 2),
+                   "p50_us_without": round(float(np.percentile(w_without, 50)), 2),
+                   "batches_each": len(w_with),
+                   "path": "fdbwl_run_resolver_sampled: the Resolver window + fdbcs_sample_add_batch(cs, NULL) after "
+                           "detectConflicts, the sample attached (fdbcs_sample_attach: the ingest rolls on the device, "
+                           "entries return with the verdicts); alternating runs of 10 batches with / without"}
         t_add, sampled, n_rng = 0.0, 0, 0
         for j in range(args.lm_batches):
             b, now, nold = wl.batch(next_i + j)
@@ -575,11 +607,15 @@ def run_single(args):
             t_add += time.perf_counter() - t0
             n_rng += b.R + b.W
             smp.poll(j * 0.01)
-        lm = {"us_per_batch": round(t_add / args.lm_batches * 1e6, 2), "ranges_per_batch": n_rng // args.lm_batches,
+        next_i += args.lm_batches
+        lm = {"resolver_window": win,
+              "sync_roll_us_per_batch": round(t_add / args.lm_batches * 1e6, 2),
+              "ranges_per_batch": n_rng // args.lm_batches,
               "sampled_per_batch": round(sampled / args.lm_batches, 1), "sample_size": smp.size(),
               "units_per_sample": KEY_BYTES_PER_SAMPLE, "batches": args.lm_batches,
-              "path": "fdbcs_sample_add_batch on the batch resident in HBM: device roll + ordered compaction + key "
-                      "gather written to pinned host memory, host sample insert (synchronous wall time)"}
+              "sync_path": "fdbcs_sample_add_batch on a packed batch resident in HBM (no attachment): device roll "
+                           "+ ordered compaction + key gather to pinned memory behind the history update, stream "
+                           "sync, host insert (wall time of the call)"}
         smp.close()
     cs.close()
 

@@ -118,6 +118,7 @@ FDBCS_FUNCS = [
     ("fdbcs_sample_size", C.c_int64, [C.c_void_p]),
     ("fdbcs_sample_queue_size", C.c_int64, [C.c_void_p]),
     ("fdbcs_sample_entry", C.c_int32, [C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.POINTER(C.c_int64)]),
+    ("fdbcs_sample_attach", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
     ("fdbcs_strerror", C.c_char_p, [C.c_int]),
     ("fdbcs_version", C.c_char_p, []),
     ("fdbcs_comm_unique_id", C.c_int, [C.c_void_p]),
@@ -153,6 +154,8 @@ WL_FUNCS = [
     ("fdbwl_run_destroy", None, [C.c_void_p]),
     ("fdbwl_run_txns", C.c_int32, [C.c_void_p]),
     ("fdbwl_run_resolver", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fdbwl_run_resolver_sampled", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_double,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fdbwl_prefill", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
     ("fdbwl_set_successor", None, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fdbwl_run_adds", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

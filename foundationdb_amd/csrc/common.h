@@ -280,7 +280,49 @@ struct Scalars {
     int32_t tail_flags;     // TF_* below
     int32_t free_base;      // free-stack slot where the merge's freed pages go (free_top - extra_total before
                             // k_bmax_commit moves free_top: its blocks read this, not free_top)
+    // load-metrics roll inside the per-transaction ingest (LmArgs below):
+    // entries / key bytes appended this batch; at the end of the batch they
+    // move to lm_out_* (what a synchronized host reads) and restart at 0
+    int32_t lm_count;
+    int32_t lm_out_count;
+    uint64_t lm_bytes;
+    uint64_t lm_out_bytes;
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
+};
+
+// ---- Resolver load metrics (load_metrics.hip; Resolver.actor.cpp:146-151) ----
+// The draw of position `pos` of batch `seq` of a sample (counter-based, every
+// thread computes its own: DESIGN.md §6.3) and TransientStorageMetricSample::
+// add's decision (StorageMetrics.actor.h:167-181): the amount added, 0 if not
+// sampled.  oracle/load_sample.py restates both.
+__host__ __device__ inline uint64_t roll_hash(uint64_t seed, uint64_t seq, uint64_t pos) {
+    uint64_t z = seed + seq * 0xD1B54A32D192ED03ull + pos * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline int64_t roll_amount(uint64_t h, int64_t metric, int64_t units) {
+    if (metric <= 0) return 0;
+    if (metric >= units) return metric;
+    return (int64_t)(h % (uint64_t)units) < metric ? units : 0;
+}
+
+// The roll of an attached sample (fdbcs_sample_attach) done by the
+// per-transaction ingest as it encodes each range: a sampled range appends
+// (amount, begin length, byte offset, add-order position) and its begin key's
+// bytes straight into pinned host memory (entries at Scalars::lm_count,
+// bytes at lm_bytes; past the capacities only the counters move).
+struct LmArgs {
+    int32_t on;
+    uint64_t seed, seq;
+    int64_t units, offset_per_key;
+    int64_t* amount;
+    uint32_t* len;
+    uint64_t* off;
+    uint32_t* pos;
+    uint8_t* bytes;
+    uint32_t cap_n;
+    uint64_t cap_b;
 };
 
 constexpr int32_t TF_NOGC = 1;        // a survivor's tail could not be moved this sweep: no swap

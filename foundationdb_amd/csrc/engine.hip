@@ -195,6 +195,29 @@ struct fdbcs {
     hipEvent_t ev_end = nullptr;
     bool end_mirror = false;
     int64_t sub_head = 0, sub_tail = 0;  // batches submitted / waited for
+    // The Resolver's load-metrics roll (iopsSample, Resolver.actor.cpp:146-151)
+    // of an attached sample (fdbcs_sample_attach), done by the per-transaction
+    // ingest while it encodes the ranges; the entries land in pinned host
+    // memory and their count arrives with the verdicts, so
+    // fdbcs_sample_add_batch needs no launch and no wait (load_metrics.hip).
+    struct Lm {
+        const void* owner = nullptr;    // the attached fdbcs_sample
+        const uint64_t* seq = nullptr;  // its draw counter (read at each detect)
+        uint64_t seed = 0;
+        int64_t units = 0, opk = 0;
+        int64_t* amount = nullptr;
+        uint32_t* len = nullptr;
+        uint64_t* off = nullptr;
+        uint32_t* pos = nullptr;
+        uint8_t* bytes = nullptr;
+        size_t cap_n = 0, cap_b = 0;
+        bool armed = false;       // this batch's ingest rolls
+        bool rolled = false;      // the last detected batch was rolled ...
+        uint64_t rolled_seq = 0;  // ... with this draw counter
+        int64_t count = 0;        // ... into this many entries
+        uint64_t batch = 0;       // ... and it was batch number `batch`
+    } lm;
+    uint64_t batches = 0;  // batches run (run_batch / sh_run)
 };
 
 namespace {
@@ -700,10 +723,11 @@ void read_stage_times(fdbcs* cs) {
 int debug_check_dir(fdbcs* cs, const char* where);
 
 int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* dev_verdict,
-              bool sync, bool early = false) {
+              bool sync, bool early = false, const LmArgs* lm = nullptr) {
     int r;
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
     if (T < 0 || R < 0 || W < 0) return FDBCS_E_ARG;
+    cs->batches++;
     cs->edges_known = false;
     cs->have_last_dv = false;  // (the host paths set it again once this batch succeeded)
     // (a staged batch's keys can outnumber its stream's bytes: point ranges
@@ -736,7 +760,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
-                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
+                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0, lm);
     record(cs, 1);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
         cs->sorts++;
@@ -794,7 +818,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
 // update behind them) and check the scalar snapshot taken with them: err =
 // this batch's stages so far, last_err = the previous batch's history update
 // (so a failed update is reported by the next detectConflicts).
-int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
+int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nullptr) {
     int r;
     if (cs->early_mapped) {
         // poll the flag the decision kernel sets after its verdicts (no copy,
@@ -812,6 +836,7 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
         const int32_t* err = reinterpret_cast<const int32_t*>(cs->vmap + 4);
         if (err[0]) return err[0];
         if (err[1]) return err[1];
+        if (lm_count) *lm_count = (int64_t)reinterpret_cast<const uint32_t*>(cs->vmap)[3];
         if (T) memcpy(verdict, cs->vmap + 64, (size_t)T);
         return FDBCS_OK;
     }
@@ -819,8 +844,59 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict) {
     const Scalars* snap = reinterpret_cast<const Scalars*>(cs->vpin + vpin_scalars_off(T));
     if (snap->err) return snap->err;
     if (snap->last_err) return snap->last_err;
+    if (lm_count) *lm_count = snap->lm_count;
     if (T) memcpy(verdict, cs->vpin, (size_t)T);
     return FDBCS_OK;
+}
+
+// Arm the attached sample's roll for the staged batch dv: its pinned outputs
+// hold every range (a batch whose ranges were all sampled) and every key
+// byte of the record stream (the begin keys sampled are disjoint parts of it).
+int lm_arm(fdbcs* cs, const fdbcs_batch_view& dv, LmArgs& la) {
+    fdbcs::Lm& L = cs->lm;
+    const size_t n = (size_t)dv.read_count + (size_t)dv.write_count;
+    const size_t nb = (size_t)dv.key_bytes_len + 64;
+    auto grow = [](auto*& p, size_t& cap, size_t need, size_t elem) {
+        if (need <= cap && p) return FDBCS_OK;
+        const size_t c = std::max<size_t>(need + need / 4, 4096);
+        if (p) hipHostFree(p);
+        p = nullptr;
+        if (hipHostMalloc((void**)&p, c * elem, hipHostMallocDefault) != hipSuccess) return (int)FDBCS_E_NOMEM;
+        cap = c;
+        return FDBCS_OK;
+    };
+    size_t cn = L.cap_n, cn2 = L.cap_n, cn3 = L.cap_n, cn4 = L.cap_n;
+    int r;
+    if (n > L.cap_n || !L.amount) {
+        if ((r = grow(L.amount, cn, n, sizeof(int64_t))) || (r = grow(L.len, cn2, n, sizeof(uint32_t))) ||
+            (r = grow(L.off, cn3, n, sizeof(uint64_t))) || (r = grow(L.pos, cn4, n, sizeof(uint32_t)))) {
+            L.cap_n = 0;
+            return r;
+        }
+        L.cap_n = std::min(std::min(cn, cn2), std::min(cn3, cn4));
+    }
+    if ((r = grow(L.bytes, L.cap_b, nb, 1))) {
+        L.cap_b = 0;
+        return r;
+    }
+    la = LmArgs{1, L.seed, *L.seq, L.units, L.opk, L.amount, L.len, L.off, L.pos, L.bytes,
+                (uint32_t)std::min<size_t>(L.cap_n, UINT32_MAX), (uint64_t)L.cap_b};
+    L.rolled_seq = *L.seq;
+    return FDBCS_OK;
+}
+
+void lm_release(fdbcs::Lm& L) {
+    if (L.amount) hipHostFree(L.amount);
+    if (L.len) hipHostFree(L.len);
+    if (L.off) hipHostFree(L.off);
+    if (L.pos) hipHostFree(L.pos);
+    if (L.bytes) hipHostFree(L.bytes);
+    L.amount = nullptr;
+    L.len = nullptr;
+    L.off = nullptr;
+    L.pos = nullptr;
+    L.bytes = nullptr;
+    L.cap_n = L.cap_b = 0;
 }
 
 // FDBCS_DEBUG_DIR (debugging): after each history stage, wait and check the
@@ -1020,18 +1096,34 @@ int check_host_view(const fdbcs_batch_view& hv) {
 // on return); the history update (merge, compaction) is still running and the
 // next batch's kernels queue behind it on the stream.  With stage timing on,
 // the whole batch is waited for (the stage events).
-int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
+// staged: a per-transaction batch (its ingest reads the record stream and,
+// with a sample attached, rolls the load metrics on the way)
+int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t new_oldest, uint8_t* verdict,
+                  bool staged = false) {
     int r;
     const int64_t T = dv.txn_count;
     const bool early = !cs->timing;
-    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early))) return r;
-    if (early) return verdict_wait(cs, T, verdict);
-    if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
-    if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
-    if ((r = sync_batch(cs))) return r;
-    read_stage_times(cs);
-    if (cs->sc_host->last_err) return cs->sc_host->last_err;
-    if (T) memcpy(verdict, cs->vpin, (size_t)T);
+    LmArgs la{};
+    const bool roll = staged && cs->lm.owner && lm_arm(cs, dv, la) == FDBCS_OK;
+    cs->lm.rolled = false;
+    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early, roll ? &la : nullptr))) return r;
+    int64_t count = 0;
+    if (early) {
+        if ((r = verdict_wait(cs, T, verdict, &count))) return r;
+    } else {
+        if ((r = ensure_pinned(cs->vpin, cs->vpin_cap, (size_t)T + 1))) return r;
+        if (T) HIPOK(hipMemcpyAsync(cs->vpin, cs->b.verdict, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
+        if ((r = sync_batch(cs))) return r;
+        read_stage_times(cs);
+        if (cs->sc_host->last_err) return cs->sc_host->last_err;
+        if (T) memcpy(verdict, cs->vpin, (size_t)T);
+        count = cs->sc_host->lm_out_count;
+    }
+    if (roll) {
+        cs->lm.rolled = true;
+        cs->lm.count = count;
+        cs->lm.batch = cs->batches;
+    }
     return FDBCS_OK;
 }
 
@@ -1087,6 +1179,23 @@ int check_batch_shape(const fdbcs_batch_view& v) {
 
 namespace fdbcs_dev {
 int engine_device(const fdbcs* cs) { return cs->device; }
+
+void engine_lm_attach(fdbcs* cs, const void* owner, const uint64_t* seq, uint64_t seed, int64_t units, int64_t opk) {
+    fdbcs::Lm& L = cs->lm;
+    L.owner = owner;
+    L.seq = seq;
+    L.seed = seed;
+    L.units = units;
+    L.opk = opk;
+    L.rolled = false;
+}
+
+bool engine_lm_take(fdbcs* cs, const void* owner, uint64_t seq, int64_t opk, LmTake& out) {
+    const fdbcs::Lm& L = cs->lm;
+    if (!L.rolled || L.owner != owner || L.batch != cs->batches || L.rolled_seq != seq || L.opk != opk) return false;
+    out = LmTake{L.count, L.amount, L.len, L.off, L.pos, L.bytes, L.cap_n, L.cap_b};
+    return true;
+}
 }  // namespace fdbcs_dev
 
 // ============================================================== C ABI ====
@@ -1174,6 +1283,8 @@ int fdbcs_set_version(fdbcs* cs, int64_t v) { return fdbcs_clear(cs, v); }
 void fdbcs_destroy(fdbcs* cs) {
     if (!cs) return;
     if (cs->stream) hipStreamSynchronize(cs->stream);
+    if (cs->lm.owner) sample_unlink(cs->lm.owner, cs);  // (an attached sample forgets this engine)
+    lm_release(cs->lm);
     free_batch(cs->b);
     free_pool(cs->h);
     dfree(cs->h.tail_arena);
@@ -1245,7 +1356,7 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     fdbcs_batch_view dv;
     if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
     cs->stage_key_total = cs->st.key_total();
-    r = finish_detect(cs, dv, now, new_oldest, verdict);
+    r = finish_detect(cs, dv, now, new_oldest, verdict, true);
     cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};  // (the ingest that reads it was launched)
     if (r) return r;
@@ -1610,6 +1721,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     (void)now;
     (void)new_oldest;
     if (!cs || !db) return FDBCS_E_ARG;
+    cs->batches++;
     const fdbcs_batch_view& v = *db;
     int r;
     if ((r = check_batch_shape(v))) return r;
@@ -1977,6 +2089,7 @@ int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, ui
 int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
     sh->cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     fdbcs* cs = sh->cs;
+    cs->batches++;
     int r;
     if ((r = check_batch_shape(v))) return r;
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;

@@ -239,8 +239,9 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // the sort records into their buckets itself (launch_sort_ranges(scattered))
 // hd: the directory the batch's read check will search (its bmax2 level is
 // built here, from the maxima the last history update left)
+// lm: an attached sample's load-metrics roll (staged batches only; null: none)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   const Dir& hd, hipStream_t s, bool sharded = false);
+                   const Dir& hd, hipStream_t s, bool sharded = false, const LmArgs* lm = nullptr);
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s);
@@ -324,6 +325,25 @@ void launch_sh_plan(HistBufs& h, int cur, Scalars* sc, const int64_t* infos, int
 constexpr size_t SHARD_TAIL_STRIDE = ((size_t)FDBCS_MAX_KEY + 16 + 7) & ~(size_t)7;
 // the HIP device an engine lives on (engine.hip)
 int engine_device(const fdbcs* cs);
+// The load-metrics roll inside the per-transaction ingest (common.h LmArgs).
+// engine_lm_attach: the sample `owner` (its draw counter at *seq, read at each
+// detect) rolls with every staged batch of cs from now on (owner null: none).
+// engine_lm_take: the last detected batch's entries, if it was rolled for
+// (owner, seq, offset_per_key) and no batch ran since.  sample_unlink
+// (load_metrics.hip): cs is being destroyed, its attached sample forgets it.
+struct LmTake {
+    int64_t count;
+    const int64_t* amount;
+    const uint32_t* len;
+    const uint64_t* off;
+    const uint32_t* pos;
+    const uint8_t* bytes;
+    size_t cap_n, cap_b;
+};
+void engine_lm_attach(fdbcs* cs, const void* owner, const uint64_t* seq, uint64_t seed, int64_t units,
+                      int64_t offset_per_key);
+bool engine_lm_take(fdbcs* cs, const void* owner, uint64_t seq, int64_t offset_per_key, LmTake& out);
+void sample_unlink(const void* owner, const fdbcs* cs);
 // protocol B's edge exchange (kernels_hist.hip)
 void launch_sh_edges_count(const Scalars* sc, int64_t* slots, int rank, int G, int64_t edge_cap, hipStream_t s);
 void launch_sh_edges_plan(const int64_t* slots, int G, int rank, uint64_t* map, uint64_t seq, hipStream_t s);

@@ -98,7 +98,24 @@ struct IngestArgs {
     uint8_t* btail;
     uint64_t btail_cap;
     Scalars* sc;
+    LmArgs lm;  // the attached sample's roll (per-transaction path; lm.on = 0 otherwise)
 };
+
+// A sampled range of the load-metrics roll (common.h LmArgs): its entry and
+// begin key into pinned host memory, at places claimed by two counters (the
+// host orders the ~200 entries of a batch by position afterwards).
+__device__ inline void lm_append(const LmArgs& L, Scalars* sc, int64_t amt, const uint8_t* key, uint32_t len,
+                                 uint64_t pos) {
+    const uint32_t i = (uint32_t)atomicAdd(&sc->lm_count, 1);
+    const uint64_t o = atomicAdd((unsigned long long*)&sc->lm_bytes, (unsigned long long)len);
+    if (i >= L.cap_n) return;  // (the host sees the count past the capacity and rolls the batch again)
+    L.amount[i] = amt;
+    L.len[i] = len;
+    L.off[i] = o;
+    L.pos[i] = (uint32_t)pos;
+    if (o + len <= L.cap_b)
+        for (uint32_t k = 0; k < len; k++) L.bytes[o + k] = key[k];
+}
 
 // ---------------------------------------------------------- read check ----
 // Per read range: conflict iff max(version over boundaries in
@@ -708,6 +725,13 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
         }
         const uint64_t ob = base + e.kofs, oe = base + stage_end_ofs(e);
         const uint32_t el = stage_end_len(e);
+        if (A.lm.on) {  // iopsSample.addAndExpire of the range's begin, in the Resolver's add order (writes first)
+            const int nwj = s_pre[wv][j] - (j ? s_pre[wv][j - 1] : 0) - nrj;
+            const uint64_t pos = (uint64_t)s_ro[wv][j] + (uint64_t)s_wo[wv][j] + (uint64_t)(q < nrj ? nwj + q : q - nrj);
+            const int64_t amt = roll_amount(roll_hash(A.lm.seed, A.lm.seq, pos), A.lm.offset_per_key + e.blen,
+                                            A.lm.units);
+            if (amt) lm_append(A.lm, A.sc, amt, S.stream + ob, e.blen, pos);
+        }
         S.view.koff[2 * i] = ob;
         S.view.klen[2 * i] = e.blen;
         S.view.koff[2 * i + 1] = oe;
@@ -1365,9 +1389,10 @@ void launch_unpack(const uint8_t* stream, const uint64_t* toff, int T, int R, in
 }
 
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
-                   const Dir& hd, hipStream_t s, bool sharded) {
+                   const Dir& hd, hipStream_t s, bool sharded, const LmArgs* lm) {
     constexpr int IB = FDBCS_INGEST_BLOCK;  // (A/B: scripts/build_variants.sh)
     IngestArgs A;
+    A.lm = lm && b.staged.stream ? *lm : LmArgs{};  // (k_ingest, the view path, does not roll)
     A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
     A.prep_blocks = std::max(1, cdiv(v.txn_count, IB));
     A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
@@ -2299,6 +2324,7 @@ decided:
         if (tid == 0) {
             A.eo.flag[1] = (uint32_t)sc->err;
             A.eo.flag[2] = (uint32_t)sc->last_err;
+            A.eo.flag[3] = (uint32_t)sc->lm_count;  // (the ingest's load-metrics entries, if a sample is attached)
         }
         __threadfence_system();
         __syncthreads();

@@ -1156,6 +1156,15 @@ void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
     hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
 }
 
+// the batch's load-metrics roll counters (common.h LmArgs) become the
+// synchronized host's view; the next batch's ingest starts from zero
+__device__ inline void lm_end_of_batch(Scalars* sc) {
+    sc->lm_out_count = sc->lm_count;
+    sc->lm_out_bytes = sc->lm_bytes;
+    sc->lm_count = 0;
+    sc->lm_bytes = 0;
+}
+
 // the scalars to the host-mapped mirror: one wavefront of a block whose
 // thread 0 just committed (after a barrier), 8 bytes per lane
 __device__ inline void publish_scalars(const Scalars* sc, Scalars* mirror) {
@@ -1201,6 +1210,7 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
             sc->last_err = sc->err;
             sc->err = 0;
             sc->btail_used = 0;
+            lm_end_of_batch(sc);
         }
     }
     if (end_of_batch && blockIdx.x == 0) {
@@ -1461,6 +1471,7 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         sc->last_err = sc->err;  // end of batch: the next batch's encoder allocates from these
         sc->err = 0;
         sc->btail_used = 0;
+        lm_end_of_batch(sc);
     }
     __syncthreads();
     if (threadIdx.x < 64) publish_scalars(sc, mirror);
@@ -1835,6 +1846,8 @@ __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int c
         sc->tail_half = 0;
         sc->tail_flags = 0;
         sc->err = 0;
+        sc->lm_count = 0;
+        sc->lm_bytes = 0;
     }
 }
 

@@ -51,20 +51,8 @@ namespace {
 
 constexpr int RB = 256;  // ranges per workgroup (4 wavefronts)
 
-__host__ __device__ inline uint64_t roll_hash(uint64_t seed, uint64_t seq, uint64_t pos) {
-    uint64_t z = seed + seq * 0xD1B54A32D192ED03ull + pos * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// TransientStorageMetricSample::add's decision (StorageMetrics.actor.h:167-181)
-// for a positive metric: the amount added to the sample, 0 when not sampled.
-__host__ __device__ inline int64_t roll_amount(uint64_t h, int64_t metric, int64_t units) {
-    if (metric <= 0) return 0;
-    if (metric >= units) return metric;
-    return (int64_t)(h % (uint64_t)units) < metric ? units : 0;
-}
+using fdbcs_dev::roll_amount;  // (common.h: the draw and the add decision, shared with the ingest's roll)
+using fdbcs_dev::roll_hash;
 
 struct RollArgs {
     const int32_t* read_off;   // [T+1]
@@ -330,6 +318,7 @@ struct fdbcs_sample {
     int64_t units = 0;
     uint64_t seed = 0;
     uint64_t seq = 0;  // batches rolled so far (draw counter)
+    fdbcs* attached = nullptr;  // fdbcs_sample_attach: the engine whose ingest rolls for this sample
     FlatSample sample;
     struct GItem {
         uint64_t h, off;
@@ -486,11 +475,83 @@ int fdbcs_sample_create(fdbcs_sample** out, int64_t units_per_sample, uint64_t s
     return FDBCS_OK;
 }
 
-void fdbcs_sample_destroy(fdbcs_sample* s) { delete s; }
+void fdbcs_sample_destroy(fdbcs_sample* s) {
+    if (s && s->attached) fdbcs_dev::engine_lm_attach(s->attached, nullptr, nullptr, 0, 0, 0);
+    delete s;
+}
+
+int fdbcs_sample_attach(fdbcs_sample* s, fdbcs* cs, int64_t offset_per_key) {
+    if (!s || offset_per_key < 0) return FDBCS_E_ARG;
+    if (s->attached) fdbcs_dev::engine_lm_attach(s->attached, nullptr, nullptr, 0, 0, 0);
+    s->attached = cs;
+    if (cs) fdbcs_dev::engine_lm_attach(cs, s, &s->seq, s->seed, s->units, offset_per_key);
+    return FDBCS_OK;
+}
+
+}  // extern "C"
+
+namespace fdbcs_dev {
+void sample_unlink(const void* owner, const fdbcs* cs) {
+    fdbcs_sample* s = static_cast<fdbcs_sample*>(const_cast<void*>(owner));
+    if (s->attached == cs) s->attached = nullptr;
+}
+}  // namespace fdbcs_dev
+
+namespace {
+
+// The batch's entries into the sample and its expiry group, in the Resolver's
+// add order (addAndExpire, StorageMetrics.actor.h:108-113): entry i of the m
+// taken is entries[order[i]]; key bytes at bytes + off.
+int sample_take(fdbcs_sample* s, double expiration, uint64_t m, const int64_t* amt, const uint32_t* len,
+                const uint64_t* off, const uint8_t* bytes, const std::vector<uint32_t>* order) {
+    fdbcs_sample::Group g{expiration, std::string(), {}};
+    g.items.reserve(m);
+    uint64_t nb = 0;
+    for (uint64_t i = 0; i < m; i++) nb += len[order ? (*order)[i] : i];
+    g.bytes.reserve(nb);
+    for (uint64_t i = 0; i < m; i++) {
+        const uint32_t e = order ? (*order)[i] : (uint32_t)i;
+        g.bytes.append((const char*)bytes + off[e], len[e]);
+    }
+    s->dirty = true;
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < m; i++) {
+        const uint32_t e = order ? (*order)[i] : (uint32_t)i;
+        const uint8_t* k = (const uint8_t*)g.bytes.data() + o;
+        const uint64_t h = FlatSample::hash(k, len[e]);
+        s->sample.add(k, len[e], h, amt[e]);
+        g.items.push_back({h, o, len[e], -amt[e]});
+        o += len[e];
+    }
+    s->queued += m;
+    s->queue.push_back(std::move(g));
+    s->seq++;
+    return FDBCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* dev_batch, int64_t offset_per_key,
                            double expiration, int64_t* out_sampled) {
     if (!s || !cs || offset_per_key < 0) return FDBCS_E_ARG;
+    if (!dev_batch) {  // the engine's ingest rolled this batch already (fdbcs_sample_attach): no launch, no wait
+        fdbcs_dev::LmTake tk;
+        if (fdbcs_dev::engine_lm_take(cs, s, s->seq, offset_per_key, tk)) {
+            const uint64_t m = (uint64_t)tk.count;
+            bool fits = m <= tk.cap_n;
+            for (uint64_t i = 0; fits && i < m; i++) fits = tk.off[i] + tk.len[i] <= tk.cap_b;
+            if (fits) {
+                std::vector<uint32_t> order(m);
+                for (uint64_t i = 0; i < m; i++) order[i] = (uint32_t)i;
+                std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return tk.pos[a] < tk.pos[b]; });
+                if (out_sampled) *out_sampled = (int64_t)m;
+                return sample_take(s, expiration, m, tk.amount, tk.len, tk.off, tk.bytes, &order);
+            }
+            // (past the pinned outputs' capacities: the rest below rolls the still-resident batch again)
+        }
+    }
     // the buffers and launches belong on the engine's device, whatever the
     // calling thread's current one (the shim's G-GPU mode hands rank 0's
     // engine to the Resolver's thread); restored on every return
@@ -548,25 +609,10 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
     }
     const uint64_t m = s->h_tot[0];
     if (out_sampled) *out_sampled = (int64_t)m;
-    const int64_t* amt = s->h_amt;
-    const uint32_t* len = s->h_len;
-    const uint64_t* off = s->h_off;
-    const uint8_t* bytes = s->h_out;
-    // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order;
-    // the batch's queue entries form one group sharing its key bytes
-    fdbcs_sample::Group g{expiration, std::string((const char*)bytes, s->h_tot[1]), {}};
-    g.items.reserve(m);
-    s->dirty = true;
-    for (uint64_t i = 0; i < m; i++) {
-        const uint8_t* k = (const uint8_t*)g.bytes.data() + off[i];
-        const uint64_t h = FlatSample::hash(k, len[i]);
-        s->sample.add(k, len[i], h, amt[i]);
-        g.items.push_back({h, off[i], len[i], -amt[i]});
-    }
-    s->queued += m;
-    s->queue.push_back(std::move(g));
-    s->seq++;
-    return FDBCS_OK;
+    // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order
+    // (the ordered compaction's); the batch's queue entries form one group
+    // sharing its key bytes
+    return sample_take(s, expiration, m, s->h_amt, s->h_len, s->h_off, s->h_out, nullptr);
 }
 
 int fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric) {

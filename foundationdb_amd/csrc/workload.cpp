@@ -452,7 +452,13 @@ static void trace_mark() {
 }
 
 int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts) {
+    return fdbwl_run_resolver_sampled(r, cs, nullptr, 0, 0.0, 0.0, batch_us, add_us, verdicts);
+}
+
+int fdbwl_run_resolver_sampled(fdbwl_run* r, fdbcs* cs, void* sample, int64_t offset_per_key, double expire0,
+                               double expire_step, double* batch_us, double* add_us, uint8_t* verdicts) {
     if (!r || !cs) return FDBCS_E_ARG;
+    fdbcs_sample* smp = static_cast<fdbcs_sample*>(sample);
     std::vector<uint8_t> scratch(std::max<int32_t>(r->T, 1));
     for (size_t i = 0; i < r->b.size(); i++) {
         const fdbwl_run::Batch& B = r->b[i];
@@ -474,6 +480,8 @@ int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us
         const auto ta = std::chrono::steady_clock::now();
         trace_mark();
         if (st == FDBCS_OK) st = fdbcs_batch_detect(cs, B.now, B.nold, out);  // detectConflicts(...)
+        if (st == FDBCS_OK && smp)  // if (self->resolverCount > 1): the batch's iopsSample adds
+            st = fdbcs_sample_add_batch(smp, cs, nullptr, offset_per_key, expire0 + (double)i * expire_step, nullptr);
         const auto t1 = std::chrono::steady_clock::now();
         trace_mark();
         if (st != FDBCS_OK) return st;

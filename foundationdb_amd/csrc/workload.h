@@ -71,6 +71,12 @@ uint64_t   fdbwl_run_key_bytes(const fdbwl_run* r, int32_t i);
  * wall time of batch i's window, add_us[i] its addTransaction part (both
  * optional); verdicts (optional) = n x T bytes. */
 int fdbwl_run_resolver(fdbwl_run* r, fdbcs* cs, double* batch_us, double* add_us, uint8_t* verdicts);
+/* The same loop with resolverCount > 1 (Resolver.actor.cpp:146-151): after
+ * each detectConflicts, fdbcs_sample_add_batch(sample, cs, NULL,
+ * offset_per_key, expire0 + i * expire_step, NULL) inside the batch's window
+ * (sample: an fdbcs_sample, attached to cs or not). */
+int fdbwl_run_resolver_sampled(fdbwl_run* r, fdbcs* cs, void* sample, int64_t offset_per_key, double expire0,
+                               double expire_step, double* batch_us, double* add_us, uint8_t* verdicts);
 /* The same loop on one rank of an exact sharded resolver
  * (fdbcs_sharded_batch_begin / _add / _detect). */
 int fdbwl_run_resolver_sharded(fdbwl_run* r, fdbcs_sharded* sh, double* batch_us, double* add_us,

@@ -59,6 +59,13 @@ class IopsSample:
                                                     float(expiration), C.byref(n)), "fdbcs_sample_add_batch")
         return n.value
 
+    def attach(self, cs, offset_per_key=SAMPLE_OFFSET_PER_KEY):
+        """fdbcs_sample_attach: ``cs``'s per-transaction ingest rolls every
+        batch for this sample on the device (None: detach); ``add_batch(cs,
+        ...)`` after ``detect_conflicts`` then only inserts the entries."""
+        _abi.check(self._lib.fdbcs_sample_attach(self._h, cs.handle if cs is not None else None,
+                                                 int(offset_per_key)), "fdbcs_sample_attach")
+
     def add_metric(self, key: bytes, metric: int):
         _abi.check(self._lib.fdbcs_sample_add_metric(self._h, key, len(key), int(metric)), "fdbcs_sample_add_metric")
 

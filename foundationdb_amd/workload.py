@@ -86,16 +86,24 @@ class ResolverRun:
         self.n = n
         self.T = self._lib.fdbwl_run_txns(self._r)
 
-    def run(self, cs, verdicts=True):
+    def run(self, cs, verdicts=True, sample=None, expire0=1.0, expire_step=0.01):
         """Runs every batch; returns (per-batch window in us, its addTransaction
         part in us, verdicts n x T or None).  cs: a ConflictSet, or a
-        sharded.ShardedResolver (this rank's fdbcs_sharded calls)."""
+        sharded.ShardedResolver (this rank's fdbcs_sharded calls).  sample: a
+        load_metrics.IopsSample -- each window then ends with the batch's
+        iopsSample adds (resolverCount > 1, Resolver.actor.cpp:146-151)."""
         us = np.zeros(max(self.n, 1), np.float64)
         add = np.zeros(max(self.n, 1), np.float64)
         out = np.zeros((max(self.n, 1), max(self.T, 1)), np.uint8) if verdicts else None
-        fn = self._lib.fdbwl_run_resolver_sharded if getattr(cs, "sharded", False) else self._lib.fdbwl_run_resolver
-        _abi.check(fn(self._r, cs.handle, us.ctypes.data, add.ctypes.data, out.ctypes.data if verdicts else None),
-                   "resolver loop")
+        optr = out.ctypes.data if verdicts else None
+        if sample is not None:
+            from .load_metrics import SAMPLE_OFFSET_PER_KEY
+            _abi.check(self._lib.fdbwl_run_resolver_sampled(self._r, cs.handle, sample._h, SAMPLE_OFFSET_PER_KEY,
+                                                            float(expire0), float(expire_step), us.ctypes.data,
+                                                            add.ctypes.data, optr), "resolver loop (sampled)")
+        else:
+            fn = self._lib.fdbwl_run_resolver_sharded if getattr(cs, "sharded", False) else self._lib.fdbwl_run_resolver
+            _abi.check(fn(self._r, cs.handle, us.ctypes.data, add.ctypes.data, optr), "resolver loop")
         return us[:self.n], add[:self.n], (out[:self.n, :self.T] if verdicts else None)
 
     def key_bytes(self, i=0):

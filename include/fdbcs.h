@@ -359,9 +359,23 @@ void fdbcs_sample_destroy(fdbcs_sample* s);
  * Knobs.cpp:278, 100; expiration = now() + SAMPLE_EXPIRATION_TIME).  The roll
  * and the gather of the sampled keys run on the device, over dev_batch (a
  * device-resident batch view; NULL = fdbcs_last_device_batch(cs)), on cs's
- * stream; synchronous.  *out_sampled (optional) = keys sampled. */
+ * stream; synchronous.  *out_sampled (optional) = keys sampled.
+ * With the sample attached to cs (fdbcs_sample_attach) and dev_batch NULL
+ * after a per-transaction batch (fdbcs_batch_detect), the roll was already
+ * done by that batch's ingest on the device, and its entries came back with
+ * the verdicts: the call only inserts them (no launch, no wait). */
 int  fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* dev_batch,
                             int64_t offset_per_key, double expiration, int64_t* out_sampled);
+
+/* Attach the sample to cs (NULL: detach): from the next fdbcs_batch_detect
+ * on, the per-transaction ingest rolls every range for this sample as it
+ * encodes it (Resolver.actor.cpp:146-151, with this offset_per_key), writing
+ * the sampled entries and begin keys to pinned host memory; the following
+ * fdbcs_sample_add_batch(s, cs, NULL, offset_per_key, ...) consumes them.  A
+ * batch the caller does not add (resolverCount <= 1) costs its draws nothing:
+ * the draw counter advances only when a batch enters the sample.  One sample
+ * per conflict set; destroying either detaches them. */
+int  fdbcs_sample_attach(fdbcs_sample* s, fdbcs* cs, int64_t offset_per_key);
 
 /* IndexedSet::addMetric on the sample without the roll or the queue
  * (flow/IndexedSet.h:587-598; StorageMetrics.actor.h's own test inserts this
