@@ -762,7 +762,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
                   (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0, lm);
     record(cs, 1);
-    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, cs->v0)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
@@ -1750,7 +1750,8 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     launch_ingest(v, cs->oldest, b, cs->sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
                   (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
     if ((r = stage_ok("ingest"))) return r;
-    if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
+    if (launch_sort_ranges(v, b, cs->sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur,
+                           carry_in)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
@@ -2135,7 +2136,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     const bool scatter = cs->have_quantiles && !b.large;
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
                   (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
-    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s)) {
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, sh->v0)) {
         cs->sorts++;
         cs->have_quantiles = true;
     }

@@ -145,6 +145,7 @@ struct BatchBufs {
     bool dir_join;       // directory entries of the sorted keys by merge-join (large batches; long keys over a
                          // small directory, engine.hip edges_read_check)
     bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
+    bool rc_fused;       // this batch's history read check ran in the sort's bucket launch
     // rounds mode (kernels_batch.hip k_decide_rounds)
     int32_t* rq;         // [2R] sorted write endpoints <= each read's begin / < its end
     int32_t* plist;      // [R + W] candidate reads: some write of the batch may overlap them (duplicates)
@@ -243,8 +244,11 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
                    const Dir& hd, hipStream_t s, bool sharded = false, const LmArgs* lm = nullptr);
 
+// h (optional): the history the batch's read check searches -- the check of
+// every read then runs in the sort's bucket launch (b.rc_fused), and the next
+// launch_edges_read_check leaves it out; v0: as launch_edges_read_check's
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        bool scattered, hipStream_t s);
+                        bool scattered, hipStream_t s, HistBufs* h = nullptr, int cur = 0, int64_t v0 = 0);
 int64_t sort_staging_records(int R, int W, bool large);
 // Large-batch mode (T > LARGE_T, or forced by FDBCS_TEST_LARGE_BATCH for tests):
 // the endpoint sort is a merge sort (no per-batch splitter balance limits)

@@ -130,6 +130,9 @@ __device__ inline void lm_append(const LmArgs& L, Scalars* sc, int64_t amt, cons
 // two pages the directory's page maxima (64-entry block maxima for long
 // ranges) -- and ORs the result.
 static constexpr int RC_G = SIDX_B;
+#ifndef FDBCS_RC_WIDE
+#define FDBCS_RC_WIDE 1  // (0: the two-level range maximum, kept for A/B)
+#endif
 
 struct ReadCheckArgs {
     int R;
@@ -761,18 +764,19 @@ __device__ inline void emit_quantiles(const SortJobs& J, int job, int64_t pos, c
         put_quantile(J, job, (int)q, x, tails);
 }
 
-__global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_buf[3 * SS_ROW];
+// One bucket of the sample sort by one 64-lane workgroup (bid < nb[0] + nb[1]).
+__device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid, uint64_t* s_buf) {
     uint64_t *s_hi = s_buf, *s_lo = s_buf + SS_ROW, *s_mi = s_buf + 2 * SS_ROW;  // LDS path
     uint4* s_r4 = reinterpret_cast<uint4*>(s_buf);  // rank path: 32-byte records
     static_assert(3 * SS_ROW * 8 >= 2 * (SS_WAVE + 8) * 16, "rank path staging");
-    const int job = blockIdx.x < J.nb[0] ? 0 : 1;
-    const int b = job ? blockIdx.x - J.nb[0] : blockIdx.x;
+    const int nbk = J.nb[0] + J.nb[1];
+    const int job = bid < J.nb[0] ? 0 : 1;
+    const int b = job ? bid - J.nb[0] : bid;
     const int lane = threadIdx.x;
     const int32_t* cnt = J.cnt + job * SS_MAXB;
     const uint8_t* const* tails = keys.tail;
     const int64_t c0 = PCLK();
-    for (int k = blockIdx.x * 64 + lane; k < 2 * SS_MAXB; k += gridDim.x * 64) J.cnt_next[k] = 0;
+    for (int k = bid * 64 + lane; k < 2 * SS_MAXB; k += nbk * 64) J.cnt_next[k] = 0;
     // offset = counts of the earlier buckets: lane L sums counts [16L, 16L+16)
     // below b with four independent 16-byte loads (one round trip)
     int part = 0;
@@ -872,6 +876,27 @@ __global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
         if (job) J.out_slot[offset + rank] = x.idx;
         emit_quantiles(J, job, (int64_t)offset + rank, x, tails);
     }
+}
+
+__global__ __launch_bounds__(64) void k_ss_bucket(SortJobs J, KeyArrays keys) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_buf[3 * SS_ROW];
+    ss_bucket_wave(J, keys, (int)blockIdx.x, s_buf);
+}
+
+// The sort's buckets and the history read check of every read in one launch
+// of 64-lane workgroups: the read check needs only the encoded keys and the
+// history, not the sorted records, so its dependent searches fill the CUs
+// while the buckets sort -- one dependent launch fewer on the way to the
+// verdicts (the edge lanes, which need the sorted records, follow).
+template <bool WIDE>
+__global__ __launch_bounds__(64) void k_ss_bucket_rc(SortJobs J, KeyArrays keys, ReadCheckArgs RA, int nbk) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_buf[3 * SS_ROW];
+    if ((int)blockIdx.x < nbk) {
+        ss_bucket_wave(J, keys, (int)blockIdx.x, s_buf);
+        return;
+    }
+    const Group<RC_G> g;
+    read_check_group<WIDE>(RA, g, (int)(((blockIdx.x - nbk) * 64 + threadIdx.x) / RC_G));
 }
 
 // ---- large batches: merge sort ------------------------------------------
@@ -1420,10 +1445,11 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
 }
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        bool scattered, hipStream_t s) {
+                        bool scattered, hipStream_t s, HistBufs* h, int cur, int64_t v0) {
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
+    b.rc_fused = false;
     if (J.n[0] + J.n[1] == 0) return false;
     if (b.large) {  // bucketed merge sort once splitters exist; the plain merge sort on the first batch
         static const bool plain = getenv("FDBCS_LARGE_SORT_PLAIN") != nullptr;  // (A/B measurements)
@@ -1435,7 +1461,21 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
         hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
     }
     hipLaunchKernelGGL(k_ss_guard, dim3(2), dim3(1024), 0, s, J, b.keys, b.ss_gsamp);  // overflow guard
-    hipLaunchKernelGGL(k_ss_bucket, dim3(J.nb[0] + J.nb[1]), dim3(64), 0, s, J, b.keys);
+    const int nbk = J.nb[0] + J.nb[1];
+    static const bool separate = getenv("FDBCS_SEPARATE_READ_CHECK") != nullptr;  // (A/B measurements)
+    const int R = v.read_count;
+    if (h && R > 0 && !b.dir_join && !separate) {  // the history read check rides in the buckets' launch
+        const ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h->pool, h->dir[cur], sc, v0, h->shard,
+                               nullptr};
+        const int rc_blocks = cdiv((int64_t)R * RC_G, 64);
+        if (FDBCS_RC_WIDE)
+            hipLaunchKernelGGL(k_ss_bucket_rc<true>, dim3(nbk + rc_blocks), dim3(64), 0, s, J, b.keys, RA, nbk);
+        else
+            hipLaunchKernelGGL(k_ss_bucket_rc<false>, dim3(nbk + rc_blocks), dim3(64), 0, s, J, b.keys, RA, nbk);
+        b.rc_fused = true;
+        return true;
+    }
+    hipLaunchKernelGGL(k_ss_bucket, dim3(nbk), dim3(64), 0, s, J, b.keys);
     return true;  // the counters of the other parity are zero now
 }
 
@@ -1955,15 +1995,14 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     EdgesArgs EA{R,     W,    b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
                  b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv, b.rstamp, b.rseq};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
-    const int rc_blocks = cdiv((int64_t)R * RC_G, 256);
+    // (rc_fused: the history read check already ran in the sort's bucket launch)
+    const int rc_blocks = b.rc_fused ? 0 : cdiv((int64_t)R * RC_G, 256);
+    b.rc_fused = false;
     b.ws_deferred = defer_ws && !dj;
     const int ws_blocks = b.ws_deferred ? 0 : cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
-#ifndef FDBCS_RC_WIDE
-#define FDBCS_RC_WIDE 1
-#endif
     const bool wide = FDBCS_RC_WIDE;  // (WIDE = false: the two-level range maximum, kept for A/B)
     if (rc_blocks + ws_blocks + e_blocks > 0) {
         if (wide)
