@@ -287,8 +287,18 @@ struct Scalars {
     int32_t lm_out_count;
     uint64_t lm_bytes;
     uint64_t lm_out_bytes;
+    // live ingest (kernels_batch.hip k_live_ingest): the host's progress as
+    // the kernel's poller mirrors it, and the batch's final shape
+    // (tagged with the live batch's generation, so nothing needs resetting
+    // between batches: a word of an earlier batch reads as "nothing yet")
+    uint64_t lv_pub;        // gen << 32 | transactions published so far
+    uint32_t lv_state;      // gen << 2 | LV_*: final (lv_T/R/W set), cancelled, timed out
+    int32_t lv_T, lv_R, lv_W;
+    int32_t lv_err;         // a transaction past the live capacities (the host falls back)
+    uint64_t lv_used;       // stream bytes the host has written whole (>= the published transactions' records)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
+constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;
 
 // ---- Resolver load metrics (load_metrics.hip; Resolver.actor.cpp:146-151) ----
 // The draw of position `pos` of batch `seq` of a sample (counter-based, every
@@ -308,19 +318,25 @@ __host__ __device__ inline int64_t roll_amount(uint64_t h, int64_t metric, int64
 }
 
 // The roll of an attached sample (fdbcs_sample_attach) done by the
-// per-transaction ingest as it encodes each range: a sampled range appends
-// (amount, begin length, byte offset, add-order position) and its begin key's
-// bytes straight into pinned host memory (entries at Scalars::lm_count,
-// bytes at lm_bytes; past the capacities only the counters move).
+// per-transaction ingest as it encodes each range: a sampled range appends an
+// entry (amount, add-order position, begin length, byte offset) and its begin
+// key's bytes straight into pinned host memory -- entries at Scalars::
+// lm_count, bytes at lm_bytes in 16-byte-aligned pieces, every store 16
+// bytes wide (each store over PCIe is a transaction of its own); past the
+// capacities only the counters move.
+struct alignas(16) LmEntry {
+    int64_t amount;
+    uint32_t pos, len;
+    uint64_t off;
+    uint64_t pad;
+};
+static_assert(sizeof(LmEntry) == 32, "load-metrics entry");
 struct LmArgs {
     int32_t on;
     uint64_t seed, seq;
     int64_t units, offset_per_key;
-    int64_t* amount;
-    uint32_t* len;
-    uint64_t* off;
-    uint32_t* pos;
-    uint8_t* bytes;
+    LmEntry* ent;
+    uint8_t* bytes;  // 16-byte aligned
     uint32_t cap_n;
     uint64_t cap_b;
 };
@@ -342,7 +358,16 @@ __host__ __device__ inline uint64_t tail_half_bytes(uint64_t cap) { return (cap 
 // per-wave cycle accumulators in ph[16..31] (cumulative across batches)
 #define PACC(sc, i, v) atomicAdd((unsigned long long*)&(sc)->ph[(i)], (unsigned long long)(v))
 #define PCLK() ((int64_t)clock64())
+// ph[i] = max(ph[i], the wall clock) from any lane
+#define PMAX(sc, i) atomicMax((unsigned long long*)&(sc)->ph[(i)], (unsigned long long)wall_clock64())
+#define PSET(sc, i) ((sc)->ph[(i)] = (int64_t)wall_clock64())
 #else
+#define PMAX(sc, i) \
+    do {            \
+    } while (0)
+#define PSET(sc, i) \
+    do {            \
+    } while (0)
 #define PHASE(sc, i) \
     do {             \
     } while (0)

@@ -205,11 +205,8 @@ struct fdbcs {
         const uint64_t* seq = nullptr;  // its draw counter (read at each detect)
         uint64_t seed = 0;
         int64_t units = 0, opk = 0;
-        int64_t* amount = nullptr;
-        uint32_t* len = nullptr;
-        uint64_t* off = nullptr;
-        uint32_t* pos = nullptr;
-        uint8_t* bytes = nullptr;
+        LmEntry* ent = nullptr;  // pinned: the sampled entries
+        uint8_t* bytes = nullptr;  // pinned: their begin keys (16-byte pieces)
         size_t cap_n = 0, cap_b = 0;
         bool armed = false;       // this batch's ingest rolls
         bool rolled = false;      // the last detected batch was rolled ...
@@ -218,6 +215,12 @@ struct fdbcs {
         uint64_t batch = 0;       // ... and it was batch number `batch`
     } lm;
     uint64_t batches = 0;  // batches run (run_batch / sh_run)
+    // live ingest (k_live_ingest)
+    uint32_t lv_gen = 0;   // generation of the last live batch
+    bool lv_lm = false;    // the live kernel rolls for the attached sample
+    int64_t lv_prev_T = 0, lv_prev_R = 0, lv_prev_W = 0;  // shape of the last per-transaction batch
+    uint64_t lv_prev_K = 0;
+    int64_t lv_done = 0, lv_cancelled = 0;  // batches ingested live / cancelled on the way (stats)
 };
 
 namespace {
@@ -290,7 +293,18 @@ static bool verbose() {
         if (verbose()) fprintf(stderr, "# fdbcs grow: " __VA_ARGS__); \
     } while (0)
 
+// A live batch still open (between fdbcs_batch_begin and fdbcs_batch_detect)
+// holds the stream with its kernel: anything else that queues on the stream,
+// or waits for it, first cancels it (the kernel leaves, its partial work is
+// undone behind it; the batch is then ingested whole at detectConflicts).
+void live_quiesce(fdbcs* cs) {
+    if (!cs->st.live_active()) return;
+    cs->st.live_cancel();
+    launch_live_reset(cs->b, cs->sc, (int)(cs->sorts & 1), cs->stream);
+}
+
 int sync_state(fdbcs* cs) {
+    live_quiesce(cs);
     HIPOK(hipMemcpyAsync(cs->sc_host, cs->sc, sizeof(Scalars), hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
     adopt_scalars(cs);
@@ -457,6 +471,8 @@ void free_batch(BatchBufs& b) {
     dfree(b.desc_fmeta); dfree(b.desc_ftail);
     dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
     dfree(b.scan_tmp);
+    free_keys(b.lv_wkeys); dfree(b.lv_wkoff); dfree(b.lv_wklen);
+    b.lv_wcap = 0;
 }
 
 
@@ -759,8 +775,17 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
-    launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
-                  (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0, lm);
+    if (b.staged.live) {  // k_live_ingest encoded the batch during the adds: place its writes
+        launch_live_finish(v, b, sc, (int)(cs->sorts & 1), cs->h.dir[cs->cur], cs->lv_gen, s);
+        cs->lv_done++;
+    } else {
+        if (b.staged.live_failed) {
+            launch_live_reset(b, sc, (int)(cs->sorts & 1), s);
+            cs->lv_cancelled++;
+        }
+        launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
+                      (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0, lm);
+    }
     record(cs, 1);
     if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, cs->v0)) {
         cs->sorts++;
@@ -852,49 +877,83 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nul
 // Arm the attached sample's roll for the staged batch dv: its pinned outputs
 // hold every range (a batch whose ranges were all sampled) and every key
 // byte of the record stream (the begin keys sampled are disjoint parts of it).
-int lm_arm(fdbcs* cs, const fdbcs_batch_view& dv, LmArgs& la) {
+int lm_arm(fdbcs* cs, uint64_t n_ranges, uint64_t key_bytes, LmArgs& la) {
     fdbcs::Lm& L = cs->lm;
-    const size_t n = (size_t)dv.read_count + (size_t)dv.write_count;
-    const size_t nb = (size_t)dv.key_bytes_len + 64;
+    // every range may be sampled; every begin key is a disjoint part of the
+    // stream, plus at most 15 bytes of padding each
+    const size_t n = (size_t)n_ranges, nb = (size_t)key_bytes + 16 * n + 64;
     auto grow = [](auto*& p, size_t& cap, size_t need, size_t elem) {
-        if (need <= cap && p) return FDBCS_OK;
+        if (need <= cap && p) return (int)FDBCS_OK;
         const size_t c = std::max<size_t>(need + need / 4, 4096);
         if (p) hipHostFree(p);
         p = nullptr;
+        cap = 0;
         if (hipHostMalloc((void**)&p, c * elem, hipHostMallocDefault) != hipSuccess) return (int)FDBCS_E_NOMEM;
         cap = c;
-        return FDBCS_OK;
+        return (int)FDBCS_OK;
     };
-    size_t cn = L.cap_n, cn2 = L.cap_n, cn3 = L.cap_n, cn4 = L.cap_n;
     int r;
-    if (n > L.cap_n || !L.amount) {
-        if ((r = grow(L.amount, cn, n, sizeof(int64_t))) || (r = grow(L.len, cn2, n, sizeof(uint32_t))) ||
-            (r = grow(L.off, cn3, n, sizeof(uint64_t))) || (r = grow(L.pos, cn4, n, sizeof(uint32_t)))) {
-            L.cap_n = 0;
-            return r;
-        }
-        L.cap_n = std::min(std::min(cn, cn2), std::min(cn3, cn4));
-    }
-    if ((r = grow(L.bytes, L.cap_b, nb, 1))) {
-        L.cap_b = 0;
-        return r;
-    }
-    la = LmArgs{1, L.seed, *L.seq, L.units, L.opk, L.amount, L.len, L.off, L.pos, L.bytes,
-                (uint32_t)std::min<size_t>(L.cap_n, UINT32_MAX), (uint64_t)L.cap_b};
+    if ((r = grow(L.ent, L.cap_n, n, sizeof(LmEntry))) || (r = grow(L.bytes, L.cap_b, nb, 1))) return r;
+    la = LmArgs{1, L.seed, *L.seq, L.units, L.opk, L.ent, L.bytes, (uint32_t)std::min<size_t>(L.cap_n, UINT32_MAX),
+                (uint64_t)L.cap_b};
     L.rolled_seq = *L.seq;
     return FDBCS_OK;
 }
 
+// FDBCS_LIVE=0: no live ingest (A/B measurements)
+bool live_enabled() {
+    static const bool on = !(getenv("FDBCS_LIVE") && !atoi(getenv("FDBCS_LIVE"))) &&
+                           !getenv("FDBCS_SEPARATE_SCATTER") && !getenv("FDBCS_SEPARATE_UNPACK");
+    return on;
+}
+
+// Live ingest: at fdbcs_batch_begin, k_live_ingest is queued
+// behind the previous batch's history update and encodes this batch's
+// transactions while the Resolver is still adding them (TxnStage publishes its
+// progress every FDBCS_LIVE_PUB transactions); detectConflicts then only
+// places the writes (k_live_finish).  Capacities: the last batch's shape plus
+// a quarter -- a batch that outgrows them is cancelled on the way and ingested
+// whole, as without live ingest.  Only the steady state goes live: splitters
+// from an earlier batch, an unsharded set, small batches, no stage timing.
+void live_begin(fdbcs* cs) {
+    cs->lv_lm = false;
+    if (!live_enabled() || cs->timing || !cs->have_quantiles || cs->lv_prev_T <= 0 || cs->sparse_edges ||
+        (cs->h.shard.has_lo | cs->h.shard.has_hi))
+        return;
+    auto up = [](int64_t x) { return x + x / 4 + 256; };
+    LiveCaps c{};
+    c.T = (int32_t)std::min<int64_t>(up(cs->lv_prev_T), LARGE_T);
+    c.R = (int32_t)up(cs->lv_prev_R);
+    c.W = (int32_t)up(cs->lv_prev_W);
+    c.key_bytes = cs->lv_prev_K + cs->lv_prev_K / 4 + 65536;
+    c.nb0 = 0;  // (launch_live_ingest: from c.R)
+    if (large_batch_mode(c.T) || large_batch_mode(cs->lv_prev_T)) return;
+    // the batch buffers at their final size before the kernel writes them (the
+    // detect's ensure_batch must not move them): keys and the stream's bytes
+    const uint64_t kb = c.key_bytes + 32 * (uint64_t)c.T + 8 * ((uint64_t)c.R + c.W) + 64;
+    BatchBufs& b = cs->b;
+    if (ensure_batch(cs, c.T, c.R, c.W, kb)) return;
+    if (2 * (int64_t)c.W > b.lv_wcap) {
+        const int64_t n = std::max<int64_t>(2 * (int64_t)c.W, 4096);
+        free_keys(b.lv_wkeys);
+        dfree(b.lv_wkoff);
+        dfree(b.lv_wklen);
+        b.lv_wcap = 0;
+        if (alloc_keys(b.lv_wkeys, n) || dalloc(b.lv_wkoff, n) || dalloc(b.lv_wklen, n)) return;
+        b.lv_wcap = n;
+    }
+    if (cs->st.begin_live(c)) return;
+    LmArgs la{};
+    cs->lv_lm = cs->lm.owner && lm_arm(cs, (uint64_t)c.R + c.W, c.key_bytes, la) == FDBCS_OK;
+    if (++cs->lv_gen == 0) cs->lv_gen = 1;
+    launch_live_ingest(b, cs->sc, c, cs->oldest, (int)(cs->sorts & 1), cs->st.stream_dev(), cs->st.stream_cap(), cs->st.toff_dev(),
+                       cs->st.prog_dev(), cs->st.live_view(), cs->lv_lm ? &la : nullptr, cs->lv_gen, cs->stream);
+}
+
 void lm_release(fdbcs::Lm& L) {
-    if (L.amount) hipHostFree(L.amount);
-    if (L.len) hipHostFree(L.len);
-    if (L.off) hipHostFree(L.off);
-    if (L.pos) hipHostFree(L.pos);
+    if (L.ent) hipHostFree(L.ent);
     if (L.bytes) hipHostFree(L.bytes);
-    L.amount = nullptr;
-    L.len = nullptr;
-    L.off = nullptr;
-    L.pos = nullptr;
+    L.ent = nullptr;
     L.bytes = nullptr;
     L.cap_n = L.cap_b = 0;
 }
@@ -1104,9 +1163,13 @@ int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t ne
     const int64_t T = dv.txn_count;
     const bool early = !cs->timing;
     LmArgs la{};
-    const bool roll = staged && cs->lm.owner && lm_arm(cs, dv, la) == FDBCS_OK;
+    const bool live = staged && cs->b.staged.live;
+    // (a live batch's kernel rolled already, armed when the batch began)
+    const bool roll = staged && cs->lm.owner &&
+                      (live ? cs->lv_lm
+                            : lm_arm(cs, (uint64_t)dv.read_count + dv.write_count, dv.key_bytes_len, la) == FDBCS_OK);
     cs->lm.rolled = false;
-    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early, roll ? &la : nullptr))) return r;
+    if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early, roll && !live ? &la : nullptr))) return r;
     int64_t count = 0;
     if (early) {
         if ((r = verdict_wait(cs, T, verdict, &count))) return r;
@@ -1129,6 +1192,7 @@ int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t ne
 
 int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t new_oldest, uint8_t* verdict) {
     int r;
+    live_quiesce(cs);
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_ARG;  // (pipelined batches still in flight)
     if ((r = check_host_view(hv))) return r;
     fdbcs_batch_view dv;
@@ -1181,6 +1245,7 @@ namespace fdbcs_dev {
 int engine_device(const fdbcs* cs) { return cs->device; }
 
 void engine_lm_attach(fdbcs* cs, const void* owner, const uint64_t* seq, uint64_t seed, int64_t units, int64_t opk) {
+    live_quiesce(cs);  // (an open live batch rolls for the sample it began with)
     fdbcs::Lm& L = cs->lm;
     L.owner = owner;
     L.seq = seq;
@@ -1193,7 +1258,7 @@ void engine_lm_attach(fdbcs* cs, const void* owner, const uint64_t* seq, uint64_
 bool engine_lm_take(fdbcs* cs, const void* owner, uint64_t seq, int64_t opk, LmTake& out) {
     const fdbcs::Lm& L = cs->lm;
     if (!L.rolled || L.owner != owner || L.batch != cs->batches || L.rolled_seq != seq || L.opk != opk) return false;
-    out = LmTake{L.count, L.amount, L.len, L.off, L.pos, L.bytes, L.cap_n, L.cap_b};
+    out = LmTake{L.count, L.ent, L.bytes, L.cap_n, L.cap_b};
     return true;
 }
 }  // namespace fdbcs_dev
@@ -1274,6 +1339,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
 }
 
 int fdbcs_clear(fdbcs* cs, int64_t v) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     return reset_history(cs, v);  // oldestVersion and removalKey are kept (SkipList.cpp:957-959)
 }
@@ -1282,6 +1348,7 @@ int fdbcs_set_version(fdbcs* cs, int64_t v) { return fdbcs_clear(cs, v); }
 
 void fdbcs_destroy(fdbcs* cs) {
     if (!cs) return;
+    live_quiesce(cs);
     if (cs->stream) hipStreamSynchronize(cs->stream);
     if (cs->lm.owner) sample_unlink(cs->lm.owner, cs);  // (an attached sample forgets this engine)
     lm_release(cs->lm);
@@ -1319,10 +1386,12 @@ void fdbcs_destroy(fdbcs* cs) {
 int fdbcs_batch_begin(fdbcs* cs) {
     if (!cs) return FDBCS_E_ARG;
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_STATE;  // (pipelined batches still in flight)
+    live_quiesce(cs);  // (a live batch begun and never detected)
     int r;
     if ((r = cs->st.begin())) return r;
     cs->have_last_dv = false;  // (the staged bytes of the last batch are overwritten from here on)
     cs->in_batch = true;
+    live_begin(cs);
     return FDBCS_OK;
 }
 
@@ -1356,6 +1425,10 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     fdbcs_batch_view dv;
     if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
     cs->stage_key_total = cs->st.key_total();
+    cs->lv_prev_T = dv.txn_count;  // (the next batch's live capacities)
+    cs->lv_prev_R = dv.read_count;
+    cs->lv_prev_W = dv.write_count;
+    cs->lv_prev_K = cs->st.key_total();
     r = finish_detect(cs, dv, now, new_oldest, verdict, true);
     cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};  // (the ingest that reads it was launched)
@@ -1373,6 +1446,7 @@ int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
 }
 
 int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest) {
+    if (cs) live_quiesce(cs);
     if (cs) cs->have_last_dv = false;
     if (!cs || !hb || cs->in_batch) return FDBCS_E_ARG;
     if (cs->sub_head - cs->sub_tail >= 2) return FDBCS_E_ARG;  // two in flight: fdbcs_batch_wait first
@@ -1409,6 +1483,7 @@ int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
 }
 
 int fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict) {
+    if (cs) live_quiesce(cs);
     if (!cs || cs->sub_tail == cs->sub_head) return FDBCS_E_ARG;
     fdbcs::Slot& S = cs->slot[cs->sub_tail & 1];
     int r;
@@ -1427,11 +1502,13 @@ int fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict) {
 
 int fdbcs_detect_device(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest,
                         uint8_t* dev_verdict, int sync) {
+    if (cs) live_quiesce(cs);
     if (!cs || !db) return FDBCS_E_ARG;
     return run_batch(cs, *db, now, new_oldest, dev_verdict, sync != 0);
 }
 
 int64_t fdbcs_history_size(fdbcs* cs) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     int r = sync_state(cs);
     return r ? r : cs->known_H;
@@ -1442,6 +1519,7 @@ int64_t fdbcs_oldest_version(const fdbcs* cs) { return cs ? cs->oldest : 0; }
 
 int64_t fdbcs_dump_history(fdbcs* cs, int64_t cap, int64_t* versions, uint32_t* key_len, uint64_t* key_off,
                            uint8_t* key_bytes, uint64_t key_bytes_cap) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     int r;
     if ((r = sync_state(cs))) return r;
@@ -1493,6 +1571,7 @@ int64_t fdbcs_dump_history(fdbcs* cs, int64_t cap, int64_t* versions, uint32_t* 
 int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint32_t* key_len,
                        const uint64_t* key_off, const uint8_t* key_bytes, int64_t v0, int64_t oldest,
                        const uint8_t* removal_key, uint32_t removal_key_len) {
+    if (cs) live_quiesce(cs);
     if (!cs || n < 0) return FDBCS_E_ARG;
     if (removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_KEY;
     int r;
@@ -1595,6 +1674,7 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
 }
 
 int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     uint64_t hi = 0, lo = 0;
     uint32_t meta = 0;
@@ -1617,6 +1697,7 @@ int32_t fdbcs_removal_key(fdbcs* cs, uint8_t* buf, int32_t cap) {
 }
 
 int fdbcs_enable_stage_timing(fdbcs* cs, int on) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     cs->timing = on != 0;
     return FDBCS_OK;
@@ -1637,13 +1718,15 @@ int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
     const Scalars& h = *cs->sc_host;
     const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
                                     h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc,
-                                    (int64_t)cs->h.tail_cap, (int64_t)h.tail_used, h.tail_half};
+                                    (int64_t)cs->h.tail_cap, (int64_t)h.tail_used, h.tail_half, cs->lv_done,
+                                    cs->lv_cancelled};
     const int n = std::min(cap, (int)FDBCS_STATS);
     for (int i = 0; i < n; i++) out[i] = v[i];
     return n;
 }
 
 int fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap) {
+    if (cs) live_quiesce(cs);
 #ifdef FDBCS_PHASES
     if (!cs || !out) return FDBCS_E_ARG;
     const int n = std::min(cap, 32);
@@ -1660,6 +1743,7 @@ int fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap) {
 void* fdbcs_stream(fdbcs* cs) { return cs ? (void*)cs->stream : nullptr; }
 
 int fdbcs_last_device_batch(fdbcs* cs, fdbcs_batch_view* out) {
+    if (cs) live_quiesce(cs);
     if (!cs || !out) return FDBCS_E_ARG;
     if (!cs->have_last_dv) return FDBCS_E_STATE;
     *out = cs->last_dv;
@@ -1691,6 +1775,7 @@ const char* fdbcs_version(void) { return "fdbcs gfx950 0.1.0"; }
 
 int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, const uint8_t* hi, uint32_t hi_len,
                     int has_hi) {
+    if (cs) live_quiesce(cs);
     if (!cs || lo_len > FDBCS_MAX_KEY || hi_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
     ShardBounds sb{};
     sb.has_lo = has_lo != 0;
@@ -1717,6 +1802,7 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
 
 int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
                       uint8_t* dev_hist) {
+    if (cs) live_quiesce(cs);
     if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     (void)now;
     (void)new_oldest;
@@ -1770,6 +1856,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
 int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
                       const uint8_t* removal_key, int32_t removal_key_len, const uint8_t* dev_hist,
                       uint8_t* dev_verdict, int64_t* info) {
+    if (cs) live_quiesce(cs);
     if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     if (!cs || !db || !info || removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
     cs->edges_known = false;
@@ -1817,6 +1904,7 @@ int fdbcs_shard_set_protocol(fdbcs* cs, int sparse_edges) {
 }
 
 int64_t fdbcs_shard_edge_count(fdbcs* cs) {
+    if (cs) live_quiesce(cs);
     if (!cs) return FDBCS_E_ARG;
     if (cs->edges_known) return cs->sc_host->edges_total;  // (copied by fdbcs_shard_check)
     int32_t n = 0;
@@ -1826,6 +1914,7 @@ int64_t fdbcs_shard_edge_count(fdbcs* cs) {
 }
 
 int fdbcs_shard_get_edges(fdbcs* cs, int32_t* dev_et, int32_t* dev_eu, int64_t n) {
+    if (cs) live_quiesce(cs);
     if (!cs || n < 0 || n > cs->b.edge_cap || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
     if (n) {
         HIPOK(hipMemcpyAsync(dev_et, cs->b.et, (size_t)n * 4, hipMemcpyDeviceToDevice, cs->stream));
@@ -1836,6 +1925,7 @@ int fdbcs_shard_get_edges(fdbcs* cs, int32_t* dev_et, int32_t* dev_eu, int64_t n
 }
 
 int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_eu, int64_t n) {
+    if (cs) live_quiesce(cs);
     if (!cs || n < 0 || n > INT32_MAX || (n && (!dev_et || !dev_eu))) return FDBCS_E_ARG;
     cs->edges_known = false;
     BatchBufs& b = cs->b;
@@ -1848,6 +1938,7 @@ int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_e
 
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
                         int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {
+    if (cs) live_quiesce(cs);
     if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
     // (the window lies in the history the last apply left: known_H, synchronized there)
     if (!cs || !info || a < 0 || b < a || b > cs->known_H || key_index >= cs->known_H) return FDBCS_E_ARG;
@@ -2314,6 +2405,7 @@ int fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_b
 int fdbcs_sharded_batch_begin(fdbcs_sharded* sh) {
     if (!sh) return FDBCS_E_ARG;
     int r;
+    sh->cs->lv_prev_T = 0;  // (no live ingest: sh_run ingests the whole batch)
     if ((r = fdbcs_batch_begin(sh->cs))) return r;
     sh->in_batch = true;
     return FDBCS_OK;
@@ -2408,6 +2500,7 @@ int64_t fdbcs_sharded_header_version(const fdbcs_sharded* sh) { return sh ? sh->
 extern "C" int fdbcs_nth_after(fdbcs* cs, int32_t n, const uint8_t* key_bytes, const uint64_t* key_off,
                                const uint32_t* key_len, const int64_t* steps, uint8_t* out, uint32_t out_stride,
                                int32_t* out_len) {
+    if (cs) live_quiesce(cs);
     if (!cs || n < 0 || (n && (!key_bytes || !key_off || !key_len || !steps || !out || !out_len))) return FDBCS_E_ARG;
     if (n == 0) return FDBCS_OK;
     hipStream_t s = cs->stream;

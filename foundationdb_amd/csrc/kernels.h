@@ -103,6 +103,22 @@ struct StagedBatch {
     const uint8_t* stream = nullptr;  // device copy of the record stream
     const uint64_t* toff = nullptr;   // [T] record offsets (device)
     UnpackOut view{};                 // the batch view's arrays, written on the way
+    // live ingest (stage.h): k_live_ingest already encoded the batch from the
+    // host-mapped stream while the adds ran; run_batch launches
+    // k_live_finish instead of the ingest
+    bool live = false;
+    // a live batch that outgrew its capacities: its partial work is undone
+    // (launch_live_reset) before the ingest of the whole stream
+    bool live_failed = false;
+};
+
+// Live ingest: the shape a live batch may reach, fixed
+// when the batch begins (the buffers are sized for it; a batch past it falls
+// back to the ingest at detectConflicts).
+struct LiveCaps {
+    int32_t T, R, W;
+    uint64_t key_bytes;
+    int32_t nb0;  // buckets of the read-begin sort (the live kernel scatters into them)
 };
 
 struct BatchBufs {
@@ -146,6 +162,14 @@ struct BatchBufs {
                          // small directory, engine.hip edges_read_check)
     bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
     bool rc_fused;       // this batch's history read check ran in the sort's bucket launch
+    // live ingest: the read-begin sort's bucket count the live kernel used
+    // (0: none; make_sort_jobs keeps it), and the write endpoints by 2w until
+    // k_live_finish places them at 2R + 2w
+    int32_t lv_nb0;
+    KeyArrays lv_wkeys;
+    uint64_t* lv_wkoff;
+    uint32_t* lv_wklen;
+    int64_t lv_wcap;
     // rounds mode (kernels_batch.hip k_decide_rounds)
     int32_t* rq;         // [2R] sorted write endpoints <= each read's begin / < its end
     int32_t* plist;      // [R + W] candidate reads: some write of the batch may overlap them (duplicates)
@@ -240,6 +264,21 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // the sort records into their buckets itself (launch_sort_ranges(scattered))
 // hd: the directory the batch's read check will search (its bmax2 level is
 // built here, from the maxima the last history update left)
+// Live ingest (kernels_batch.hip).  launch_live_ingest: the persistent kernel
+// that encodes the per-transaction stream from host-mapped memory as the
+// host publishes it (prog: host-mapped progress words, stage.h), launched
+// when the batch begins; parity: the sort counters' (cs->sorts & 1).
+// launch_live_finish: after the host's final word, the write endpoints'
+// places and sort records, the per-batch resets and bmax2 (in place of
+// launch_ingest).  launch_live_reset: undo a failed live batch's partial work
+// before the whole stream is ingested again.
+// gen: the live batch's generation (tags the progress words in Scalars)
+void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
+                        const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, hipStream_t s);
+void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity, const Dir& hd,
+                        uint32_t gen, hipStream_t s);
+void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s);
 // lm: an attached sample's load-metrics roll (staged batches only; null: none)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,
                    const Dir& hd, hipStream_t s, bool sharded = false, const LmArgs* lm = nullptr);
@@ -337,10 +376,7 @@ int engine_device(const fdbcs* cs);
 // (load_metrics.hip): cs is being destroyed, its attached sample forgets it.
 struct LmTake {
     int64_t count;
-    const int64_t* amount;
-    const uint32_t* len;
-    const uint64_t* off;
-    const uint32_t* pos;
+    const LmEntry* ent;
     const uint8_t* bytes;
     size_t cap_n, cap_b;
 };

@@ -104,17 +104,37 @@ struct IngestArgs {
 // A sampled range of the load-metrics roll (common.h LmArgs): its entry and
 // begin key into pinned host memory, at places claimed by two counters (the
 // host orders the ~200 entries of a batch by position afterwards).
-__device__ inline void lm_append(const LmArgs& L, Scalars* sc, int64_t amt, const uint8_t* key, uint32_t len,
-                                 uint64_t pos) {
+// The key's bytes come from its encoding (Key: hi, lo big-endian, byte 16 in
+// meta, bytes 17.. in the 8-aligned zero-padded tail), written 16 at a time.
+__device__ inline void lm_append(const LmArgs& L, Scalars* sc, int64_t amt, const Key& k, uint64_t pos) {
+    const uint32_t len = key_len(k.meta);
+    const uint64_t padded = ((uint64_t)len + 15) & ~15ull;
     const uint32_t i = (uint32_t)atomicAdd(&sc->lm_count, 1);
-    const uint64_t o = atomicAdd((unsigned long long*)&sc->lm_bytes, (unsigned long long)len);
+    const uint64_t o = atomicAdd((unsigned long long*)&sc->lm_bytes, (unsigned long long)padded);
     if (i >= L.cap_n) return;  // (the host sees the count past the capacity and rolls the batch again)
-    L.amount[i] = amt;
-    L.len[i] = len;
-    L.off[i] = o;
-    L.pos[i] = (uint32_t)pos;
-    if (o + len <= L.cap_b)
-        for (uint32_t k = 0; k < len; k++) L.bytes[o + k] = key[k];
+    uint4* e = reinterpret_cast<uint4*>(L.ent + i);
+    e[0] = make_uint4((uint32_t)amt, (uint32_t)((uint64_t)amt >> 32), (uint32_t)pos, len);
+    e[1] = make_uint4((uint32_t)o, (uint32_t)(o >> 32), 0, 0);
+    if (o + padded > L.cap_b) return;
+    uint64_t* d = reinterpret_cast<uint64_t*>(L.bytes + o);
+    const uint64_t w0 = __builtin_bswap64(k.hi), w1 = __builtin_bswap64(k.lo);
+    *reinterpret_cast<uint4*>(d) = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+    if (len <= 16) return;
+    // bytes 16.. : byte 16, then the tail's words shifted up one byte
+    const uint64_t* t = reinterpret_cast<const uint64_t*>(k.tail);
+    const uint32_t rest = len - 16, words = (rest + 7) / 8;
+    uint64_t prev = (uint64_t)(k.meta >> 24);
+    for (uint32_t w = 0; w < words; w += 2) {
+        uint64_t x[2];
+        for (int h = 0; h < 2; h++) {
+            const uint32_t ww = w + h;
+            const uint64_t tw = ww < words && len > 17 && ww < (len - 17 + 7) / 8 ? t[ww] : 0;
+            x[h] = ww < words ? (prev | (tw << 8)) : 0;
+            prev = tw >> 56;
+        }
+        *reinterpret_cast<uint4*>(d + 2 + w) =
+            make_uint4((uint32_t)x[0], (uint32_t)(x[0] >> 32), (uint32_t)x[1], (uint32_t)(x[1] >> 32));
+    }
 }
 
 // ---------------------------------------------------------- read check ----
@@ -654,12 +674,171 @@ constexpr int STG_TPW = FDBCS_STG_TPW;
 constexpr int STG_BLOCK = FDBCS_STG_BLOCK;
 static_assert(STG_TPW >= 1 && STG_TPW <= 64 && STG_BLOCK % 64 == 0, "staged ingest shape");
 
+// a wavefront's transactions in LDS (k_ingest_staged, k_live_ingest)
+struct StgShared {
+    uint64_t base[STG_BLOCK / 64][STG_TPW];
+    int64_t snap[STG_BLOCK / 64][STG_TPW];
+    int32_t ro[STG_BLOCK / 64][STG_TPW], wo[STG_BLOCK / 64][STG_TPW], nr[STG_BLOCK / 64][STG_TPW],
+        pre[STG_BLOCK / 64][STG_TPW];
+};
+
+// LIVE's destinations for the write endpoints (by 2w until k_live_finish
+// places them at 2R + 2w) and its capacities
+struct LiveOut {
+    KeyArrays wkeys;
+    uint64_t* wkoff;
+    uint32_t* wklen;
+    int32_t capT, capR, capW;
+    // the window copy stays below this: the stream allocation's size, and in
+    // the live kernel the bytes the host has written whole, rounded up to 16
+    // (reading lines the host is still appending to made its adds stall)
+    uint64_t stream_cap;
+};
+
+// LIVE: a wavefront's records come over PCIe into an LDS window first -- its
+// transactions' record bytes from the first one on, 16 bytes a lane, one
+// round trip for the group instead of dependent header / entry / key reads
+// per lane (measured: ~36 transactions per us with the per-lane reads, slower
+// than the Resolver's adds arrive at the end of a batch); a key or record
+// past the window is read from the host-mapped stream directly.
+constexpr int LIVE_WIN = 4096;  // bytes per wavefront (config 2: 8 records of ~300 bytes)
+struct LiveWin {
+    const uint8_t* win;  // LDS
+    uint64_t lo, hi;     // the stream bytes [lo, hi) it holds
+    const uint8_t* host;
+    __device__ const uint8_t* at(uint64_t off, uint64_t len) const {
+        // (+8: encode_key reads the aligned words around a key)
+        return off >= lo && off + len + 8 <= hi ? win + (off - lo) : host + off;
+    }
+};
+
+// One wavefront's group of transactions [t0, t0 + nt) (nt <= STG_TPW) of a
+// per-transaction record stream.  LIVE (k_live_ingest): the stream is
+// host-mapped and the batch's read count is not known yet, so a write's keys
+// and view entries go to O by 2w and only the read begins are scattered; a
+// transaction past the live capacities marks lv_err (the host falls back).
+template <bool SCATTER, bool LIVE>
+__device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, const StagedBatch& S, const LiveOut& O,
+                                    int t0, int nt, StgShared& L, const uint64_t* sp0, const uint64_t* sp1,
+                                    uint8_t* win = nullptr) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // ---- headers: lane q < nt reads transaction t0 + q
+    const int t = t0 + lane;
+    const bool ht = lane < nt;
+    int n = 0;
+    const uint64_t to = ht ? S.toff[t] : STAGE_EMPTY;
+    LiveWin X{win, 0, 0, S.stream};
+    if constexpr (LIVE) {  // the group's records into the LDS window (16-byte aligned, coalesced)
+        uint64_t first = ~0ull;
+        for (int q = 0; q < nt; q++) {
+            const uint64_t o = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)to, q) |
+                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(to >> 32), q) << 32);
+            if (!(o & STAGE_EMPTY)) {
+                first = o;
+                break;
+            }
+        }
+        if (first != ~0ull) {
+            X.lo = first & ~uint64_t(15);
+            X.hi = min(X.lo + (uint64_t)LIVE_WIN, O.stream_cap & ~uint64_t(15));
+            const int n16 = (int)((X.hi - X.lo) >> 4);
+            const uint4* src = reinterpret_cast<const uint4*>(S.stream + X.lo);
+            uint4* dst = reinterpret_cast<uint4*>(win);
+            for (int k = lane; k < n16; k += 64) dst[k] = src[k];
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (ht) {
+        const StageTxn h = (to & STAGE_EMPTY) ? stage_txn(S.stream, to) : stage_txn(X.at(to, sizeof(StageHdr)) - to, to);
+        n = h.nr + h.nw;
+        if (LIVE && (t >= O.capT || h.ro + h.nr > O.capR || h.wo + h.nw > O.capW)) {
+            atomicOr(&A.sc->lv_err, 1);
+            n = 0;
+        }
+        L.base[wv][lane] = h.base;
+        L.snap[wv][lane] = h.snap < A.oldest && h.nr > 0 ? INT64_MAX : h.snap;  // (tooOld: nothing to check)
+        L.ro[wv][lane] = h.ro;
+        L.wo[wv][lane] = h.wo;
+        L.nr[wv][lane] = h.nr;
+        if (!LIVE || t < O.capT) {
+            S.view.snap[t] = h.snap;
+            S.view.ro[t] = h.ro;
+            S.view.wo[t] = h.wo;
+            A.too_old[t] = h.snap < A.oldest && h.nr > 0 ? 1 : 0;  // addTransaction's rule (SkipList.cpp:985)
+            A.hist[t] = 0;
+            A.deg[t] = 0;
+        }
+    }
+    const int incl = wave_incl_scan(n);
+    if (lane < STG_TPW) L.pre[wv][lane] = lane < nt ? incl : 1 << 30;
+    const int ntot = __builtin_amdgcn_readlane(incl, STG_TPW - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wavefront's LDS writes, read below)
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* const* tails = A.keys.tail;
+    // ---- the wavefront's ranges, one per lane
+    for (int k = lane; k < ntot; k += 64) {
+        int j = 0;  // owner: the transactions whose range prefix ends at or before k
+#pragma unroll
+        for (int q = 0; q < STG_TPW - 1; q++) j += L.pre[wv][q] <= k;
+        const int q = k - (j ? L.pre[wv][j - 1] : 0);
+        const uint64_t base = L.base[wv][j];
+        const uint64_t eo = base + sizeof(StageHdr) + sizeof(StageRange) * (uint64_t)q;
+        const StageRange e = *reinterpret_cast<const StageRange*>(LIVE ? X.at(eo, sizeof(StageRange)) : S.stream + eo);
+        const int nrj = L.nr[wv][j];
+        int64_t i;  // range index: reads first, then writes (the slot layout of fdbcs_batch_view)
+        int w = -1;
+        if (q < nrj) {
+            const int r = L.ro[wv][j] + q;
+            i = r;
+            A.read_txn[r] = t0 + j;
+            A.read_snap[r] = L.snap[wv][j];
+        } else {
+            w = L.wo[wv][j] + q - nrj;
+            i = (int64_t)A.R + w;
+            A.write_txn[w] = t0 + j;
+        }
+        const uint64_t ob = base + e.kofs, oe = base + stage_end_ofs(e);
+        const uint32_t el = stage_end_len(e);
+        const Key b = encode_key(LIVE ? X.at(ob, e.blen) : S.stream + ob, e.blen, A.btail, A.btail_cap, A.sc);
+        const Key en = encode_key(LIVE ? X.at(oe, el) : S.stream + oe, el, A.btail, A.btail_cap, A.sc);
+        if (A.lm.on) {  // iopsSample.addAndExpire of the range's begin, in the Resolver's add order (writes first)
+            const int nwj = L.pre[wv][j] - (j ? L.pre[wv][j - 1] : 0) - nrj;
+            const uint64_t pos = (uint64_t)L.ro[wv][j] + (uint64_t)L.wo[wv][j] + (uint64_t)(q < nrj ? nwj + q : q - nrj);
+            const int64_t amt = roll_amount(roll_hash(A.lm.seed, A.lm.seq, pos), A.lm.offset_per_key + e.blen,
+                                            A.lm.units);
+            if (amt) lm_append(A.lm, A.sc, amt, b, pos);
+        }
+        if (kcmp(b, en) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
+        if (LIVE && w >= 0) {  // (its slot 2R + 2w is not known yet)
+            O.wkoff[2 * w] = ob;
+            O.wklen[2 * w] = e.blen;
+            O.wkoff[2 * w + 1] = oe;
+            O.wklen[2 * w + 1] = el;
+            O.wkeys.put(2 * (int64_t)w, b);
+            O.wkeys.put(2 * (int64_t)w + 1, en);
+            continue;
+        }
+        S.view.koff[2 * i] = ob;
+        S.view.klen[2 * i] = e.blen;
+        S.view.koff[2 * i + 1] = oe;
+        S.view.klen[2 * i + 1] = el;
+        A.keys.put(2 * i, b);
+        A.keys.put(2 * i + 1, en);
+        if constexpr (SCATTER) {
+            if (w < 0) {
+                scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp0);
+            } else {
+                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp1);
+                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(2 * i + 1), 0}, tails, sp1);
+            }
+        }
+    }
+}
+
 template <bool SCATTER>
 __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJobs J, StagedBatch S, int stg_blocks) {
-    __shared__ uint64_t s_base[STG_BLOCK / 64][STG_TPW];
-    __shared__ int64_t s_snap[STG_BLOCK / 64][STG_TPW];
-    __shared__ int32_t s_ro[STG_BLOCK / 64][STG_TPW], s_wo[STG_BLOCK / 64][STG_TPW], s_nr[STG_BLOCK / 64][STG_TPW],
-        s_pre[STG_BLOCK / 64][STG_TPW];
+    __shared__ StgShared L;
     [[maybe_unused]] __shared__ uint64_t sp[2][SCATTER ? SS_MAXB : 1];
     if ((int)blockIdx.x >= stg_blocks) {  // bmax2: one word per block
         bmax2_block(A.hd, A.sc->D, (int)blockIdx.x - stg_blocks);
@@ -678,81 +857,194 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
         S.view.ro[A.T] = A.R;
         S.view.wo[A.T] = A.W;
     }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wv = threadIdx.x >> 6;
     const int t0 = ((int)blockIdx.x * (STG_BLOCK / 64) + wv) * STG_TPW;
     if (t0 >= A.T) return;  // (the whole wavefront)
-    // ---- headers: lane q < STG_TPW reads transaction t0 + q
-    const int t = t0 + lane;
-    const bool ht = lane < STG_TPW && t < A.T;
-    int n = 0;
-    if (ht) {
-        const StageTxn h = stage_txn(S.stream, S.toff[t]);
-        n = h.nr + h.nw;
-        s_base[wv][lane] = h.base;
-        s_snap[wv][lane] = h.snap < A.oldest && h.nr > 0 ? INT64_MAX : h.snap;  // (tooOld: nothing to check)
-        s_ro[wv][lane] = h.ro;
-        s_wo[wv][lane] = h.wo;
-        s_nr[wv][lane] = h.nr;
-        S.view.snap[t] = h.snap;
-        S.view.ro[t] = h.ro;
-        S.view.wo[t] = h.wo;
-        A.too_old[t] = h.snap < A.oldest && h.nr > 0 ? 1 : 0;  // addTransaction's rule (SkipList.cpp:985)
-        A.hist[t] = 0;
-        A.deg[t] = 0;
-    }
-    const int incl = wave_incl_scan(n);
-    if (lane < STG_TPW) s_pre[wv][lane] = incl;
-    const int ntot = __builtin_amdgcn_readlane(incl, STG_TPW - 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wavefront's LDS writes, read below)
-    __builtin_amdgcn_wave_barrier();
-    const uint8_t* const* tails = A.keys.tail;
-    // ---- the wavefront's ranges, one per lane
-    for (int k = lane; k < ntot; k += 64) {
-        int j = 0;  // owner: the transactions whose range prefix ends at or before k
-#pragma unroll
-        for (int q = 0; q < STG_TPW - 1; q++) j += s_pre[wv][q] <= k;
-        const int q = k - (j ? s_pre[wv][j - 1] : 0);
-        const uint64_t base = s_base[wv][j];
-        const StageRange e = reinterpret_cast<const StageRange*>(S.stream + base + sizeof(StageHdr))[q];
-        const int nrj = s_nr[wv][j];
-        int64_t i;  // range index: reads first, then writes (the slot layout of fdbcs_batch_view)
-        if (q < nrj) {
-            const int r = s_ro[wv][j] + q;
-            i = r;
-            A.read_txn[r] = t0 + j;
-            A.read_snap[r] = s_snap[wv][j];
-        } else {
-            const int w = s_wo[wv][j] + q - nrj;
-            i = (int64_t)A.R + w;
-            A.write_txn[w] = t0 + j;
-        }
-        const uint64_t ob = base + e.kofs, oe = base + stage_end_ofs(e);
-        const uint32_t el = stage_end_len(e);
-        if (A.lm.on) {  // iopsSample.addAndExpire of the range's begin, in the Resolver's add order (writes first)
-            const int nwj = s_pre[wv][j] - (j ? s_pre[wv][j - 1] : 0) - nrj;
-            const uint64_t pos = (uint64_t)s_ro[wv][j] + (uint64_t)s_wo[wv][j] + (uint64_t)(q < nrj ? nwj + q : q - nrj);
-            const int64_t amt = roll_amount(roll_hash(A.lm.seed, A.lm.seq, pos), A.lm.offset_per_key + e.blen,
-                                            A.lm.units);
-            if (amt) lm_append(A.lm, A.sc, amt, S.stream + ob, e.blen, pos);
-        }
-        S.view.koff[2 * i] = ob;
-        S.view.klen[2 * i] = e.blen;
-        S.view.koff[2 * i + 1] = oe;
-        S.view.klen[2 * i + 1] = el;
-        const Key b = encode_key(S.stream + ob, e.blen, A.btail, A.btail_cap, A.sc);
-        const Key en = encode_key(S.stream + oe, el, A.btail, A.btail_cap, A.sc);
-        A.keys.put(2 * i, b);
-        A.keys.put(2 * i + 1, en);
-        if (kcmp(b, en) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
-        if constexpr (SCATTER) {
-            if (i < A.R) {
-                scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
-            } else {
-                const int w = (int)(i - A.R);
-                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
-                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(2 * i + 1), 0}, tails, sp[1]);
+    staged_group<SCATTER, false>(A, J, S, LiveOut{}, t0, min(STG_TPW, A.T - t0), L, sp[0], sp[SCATTER ? 1 : 0]);
+}
+
+// ---- live ingest ------------------------------------------------------------
+// The Resolver adds T transactions one by one before detectConflicts
+// (Resolver.actor.cpp:140-153).  At fdbcs_batch_begin this persistent kernel
+// is queued on the engine's stream (behind the previous batch's history
+// update); it encodes each group of STG_TPW transactions as soon as the host
+// has published it, reading the records straight from the host-mapped
+// stream, so that by detectConflicts only the last groups remain.
+//   block 0, wave 0: the poller -- reads the host's progress words (one PCIe
+//                    read per ~1 us) and mirrors them to Scalars::lv_pub /
+//                    lv_state, which the other waves poll in device memory;
+//   other waves:     group g = wave, wave + waves, ... once published.
+// Every wave leaves when the host's final word says its groups are past the
+// batch, when the host cancels, or after LIVE_TIMEOUT (the poller: lv_state
+// = LV_TIMEOUT, and k_live_finish then fails the batch).
+struct LiveArgs {
+    IngestArgs A;      // T, R: the live capacities (the real counts come with the final word)
+    SortJobs J;        // job 0: the read begins' buckets (nb[0] = caps.nb0)
+    StagedBatch S;     // stream, toff: host-mapped; view: the batch view's arrays (capacity layout)
+    LiveOut O;
+    const uint64_t* prog;  // host-mapped: [0] published T, [2] state, [3..5] final T, R, W (stage.h)
+    uint64_t timeout;      // wall_clock64 ticks (100 MHz)
+    uint32_t gen;          // this live batch's generation (tags lv_pub / lv_state)
+};
+constexpr int LIVE_BLOCKS = 64;  // (255 worker waves: ~5 us a group, ~3 groups arrive per us)
+constexpr uint64_t LIVE_TIMEOUT_TICKS = 8ull * 100000000ull;  // 8 s of the 100 MHz wall clock
+
+// Polling (MI355X_MICROARCH.md, inter-workgroup visibility): relaxed
+// agent-scope loads and stores (sc1: past this CU's L1) for the mirrored
+// words, relaxed system-scope loads of the host's; ONE agent acquire per
+// group a wave takes (its L1 may hold host lines an earlier window read
+// before the host wrote them).  Acquire loads in the poll loops (an L1
+// invalidate per poll in up to 511 waves) held the kernel ~45 us behind the
+// adds at config 2.
+template <class T>
+__device__ inline T lv_load(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ inline void lv_store(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint64_t host_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
+    __shared__ StgShared L;
+    __shared__ uint64_t sp0[SS_MAXB];
+    __shared__ __attribute__((aligned(16))) uint8_t win[STG_BLOCK / 64][LIVE_WIN];
+    Scalars* sc = V.A.sc;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wid = (int)blockIdx.x * (STG_BLOCK / 64) + wv;
+    splitter_fill(V.J, 0, sp0);  // (every wave, the poller's too, before the barrier)
+    __syncthreads();
+    const uint32_t gen = V.gen;
+    if (wid == 0) {  // the poller
+        if (lane == 0) {
+            const uint64_t t_start = wall_clock64();
+            PSET(sc, 13);
+            int64_t last = -1;
+            for (;;) {
+                // (the three words in one round trip: independent loads)
+                const uint64_t st = host_load(V.prog + 2);
+                const int64_t pub = (int64_t)host_load(V.prog);
+                const uint64_t used = host_load(V.prog + 1);
+                if (st != LV_RUNNING) {
+                    PSET(sc, 10);
+                    if (st == LV_FINAL) {
+                        lv_store(&sc->lv_T, (int32_t)host_load(V.prog + 3));
+                        lv_store(&sc->lv_R, (int32_t)host_load(V.prog + 4));
+                        lv_store(&sc->lv_W, (int32_t)host_load(V.prog + 5));
+                        lv_store(&sc->lv_used, host_load(V.prog + 1));
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the counts land before the state word)
+                    }
+                    lv_store(&sc->lv_state, gen << 2 | (st == LV_FINAL ? LV_FINAL : LV_CANCEL));
+                    break;
+                }
+                if (pub != last) {
+                    // (used may be an older publish's: it only bounds the LDS
+                    // window -- records past it are read from the stream itself)
+                    lv_store(&sc->lv_used, used);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    lv_store(&sc->lv_pub, (uint64_t)gen << 32 | (uint64_t)(uint32_t)pub);
+                    last = pub;
+                }
+                if (wall_clock64() - t_start > V.timeout) {
+                    lv_store(&sc->lv_state, gen << 2 | LV_TIMEOUT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
             }
         }
+        return;
+    }
+    const int nwk = (int)gridDim.x * (STG_BLOCK / 64) - 1;
+    for (int g = wid - 1;; g += nwk) {
+        const int t0 = g * STG_TPW;
+        int tav;
+        for (;;) {  // (wave-uniform: every lane reads the same words; another batch's words read as "nothing yet")
+            const uint32_t sw = __builtin_amdgcn_readfirstlane(lv_load(&sc->lv_state));
+            const int st = (sw >> 2) == gen ? (int)(sw & 3) : LV_RUNNING;
+            if (st == LV_CANCEL || st == LV_TIMEOUT) return;
+            if (st == LV_FINAL) {
+                tav = __builtin_amdgcn_readfirstlane(lv_load(&sc->lv_T));
+                break;
+            }
+            const uint64_t pw = lv_load(&sc->lv_pub);
+            const int pub = __builtin_amdgcn_readfirstlane((uint32_t)(pw >> 32) == gen ? (int)(uint32_t)pw : 0);
+            if (pub >= t0 + STG_TPW) {
+                tav = pub;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (t0 >= tav) {
+            if (lane == 0) PMAX(sc, 11);
+            return;
+        }
+        LiveOut O = V.O;
+        const uint64_t used = lv_load(&sc->lv_used);
+        const uint64_t used_u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)used) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(used >> 32)) << 32);
+        O.stream_cap = min(O.stream_cap, used_u + 15);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (ONE per group: see above)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp0, sp0, win[wv]);
+    }
+}
+
+// After the host's final word: every write's keys to slots 2R + 2w, 2R + 2w + 1
+// with its view entries and sort records (the read begins were scattered
+// live), the per-batch resets, bmax2; a cancelled / timed-out / overflowed
+// live batch fails here (the host only lets complete ones through).
+__global__ __launch_bounds__(256) void k_live_finish(IngestArgs A, SortJobs J, StagedBatch S, LiveOut O, int w_blocks,
+                                                     uint32_t gen) {
+    __shared__ uint64_t sp1[SS_MAXB];
+    if ((int)blockIdx.x >= w_blocks) {  // bmax2: one word per block
+        bmax2_block(A.hd, A.sc->D, (int)blockIdx.x - w_blocks);
+        return;
+    }
+    Scalars* sc = A.sc;
+    PHASE(sc, 12);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sc->n_comb = 0;
+        sc->n_comb_own = 0;
+        sc->ss_resample = 0;
+        sc->ss_maxc = 0;
+        S.view.ro[A.T] = A.R;
+        S.view.wo[A.T] = A.W;
+        if (sc->lv_state != (gen << 2 | LV_FINAL) || sc->lv_err || sc->lv_T != A.T || sc->lv_R != A.R ||
+            sc->lv_W != A.W)
+            atomicCAS(&sc->err, 0, FDBCS_E_STATE);
+        sc->lv_err = 0;
+    }
+    splitter_fill(J, 1, sp1);
+    __syncthreads();
+    const int w = (int)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= A.W) return;
+    const int64_t s = 2 * (int64_t)A.R + 2 * (int64_t)w;
+    const Key b = O.wkeys.get(2 * (int64_t)w), e = O.wkeys.get(2 * (int64_t)w + 1);
+    A.keys.put(s, b);
+    A.keys.put(s + 1, e);
+    S.view.koff[s] = O.wkoff[2 * w];
+    S.view.klen[s] = O.wklen[2 * w];
+    S.view.koff[s + 1] = O.wkoff[2 * w + 1];
+    S.view.klen[s + 1] = O.wklen[2 * w + 1];
+    const uint8_t* const* tails = A.keys.tail;
+    scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)s, 0}, tails, sp1);
+    scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(s + 1), 0}, tails, sp1);
+}
+
+// a failed live batch: its sort counters (this parity), load-metrics entries,
+// tails and flags back to a batch's start
+__global__ void k_live_reset(int32_t* cnt, Scalars* sc) {
+    for (int k = threadIdx.x; k < 2 * SS_MAXB; k += blockDim.x) cnt[k] = 0;
+    if (threadIdx.x == 0) {
+        sc->ss_over[0] = sc->ss_over[1] = 0;
+        sc->lm_count = 0;
+        sc->lm_bytes = 0;
+        sc->btail_used = 0;
+        sc->lv_err = 0;
+        sc->err = 0;
     }
 }
 
@@ -1360,6 +1652,7 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
     J.tmp = b.ss_tmp;
     J.sc = sc;
     for (int j = 0; j < 2; j++) J.nb[j] = ss_buckets(J.n[j]);
+    if (b.lv_nb0 > 0) J.nb[0] = b.lv_nb0;  // (the live ingest scattered the read begins into that many)
     J.blocks0 = cdiv(J.n[0], 256);
     return J;
 }
@@ -1444,9 +1737,51 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
         hipLaunchKernelGGL(k_ingest<false>, dim3(blocks), dim3(IB), 0, s, A, J);
 }
 
+void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
+                        const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, hipStream_t s) {
+    IngestArgs A{};
+    A.T = caps.T; A.R = caps.R; A.W = caps.W;
+    A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
+    A.write_txn = b.write_txn;
+    A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
+    A.lm = lm ? *lm : LmArgs{};
+    b.lv_nb0 = caps.nb0 > 0 ? caps.nb0 : ss_buckets(caps.R);  // (make_sort_jobs keeps it until this batch's sort)
+    fdbcs_batch_view vc{};
+    vc.read_count = caps.R;
+    vc.write_count = caps.W;
+    const SortJobs J = make_sort_jobs(vc, b, sc, parity);
+    StagedBatch S;
+    S.stream = stream;
+    S.toff = toff;
+    S.view = view;
+    S.live = true;
+    const LiveOut O{b.lv_wkeys, b.lv_wkoff, b.lv_wklen, caps.T, caps.R, caps.W, stream_cap};
+    const LiveArgs V{A, J, S, O, prog, LIVE_TIMEOUT_TICKS, gen};
+    hipLaunchKernelGGL(k_live_ingest, dim3(LIVE_BLOCKS), dim3(STG_BLOCK), 0, s, V);
+}
+
+void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity, const Dir& hd,
+                        uint32_t gen, hipStream_t s) {
+    IngestArgs A{};
+    A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
+    A.keys = b.keys; A.sc = sc; A.hd = hd;
+    const SortJobs J = make_sort_jobs(v, b, sc, parity);
+    const LiveOut O{b.lv_wkeys, b.lv_wkoff, b.lv_wklen, 0, 0, 0, 0};
+    const int w_blocks = std::max(1, cdiv((int64_t)v.write_count, 256));
+    const int bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
+    hipLaunchKernelGGL(k_live_finish, dim3(w_blocks + bmax2_blocks), dim3(256), 0, s, A, J, b.staged, O, w_blocks,
+                       gen);
+}
+
+void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {
+    hipLaunchKernelGGL(k_live_reset, dim3(1), dim3(256), 0, s, b.ss_cnt + parity * 2 * SS_MAXB, sc);
+}
+
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s, HistBufs* h, int cur, int64_t v0) {
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
+    b.lv_nb0 = 0;  // (a live batch's read-begin bucket count, kept by the jobs above)
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
     b.rc_fused = false;

@@ -319,6 +319,16 @@ struct fdbcs_sample {
     uint64_t seed = 0;
     uint64_t seq = 0;  // batches rolled so far (draw counter)
     fdbcs* attached = nullptr;  // fdbcs_sample_attach: the engine whose ingest rolls for this sample
+    // batches rolled by the attached engine, not yet in the sample: the
+    // Resolver's commit path only copies their entries; the inserts happen at
+    // the next poll / query (drain), in batch order, before anything reads or
+    // expires the sample -- nothing observable changes
+    struct Pending {
+        double exp;
+        std::vector<fdbcs_dev::LmEntry> ent;
+        std::vector<uint8_t> bytes;
+    };
+    std::deque<Pending> pending;
     FlatSample sample;
     struct GItem {
         uint64_t h, off;
@@ -501,33 +511,51 @@ namespace {
 
 // The batch's entries into the sample and its expiry group, in the Resolver's
 // add order (addAndExpire, StorageMetrics.actor.h:108-113): entry i of the m
-// taken is entries[order[i]]; key bytes at bytes + off.
-int sample_take(fdbcs_sample* s, double expiration, uint64_t m, const int64_t* amt, const uint32_t* len,
-                const uint64_t* off, const uint8_t* bytes, const std::vector<uint32_t>* order) {
+// taken is entry order[i] (amt, len, off: its amount, key length, key bytes
+// at bytes + off).
+template <class A, class L, class O>
+void sample_insert(fdbcs_sample* s, double expiration, uint64_t m, A amt, L len, O off, const uint8_t* bytes,
+                   const std::vector<uint32_t>* order) {
     fdbcs_sample::Group g{expiration, std::string(), {}};
     g.items.reserve(m);
     uint64_t nb = 0;
-    for (uint64_t i = 0; i < m; i++) nb += len[order ? (*order)[i] : i];
+    for (uint64_t i = 0; i < m; i++) nb += len(order ? (*order)[i] : (uint32_t)i);
     g.bytes.reserve(nb);
     for (uint64_t i = 0; i < m; i++) {
         const uint32_t e = order ? (*order)[i] : (uint32_t)i;
-        g.bytes.append((const char*)bytes + off[e], len[e]);
+        g.bytes.append((const char*)bytes + off(e), len(e));
     }
     s->dirty = true;
     uint64_t o = 0;
     for (uint64_t i = 0; i < m; i++) {
         const uint32_t e = order ? (*order)[i] : (uint32_t)i;
+        const uint32_t ln = len(e);
         const uint8_t* k = (const uint8_t*)g.bytes.data() + o;
-        const uint64_t h = FlatSample::hash(k, len[e]);
-        s->sample.add(k, len[e], h, amt[e]);
-        g.items.push_back({h, o, len[e], -amt[e]});
-        o += len[e];
+        const uint64_t h = FlatSample::hash(k, ln);
+        s->sample.add(k, ln, h, amt(e));
+        g.items.push_back({h, o, ln, -amt(e)});
+        o += ln;
     }
     s->queued += m;
     s->queue.push_back(std::move(g));
-    s->seq++;
-    return FDBCS_OK;
 }
+
+// the pending batches of the attached engine's rolls into the sample, oldest first
+void drain(fdbcs_sample* s) {
+    while (!s->pending.empty()) {
+        fdbcs_sample::Pending& p = s->pending.front();
+        const uint64_t m = p.ent.size();
+        std::vector<uint32_t> order(m);
+        for (uint64_t i = 0; i < m; i++) order[i] = (uint32_t)i;
+        const auto& E = p.ent;
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return E[a].pos < E[b].pos; });
+        sample_insert(
+            s, p.exp, m, [&](uint32_t e) { return E[e].amount; }, [&](uint32_t e) { return E[e].len; },
+            [&](uint32_t e) { return E[e].off; }, p.bytes.data(), &order);
+        s->pending.pop_front();
+    }
+}
+void drain(const fdbcs_sample* s) { drain(const_cast<fdbcs_sample*>(s)); }  // (queries: nothing observable moves)
 
 }  // namespace
 
@@ -541,17 +569,23 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
         if (fdbcs_dev::engine_lm_take(cs, s, s->seq, offset_per_key, tk)) {
             const uint64_t m = (uint64_t)tk.count;
             bool fits = m <= tk.cap_n;
-            for (uint64_t i = 0; fits && i < m; i++) fits = tk.off[i] + tk.len[i] <= tk.cap_b;
-            if (fits) {
-                std::vector<uint32_t> order(m);
-                for (uint64_t i = 0; i < m; i++) order[i] = (uint32_t)i;
-                std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return tk.pos[a] < tk.pos[b]; });
+            uint64_t nb = 0;
+            for (uint64_t i = 0; fits && i < m; i++) {
+                fits = tk.ent[i].off + tk.ent[i].len <= tk.cap_b;
+                nb = std::max<uint64_t>(nb, tk.ent[i].off + tk.ent[i].len);
+            }
+            if (fits) {  // (copied now: the next batch's ingest reuses the pinned outputs)
+                s->pending.push_back({expiration, std::vector<fdbcs_dev::LmEntry>(tk.ent, tk.ent + m),
+                                      std::vector<uint8_t>(tk.bytes, tk.bytes + nb)});
+                s->seq++;
+                if (s->pending.size() > 64) drain(s);  // (a caller that never polls: bounded)
                 if (out_sampled) *out_sampled = (int64_t)m;
-                return sample_take(s, expiration, m, tk.amount, tk.len, tk.off, tk.bytes, &order);
+                return FDBCS_OK;
             }
             // (past the pinned outputs' capacities: the rest below rolls the still-resident batch again)
         }
     }
+    drain(s);  // (the batches before this one enter the sample first)
     // the buffers and launches belong on the engine's device, whatever the
     // calling thread's current one (the shim's G-GPU mode hands rank 0's
     // engine to the Resolver's thread); restored on every return
@@ -612,11 +646,19 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
     // addAndExpire (StorageMetrics.actor.h:108-113), in the Resolver's order
     // (the ordered compaction's); the batch's queue entries form one group
     // sharing its key bytes
-    return sample_take(s, expiration, m, s->h_amt, s->h_len, s->h_off, s->h_out, nullptr);
+    const int64_t* amt = s->h_amt;
+    const uint32_t* len = s->h_len;
+    const uint64_t* off = s->h_off;
+    sample_insert(
+        s, expiration, m, [&](uint32_t e) { return amt[e]; }, [&](uint32_t e) { return len[e]; },
+        [&](uint32_t e) { return off[e]; }, s->h_out, nullptr);
+    s->seq++;
+    return FDBCS_OK;
 }
 
 int fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, int64_t metric) {
     if (!s || (len && !key)) return FDBCS_E_ARG;
+    drain(s);
     // an entry's metric stays >= 0 (a negative one would break the prefix-sum
     // index; the Resolver's amounts are positive and expire back to 0)
     if (metric < 0 && s->sample.get(key, len, FlatSample::hash(key, len)) + metric < 0) return FDBCS_E_ARG;
@@ -626,6 +668,7 @@ int fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, i
 
 int fdbcs_sample_poll(fdbcs_sample* s, double now) {
     if (!s) return FDBCS_E_ARG;
+    drain(s);
     // TransientStorageMetricSample::poll() (StorageMetrics.actor.h:150-164)
     while (!s->queue.empty() && s->queue.front().exp <= now) {
         const auto& g = s->queue.front();
@@ -642,12 +685,14 @@ int fdbcs_sample_poll(fdbcs_sample* s, double now) {
 
 int64_t fdbcs_sample_estimate(const fdbcs_sample* s, const uint8_t* b, uint32_t bl, const uint8_t* e, uint32_t el) {
     if (!s || (bl && !b) || (el && !e)) return FDBCS_E_ARG;
+    drain(s);
     return s->estimate(b, bl, e, el);
 }
 
 int32_t fdbcs_sample_split(const fdbcs_sample* s, const uint8_t* b, uint32_t bl, const uint8_t* e, uint32_t el,
                            int64_t offset, int front, uint8_t* out, uint32_t cap) {
     if (!s || (bl && !b) || (el && !e) || (cap && !out)) return FDBCS_E_ARG;
+    drain(s);
     const std::string k = split_estimate(s, std::string((const char*)b, bl), std::string((const char*)e, el), offset,
                                          front != 0);
     if (k.size() > cap) return FDBCS_E_CAPACITY;
@@ -655,12 +700,21 @@ int32_t fdbcs_sample_split(const fdbcs_sample* s, const uint8_t* b, uint32_t bl,
     return (int32_t)k.size();
 }
 
-int64_t fdbcs_sample_size(const fdbcs_sample* s) { return s ? (int64_t)s->sample.live : FDBCS_E_ARG; }
+int64_t fdbcs_sample_size(const fdbcs_sample* s) {
+    if (!s) return FDBCS_E_ARG;
+    drain(s);
+    return (int64_t)s->sample.live;
+}
 
-int64_t fdbcs_sample_queue_size(const fdbcs_sample* s) { return s ? (int64_t)s->queued : FDBCS_E_ARG; }
+int64_t fdbcs_sample_queue_size(const fdbcs_sample* s) {
+    if (!s) return FDBCS_E_ARG;
+    drain(s);
+    return (int64_t)s->queued;
+}
 
 int32_t fdbcs_sample_entry(const fdbcs_sample* s, int64_t i, uint8_t* out, uint32_t cap, int64_t* metric) {
     if (!s || i < 0 || (cap && !out)) return FDBCS_E_ARG;
+    drain(s);
     s->view();
     if (i >= (int64_t)s->keys.size()) return FDBCS_E_ARG;
     const std::string& k = *s->keys[i];

@@ -45,6 +45,22 @@ class TxnStage {
     void release();
 
     int begin();
+    // Live ingest: after begin(), make this batch live --
+    // the stream, offsets and view sized for `caps`, the progress words reset
+    // -- before the engine launches k_live_ingest over them.  The adds then
+    // publish their progress instead of copying chunks; a batch that leaves
+    // `caps` (or a buffer that must grow) is cancelled and ingested at
+    // finish() as usual.
+    int begin_live(const LiveCaps& caps);
+    // the live kernel's inputs (device pointers of the host-mapped buffers)
+    const uint8_t* stream_dev() const { return pin_dev_; }
+    uint64_t stream_cap() const { return cap_; }
+    const uint64_t* toff_dev() const { return toff_dev_; }
+    const uint64_t* prog_dev() const { return prog_dev_; }
+    UnpackOut live_view() const { return lview_; }
+    bool live_active() const { return live_ && !live_broken_; }
+    // cancel a live batch (the kernel leaves; finish() ingests the whole stream)
+    void live_cancel();
     // addTransaction: FDBCS_E_KEY / FDBCS_E_RANGE (begin >= end, SURVEY.md
     // §0.6) refuse the transaction, which is then not part of the batch.
     int add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw);
@@ -53,9 +69,14 @@ class TxnStage {
     // Sends the rest; dv = the device batch view (valid until the next
     // begin()).  With `staged`, the next ingest builds dv's arrays itself
     // straight from the stream (*staged: where to find it); else k_unpack
-    // builds them now (FDBCS_SEPARATE_UNPACK: always).
+    // builds them now (FDBCS_SEPARATE_UNPACK: always).  A live batch: the
+    // final progress word instead (staged->live; dv over the host-mapped
+    // stream and the live view layout).
     int finish(fdbcs_batch_view& dv, StagedBatch* staged = nullptr);
     int64_t txns() const { return T_; }
+    int64_t reads() const { return R_; }
+    int64_t writes() const { return W_; }
+    uint64_t stream_bytes() const { return used_; }
     // the batch's key bytes (every begin and end key): more than the stream
     // holds when point ranges share their bytes; sizes the tail buffers
     uint64_t key_total() const { return K_; }
@@ -63,6 +84,8 @@ class TxnStage {
 
    private:
     int grow(int64_t need_txns, uint64_t need_bytes);
+    void publish();
+    void live_check();
 
     void sync();
     static bool pull_rest();
@@ -83,10 +106,22 @@ class TxnStage {
     bool chunk_sent_ = false;     // a chunk copy (and its event) since begin()
     uint64_t cap_ = 0;
     uint64_t used_ = 0, sent_ = 0;
-    uint64_t* toff_ = nullptr;    // host [T]: record offsets (appended to the stream at finish)
+    uint64_t* toff_ = nullptr;    // pinned, host-mapped [T]: record offsets (appended to the stream at finish)
+    uint64_t* toff_dev_ = nullptr;
     int64_t toff_cap_ = 0;
     uint8_t* view_ = nullptr;     // device: the unpacked arrays
     uint64_t view_cap_ = 0;
+    // live ingest
+    bool live_ = false;           // this batch began live ...
+    bool live_broken_ = false;    // ... and was cancelled (finish() ingests it whole)
+    LiveCaps lcaps_{};
+    UnpackOut lview_{};           // the view's arrays in the live layout (sized by lcaps_)
+    int64_t pub_every_ = 16;      // FDBCS_LIVE_PUB: transactions per progress word
+    int64_t next_pub_ = 0;
+    // host-mapped progress: [0] published T, [1] published stream bytes,
+    // [2] state (LV_RUNNING / LV_FINAL / LV_CANCEL), [3..5] final T, R, W
+    uint64_t* prog_ = nullptr;
+    uint64_t* prog_dev_ = nullptr;
 };
 
 }  // namespace fdbcs_dev

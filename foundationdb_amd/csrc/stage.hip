@@ -84,14 +84,18 @@ void TxnStage::sync() {
 }
 
 void TxnStage::release() {
+    live_cancel();  // (a live kernel waiting for this batch leaves: the syncs below return)
     sync();
     if (pin_) hipHostFree(pin_);
     if (dev_) hipFree(dev_);
     if (view_) hipFree(view_);
     if (copied_) hipEventDestroy(copied_);
-    free(toff_);
+    if (toff_) hipHostFree(toff_);
+    if (prog_) hipHostFree(prog_);
     pin_ = dev_ = view_ = nullptr;
-    toff_ = nullptr;
+    toff_ = toff_dev_ = nullptr;
+    prog_ = prog_dev_ = nullptr;
+    live_ = false;
     copied_ = nullptr;
     cap_ = view_cap_ = 0;
     toff_cap_ = 0;
@@ -104,15 +108,24 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
     copy_ = copy;
     chunk_ = std::max<uint64_t>(4096, chunk);
     if (const char* e = getenv("FDBCS_STAGE_EARLY")) early_ = strtoull(e, nullptr, 0);
+    if (const char* e = getenv("FDBCS_LIVE_PUB")) pub_every_ = std::max<int64_t>(8, strtoll(e, nullptr, 0));  // (default 16)
     if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
+    if (!prog_) {  // (the live kernel reads it over PCIe: coherent, uncached on the device)
+        if (hipHostMalloc((void**)&prog_, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        memset(prog_, 0, 64);
+        if (hipHostGetDevicePointer((void**)&prog_dev_, prog_, 0) != hipSuccess) return FDBCS_E_HIP;
+    }
     return FDBCS_OK;
 }
 
 int TxnStage::begin() {
+    live_cancel();  // (a batch begun and never detected)
     T_ = R_ = W_ = 0;
     K_ = 0;
     used_ = sent_ = 0;
     chunk_sent_ = false;
+    live_ = live_broken_ = false;
     if (!pin_) {
         int r = grow(8192, 4 << 20);
         if (r) return r;
@@ -124,18 +137,28 @@ int TxnStage::begin() {
 // Grow the offsets and / or the stream.  Chunks already sent went to the old
 // device buffer: the whole stream is sent again (sent_ = 0).
 int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
+    if (need_txns > toff_cap_ || need_bytes > cap_) {
+        live_cancel();  // (the live kernel reads the old buffers: it leaves first)
+        sync();         // copies in flight read the old buffers
+    }
     if (need_txns > toff_cap_) {
         const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
-        uint64_t* nt = static_cast<uint64_t*>(realloc(toff_, (size_t)nc * 8));
-        if (!nt) return FDBCS_E_NOMEM;
+        uint64_t* nt = nullptr;
+        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
+        if (toff_) hipHostFree(toff_);
         toff_ = nt;
         toff_cap_ = nc;
+        if (hipHostGetDevicePointer((void**)&toff_dev_, toff_, 0) != hipSuccess) return FDBCS_E_HIP;
     }
     if (need_bytes > cap_) {
-        sync();  // copies in flight read the old buffers
         const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
         uint8_t* np = nullptr;
-        if (hipHostMalloc((void**)&np, nc, hipHostMallocMapped) != hipSuccess) return FDBCS_E_NOMEM;
+        // (coherent: the live kernel reads the records over PCIe as they are
+        // written, which a device-cached line of a half-written record would break)
+        if (hipHostMalloc((void**)&np, nc, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FDBCS_E_NOMEM;
         if (used_) memcpy(np, pin_, used_);
         if (pin_) hipHostFree(pin_);
         pin_ = np;
@@ -202,6 +225,10 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     K_ += kbytes;
     R_ += nr;
     W_ += nw;
+    if (live_) {
+        live_check();
+        if (!live_broken_) return FDBCS_OK;  // (no chunk copies: the live kernel reads the stream itself)
+    }
     // a chunk every chunk_ bytes, and one more `early_` bytes before where the
     // previous batch ended (batches are alike): detectConflicts then sends
     // only that much and the record offsets
@@ -236,12 +263,98 @@ int TxnStage::skip(int32_t n) {
     const uint64_t e = STAGE_EMPTY | ((uint64_t)W_ << 32) | (uint64_t)R_;
     std::fill(toff_ + T_, toff_ + T_ + n, e);
     T_ += n;
+    if (live_) live_check();
+    return FDBCS_OK;
+}
+
+// ---- live ingest --------------------------------------------------------------
+void TxnStage::publish() {
+    prog_[1] = used_;
+    __atomic_store_n(&prog_[0], (uint64_t)T_, __ATOMIC_RELEASE);  // (after the records and their offsets)
+    next_pub_ = T_ + pub_every_;
+}
+
+void TxnStage::live_check() {
+    if (live_broken_) return;
+    if (T_ > lcaps_.T || R_ > lcaps_.R || W_ > lcaps_.W || K_ > lcaps_.key_bytes) {
+        live_cancel();
+        return;
+    }
+    if (T_ >= next_pub_) publish();
+}
+
+void TxnStage::live_cancel() {
+    if (!live_ || live_broken_ || !prog_) return;
+    live_broken_ = true;
+    __atomic_store_n(&prog_[2], (uint64_t)LV_CANCEL, __ATOMIC_RELEASE);
+}
+
+int TxnStage::begin_live(const LiveCaps& caps) {
+    if (!open_ || T_ || live_) return FDBCS_E_STATE;
+    // records (header, range entries, keys, padding) and, should the batch
+    // fall back, the offsets appended at finish
+    const uint64_t slots = 2 * ((uint64_t)caps.R + (uint64_t)caps.W);
+    const uint64_t need = 32 * (uint64_t)caps.T + 4 * slots + caps.key_bytes + 8 * ((uint64_t)caps.T + 1) + 64;
+    int r;
+    if ((r = grow(caps.T + 1, need))) return r;
+    auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
+    const uint64_t o_ro = al(8 * (uint64_t)caps.T), o_wo = al(o_ro + 4 * ((uint64_t)caps.T + 1)),
+                   o_ko = al(o_wo + 4 * ((uint64_t)caps.T + 1)), o_kl = al(o_ko + 8 * slots),
+                   total = al(o_kl + 4 * slots) + 16;
+    if (total > view_cap_) {
+        if (view_) {
+            sync();
+            hipFree(view_);
+            view_ = nullptr;
+        }
+        const uint64_t nc = std::max<uint64_t>(total, 2 * view_cap_);
+        view_cap_ = 0;
+        if (hipMalloc((void**)&view_, nc) != hipSuccess) return FDBCS_E_NOMEM;
+        view_cap_ = nc;
+    }
+    lview_ = UnpackOut{(int64_t*)view_, (int32_t*)(view_ + o_ro), (int32_t*)(view_ + o_wo),
+                       (uint64_t*)(view_ + o_ko), (uint32_t*)(view_ + o_kl)};
+    for (int i = 0; i < 8; i++) prog_[i] = 0;  // LV_RUNNING, nothing published (read by the kernel launched next)
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    lcaps_ = caps;
+    next_pub_ = pub_every_;
+    live_ = true;
+    live_broken_ = false;
     return FDBCS_OK;
 }
 
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
+    if (live_ && !live_broken_ && staged) {
+        // the final word: the kernel finishes the last groups and leaves
+        prog_[3] = (uint64_t)T_;
+        prog_[4] = (uint64_t)R_;
+        prog_[5] = (uint64_t)W_;
+        prog_[1] = used_;
+        __atomic_store_n(&prog_[2], (uint64_t)LV_FINAL, __ATOMIC_RELEASE);
+        live_ = false;
+        dv = fdbcs_batch_view{};
+        dv.txn_count = (int32_t)T_;
+        dv.read_count = (int32_t)R_;
+        dv.write_count = (int32_t)W_;
+        dv.snapshot = lview_.snap;
+        dv.read_off = lview_.ro;
+        dv.write_off = lview_.wo;
+        dv.key_off = lview_.koff;
+        dv.key_len = lview_.klen;
+        dv.key_bytes = pin_dev_;  // (the stream itself, host-mapped: only the rare view readers go there)
+        dv.key_bytes_len = used_;
+        *staged = StagedBatch{};
+        staged->stream = pin_dev_;
+        staged->toff = toff_dev_;
+        staged->view = lview_;
+        staged->live = true;
+        return FDBCS_OK;
+    }
+    const bool failed = live_;  // (a live batch cancelled on the way: ingested whole below)
+    live_cancel();
+    live_ = false;
     // the record offsets go after the records (8-byte aligned: records are),
     // and the rest of the stream in one copy
     const uint64_t o_toff = used_;
@@ -297,7 +410,12 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     static const bool separate = getenv("FDBCS_SEPARATE_UNPACK") != nullptr;  // (A/B measurements)
     if (staged && !separate) {
         *staged = StagedBatch{dev_, dtoff, out};
+        staged->live_failed = failed;
         return FDBCS_OK;
+    }
+    if (staged) {
+        *staged = StagedBatch{};
+        staged->live_failed = failed;
     }
     launch_unpack(dev_, dtoff, (int)T_, (int)R_, (int)W_, out, stream_);
     return FDBCS_OK;

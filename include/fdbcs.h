@@ -322,9 +322,12 @@ int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
  * overflowed and the batch's endpoints were bucketed again by splitters from
  * its own sample  [12] largest sort bucket above 128 records (0: none)
  * [13] tail arena bytes (both halves)  [14] bytes used in its current half
- * [15] current half (flips when a compaction sweep freed the other).
+ * [15] current half (flips when a compaction sweep freed the other)
+ * [16] per-transaction batches ingested live (during their adds) so far
+ * [17] live batches cancelled on the way (outgrew the live capacities, or
+ * another call needed the stream) and ingested whole at detect.
  * Returns the count written. */
-#define FDBCS_STATS 16
+#define FDBCS_STATS 18
 int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
 
 /* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the

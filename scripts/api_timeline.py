@@ -74,7 +74,11 @@ def main():
         agg["detect"].append(t1 - ta)
         ev = [e for e in dev if ta - 400_000 <= e[0] <= t1]
         ks = [e for e in ev if e[2].startswith("K ") and e[0] >= ta - 50_000]
-        ing = [e for e in ks if "ingest" in e[2] and e[0] >= ta]
+        ing = [e for e in ks if ("ingest" in e[2] or "live_finish" in e[2]) and e[0] >= ta]
+        live = [e for e in ev if "k_live_ingest" in e[2] and e[0] <= ta]
+        if live:  # (live ingest: the kernel began at fdbcs_batch_begin, before the adds ended)
+            agg["live_ingest_end-adds_end"].append(live[-1][1] - ta)
+            agg["live_ingest_start-window_start"].append(live[-1][0] - t0)
         dec = [e for e in ks if "decide" in e[2] and e[0] >= ta]
         cps = [e for e in ev if e[2].startswith("C HOST_TO_DEVICE") and e[0] <= (ing[0][0] if ing else t1)]
         prev_end = max((e[1] for e in dev if e[1] <= (ing[0][0] if ing else t1) and e[2].startswith("K ")), default=None)
