@@ -83,6 +83,12 @@ def parse():
                         "config 5: 0)")
     p.add_argument("--window-prefill", type=int, default=200,
                    help="of the prefill batches, the last this many run through the Resolver's window (untimed)")
+    p.add_argument("--preload", type=int, default=None,
+                   help="config 5: blind-write preload batches of 10^6 point writes (default 50: the 10^8-boundary "
+                        "history of SURVEY.md §8d; fewer for rehearsals)")
+    p.add_argument("--oracle-check", action="store_true",
+                   help="N > 1: gather every rank's history before the timed region and replay the timed global "
+                        "batches on rank 0 through the CPU oracle, verdicts compared (rehearsal sizes only)")
     p.add_argument("--protocol", choices=["a", "b"], default="b",
                    help="exact mode: A = every GPU receives the whole batch; B = each GPU receives only the ranges "
                         "intersecting its keys and the overlap edges are all-gathered (SURVEY.md §8e)")
@@ -96,6 +102,8 @@ def parse():
         a.prefill = PREFILL.get(a.config, 0)
     if a.latency_batches is None:
         a.latency_batches = {4: 200, 5: 0}.get(a.config, 500)
+    if a.preload is None:
+        a.preload = PRELOAD_BATCHES
     return a
 
 
@@ -366,7 +374,7 @@ def run_single(args):
     # ---- steady state (untimed, regardless of --warmup) -------------------------
     t_w = time.time()
     if cfg == 5:  # preload: 50 blind-write batches of 10^6 point writes, no compaction
-        Workload(50, txns=args.txns).prefill(cs, 0, PRELOAD_BATCHES)
+        Workload(50, txns=args.txns).prefill(cs, 0, args.preload)
     if args.prefill:
         # the prefill's last batches go through the Resolver's window itself
         # (untimed): the host path's buffers, caches and pages are warm when
@@ -686,6 +694,32 @@ class Source:
         return sub.view(), now, nold, batch.T, (None if self.keep_all else idx), (sub, batch)
 
 
+def gather_history(cs, rank, world):
+    """Every rank's history slice (ranks hold ascending key ranges) as one
+    history on rank 0: (versions, lengths, offsets, key bytes, header version,
+    oldest version); None on the other ranks.  Rehearsal sizes only (gloo
+    gather of whole dumps).  A shard's first boundary (its carried-in version
+    at its lower bound) may repeat the previous shard's last version: a
+    redundant boundary, which changes no verdict."""
+    import torch.distributed as dist
+    v, l, o, k = cs.dump_arrays()
+    lens = np.asarray(l, np.int64)
+    excl = np.cumsum(lens) - lens  # (the keys packed back to back)
+    flat = np.repeat(np.asarray(o, np.int64) - excl, lens) + np.arange(int(lens.sum()), dtype=np.int64)
+    mine = (np.asarray(v), np.asarray(l), np.asarray(k)[flat], cs.header_version, cs.oldest_version)
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object(mine, parts, dst=0)
+    if rank != 0:
+        return None
+    vers = np.concatenate([p[0] for p in parts]).astype(np.int64)
+    lens = np.concatenate([p[1] for p in parts]).astype(np.uint32)
+    kb = np.concatenate([p[2] for p in parts]).astype(np.uint8)
+    offs = np.zeros(len(lens), np.uint64)
+    if len(lens):
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return vers, lens, offs, kb, parts[0][3], max(p[4] for p in parts)  # (header: rank 0's, whose keys start at "")
+
+
 def run_multi(args, rank, world):
     """N > 1, --mode exact: one exact resolver sharded by key range over N
     GPUs behind the C ABI (fdbcs_sharded, protocol B by default), each rank
@@ -759,7 +793,7 @@ def run_multi(args, rank, world):
     t_w = time.time()
     if cfg == 5:  # preload: 50 blind-write global batches of 10^6 point writes, no compaction
         pre = Workload(50, txns=T_global)
-        for j in range(PRELOAD_BATCHES):
+        for j in range(args.preload):
             run = pre.prepare_run(j, 1, split)
             run.run(eng, verdicts=False)
             del run
@@ -787,6 +821,8 @@ def run_multi(args, rank, world):
     if rank == 0:
         print(f"# steady state: {n_pre} prefill + {args.warmup} warmup global batches, H={H_pre} "
               f"per rank {H_ranks_pre} ({time.time() - t_w:.1f}s)", file=sys.stderr, flush=True)
+    # (rehearsals: the whole history on rank 0, for the oracle replay below)
+    check_snap = gather_history(eng.local, rank, world) if args.oracle_check else None
     # ---- timed region: K batches through the Resolver's window on every rank ----
     run = wl.prepare_run(first, args.steps, split)
     T = run.T
@@ -835,6 +871,23 @@ def run_multi(args, rank, world):
                 "algo_bytes_terms": {"key_bytes": kb, "txn_bytes": 9 * T,
                                      "history_bytes": round((32.0 if cfg == 4 else E_HIST) * (H_loc_pre + H_loc_post))},
                 "history_pre_rank0": H_loc_pre, "ms_per_step": round(step_s * 1e3, 4)}
+    # ---- oracle check (rehearsals): the timed global batches on the CPU ----------
+    check = None
+    if check_snap is not None and rank == 0:
+        from oracle import CpuSpec
+        vers, lens, offs, kbytes, v0, oldest = check_snap
+        c = CpuSpec()
+        c.load_history_arrays(len(vers), vers, lens, offs, kbytes, v0=v0, oldest=oldest, removal_key=b"")
+        mism = 0
+        for k in range(args.steps):
+            b, now, nold = wl.batch(first + k)
+            mism += int((c.detect_packed(b, now, nold) != verdicts[k][:b.T]).sum())
+        c.close()
+        check = {"batches": args.steps, "txns": args.steps * T, "verdict_mismatches": mism, "history": len(vers),
+                 "how": "every rank's history gathered to rank 0 before the timed region (one global history, "
+                        "ranks in key order), the timed global batches replayed through oracle/cpu_spec.cpp"}
+        print(f"# oracle check: {mism} verdict mismatches over {args.steps} x {T} txns (H={len(vers)})",
+              file=sys.stderr, flush=True)
     # ---- CPU baseline (rank 0): the oracle on rank 0's share -------------------
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -886,6 +939,8 @@ def run_multi(args, rank, world):
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if check is not None:
+            out["oracle_check"] = check
         print(json.dumps(out), flush=True)
     eng.close()
     dist.destroy_process_group()

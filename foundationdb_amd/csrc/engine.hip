@@ -946,8 +946,9 @@ void live_begin(fdbcs* cs) {
     LmArgs la{};
     cs->lv_lm = cs->lm.owner && lm_arm(cs, (uint64_t)c.R + c.W, c.key_bytes, la) == FDBCS_OK;
     if (++cs->lv_gen == 0) cs->lv_gen = 1;
-    launch_live_ingest(b, cs->sc, c, cs->oldest, (int)(cs->sorts & 1), cs->st.stream_dev(), cs->st.stream_cap(), cs->st.toff_dev(),
-                       cs->st.prog_dev(), cs->st.live_view(), cs->lv_lm ? &la : nullptr, cs->lv_gen, cs->stream);
+    launch_live_ingest(b, cs->sc, c, cs->oldest, (int)(cs->sorts & 1), cs->st.stream_dev(), cs->st.stream_cap(),
+                       cs->st.toff_dev(), cs->st.prog_dev(), cs->st.live_view(), cs->lv_lm ? &la : nullptr,
+                       cs->lv_gen, cs->h.dir[cs->cur], cs->stream);
 }
 
 void lm_release(fdbcs::Lm& L) {

@@ -275,7 +275,7 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // gen: the live batch's generation (tags the progress words in Scalars)
 void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
                         const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
-                        UnpackOut view, const LmArgs* lm, uint32_t gen, hipStream_t s);
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, hipStream_t s);
 void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity, const Dir& hd,
                         uint32_t gen, hipStream_t s);
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s);

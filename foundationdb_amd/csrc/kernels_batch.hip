@@ -917,6 +917,14 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
     const int wid = (int)blockIdx.x * (STG_BLOCK / 64) + wv;
     splitter_fill(V.J, 0, sp0);  // (every wave, the poller's too, before the barrier)
     __syncthreads();
+    {  // bmax2 of the directory this batch's read check uses (the previous
+       // batch's update ran before this kernel): off the path after the adds
+        const int D = sc->D;
+        for (int k = (int)blockIdx.x; k * BMAX2_SPAN < D; k += (int)gridDim.x) {
+            bmax2_block(V.A.hd, D, k);
+            __syncthreads();  // (bmax2_block's LDS is reused by the next word)
+        }
+    }
     const uint32_t gen = V.gen;
     if (wid == 0) {  // the poller
         if (lane == 0) {
@@ -1739,8 +1747,9 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
 
 void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
                         const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
-                        UnpackOut view, const LmArgs* lm, uint32_t gen, hipStream_t s) {
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, hipStream_t s) {
     IngestArgs A{};
+    A.hd = hd;
     A.T = caps.T; A.R = caps.R; A.W = caps.W;
     A.oldest = oldest; A.too_old = b.too_old; A.hist = b.hist; A.read_txn = b.read_txn; A.read_snap = b.read_snap;
     A.write_txn = b.write_txn;
@@ -1768,10 +1777,8 @@ void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, in
     A.keys = b.keys; A.sc = sc; A.hd = hd;
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     const LiveOut O{b.lv_wkeys, b.lv_wkoff, b.lv_wklen, 0, 0, 0, 0};
-    const int w_blocks = std::max(1, cdiv((int64_t)v.write_count, 256));
-    const int bmax2_blocks = v.read_count > 0 ? cdiv(hd.cap, BMAX2_SPAN) : 0;  // (D <= cap; idle blocks exit)
-    hipLaunchKernelGGL(k_live_finish, dim3(w_blocks + bmax2_blocks), dim3(256), 0, s, A, J, b.staged, O, w_blocks,
-                       gen);
+    const int w_blocks = std::max(1, cdiv((int64_t)v.write_count, 256));  // (bmax2: k_live_ingest did it)
+    hipLaunchKernelGGL(k_live_finish, dim3(w_blocks), dim3(256), 0, s, A, J, b.staged, O, w_blocks, gen);
 }
 
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {
