@@ -461,7 +461,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.rec_r0); dfree(b.rec_w0); dfree(b.sw_slot);
     dfree(b.ss_cnt); dfree(b.ss_gsamp); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
     dfree(b.et); dfree(b.eu); dfree(b.csr);
-    dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv);
+    dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv); dfree(b.wcov);
     dfree(b.cb_pos); dfree(b.ce_pos); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.wh.b); dfree(b.wh.e);
@@ -534,8 +534,8 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
         dfree(b.wh.b); dfree(b.wh.e);
         dfree(b.ne.hi); dfree(b.ne.lo); dfree(b.ne.meta); dfree(b.ne.ver); dfree(b.ne.tail); dfree(b.ne_ins);
-        dfree(b.wnew); dfree(b.winv);
-        if ((r = dalloc(b.wnew, 2 * n + 64)) || (r = dalloc(b.winv, 2 * n))) return r;
+        dfree(b.wnew); dfree(b.winv); dfree(b.wcov);
+        if ((r = dalloc(b.wnew, 2 * n + 64)) || (r = dalloc(b.winv, 2 * n)) || (r = dalloc(b.wcov, 2 * n))) return r;
         if ((r = dalloc(b.write_txn, n + 32)) ||  // +32: read as 32-entry words by k_decide_rounds
              (r = dalloc(b.rec_w0, 2 * n)) || (r = dalloc(b.sw_slot, 2 * n)) ||
             (r = dalloc(b.cb_pos, n)) || (r = dalloc(b.ce_pos, n)) || (r = dalloc(b.comb_blk, 2 * (n / 2048 + 2))) ||
@@ -560,11 +560,11 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         b.list_cap = n;
     }
     if (!b.ss_cnt) {
-        if ((r = dalloc(b.ss_cnt, 2 * 2 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)) ||
+        if ((r = dalloc(b.ss_cnt, 2 * 3 * 1024)) || (r = dalloc(b.ss_q, 2 * 1024)) ||
             (r = dalloc(b.ss_qt, 2 * 1024 * SS_QT)) || (r = dalloc(b.ss_gsamp, 2 * 3 * 4096)))
             return r;
         HIPOK(hipMemsetAsync(b.ss_qt, 0, 2 * 1024 * SS_QT, s));
-        HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 2 * 1024 * sizeof(int32_t), s));
+        HIPOK(hipMemsetAsync(b.ss_cnt, 0, 2 * 3 * 1024 * sizeof(int32_t), s));  // (kernels_batch.hip SS_CNT per parity)
         HIPOK(hipMemsetAsync(b.ss_q, 0, 2 * 1024 * sizeof(SRec), s));  // equal records: valid (sorted) splitters
     }
     if (!b.lb_meta && (r = dalloc(b.lb_meta, lb_meta_words()))) return r;
@@ -888,7 +888,12 @@ int lm_arm(fdbcs* cs, uint64_t n_ranges, uint64_t key_bytes, LmArgs& la) {
         if (p) hipHostFree(p);
         p = nullptr;
         cap = 0;
-        if (hipHostMalloc((void**)&p, c * elem, hipHostMallocDefault) != hipSuccess) return (int)FDBCS_E_NOMEM;
+        // (coherent: the ingest's blocks on every XCD store here and the host
+        // reads right after the verdict flag; from default pinned memory the
+        // stores of XCDs other than the deciding one's could still sit in
+        // their L2 -- a sampled key then read as zeros)
+        if (hipHostMalloc((void**)&p, c * elem, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return (int)FDBCS_E_NOMEM;
         cap = c;
         return (int)FDBCS_OK;
     };
@@ -926,13 +931,12 @@ void live_begin(fdbcs* cs) {
     c.R = (int32_t)up(cs->lv_prev_R);
     c.W = (int32_t)up(cs->lv_prev_W);
     c.key_bytes = cs->lv_prev_K + cs->lv_prev_K / 4 + 65536;
-    c.nb0 = 0;  // (launch_live_ingest: from c.R)
     if (large_batch_mode(c.T) || large_batch_mode(cs->lv_prev_T)) return;
     // the batch buffers at their final size before the kernel writes them (the
     // detect's ensure_batch must not move them): keys and the stream's bytes
     const uint64_t kb = c.key_bytes + 32 * (uint64_t)c.T + 8 * ((uint64_t)c.R + c.W) + 64;
     BatchBufs& b = cs->b;
-    if (ensure_batch(cs, c.T, c.R, c.W, kb)) return;
+    if (ensure_batch(cs, c.T, c.R, c.W, kb) || !b.rounds) return;  // (the live kernel leaves the reads unsorted)
     if (2 * (int64_t)c.W > b.lv_wcap) {
         const int64_t n = std::max<int64_t>(2 * (int64_t)c.W, 4096);
         free_keys(b.lv_wkeys);

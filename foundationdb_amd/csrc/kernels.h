@@ -118,7 +118,6 @@ struct StagedBatch {
 struct LiveCaps {
     int32_t T, R, W;
     uint64_t key_bytes;
-    int32_t nb0;  // buckets of the read-begin sort (the live kernel scatters into them)
 };
 
 struct BatchBufs {
@@ -148,7 +147,8 @@ struct BatchBufs {
     SRec* sw;            // sorted write endpoints
     uint32_t* sw_slot;   // [2W]  their slots (compact copy for the combine)
     // sample sort scratch
-    int32_t* ss_cnt;     // [2 parities][2 * 1024] bucket counts; a batch zeroes the next batch's
+    int32_t* ss_cnt;     // [2 parities][3 * 1024] bucket counts of both jobs, then job 1's cover deltas;
+                         // a batch zeroes the next batch's
     SRec* ss_q;          // [2 * 1024] quantiles of the previous batch's sorted output
     uint8_t* ss_qt;      // [2 * 1024 * SS_QT] their tail bytes (the batch keys they came from are gone)
     int32_t* ss_bkt;     // [R + 2W] bucket of each record
@@ -162,10 +162,8 @@ struct BatchBufs {
                          // small directory, engine.hip edges_read_check)
     bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
     bool rc_fused;       // this batch's history read check ran in the sort's bucket launch
-    // live ingest: the read-begin sort's bucket count the live kernel used
-    // (0: none; make_sort_jobs keeps it), and the write endpoints by 2w until
-    // k_live_finish places them at 2R + 2w
-    int32_t lv_nb0;
+    // live ingest: the write endpoints by 2w until k_live_finish places them
+    // at 2R + 2w
     KeyArrays lv_wkeys;
     uint64_t* lv_wkoff;
     uint32_t* lv_wklen;
@@ -175,6 +173,7 @@ struct BatchBufs {
     int32_t* plist;      // [R + W] candidate reads: some write of the batch may overlap them (duplicates)
     uint8_t* wnew;       // [2W + 64] sorted write endpoint p starts a new distinct key
     int32_t* winv;       // [2W] sorted position of each write endpoint (by slot - 2R)
+    int32_t* wcov;       // [2W] write cover: begins minus ends among the sorted write endpoints up to each
     uint2* items;        // [R + W] the rounds' writes and reads when they do not fit in LDS
     int64_t list_cap;    // entries of plist (items: 2 * list_cap)
     bool ws_deferred;    // this batch's write searches wait for launch_write_search

@@ -115,7 +115,9 @@ __device__ inline void lm_append(const LmArgs& L, Scalars* sc, int64_t amt, cons
     uint4* e = reinterpret_cast<uint4*>(L.ent + i);
     e[0] = make_uint4((uint32_t)amt, (uint32_t)((uint64_t)amt >> 32), (uint32_t)pos, len);
     e[1] = make_uint4((uint32_t)o, (uint32_t)(o >> 32), 0, 0);
-    if (o + padded > L.cap_b) return;
+    // (the empty key claims no bytes: its offset is the next key's, whose
+    // bytes a store here would zero)
+    if (padded == 0 || o + padded > L.cap_b) return;
     uint64_t* d = reinterpret_cast<uint64_t*>(L.bytes + o);
     const uint64_t w0 = __builtin_bswap64(k.hi), w1 = __builtin_bswap64(k.lo);
     *reinterpret_cast<uint4*>(d) = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
@@ -268,6 +270,7 @@ static constexpr int SS_MAXB = 1024;     // buckets per job (power of two)
 static constexpr int SS_Q = 1024;        // quantile records kept per job
 static constexpr int SS_WAVE = 128;      // bucket size sorted in registers
 static constexpr int SS_ROW = 512;       // staging row per bucket (LDS path)
+static constexpr int SS_CNT = 3 * SS_MAXB;  // counter words per parity: counts of both jobs, job 1's cover deltas
 
 // Total order on sort records: key, then END (odd slot) before BEGIN, then
 // slot.  Branch-free on the fixed-width part; the tails are consulted only
@@ -317,8 +320,10 @@ struct SortJobs {
     uint32_t* out_slot;    // [n1] slots of job 1's sorted records (compact copy)
     SRec* quant;           // [2][SS_Q] quantiles (persist across batches)
     uint8_t* qtail;        // [2][SS_Q][SS_QT] their first SS_QT tail bytes
-    int32_t* cnt;          // [2][SS_MAXB] this batch's bucket counts
-    int32_t* cnt_next;     // [2][SS_MAXB] the next batch's (zeroed here)
+    int32_t* cnt;          // [SS_CNT] this batch's bucket counts: [2][SS_MAXB], then job 1's cover deltas
+    int32_t* cnt_next;     // [SS_CNT] the next batch's (zeroed here)
+    int32_t* dcnt;         // [SS_MAXB] = cnt + 2 SS_MAXB: per bucket of job 1, write begins minus write ends
+    int32_t* wcov;         // [2W] or null: per sorted write endpoint, the begins minus ends at or before it
     int32_t* bkt;          // [n0 + n1] bucket of each record
     SRec* tmp;             // [2][SS_MAXB][SS_ROW] staging rows
     Scalars* sc;
@@ -469,6 +474,7 @@ __device__ int sample_quantiles(const SortJobs& J, int job, const KeyArrays& key
 // record i of a job goes to bucket b: count, bucket id, staging row
 __device__ inline void place_rec(const SortJobs& J, int job, int i, int b, const SRec& x) {
     const int slot = atomicAdd(&J.cnt[job * SS_MAXB + b], 1);
+    if (job && J.wcov) atomicAdd(&J.dcnt[b], (x.idx & 1) ? -1 : 1);  // (the write cover: a begin opens, an end closes)
     J.bkt[(job ? J.n[0] : 0) + i] = b;
     if (slot < SS_ROW) J.tmp[((int64_t)job * SS_MAXB + b) * SS_ROW + slot] = x;
     else if (slot == SS_ROW) J.sc->ss_over[job] = 1;  // the bucket kernel would rank it from global memory
@@ -488,7 +494,10 @@ __device__ void ss_sample_job(const SortJobs& J, const KeyArrays& keys, const Ld
     const int ns = sample_quantiles(J, job, keys, L);
     if (!guard) return;
     const int nb = J.nb[job], step = SS_Q / nb;
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) J.cnt[job * SS_MAXB + b] = 0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        J.cnt[job * SS_MAXB + b] = 0;
+        if (job) J.dcnt[b] = 0;
+    }
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) J.sc->ss_resample = 1;  // (stats: the batch was bucketed twice)
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, Sor
     if constexpr (SCATTER) {
         const uint8_t* const* tails = A.keys.tail;
         if (i < A.R) {
-            scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
+            if (J.nb[0]) scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
         } else {
             const int w = (int)(i - A.R);
             scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
@@ -748,6 +757,7 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
         }
+        if (lane == 0) PMAX(A.sc, 22);
     }
     if (ht) {
         const StageTxn h = (to & STAGE_EMPTY) ? stage_txn(S.stream, to) : stage_txn(X.at(to, sizeof(StageHdr)) - to, to);
@@ -827,7 +837,7 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         A.keys.put(2 * i + 1, en);
         if constexpr (SCATTER) {
             if (w < 0) {
-                scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp0);
+                if (J.nb[0]) scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp0);
             } else {
                 scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp1);
                 scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(2 * i + 1), 0}, tails, sp1);
@@ -879,14 +889,17 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
 // = LV_TIMEOUT, and k_live_finish then fails the batch).
 struct LiveArgs {
     IngestArgs A;      // T, R: the live capacities (the real counts come with the final word)
-    SortJobs J;        // job 0: the read begins' buckets (nb[0] = caps.nb0)
+    SortJobs J;        // job 1's splitters (rounds mode: the read begins are not sorted)
     StagedBatch S;     // stream, toff: host-mapped; view: the batch view's arrays (capacity layout)
     LiveOut O;
     const uint64_t* prog;  // host-mapped: [0] published T, [2] state, [3..5] final T, R, W (stage.h)
     uint64_t timeout;      // wall_clock64 ticks (100 MHz)
     uint32_t gen;          // this live batch's generation (tags lv_pub / lv_state)
 };
-constexpr int LIVE_BLOCKS = 64;  // (255 worker waves: ~5 us a group, ~3 groups arrive per us)
+#ifndef FDBCS_LIVE_BLOCKS
+#define FDBCS_LIVE_BLOCKS 64  // (255 worker waves: ~5 us a group, ~3 groups arrive per us)
+#endif
+constexpr int LIVE_BLOCKS = FDBCS_LIVE_BLOCKS;
 constexpr uint64_t LIVE_TIMEOUT_TICKS = 8ull * 100000000ull;  // 8 s of the 100 MHz wall clock
 
 // Polling (MI355X_MICROARCH.md, inter-workgroup visibility): relaxed
@@ -994,9 +1007,15 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
         const uint64_t used_u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)used) |
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(used >> 32)) << 32);
         O.stream_cap = min(O.stream_cap, used_u + 15);
+        if (lane == 0) PMAX(sc, 20);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (ONE per group: see above)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) PMAX(sc, 21);
         staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp0, sp0, win[wv]);
+        if (lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            PMAX(sc, 23);
+        }
     }
 }
 
@@ -1045,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_live_finish(IngestArgs A, SortJobs J, S
 // a failed live batch: its sort counters (this parity), load-metrics entries,
 // tails and flags back to a batch's start
 __global__ void k_live_reset(int32_t* cnt, Scalars* sc) {
-    for (int k = threadIdx.x; k < 2 * SS_MAXB; k += blockDim.x) cnt[k] = 0;
+    for (int k = threadIdx.x; k < SS_CNT; k += blockDim.x) cnt[k] = 0;
     if (threadIdx.x == 0) {
         sc->ss_over[0] = sc->ss_over[1] = 0;
         sc->lm_count = 0;
@@ -1076,7 +1095,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
     const int32_t* cnt = J.cnt + job * SS_MAXB;
     const uint8_t* const* tails = keys.tail;
     const int64_t c0 = PCLK();
-    for (int k = bid * 64 + lane; k < 2 * SS_MAXB; k += nbk * 64) J.cnt_next[k] = 0;
+    for (int k = bid * 64 + lane; k < SS_CNT; k += nbk * 64) J.cnt_next[k] = 0;
     // offset = counts of the earlier buckets: lane L sums counts [16L, 16L+16)
     // below b with four independent 16-byte loads (one round trip)
     int part = 0;
@@ -1093,6 +1112,21 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
     const int c = cnt[b];
     const int64_t c1 = PCLK();
     if (c == 0) return;
+    // the write cover before this bucket: the cover deltas of the earlier buckets
+    const bool cover = job && J.wcov;
+    int doff = 0;
+    if (cover) {
+        const int4* d4 = reinterpret_cast<const int4*>(J.dcnt) + 4 * lane;
+        int dp = 0;
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int4 x = d4[v];
+            const int k0 = 16 * lane + 4 * v;
+            dp += (k0 < b ? x.x : 0) + (k0 + 1 < b ? x.y : 0) + (k0 + 2 < b ? x.z : 0) + (k0 + 3 < b ? x.w : 0);
+        }
+        doff = wave_reduce_sum(dp);
+    }
+    auto delta = [](uint32_t idx) { return (idx & 1) ? -1 : 1; };  // (a write begin opens, an end closes)
     SRec* out = J.out[job] + offset;
     const SRec* row = J.tmp + ((int64_t)job * SS_MAXB + b) * SS_ROW;
     if (c <= SS_WAVE) {
@@ -1113,7 +1147,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
         const int64_t c2 = PCLK();
         const int64_t c2b = c2;
         __syncthreads();
-        int rank[2] = {0, 0};
+        int rank[2] = {0, 0}, dsum[2] = {0, 0};
         for (int j0 = 0; j0 < c; j0 += 8) {  // eight records per round: their LDS reads overlap
             SRec y[8];
 #pragma unroll
@@ -1125,7 +1159,11 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
             for (int u = 0; u < 8; u++)
                 if (j0 + u < c)
 #pragma unroll
-                    for (int q = 0; q < 2; q++) rank[q] += (lane + 64 * q < c) && rec_lt(y[u], x[q], tails);
+                    for (int q = 0; q < 2; q++) {
+                        const bool lt = (lane + 64 * q < c) && rec_lt(y[u], x[q], tails);
+                        rank[q] += lt;
+                        dsum[q] += lt ? delta(y[u].idx) : 0;
+                    }
         }
         const int64_t c3 = PCLK();
 #pragma unroll
@@ -1133,6 +1171,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
             if (lane + 64 * q < c) {
                 out[rank[q]] = x[q];
                 if (job) J.out_slot[offset + rank[q]] = x[q].idx;
+                if (cover) J.wcov[offset + rank[q]] = doff + dsum[q] + delta(x[q].idx);
                 emit_quantiles(J, job, (int64_t)offset + rank[q], x[q], tails);
             }
         }
@@ -1153,8 +1192,17 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
         for (int k = lane; k < P; k += 64) L.put(k, k < c ? row[k] : rec_inf());
         __syncthreads();
         lds_bitonic(L, P, tails);
-        for (int k = lane; k < c; k += 64) {
-            const SRec x = L.get(k);
+        int run = doff;
+        for (int k0 = 0; k0 < c; k0 += 64) {
+            const int k = k0 + lane;
+            SRec x{};
+            if (k < c) x = L.get(k);
+            if (cover) {  // (every lane: the scan)
+                const int inc = wave_incl_scan(k < c ? delta(x.idx) : 0);
+                if (k < c) J.wcov[offset + k] = run + inc;
+                run += __builtin_amdgcn_readlane(inc, 63);
+            }
+            if (k >= c) continue;
             out[k] = x;
             if (job) J.out_slot[offset + k] = x.idx;
             emit_quantiles(J, job, (int64_t)offset + k, x, tails);
@@ -1167,13 +1215,17 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
     for (int i = lane; i < n; i += 64) {
         if (bkt[i] != b) continue;
         const SRec x = load_rec(keys, J.sbase[job] + (int64_t)i * J.sstride[job]);
-        int rank = 0;
+        int rank = 0, dsum = 0;
         for (int j = 0; j < n; j++) {
             if (bkt[j] != b) continue;
-            rank += rec_lt(load_rec(keys, J.sbase[job] + (int64_t)j * J.sstride[job]), x, tails);
+            const SRec y = load_rec(keys, J.sbase[job] + (int64_t)j * J.sstride[job]);
+            const bool lt = rec_lt(y, x, tails);
+            rank += lt;
+            dsum += lt ? delta(y.idx) : 0;
         }
         out[rank] = x;
         if (job) J.out_slot[offset + rank] = x.idx;
+        if (cover) J.wcov[offset + rank] = doff + dsum + delta(x.idx);
         emit_quantiles(J, job, (int64_t)offset + rank, x, tails);
     }
 }
@@ -1376,7 +1428,7 @@ __global__ __launch_bounds__(256) void k_ms_finish(MergeSortArgs M, SortJobs J, 
         const int64_t n = M.n[job];
         if (n > 0) put_quantile(J, job, q, M.buf[job][0][q * n / SS_Q], keys.tail);
     }
-    if (g < 2 * SS_MAXB) J.cnt_next[g] = 0;  // (this path leaves the current parity's counters zero)
+    if (g < SS_CNT) J.cnt_next[g] = 0;  // (this path leaves the current parity's counters zero)
 }
 
 // Bucketed large-batch sort (steady state: splitters from the previous batch's
@@ -1584,7 +1636,7 @@ static bool launch_bucket_sort(const SortJobs& J, BatchBufs& b, hipStream_t s) {
         M.n[j] = J.n[j];
         M.buf[j][0] = J.out[j];
     }
-    const int64_t fin = std::max<int64_t>(std::max(M.n[1], 2 * SS_MAXB), 2 * SS_Q);
+    const int64_t fin = std::max<int64_t>(std::max<int64_t>(M.n[1], SS_CNT), 2 * SS_Q);
     hipLaunchKernelGGL(k_ms_finish, dim3(cdiv(fin, 256)), dim3(256), 0, s, M, J, b.keys);
     return true;
 }
@@ -1615,7 +1667,7 @@ static void launch_merge_sort(const SortJobs& J, BatchBufs& b, hipStream_t s) {
         const int blocks = Mp.blocks0 + cdiv(Mp.n[1], MS_CHUNK);
         hipLaunchKernelGGL(k_ms_merge, dim3(blocks), dim3(MS_THREADS), 0, s, Mp, p, b.keys);
     }
-    const int64_t fin = std::max<int64_t>(std::max(M.n[1], 2 * SS_MAXB), 2 * SS_Q);
+    const int64_t fin = std::max<int64_t>(std::max<int64_t>(M.n[1], SS_CNT), 2 * SS_Q);
     hipLaunchKernelGGL(k_ms_finish, dim3(cdiv(fin, 256)), dim3(256), 0, s, M, J, b.keys);
 }
 
@@ -1654,13 +1706,22 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
     J.out_slot = b.sw_slot;
     J.quant = b.ss_q;
     J.qtail = b.ss_qt;
-    J.cnt = b.ss_cnt + parity * 2 * SS_MAXB;
-    J.cnt_next = b.ss_cnt + (parity ^ 1) * 2 * SS_MAXB;
+    J.cnt = b.ss_cnt + parity * SS_CNT;
+    J.cnt_next = b.ss_cnt + (parity ^ 1) * SS_CNT;
+    J.dcnt = J.cnt + 2 * SS_MAXB;
+    J.wcov = nullptr;
     J.bkt = b.ss_bkt;
     J.tmp = b.ss_tmp;
     J.sc = sc;
+    if (b.rounds && !b.large) {
+        // rounds mode: the read begins are not sorted -- the decision needs per
+        // read only its place among the sorted write endpoints, and whether
+        // some write covers its begin (the write cover, wcov), not the reads'
+        // own order (DESIGN.md §4 "Write cover")
+        J.n[0] = 0;
+        J.wcov = b.wcov;
+    }
     for (int j = 0; j < 2; j++) J.nb[j] = ss_buckets(J.n[j]);
-    if (b.lv_nb0 > 0) J.nb[0] = b.lv_nb0;  // (the live ingest scattered the read begins into that many)
     J.blocks0 = cdiv(J.n[0], 256);
     return J;
 }
@@ -1755,7 +1816,6 @@ void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t
     A.write_txn = b.write_txn;
     A.keys = b.keys; A.btail = b.btail; A.btail_cap = b.btail_cap; A.sc = sc; A.deg = b.deg;
     A.lm = lm ? *lm : LmArgs{};
-    b.lv_nb0 = caps.nb0 > 0 ? caps.nb0 : ss_buckets(caps.R);  // (make_sort_jobs keeps it until this batch's sort)
     fdbcs_batch_view vc{};
     vc.read_count = caps.R;
     vc.write_count = caps.W;
@@ -1782,13 +1842,12 @@ void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, in
 }
 
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {
-    hipLaunchKernelGGL(k_live_reset, dim3(1), dim3(256), 0, s, b.ss_cnt + parity * 2 * SS_MAXB, sc);
+    hipLaunchKernelGGL(k_live_reset, dim3(1), dim3(256), 0, s, b.ss_cnt + parity * SS_CNT, sc);
 }
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
                         bool scattered, hipStream_t s, HistBufs* h, int cur, int64_t v0) {
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
-    b.lv_nb0 = 0;  // (a live batch's read-begin bucket count, kept by the jobs above)
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
     b.rc_fused = false;
@@ -1933,6 +1992,7 @@ struct EdgesArgs {
     int32_t* plist;  // candidate reads (appended at sc->n_pot; duplicates allowed)
     int64_t plist_cap;
     int32_t* winv;   // [2W] sorted position of each write endpoint
+    const int32_t* wcov;  // [2W] write cover at each sorted write endpoint (rounds mode)
     uint32_t* rstamp;  // [R] batch stamp of reads already on plist
     uint32_t rseq;     // this batch's stamp
 };
@@ -1999,18 +2059,19 @@ __device__ inline bool rec_key_eq(const SRec& a, const SRec& b, const uint8_t* c
     return key_len(a.meta) <= 17 || tail_cmp(tails[a.idx], key_len(a.meta), tails[b.idx], key_len(b.meta)) == 0;
 }
 
-// rounds mode, three kinds of lanes:
+// rounds mode, two kinds of lanes:
 //   i < R        read i: pb = sorted write endpoints with key <= its begin (at
 //                an equal key both write endpoint types sort before a read
 //                begin, SkipList.cpp:169-172), pe = those with key < its end
 //                (a read end sorts first); a candidate if some write endpoint
 //                has a key in [begin, end) -- every overlap where the write
-//                begins at or after the read does
+//                begins at or after the read does -- or if some write covers
+//                its begin: the write cover (begins minus ends among the
+//                first pb endpoints) counts exactly the writes [wb, we) with
+//                wb <= begin < we -- the overlaps where the read begins inside
+//                the write.  (The reads need no order of their own: before the
+//                cover, a lane per write searched the sorted read begins.)
 //   R + p        sorted write endpoint p starts a new distinct key
-//   R + 2W + w   write w: the reads beginning strictly inside it (the other
-//                overlaps) become candidates; past RP_MARK of them, every
-//                read is one (dec_wide)
-constexpr int RP_MARK = 64;
 
 __device__ inline void candidate(const EdgesArgs& A, int r) {
     // once per read and batch (a read inside many writes is marked by each;
@@ -2022,8 +2083,8 @@ __device__ inline void candidate(const EdgesArgs& A, int r) {
     else A.sc->dec_wide = 1;  // (overflow: every read is a candidate)
 }
 
-__device__ inline void rounds_lane(const EdgesArgs& A, int i, const uint64_t* smp_r, const uint64_t* smp_w) {
-    const int R = A.R, W = A.W, P = 2 * A.W;
+__device__ inline void rounds_lane(const EdgesArgs& A, int i, const uint64_t* smp_w) {
+    const int R = A.R, P = 2 * A.W;
     const uint8_t* const* tails = A.keys.tail;
     if (i < R) {
         if (A.too_old[A.read_txn[i]]) return;  // (not decided by the rounds)
@@ -2034,26 +2095,12 @@ __device__ inline void rounds_lane(const EdgesArgs& A, int i, const uint64_t* sm
         bsearch2(A.sw, b, true, lb, hb, e, le, he, tails, pb, pe);
         A.rq[2 * i] = pb;
         A.rq[2 * i + 1] = pe;
-        if (pe > pb || (pb > 0 && rec_vs_key(A.sw[pb - 1], b, tails) == 0)) candidate(A, i);
+        if (pe > pb || (pb > 0 && (A.wcov[pb - 1] > 0 || rec_vs_key(A.sw[pb - 1], b, tails) == 0))) candidate(A, i);
     } else if (i < R + P) {
         const int p = i - R;
         const SRec x = A.sw[p];
         A.wnew[p] = p == 0 || !rec_key_eq(A.sw[p - 1], x, tails);
         A.winv[x.idx - 2 * (int64_t)R] = p;
-    } else if (i < R + P + W) {
-        const int w = i - R - P;
-        if (A.too_old[A.write_txn[w]] || R == 0) return;
-        const int64_t s = 2 * (int64_t)R + 2 * (int64_t)w;
-        const Key b = A.keys.get(s), e = A.keys.get(s + 1);
-        int lb, hb, le, he, k0, k1;
-        sample_narrow(smp_r, R, b.hi, lb, hb);
-        sample_narrow(smp_r, R, e.hi, le, he);
-        bsearch2(A.sr, b, true, lb, hb, e, le, he, tails, k0, k1);  // read begins in (b, e)
-        if (k1 - k0 > RP_MARK) {
-            A.sc->dec_wide = 1;
-        } else {
-            for (int k = k0; k < k1; k++) candidate(A, A.sr[k].idx >> 1);
-        }
     }
 }
 
@@ -2062,7 +2109,7 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
     const int64_t wbase = 2 * (int64_t)R;
     const uint8_t* const* tails = A.keys.tail;
     if (A.rq) {
-        rounds_lane(A, i, smp_r, smp_w);
+        rounds_lane(A, i, smp_w);
         return;
     }
     if (i < R) {
@@ -2111,7 +2158,7 @@ __global__ __launch_bounds__(256) void k_edges_read_check(ReadCheckArgs RA, int 
     } else {
         const int i0 = (blockIdx.x - rc_blocks - ws_blocks) * blockDim.x;
         if (i0 < EA.R) sample_fill(smp_w, EA.sw, 2 * EA.W);          // readers search the writes
-        if (i0 + (int)blockDim.x > EA.R) sample_fill(smp_r, EA.sr, EA.R);  // writers search the reads
+        if (!EA.rq && i0 + (int)blockDim.x > EA.R) sample_fill(smp_r, EA.sr, EA.R);  // writers search the reads
         __syncthreads();
         edges_lane(EA, i0 + threadIdx.x, smp_r, smp_w);
     }
@@ -2335,7 +2382,8 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const int32_t* qx = dj ? b.ss_bkt : nullptr;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
     EdgesArgs EA{R,     W,    b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv, b.rstamp, b.rseq};
+                 b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv,
+                 b.wcov, b.rstamp, b.rseq};
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
     // (rc_fused: the history read check already ran in the sort's bucket launch)
     const int rc_blocks = b.rc_fused ? 0 : cdiv((int64_t)R * RC_G, 256);
@@ -2344,7 +2392,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const int ws_blocks = b.ws_deferred ? 0 : cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
-    const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 3 * W : W), 256) : 0;
+    const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 2 * W : W), 256) : 0;
     const bool wide = FDBCS_RC_WIDE;  // (WIDE = false: the two-level range maximum, kept for A/B)
     if (rc_blocks + ws_blocks + e_blocks > 0) {
         if (wide)

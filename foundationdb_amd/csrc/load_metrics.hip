@@ -578,7 +578,9 @@ int fdbcs_sample_add_batch(fdbcs_sample* s, fdbcs* cs, const fdbcs_batch_view* d
                 s->pending.push_back({expiration, std::vector<fdbcs_dev::LmEntry>(tk.ent, tk.ent + m),
                                       std::vector<uint8_t>(tk.bytes, tk.bytes + nb)});
                 s->seq++;
-                if (s->pending.size() > 64) drain(s);  // (a caller that never polls: bounded)
+                // (a caller that never polls or queries: bounded, ~10 MB at config 2; the
+                // Resolver's metrics requests and polls drain it off the commit path)
+                if (s->pending.size() > 1024) drain(s);
                 if (out_sampled) *out_sampled = (int64_t)m;
                 return FDBCS_OK;
             }
