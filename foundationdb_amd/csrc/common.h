@@ -291,14 +291,25 @@ struct Scalars {
     // the kernel's poller mirrors it, and the batch's final shape
     // (tagged with the live batch's generation, so nothing needs resetting
     // between batches: a word of an earlier batch reads as "nothing yet")
-    uint64_t lv_pub;        // gen << 32 | transactions published so far
-    uint32_t lv_state;      // gen << 2 | LV_*: final (lv_T/R/W set), cancelled, timed out
-    int32_t lv_T, lv_R, lv_W;
+    // the live kernel's mirror of the host's progress, one word the workers
+    // read in one load: lv_word(gen, state, transactions, stream bytes written whole)
+    uint64_t lv_pub;
+    int32_t lv_R, lv_W;     // the final read / write counts (k_live_finish checks them)
     int32_t lv_err;         // a transaction past the live capacities (the host falls back)
-    uint64_t lv_used;       // stream bytes the host has written whole (>= the published transactions' records)
+    int32_t lv_pad;
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;
+// gen: 10 bits (another batch's word reads as "nothing yet"), state: 2,
+// transactions: 20 (live batches have T <= LARGE_T), bytes: 32 (the live
+// stream stays below 4 GB)
+__host__ __device__ inline uint64_t lv_word(uint32_t gen, int state, uint64_t T, uint64_t used) {
+    return (uint64_t)(gen & 0x3FF) << 54 | (uint64_t)(state & 3) << 52 | (T & 0xFFFFF) << 32 | (used & 0xFFFFFFFFull);
+}
+__host__ __device__ inline uint32_t lv_gen(uint64_t w) { return (uint32_t)(w >> 54); }
+__host__ __device__ inline int lv_state(uint64_t w) { return (int)((w >> 52) & 3); }
+__host__ __device__ inline int32_t lv_txns(uint64_t w) { return (int32_t)((w >> 32) & 0xFFFFF); }
+__host__ __device__ inline uint64_t lv_used(uint64_t w) { return w & 0xFFFFFFFFull; }
 
 // ---- Resolver load metrics (load_metrics.hip; Resolver.actor.cpp:146-151) ----
 // The draw of position `pos` of batch `seq` of a sample (counter-based, every

@@ -702,6 +702,7 @@ struct LiveOut {
     // the live kernel the bytes the host has written whole, rounded up to 16
     // (reading lines the host is still appending to made its adds stall)
     uint64_t stream_cap;
+    bool spec;  // read the window [stream_cap - LIVE_WIN, stream_cap) together with the offsets
 };
 
 // LIVE: a wavefront's records come over PCIe into an LDS window first -- its
@@ -717,7 +718,12 @@ struct LiveWin {
     const uint8_t* host;
     __device__ const uint8_t* at(uint64_t off, uint64_t len) const {
         // (+8: encode_key reads the aligned words around a key)
-        return off >= lo && off + len + 8 <= hi ? win + (off - lo) : host + off;
+        if (off >= lo && off + len + 8 <= hi) return win + (off - lo);
+        // past the window: plain loads of the stream itself, which this CU's
+        // L1 may hold from before the host wrote it -- drop it first (rare:
+        // a group larger than the window)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        return host + off;
     }
 };
 
@@ -735,9 +741,35 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
     const int t = t0 + lane;
     const bool ht = lane < nt;
     int n = 0;
-    const uint64_t to = ht ? S.toff[t] : STAGE_EMPTY;
+    // (LIVE: non-temporal loads of the host-mapped offsets and records skip
+    // this CU's L1, which may hold lines from before the host wrote them)
+    const uint64_t to = ht ? (LIVE ? __builtin_nontemporal_load(S.toff + t) : S.toff[t]) : STAGE_EMPTY;
     LiveWin X{win, 0, 0, S.stream};
     if constexpr (LIVE) {  // the group's records into the LDS window (16-byte aligned, coalesced)
+        // each lane's 16-byte pieces are loaded before any is stored, so the
+        // window is one round trip; speculative: the stream's last LIVE_WIN
+        // bytes, loaded while the offsets are still in flight (a group among
+        // the last published ones lies there)
+        constexpr int WPL = LIVE_WIN / 16 / 64;
+        const uint64_t shi = O.stream_cap & ~uint64_t(15);
+        const uint64_t slo = shi > (uint64_t)LIVE_WIN ? shi - LIVE_WIN : 0;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v[WPL];
+        auto load_win = [&](uint64_t lo, uint64_t hi) {
+            const u32x4* src = reinterpret_cast<const u32x4*>(S.stream + lo);
+            const int n16 = (int)((hi - lo) >> 4);
+#pragma unroll
+            for (int u = 0; u < WPL; u++)
+                if (lane + 64 * u < n16) v[u] = __builtin_nontemporal_load(src + lane + 64 * u);
+        };
+        auto store_win = [&](uint64_t lo, uint64_t hi) {
+            u32x4* dst = reinterpret_cast<u32x4*>(win);
+            const int n16 = (int)((hi - lo) >> 4);
+#pragma unroll
+            for (int u = 0; u < WPL; u++)
+                if (lane + 64 * u < n16) dst[lane + 64 * u] = v[u];
+        };
+        if (O.spec) load_win(slo, shi);
         uint64_t first = ~0ull;
         for (int q = 0; q < nt; q++) {
             const uint64_t o = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)to, q) |
@@ -748,12 +780,15 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
             }
         }
         if (first != ~0ull) {
-            X.lo = first & ~uint64_t(15);
-            X.hi = min(X.lo + (uint64_t)LIVE_WIN, O.stream_cap & ~uint64_t(15));
-            const int n16 = (int)((X.hi - X.lo) >> 4);
-            const uint4* src = reinterpret_cast<const uint4*>(S.stream + X.lo);
-            uint4* dst = reinterpret_cast<uint4*>(win);
-            for (int k = lane; k < n16; k += 64) dst[k] = src[k];
+            if (O.spec && first >= slo) {  // (the speculative window holds the group)
+                X.lo = slo;
+                X.hi = shi;
+            } else {
+                X.lo = first & ~uint64_t(15);
+                X.hi = min(X.lo + (uint64_t)LIVE_WIN, shi);
+                load_win(X.lo, X.hi);
+            }
+            store_win(X.lo, X.hi);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
         }
@@ -881,12 +916,13 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
 // has published it, reading the records straight from the host-mapped
 // stream, so that by detectConflicts only the last groups remain.
 //   block 0, wave 0: the poller -- reads the host's progress words (one PCIe
-//                    read per ~1 us) and mirrors them to Scalars::lv_pub /
-//                    lv_state, which the other waves poll in device memory;
+//                    read per ~1 us) and mirrors them to Scalars::lv_pub (one
+//                    word, common.h lv_word), which the other waves poll in
+//                    device memory;
 //   other waves:     group g = wave, wave + waves, ... once published.
 // Every wave leaves when the host's final word says its groups are past the
-// batch, when the host cancels, or after LIVE_TIMEOUT (the poller: lv_state
-// = LV_TIMEOUT, and k_live_finish then fails the batch).
+// batch, when the host cancels, or after LIVE_TIMEOUT (the poller's word
+// says LV_TIMEOUT, and k_live_finish then fails the batch).
 struct LiveArgs {
     IngestArgs A;      // T, R: the live capacities (the real counts come with the final word)
     SortJobs J;        // job 1's splitters (rounds mode: the read begins are not sorted)
@@ -894,21 +930,23 @@ struct LiveArgs {
     LiveOut O;
     const uint64_t* prog;  // host-mapped: [0] published T, [2] state, [3..5] final T, R, W (stage.h)
     uint64_t timeout;      // wall_clock64 ticks (100 MHz)
-    uint32_t gen;          // this live batch's generation (tags lv_pub / lv_state)
+    uint32_t gen;          // this live batch's generation (tags lv_pub)
 };
 #ifndef FDBCS_LIVE_BLOCKS
-#define FDBCS_LIVE_BLOCKS 64  // (255 worker waves: ~5 us a group, ~3 groups arrive per us)
+#define FDBCS_LIVE_BLOCKS 128  // (511 worker waves; 64: 1-2 us slower per window, 32: 12 us)
 #endif
 constexpr int LIVE_BLOCKS = FDBCS_LIVE_BLOCKS;
 constexpr uint64_t LIVE_TIMEOUT_TICKS = 8ull * 100000000ull;  // 8 s of the 100 MHz wall clock
 
 // Polling (MI355X_MICROARCH.md, inter-workgroup visibility): relaxed
 // agent-scope loads and stores (sc1: past this CU's L1) for the mirrored
-// words, relaxed system-scope loads of the host's; ONE agent acquire per
-// group a wave takes (its L1 may hold host lines an earlier window read
-// before the host wrote them).  Acquire loads in the poll loops (an L1
-// invalidate per poll in up to 511 waves) held the kernel ~45 us behind the
-// adds at config 2.
+// word, relaxed system-scope loads of the host's; the group's offsets and
+// records by non-temporal loads, which skip the L1 (it may hold host lines an
+// earlier window read before the host wrote them), and an agent acquire only
+// before a plain load of the stream past the window.  Acquire loads in the
+// poll loops (an L1 invalidate per poll in up to 511 waves) held the kernel
+// ~45 us behind the adds at config 2; an acquire per group cost 0.8-2.4 us on
+// the last group.
 template <class T>
 __device__ inline T lv_load(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -938,7 +976,7 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
             __syncthreads();  // (bmax2_block's LDS is reused by the next word)
         }
     }
-    const uint32_t gen = V.gen;
+    const uint32_t gen = V.gen & 0x3FF;
     if (wid == 0) {  // the poller
         if (lane == 0) {
             const uint64_t t_start = wall_clock64();
@@ -951,26 +989,24 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                 const uint64_t used = host_load(V.prog + 1);
                 if (st != LV_RUNNING) {
                     PSET(sc, 10);
+                    uint64_t w = lv_word(gen, LV_CANCEL, 0, 0);
                     if (st == LV_FINAL) {
-                        lv_store(&sc->lv_T, (int32_t)host_load(V.prog + 3));
                         lv_store(&sc->lv_R, (int32_t)host_load(V.prog + 4));
                         lv_store(&sc->lv_W, (int32_t)host_load(V.prog + 5));
-                        lv_store(&sc->lv_used, host_load(V.prog + 1));
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the counts land before the state word)
+                        // (the final T and bytes: written before the state word)
+                        w = lv_word(gen, LV_FINAL, host_load(V.prog + 3), host_load(V.prog + 1));
                     }
-                    lv_store(&sc->lv_state, gen << 2 | (st == LV_FINAL ? LV_FINAL : LV_CANCEL));
+                    lv_store(&sc->lv_pub, w);
                     break;
                 }
                 if (pub != last) {
                     // (used may be an older publish's: it only bounds the LDS
                     // window -- records past it are read from the stream itself)
-                    lv_store(&sc->lv_used, used);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    lv_store(&sc->lv_pub, (uint64_t)gen << 32 | (uint64_t)(uint32_t)pub);
+                    lv_store(&sc->lv_pub, lv_word(gen, LV_RUNNING, (uint64_t)pub, used));
                     last = pub;
                 }
                 if (wall_clock64() - t_start > V.timeout) {
-                    lv_store(&sc->lv_state, gen << 2 | LV_TIMEOUT);
+                    lv_store(&sc->lv_pub, lv_word(gen, LV_TIMEOUT, 0, 0));
                     break;
                 }
                 __builtin_amdgcn_s_sleep(4);
@@ -982,18 +1018,17 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
     for (int g = wid - 1;; g += nwk) {
         const int t0 = g * STG_TPW;
         int tav;
-        for (;;) {  // (wave-uniform: every lane reads the same words; another batch's words read as "nothing yet")
-            const uint32_t sw = __builtin_amdgcn_readfirstlane(lv_load(&sc->lv_state));
-            const int st = (sw >> 2) == gen ? (int)(sw & 3) : LV_RUNNING;
+        uint64_t used;
+        for (;;) {  // (wave-uniform: one word; another batch's word reads as "nothing yet")
+            const uint64_t w0 = lv_load(&sc->lv_pub);
+            const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w0) |
+                               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w0 >> 32)) << 32);
+            const int st = lv_gen(w) == gen ? lv_state(w) : LV_RUNNING;
             if (st == LV_CANCEL || st == LV_TIMEOUT) return;
-            if (st == LV_FINAL) {
-                tav = __builtin_amdgcn_readfirstlane(lv_load(&sc->lv_T));
-                break;
-            }
-            const uint64_t pw = lv_load(&sc->lv_pub);
-            const int pub = __builtin_amdgcn_readfirstlane((uint32_t)(pw >> 32) == gen ? (int)(uint32_t)pw : 0);
-            if (pub >= t0 + STG_TPW) {
+            const int pub = lv_gen(w) == gen ? lv_txns(w) : 0;
+            if (st == LV_FINAL || pub >= t0 + STG_TPW) {
                 tav = pub;
+                used = lv_used(w);
                 break;
             }
             __builtin_amdgcn_s_sleep(8);
@@ -1003,14 +1038,15 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
             return;
         }
         LiveOut O = V.O;
-        const uint64_t used = lv_load(&sc->lv_used);
-        const uint64_t used_u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)used) |
-                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(used >> 32)) << 32);
-        O.stream_cap = min(O.stream_cap, used_u + 15);
+        // (16 bytes past the bytes written whole: encode_key reads the aligned
+        // words around a key, so the batch's last key stays in the window)
+        O.stream_cap = min(O.stream_cap, used + 32);
         if (lane == 0) PMAX(sc, 20);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (ONE per group: see above)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) PMAX(sc, 21);
+        // a group among the last published ones: its records end at most
+        // `used`, so the window's last LIVE_WIN bytes are read together with
+        // the offsets (one round trip instead of two)
+        O.spec = tav - t0 <= 2 * STG_TPW;
         staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp0, sp0, win[wv]);
         if (lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1039,8 +1075,9 @@ __global__ __launch_bounds__(256) void k_live_finish(IngestArgs A, SortJobs J, S
         sc->ss_maxc = 0;
         S.view.ro[A.T] = A.R;
         S.view.wo[A.T] = A.W;
-        if (sc->lv_state != (gen << 2 | LV_FINAL) || sc->lv_err || sc->lv_T != A.T || sc->lv_R != A.R ||
-            sc->lv_W != A.W)
+        const uint64_t w = sc->lv_pub;
+        if (lv_gen(w) != (gen & 0x3FF) || lv_state(w) != LV_FINAL || lv_txns(w) != A.T || sc->lv_err ||
+            sc->lv_R != A.R || sc->lv_W != A.W)
             atomicCAS(&sc->err, 0, FDBCS_E_STATE);
         sc->lv_err = 0;
     }
