@@ -702,6 +702,7 @@ struct LiveOut {
     // the live kernel the bytes the host has written whole, rounded up to 16
     // (reading lines the host is still appending to made its adds stall)
     uint64_t stream_cap;
+    uint64_t valid;  // live kernel: the stream bytes the host had written whole (the published transactions' records)
     bool spec;  // read the window [stream_cap - LIVE_WIN, stream_cap) together with the offsets
 };
 
@@ -712,17 +713,30 @@ struct LiveOut {
 // than the Resolver's adds arrive at the end of a batch); a key or record
 // past the window is read from the host-mapped stream directly.
 constexpr int LIVE_WIN = 4096;  // bytes per wavefront (config 2: 8 records of ~300 bytes)
+// A host-mapped word as the host wrote it last: relaxed system-scope loads
+// (sc0 sc1) bypass the GPU's caches -- the progress words and the record
+// offsets (a 128-byte line of offsets also holds later groups' entries).
+// Plain or non-temporal loads of a line the host was still appending to left
+// it in a cache, and a later group reading that line saw its old bytes
+// (measured: wrong keys whenever groups ran before the final word); the
+// record windows avoid such lines instead (TxnStage::publish pads).
+__device__ inline uint64_t host_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct LiveWin {
     const uint8_t* win;  // LDS
     uint64_t lo, hi;     // the stream bytes [lo, hi) it holds
+    uint64_t valid;      // ... of which those below `valid` were written whole when copied
     const uint8_t* host;
     __device__ const uint8_t* at(uint64_t off, uint64_t len) const {
-        // (+8: encode_key reads the aligned words around a key)
-        if (off >= lo && off + len + 8 <= hi) return win + (off - lo);
-        // past the window: plain loads of the stream itself, which this CU's
-        // L1 may hold from before the host wrote it -- drop it first (rare:
-        // a group larger than the window)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // (+8: encode_key reads the aligned words around a key -- bytes past
+        // the key, which it masks, may be ones the host had not written yet)
+        if (off >= lo && off + len <= valid && off + len + 8 <= hi) return win + (off - lo);
+        // past the window: plain loads of the stream itself, which the caches
+        // may hold from before the host wrote it -- a system-scope acquire
+        // drops them first (rare: a group larger than the window)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         return host + off;
     }
 };
@@ -741,10 +755,8 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
     const int t = t0 + lane;
     const bool ht = lane < nt;
     int n = 0;
-    // (LIVE: non-temporal loads of the host-mapped offsets and records skip
-    // this CU's L1, which may hold lines from before the host wrote them)
-    const uint64_t to = ht ? (LIVE ? __builtin_nontemporal_load(S.toff + t) : S.toff[t]) : STAGE_EMPTY;
-    LiveWin X{win, 0, 0, S.stream};
+    const uint64_t to = ht ? (LIVE ? host_load(S.toff + t) : S.toff[t]) : STAGE_EMPTY;
+    LiveWin X{win, 0, 0, O.valid, S.stream};
     if constexpr (LIVE) {  // the group's records into the LDS window (16-byte aligned, coalesced)
         // each lane's 16-byte pieces are loaded before any is stored, so the
         // window is one round trip; speculative: the stream's last LIVE_WIN
@@ -753,6 +765,10 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         constexpr int WPL = LIVE_WIN / 16 / 64;
         const uint64_t shi = O.stream_cap & ~uint64_t(15);
         const uint64_t slo = shi > (uint64_t)LIVE_WIN ? shi - LIVE_WIN : 0;
+        // (16-byte non-temporal loads: the window never reaches past the bytes
+        // the host published, which end on a 128-byte line the host does not
+        // write again -- TxnStage::publish -- so no cache can hold an older
+        // copy of a line read here)
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         u32x4 v[WPL];
         auto load_win = [&](uint64_t lo, uint64_t hi) {
@@ -795,7 +811,8 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         if (lane == 0) PMAX(A.sc, 22);
     }
     if (ht) {
-        const StageTxn h = (to & STAGE_EMPTY) ? stage_txn(S.stream, to) : stage_txn(X.at(to, sizeof(StageHdr)) - to, to);
+        const StageTxn h = (!LIVE || (to & STAGE_EMPTY)) ? stage_txn(S.stream, to)
+                                                        : stage_txn(X.at(to, sizeof(StageHdr)) - to, to);
         n = h.nr + h.nw;
         if (LIVE && (t >= O.capT || h.ro + h.nr > O.capR || h.wo + h.nw > O.capW)) {
             atomicOr(&A.sc->lv_err, 1);
@@ -932,6 +949,9 @@ struct LiveArgs {
     uint64_t timeout;      // wall_clock64 ticks (100 MHz)
     uint32_t gen;          // this live batch's generation (tags lv_pub)
 };
+#ifndef FDBCS_LIVE_SPEC
+#define FDBCS_LIVE_SPEC 1
+#endif
 #ifndef FDBCS_LIVE_BLOCKS
 #define FDBCS_LIVE_BLOCKS 128  // (511 worker waves; 64: 1-2 us slower per window, 32: 12 us)
 #endif
@@ -940,13 +960,12 @@ constexpr uint64_t LIVE_TIMEOUT_TICKS = 8ull * 100000000ull;  // 8 s of the 100 
 
 // Polling (MI355X_MICROARCH.md, inter-workgroup visibility): relaxed
 // agent-scope loads and stores (sc1: past this CU's L1) for the mirrored
-// word, relaxed system-scope loads of the host's; the group's offsets and
-// records by non-temporal loads, which skip the L1 (it may hold host lines an
-// earlier window read before the host wrote them), and an agent acquire only
-// before a plain load of the stream past the window.  Acquire loads in the
-// poll loops (an L1 invalidate per poll in up to 511 waves) held the kernel
-// ~45 us behind the adds at config 2; an acquire per group cost 0.8-2.4 us on
-// the last group.
+// word, relaxed system-scope loads of the host's words, the group's offsets
+// and its records (host_load above), and a system-scope acquire only before a
+// plain load of the stream past the window.  Acquire loads in the poll loops
+// (an L1 invalidate per poll in up to 511 waves) held the kernel ~45 us
+// behind the adds at config 2; an acquire per group cost 0.8-2.4 us on the
+// last group.
 template <class T>
 __device__ inline T lv_load(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -954,9 +973,6 @@ __device__ inline T lv_load(const T* p) {
 template <class T>
 __device__ inline void lv_store(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline uint64_t host_load(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
@@ -985,8 +1001,9 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
             for (;;) {
                 // (the three words in one round trip: independent loads)
                 const uint64_t st = host_load(V.prog + 2);
-                const int64_t pub = (int64_t)host_load(V.prog);
-                const uint64_t used = host_load(V.prog + 1);
+                const uint64_t pw = host_load(V.prog);  // (one word: the count and the bytes stay consistent)
+                const int64_t pub = (int64_t)(pw & 0xFFFFF);
+                const uint64_t used = pw >> 20;
                 if (st != LV_RUNNING) {
                     PSET(sc, 10);
                     uint64_t w = lv_word(gen, LV_CANCEL, 0, 0);
@@ -1000,8 +1017,6 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                     break;
                 }
                 if (pub != last) {
-                    // (used may be an older publish's: it only bounds the LDS
-                    // window -- records past it are read from the stream itself)
                     lv_store(&sc->lv_pub, lv_word(gen, LV_RUNNING, (uint64_t)pub, used));
                     last = pub;
                 }
@@ -1038,15 +1053,17 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
             return;
         }
         LiveOut O = V.O;
-        // (16 bytes past the bytes written whole: encode_key reads the aligned
-        // words around a key, so the batch's last key stays in the window)
-        O.stream_cap = min(O.stream_cap, used + 32);
+        // (the published bytes end on a 128-byte line, at least 16 bytes past
+        // the last record: encode_key's aligned reads around its last key
+        // stay inside)
+        O.stream_cap = min(O.stream_cap, used);
+        O.valid = used;
         if (lane == 0) PMAX(sc, 20);
         if (lane == 0) PMAX(sc, 21);
         // a group among the last published ones: its records end at most
         // `used`, so the window's last LIVE_WIN bytes are read together with
         // the offsets (one round trip instead of two)
-        O.spec = tav - t0 <= 2 * STG_TPW;
+        O.spec = FDBCS_LIVE_SPEC && tav - t0 <= 2 * STG_TPW;
         staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp0, sp0, win[wv]);
         if (lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

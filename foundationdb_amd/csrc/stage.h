@@ -85,6 +85,7 @@ class TxnStage {
    private:
     int grow(int64_t need_txns, uint64_t need_bytes);
     void publish();
+    bool pad_published();
     void live_check();
 
     void sync();
@@ -118,8 +119,9 @@ class TxnStage {
     UnpackOut lview_{};           // the view's arrays in the live layout (sized by lcaps_)
     int64_t pub_every_ = 16;      // FDBCS_LIVE_PUB: transactions per progress word
     int64_t next_pub_ = 0;
-    // host-mapped progress: [0] published T, [1] published stream bytes,
-    // [2] state (LV_RUNNING / LV_FINAL / LV_CANCEL), [3..5] final T, R, W
+    // host-mapped progress: [0] published bytes << 20 | published T (one
+    // word), [1] final stream bytes, [2] state (LV_RUNNING / LV_FINAL /
+    // LV_CANCEL), [3..5] final T, R, W
     uint64_t* prog_ = nullptr;
     uint64_t* prog_dev_ = nullptr;
 };

@@ -9,6 +9,15 @@ namespace fdbcs_dev {
 
 namespace {
 
+// the record stream and offsets: host-mapped, coherent (the live kernel reads
+// them while they are written).  FDBCS_STAGE_NONCOHERENT builds: default
+// pinned memory (A/B of the adds' cost; live ingest must then be off)
+#ifdef FDBCS_STAGE_NONCOHERENT
+constexpr unsigned STREAM_FLAGS = hipHostMallocDefault;
+#else
+constexpr unsigned STREAM_FLAGS = hipHostMallocMapped | hipHostMallocCoherent;
+#endif
+
 // ~70,000 short keys per config-2 batch: inline word compares and copies
 // instead of a libc call per key (measured: 185 -> ~110 us per batch).
 inline uint64_t ld64(const uint8_t* p) {
@@ -144,7 +153,7 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
     if (need_txns > toff_cap_) {
         const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
         uint64_t* nt = nullptr;
-        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, STREAM_FLAGS) != hipSuccess)
             return FDBCS_E_NOMEM;
         if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
         if (toff_) hipHostFree(toff_);
@@ -157,7 +166,7 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         uint8_t* np = nullptr;
         // (coherent: the live kernel reads the records over PCIe as they are
         // written, which a device-cached line of a half-written record would break)
-        if (hipHostMalloc((void**)&np, nc, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        if (hipHostMalloc((void**)&np, nc, STREAM_FLAGS) != hipSuccess)
             return FDBCS_E_NOMEM;
         if (used_) memcpy(np, pin_, used_);
         if (pin_) hipHostFree(pin_);
@@ -268,9 +277,26 @@ int TxnStage::skip(int32_t n) {
 }
 
 // ---- live ingest --------------------------------------------------------------
+// The published bytes end on a 128-byte line (an L2 line) at least 16 bytes
+// past the last record: the next record starts on a fresh line, so the live
+// kernel, which reads only below the published end, never caches a line the
+// host writes again (k_live_ingest), and a key's aligned 8-byte reads stay
+// below it.  Records are located by their offsets; the gap is never read.
+bool TxnStage::pad_published() {
+    const uint64_t p = (used_ + 16 + 127) & ~uint64_t(127);
+    if (p + 8 * ((uint64_t)T_ + 1) + 16 > cap_) return false;  // (no room: the batch falls back)
+    used_ = p;
+    return true;
+}
+
 void TxnStage::publish() {
-    prog_[1] = used_;
-    __atomic_store_n(&prog_[0], (uint64_t)T_, __ATOMIC_RELEASE);  // (after the records and their offsets)
+    if (!pad_published()) {
+        live_cancel();
+        return;
+    }
+    // one word, T (< 2^20: live batches have T <= LARGE_T) and the bytes
+    // written whole, after the records and their offsets
+    __atomic_store_n(&prog_[0], (uint64_t)used_ << 20 | (uint64_t)T_, __ATOMIC_RELEASE);
     next_pub_ = T_ + pub_every_;
 }
 
@@ -294,7 +320,9 @@ int TxnStage::begin_live(const LiveCaps& caps) {
     // records (header, range entries, keys, padding) and, should the batch
     // fall back, the offsets appended at finish
     const uint64_t slots = 2 * ((uint64_t)caps.R + (uint64_t)caps.W);
-    const uint64_t need = 32 * (uint64_t)caps.T + 4 * slots + caps.key_bytes + 8 * ((uint64_t)caps.T + 1) + 64;
+    // (+ the padding of every publish, TxnStage::publish)
+    const uint64_t need = 32 * (uint64_t)caps.T + 4 * slots + caps.key_bytes + 8 * ((uint64_t)caps.T + 1) + 64 +
+                          160 * ((uint64_t)caps.T / (uint64_t)pub_every_ + 2);
     int r;
     if ((r = grow(caps.T + 1, need))) return r;
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
@@ -326,7 +354,7 @@ int TxnStage::begin_live(const LiveCaps& caps) {
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
-    if (live_ && !live_broken_ && staged) {
+    if (live_ && !live_broken_ && staged && pad_published()) {
         // the final word: the kernel finishes the last groups and leaves
         prog_[3] = (uint64_t)T_;
         prog_[4] = (uint64_t)R_;
