@@ -655,10 +655,19 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
 // in the worst case.
 int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
     int r;
-    const int64_t naff_max = std::min<int64_t>(cs->known_D + cs->pending_pages + 1, 2 * W + 2);
-    const int64_t need = 2 * naff_max + 2 * cdiv64(2 * W, FILL) + cdiv64(3 * W + 10 + 2 * PAGE, FILL) + 8;
+    // (worst case: every affected page splits; the directory bound counts the
+    // pages the unsynchronized batches may have added)
+    auto need_pages = [&]() {
+        const int64_t naff_max = std::min<int64_t>(cs->known_D + cs->pending_pages + 1, 2 * W + 2);
+        return 2 * naff_max + 2 * cdiv64(2 * W, FILL) + cdiv64(3 * W + 10 + 2 * PAGE, FILL) + 8;
+    };
+    int64_t need = need_pages();
     if (cs->known_free - cs->pending_pages < need) {
-        if (cs->pending_pages && (r = refresh_state(cs))) return r;
+        if (cs->pending_pages) {
+            if ((r = refresh_state(cs))) return r;
+            need = need_pages();  // (the exact directory size now: the pending bound was loose --
+                                  // config 5's unsynchronized batches asked a 312 GB pool)
+        }
         if (cs->known_free < need) {
             const int64_t used = cs->h.cap_pages - cs->known_free;
             if ((r = grow_pool(cs, used + 4 * need + 1024))) return r;  // (slack: fewer syncs behind early verdicts)
@@ -879,9 +888,13 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nul
 // byte of the record stream (the begin keys sampled are disjoint parts of it).
 int lm_arm(fdbcs* cs, uint64_t n_ranges, uint64_t key_bytes, LmArgs& la) {
     fdbcs::Lm& L = cs->lm;
-    // every range may be sampled; every begin key is a disjoint part of the
-    // stream, plus at most 15 bytes of padding each
-    const size_t n = (size_t)n_ranges, nb = (size_t)key_bytes + 16 * n + 64;
+    // Room for every range of a small batch; a large one samples ~0.6 % of its
+    // ranges (config 5: ~54 K of 9 M), so 64 K + 1/16 of them, with up to 128
+    // bytes of key each (16-byte pieces).  A batch past either capacity is
+    // rolled again by fdbcs_sample_add_batch's synchronous path (the kernel
+    // counts past the capacity and stops writing).
+    const size_t n = (size_t)std::min<uint64_t>(n_ranges, 65536 + n_ranges / 16);
+    const size_t nb = (size_t)std::min<uint64_t>((uint64_t)key_bytes + 16 * n_ranges + 64, (uint64_t)n * 128 + 65536);
     auto grow = [](auto*& p, size_t& cap, size_t need, size_t elem) {
         if (need <= cap && p) return (int)FDBCS_OK;
         const size_t c = std::max<size_t>(need + need / 4, 4096);

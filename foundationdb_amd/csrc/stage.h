@@ -109,6 +109,7 @@ class TxnStage {
     uint64_t used_ = 0, sent_ = 0;
     uint64_t* toff_ = nullptr;    // pinned, host-mapped [T]: record offsets (appended to the stream at finish)
     uint64_t* toff_dev_ = nullptr;
+    bool pin_live_ = false, toff_live_ = false;  // the stream / offsets are coherent (live ingest can read them)
     int64_t toff_cap_ = 0;
     uint8_t* view_ = nullptr;     // device: the unpacked arrays
     uint64_t view_cap_ = 0;

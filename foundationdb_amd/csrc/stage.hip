@@ -9,13 +9,18 @@ namespace fdbcs_dev {
 
 namespace {
 
-// the record stream and offsets: host-mapped, coherent (the live kernel reads
-// them while they are written).  FDBCS_STAGE_NONCOHERENT builds: default
-// pinned memory (A/B of the adds' cost; live ingest must then be off)
-#ifdef FDBCS_STAGE_NONCOHERENT
-constexpr unsigned STREAM_FLAGS = hipHostMallocDefault;
+// The record stream and offsets: host-mapped and coherent while small enough
+// for live ingest (which reads them while they are written); a stream grown
+// past LIVE_STREAM_MAX (large batches, which never go live) is default
+// pinned memory -- coherent allocations of ~10^6-transaction streams left
+// later whole-batch staging out of memory.
+constexpr uint64_t LIVE_STREAM_MAX = 256ull << 20;
+#ifdef FDBCS_STAGE_NONCOHERENT  // (A/B of the adds' cost)
+unsigned stream_flags(uint64_t) { return hipHostMallocDefault; }
 #else
-constexpr unsigned STREAM_FLAGS = hipHostMallocMapped | hipHostMallocCoherent;
+unsigned stream_flags(uint64_t bytes) {
+    return bytes <= LIVE_STREAM_MAX ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault;
+}
 #endif
 
 // ~70,000 short keys per config-2 batch: inline word compares and copies
@@ -153,8 +158,9 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
     if (need_txns > toff_cap_) {
         const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
         uint64_t* nt = nullptr;
-        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, STREAM_FLAGS) != hipSuccess)
+        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, stream_flags((uint64_t)nc * 8)) != hipSuccess)
             return FDBCS_E_NOMEM;
+        toff_live_ = (uint64_t)nc * 8 <= LIVE_STREAM_MAX;
         if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
         if (toff_) hipHostFree(toff_);
         toff_ = nt;
@@ -166,8 +172,9 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         uint8_t* np = nullptr;
         // (coherent: the live kernel reads the records over PCIe as they are
         // written, which a device-cached line of a half-written record would break)
-        if (hipHostMalloc((void**)&np, nc, STREAM_FLAGS) != hipSuccess)
+        if (hipHostMalloc((void**)&np, nc, stream_flags(nc)) != hipSuccess)
             return FDBCS_E_NOMEM;
+        pin_live_ = nc <= LIVE_STREAM_MAX;
         if (used_) memcpy(np, pin_, used_);
         if (pin_) hipHostFree(pin_);
         pin_ = np;
@@ -325,6 +332,7 @@ int TxnStage::begin_live(const LiveCaps& caps) {
                           160 * ((uint64_t)caps.T / (uint64_t)pub_every_ + 2);
     int r;
     if ((r = grow(caps.T + 1, need))) return r;
+    if (!pin_live_ || !toff_live_) return FDBCS_E_STATE;  // (grown past the live size: not coherent)
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
     const uint64_t o_ro = al(8 * (uint64_t)caps.T), o_wo = al(o_ro + 4 * ((uint64_t)caps.T + 1)),
                    o_ko = al(o_wo + 4 * ((uint64_t)caps.T + 1)), o_kl = al(o_ko + 8 * slots),
