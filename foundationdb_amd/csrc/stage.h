@@ -84,6 +84,7 @@ class TxnStage {
 
    private:
     int grow(int64_t need_txns, uint64_t need_bytes);
+    int grow_bar(int64_t need_txns, uint64_t need_bytes);
     void publish();
     bool pad_published();
     void live_check();
@@ -110,6 +111,11 @@ class TxnStage {
     uint64_t* toff_ = nullptr;    // pinned, host-mapped [T]: record offsets (appended to the stream at finish)
     uint64_t* toff_dev_ = nullptr;
     bool pin_live_ = false, toff_live_ = false;  // the stream / offsets are coherent (live ingest can read them)
+    // FDBCS_STAGE_BAR=1: the stream, offsets and progress words are device
+    // memory the host writes through the large BAR (fine-grained, uncached
+    // on the device): no chunk copies, the kernels read them from HBM
+    // (configure(); slower adds, so off by default)
+    bool bar_ = false;
     int64_t toff_cap_ = 0;
     uint8_t* view_ = nullptr;     // device: the unpacked arrays
     uint64_t view_cap_ = 0;

@@ -1,6 +1,8 @@
 // stage.hip -- host staging of the per-transaction path (see stage.h).
 #include "stage.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -100,12 +102,17 @@ void TxnStage::sync() {
 void TxnStage::release() {
     live_cancel();  // (a live kernel waiting for this batch leaves: the syncs below return)
     sync();
-    if (pin_) hipHostFree(pin_);
-    if (dev_) hipFree(dev_);
+    auto free_host_or_dev = [this](void* p) {
+        if (!p) return;
+        if (bar_) hipFree(p);
+        else hipHostFree(p);
+    };
+    free_host_or_dev(pin_);
+    if (dev_ && dev_ != pin_) hipFree(dev_);
     if (view_) hipFree(view_);
     if (copied_) hipEventDestroy(copied_);
-    if (toff_) hipHostFree(toff_);
-    if (prog_) hipHostFree(prog_);
+    free_host_or_dev(toff_);
+    free_host_or_dev(prog_);
     pin_ = dev_ = view_ = nullptr;
     toff_ = toff_dev_ = nullptr;
     prog_ = prog_dev_ = nullptr;
@@ -124,11 +131,26 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
     if (const char* e = getenv("FDBCS_STAGE_EARLY")) early_ = strtoull(e, nullptr, 0);
     if (const char* e = getenv("FDBCS_LIVE_PUB")) pub_every_ = std::max<int64_t>(8, strtoll(e, nullptr, 0));  // (default 16)
     if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
-    if (!prog_) {  // (the live kernel reads it over PCIe: coherent, uncached on the device)
-        if (hipHostMalloc((void**)&prog_, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-            return FDBCS_E_NOMEM;
-        memset(prog_, 0, 64);
-        if (hipHostGetDevicePointer((void**)&prog_dev_, prog_, 0) != hipSuccess) return FDBCS_E_HIP;
+    if (!prog_) {
+        // FDBCS_STAGE_BAR=1 (A/B): the stream in device memory the host writes
+        // through the large BAR (fine-grained, uncached on the device): the
+        // kernels read it from HBM, no copies.  Measured at config 2: detect
+        // ~6 us shorter, but the adds' small write-combined stores over PCIe
+        // took 245-270 us per batch against 192 into pinned host memory, so
+        // the default stays pinned host memory (chunk copies / live reads).
+        const bool bar = getenv("FDBCS_STAGE_BAR") && atoi(getenv("FDBCS_STAGE_BAR"));
+        bar_ = bar && hipExtMallocWithFlags((void**)&prog_, 64, hipDeviceMallocUncached) == hipSuccess;
+        if (bar_) {
+            volatile uint64_t* w = prog_;
+            for (int i = 0; i < 8; i++) w[i] = 0;  // (the host's store through the BAR: it works or faults here)
+            _mm_sfence();
+            prog_dev_ = prog_;
+        } else {
+            if (hipHostMalloc((void**)&prog_, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                return FDBCS_E_NOMEM;
+            memset(prog_, 0, 64);
+            if (hipHostGetDevicePointer((void**)&prog_dev_, prog_, 0) != hipSuccess) return FDBCS_E_HIP;
+        }
     }
     return FDBCS_OK;
 }
@@ -155,6 +177,7 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         live_cancel();  // (the live kernel reads the old buffers: it leaves first)
         sync();         // copies in flight read the old buffers
     }
+    if (bar_) return grow_bar(need_txns, need_bytes);
     if (need_txns > toff_cap_) {
         const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
         uint64_t* nt = nullptr;
@@ -185,6 +208,39 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         if (hipMalloc((void**)&dev_, nc) != hipSuccess) return FDBCS_E_NOMEM;
         cap_ = nc;
         sent_ = 0;
+    }
+    return FDBCS_OK;
+}
+
+// The BAR stream: device memory, grown by a device-to-device copy (the host
+// never reads it back: reads through the BAR are uncached PCIe round trips).
+int TxnStage::grow_bar(int64_t need_txns, uint64_t need_bytes) {
+    if (need_txns > toff_cap_) {
+        const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
+        uint64_t* nt = nullptr;
+        if (hipExtMallocWithFlags((void**)&nt, (size_t)nc * 8, hipDeviceMallocUncached) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        if (T_) {
+            _mm_sfence();
+            if (hipMemcpy(nt, toff_, (size_t)T_ * 8, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
+        }
+        if (toff_) hipFree(toff_);
+        toff_ = toff_dev_ = nt;
+        toff_cap_ = nc;
+        toff_live_ = true;
+    }
+    if (need_bytes > cap_) {
+        const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
+        uint8_t* np = nullptr;
+        if (hipExtMallocWithFlags((void**)&np, nc, hipDeviceMallocUncached) != hipSuccess) return FDBCS_E_NOMEM;
+        if (used_) {
+            _mm_sfence();
+            if (hipMemcpy(np, pin_, used_, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
+        }
+        if (pin_) hipFree(pin_);
+        pin_ = pin_dev_ = dev_ = np;
+        cap_ = nc;
+        pin_live_ = true;
     }
     return FDBCS_OK;
 }
@@ -245,6 +301,7 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
         live_check();
         if (!live_broken_) return FDBCS_OK;  // (no chunk copies: the live kernel reads the stream itself)
     }
+    if (bar_) return FDBCS_OK;  // (the stream is in device memory already)
     // a chunk every chunk_ bytes, and one more `early_` bytes before where the
     // previous batch ended (batches are alike): detectConflicts then sends
     // only that much and the record offsets
@@ -302,7 +359,9 @@ void TxnStage::publish() {
         return;
     }
     // one word, T (< 2^20: live batches have T <= LARGE_T) and the bytes
-    // written whole, after the records and their offsets
+    // written whole, after the records and their offsets (through the BAR the
+    // stores are write-combined: the fence drains them first)
+    if (bar_) _mm_sfence();
     __atomic_store_n(&prog_[0], (uint64_t)used_ << 20 | (uint64_t)T_, __ATOMIC_RELEASE);
     next_pub_ = T_ + pub_every_;
 }
@@ -319,6 +378,7 @@ void TxnStage::live_check() {
 void TxnStage::live_cancel() {
     if (!live_ || live_broken_ || !prog_) return;
     live_broken_ = true;
+    if (bar_) _mm_sfence();
     __atomic_store_n(&prog_[2], (uint64_t)LV_CANCEL, __ATOMIC_RELEASE);
 }
 
@@ -352,6 +412,7 @@ int TxnStage::begin_live(const LiveCaps& caps) {
                        (uint64_t*)(view_ + o_ko), (uint32_t*)(view_ + o_kl)};
     for (int i = 0; i < 8; i++) prog_[i] = 0;  // LV_RUNNING, nothing published (read by the kernel launched next)
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    if (bar_) _mm_sfence();
     lcaps_ = caps;
     next_pub_ = pub_every_;
     live_ = true;
@@ -368,6 +429,7 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
         prog_[4] = (uint64_t)R_;
         prog_[5] = (uint64_t)W_;
         prog_[1] = used_;
+        if (bar_) _mm_sfence();
         __atomic_store_n(&prog_[2], (uint64_t)LV_FINAL, __ATOMIC_RELEASE);
         live_ = false;
         dv = fdbcs_batch_view{};
@@ -391,9 +453,16 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     const bool failed = live_;  // (a live batch cancelled on the way: ingested whole below)
     live_cancel();
     live_ = false;
+    const uint64_t* dtoff = toff_;
+    if (bar_) {
+        // the records and offsets are in device memory already: drain the
+        // write-combined stores before the launches that read them
+        _mm_sfence();
+    } else {
     // the record offsets go after the records (8-byte aligned: records are),
     // and the rest of the stream in one copy
     const uint64_t o_toff = used_;
+    dtoff = reinterpret_cast<const uint64_t*>(dev_ + o_toff);
     early_at_ = early_ && used_ > early_ ? used_ - early_ : ~0ull;  // (the next batch's extra chunk)
     if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
     const uint64_t end = o_toff + 8 * (uint64_t)T_;
@@ -412,6 +481,7 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
         sent_ = end;
         if (hipEventRecord(copied_, copy_) != hipSuccess || hipStreamWaitEvent(stream_, copied_, 0) != hipSuccess)
             return FDBCS_E_HIP;
+    }
     }
     // the view's arrays: snapshot [T] | read_off [T+1] | write_off [T+1] | key_off [2R+2W] | key_len [2R+2W]
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
@@ -442,7 +512,6 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     dv.key_bytes_len = used_;
     const UnpackOut out{(int64_t*)dv.snapshot, (int32_t*)dv.read_off, (int32_t*)dv.write_off, (uint64_t*)dv.key_off,
                         (uint32_t*)dv.key_len};
-    const uint64_t* dtoff = reinterpret_cast<const uint64_t*>(dev_ + o_toff);
     static const bool separate = getenv("FDBCS_SEPARATE_UNPACK") != nullptr;  // (A/B measurements)
     if (staged && !separate) {
         *staged = StagedBatch{dev_, dtoff, out};
