@@ -294,7 +294,7 @@ struct Scalars {
     // the live kernel's mirror of the host's progress, one word the workers
     // read in one load: lv_word(gen, state, transactions, stream bytes written whole)
     uint64_t lv_pub;
-    int32_t lv_R, lv_W;     // the final read / write counts (k_live_finish checks them)
+    int32_t lv_R, lv_W;     // the final read / write counts (diagnostics)
     int32_t lv_err;         // a transaction past the live capacities (the host falls back)
     int32_t lv_pad;
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds

@@ -169,6 +169,7 @@ struct fdbcs {
     // device view of the last batch staged by a host path (fdbcs_last_device_batch)
     fdbcs_batch_view last_dv{};
     bool have_last_dv = false;
+    int64_t last_wbase = 0;  // a live batch's writes in last_dv sit from here (0: 2R); moved on export
     bool have_quantiles = false;  // sample-sort splitters from an earlier batch exist
     bool sparse_edges = false;    // exact sharded protocol B: this shard exports its overlap edges
     bool edges_known = false;     // sc_host->edges_total is this batch's (set by fdbcs_shard_check)
@@ -299,6 +300,8 @@ static bool verbose() {
 // undone behind it; the batch is then ingested whole at detectConflicts).
 void live_quiesce(fdbcs* cs) {
     if (!cs->st.live_active()) return;
+    cs->b.lv_wbase = 0;  // (whatever runs next lays its batch out as the view does)
+    cs->b.lv_nb1 = 0;
     cs->st.live_cancel();
     launch_live_reset(cs->b, cs->sc, (int)(cs->sorts & 1), cs->stream);
 }
@@ -471,8 +474,6 @@ void free_batch(BatchBufs& b) {
     dfree(b.desc_fmeta); dfree(b.desc_ftail);
     dfree(b.win_keep); dfree(b.win_cnt); dfree(b.win_off);
     dfree(b.scan_tmp);
-    free_keys(b.lv_wkeys); dfree(b.lv_wkoff); dfree(b.lv_wklen);
-    b.lv_wcap = 0;
 }
 
 
@@ -755,6 +756,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     cs->batches++;
     cs->edges_known = false;
     cs->have_last_dv = false;  // (the host paths set it again once this batch succeeded)
+    cs->last_wbase = 0;
     // (a staged batch's keys can outnumber its stream's bytes: point ranges
     // share theirs, stage.hip)
     const uint64_t kb = std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total);
@@ -784,10 +786,11 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
-    if (b.staged.live) {  // k_live_ingest encoded the batch during the adds: place its writes
-        launch_live_finish(v, b, sc, (int)(cs->sorts & 1), cs->h.dir[cs->cur], cs->lv_gen, s);
+    if (b.staged.live) {  // k_live_ingest encoded the batch during the adds (writes from b.lv_wbase)
         cs->lv_done++;
     } else {
+        b.lv_wbase = 0;  // (the view's own layout: writes from 2R)
+        b.lv_nb1 = 0;
         if (b.staged.live_failed) {
             launch_live_reset(b, sc, (int)(cs->sorts & 1), s);
             cs->lv_cancelled++;
@@ -928,8 +931,8 @@ bool live_enabled() {
 // Live ingest: at fdbcs_batch_begin, k_live_ingest is queued
 // behind the previous batch's history update and encodes this batch's
 // transactions while the Resolver is still adding them (TxnStage publishes its
-// progress every FDBCS_LIVE_PUB transactions); detectConflicts then only
-// places the writes (k_live_finish).  Capacities: the last batch's shape plus
+// progress every FDBCS_LIVE_PUB transactions); detectConflicts then starts
+// at the sort (the writes sit at 2 caps.R + 2w, BatchBufs::lv_wbase).  Capacities: the last batch's shape plus
 // a quarter -- a batch that outgrows them is cancelled on the way and ingested
 // whole, as without live ingest.  Only the steady state goes live: splitters
 // from an earlier batch, an unsharded set, small batches, no stage timing.
@@ -950,15 +953,6 @@ void live_begin(fdbcs* cs) {
     const uint64_t kb = c.key_bytes + 32 * (uint64_t)c.T + 8 * ((uint64_t)c.R + c.W) + 64;
     BatchBufs& b = cs->b;
     if (ensure_batch(cs, c.T, c.R, c.W, kb) || !b.rounds) return;  // (the live kernel leaves the reads unsorted)
-    if (2 * (int64_t)c.W > b.lv_wcap) {
-        const int64_t n = std::max<int64_t>(2 * (int64_t)c.W, 4096);
-        free_keys(b.lv_wkeys);
-        dfree(b.lv_wkoff);
-        dfree(b.lv_wklen);
-        b.lv_wcap = 0;
-        if (alloc_keys(b.lv_wkeys, n) || dalloc(b.lv_wkoff, n) || dalloc(b.lv_wklen, n)) return;
-        b.lv_wcap = n;
-    }
     if (cs->st.begin_live(c)) return;
     LmArgs la{};
     cs->lv_lm = cs->lm.owner && lm_arm(cs, (uint64_t)c.R + c.W, c.key_bytes, la) == FDBCS_OK;
@@ -1215,6 +1209,7 @@ int detect_host_view(fdbcs* cs, const fdbcs_batch_view& hv, int64_t now, int64_t
     if ((r = check_host_view(hv))) return r;
     fdbcs_batch_view dv;
     cs->have_last_dv = false;
+    cs->last_wbase = 0;
     if ((r = stage_batch(cs, hv, dv))) return r;
     if ((r = finish_detect(cs, dv, now, new_oldest, verdict))) return r;
     cs->last_dv = dv;
@@ -1408,6 +1403,7 @@ int fdbcs_batch_begin(fdbcs* cs) {
     int r;
     if ((r = cs->st.begin())) return r;
     cs->have_last_dv = false;  // (the staged bytes of the last batch are overwritten from here on)
+    cs->last_wbase = 0;
     cs->in_batch = true;
     live_begin(cs);
     return FDBCS_OK;
@@ -1439,6 +1435,7 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     if (T && !verdict) return FDBCS_E_ARG;
     cs->in_batch = false;
     cs->have_last_dv = false;
+    cs->last_wbase = 0;
     int r;
     fdbcs_batch_view dv;
     if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
@@ -1447,11 +1444,15 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     cs->lv_prev_R = dv.read_count;
     cs->lv_prev_W = dv.write_count;
     cs->lv_prev_K = cs->st.key_total();
+    const int64_t wbase = cs->b.staged.live ? cs->b.lv_wbase : 0;
     r = finish_detect(cs, dv, now, new_oldest, verdict, true);
     cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};  // (the ingest that reads it was launched)
+    cs->b.lv_wbase = 0;            // (every stage of the batch was launched)
+    cs->b.lv_nb1 = 0;
     if (r) return r;
     cs->last_dv = dv;
+    cs->last_wbase = wbase;
     cs->have_last_dv = true;
     return FDBCS_OK;
 }
@@ -1466,6 +1467,7 @@ int fdbcs_batch_detect_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
 int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now, int64_t new_oldest) {
     if (cs) live_quiesce(cs);
     if (cs) cs->have_last_dv = false;
+    if (cs) cs->last_wbase = 0;
     if (!cs || !hb || cs->in_batch) return FDBCS_E_ARG;
     if (cs->sub_head - cs->sub_tail >= 2) return FDBCS_E_ARG;  // two in flight: fdbcs_batch_wait first
     const fdbcs_batch_view& hv = *hb;
@@ -1764,7 +1766,28 @@ int fdbcs_last_device_batch(fdbcs* cs, fdbcs_batch_view* out) {
     if (cs) live_quiesce(cs);
     if (!cs || !out) return FDBCS_E_ARG;
     if (!cs->have_last_dv) return FDBCS_E_STATE;
-    *out = cs->last_dv;
+    fdbcs_batch_view& v = cs->last_dv;
+    const int64_t R2 = 2 * (int64_t)v.read_count, n = 2 * (int64_t)v.write_count;
+    if (cs->last_wbase && cs->last_wbase != R2 && n) {
+        // a live batch's view has its writes after a gap (BatchBufs::lv_wbase):
+        // moved down to 2R once, through a scratch copy (the two ranges overlap)
+        void* tmp = nullptr;
+        HIPOK(hipMalloc(&tmp, (size_t)n * 12));
+        uint64_t* koff = const_cast<uint64_t*>(v.key_off);
+        uint32_t* klen = const_cast<uint32_t*>(v.key_len);
+        uint64_t* t_off = static_cast<uint64_t*>(tmp);
+        uint32_t* t_len = reinterpret_cast<uint32_t*>(t_off + n);
+        hipStream_t s = cs->stream;
+        hipError_t e = hipMemcpyAsync(t_off, koff + cs->last_wbase, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(t_len, klen + cs->last_wbase, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(koff + R2, t_off, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(klen + R2, t_len, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        hipFree(tmp);
+        HIPOK(e);
+    }
+    cs->last_wbase = 0;
+    *out = v;
     return FDBCS_OK;
 }
 
@@ -1830,6 +1853,7 @@ int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
     int r;
     if ((r = check_batch_shape(v))) return r;
     cs->have_last_dv = false;
+    cs->last_wbase = 0;
     if ((r = ensure_batch(cs, v.txn_count, v.read_count, v.write_count, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
     if ((r = ensure_history(cs, v.write_count, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
     cs->last_T = v.txn_count;
@@ -2205,6 +2229,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     const int64_t T = v.txn_count, R = v.read_count, W = v.write_count;
     if (T && !verdict) return FDBCS_E_ARG;
     cs->have_last_dv = false;
+    cs->last_wbase = 0;
     cs->edges_known = false;
     if ((r = ensure_batch(cs, T, R, W, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;
     if ((r = ensure_history(cs, W, std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total)))) return r;

@@ -104,8 +104,7 @@ struct StagedBatch {
     const uint64_t* toff = nullptr;   // [T] record offsets (device)
     UnpackOut view{};                 // the batch view's arrays, written on the way
     // live ingest (stage.h): k_live_ingest already encoded the batch from the
-    // host-mapped stream while the adds ran; run_batch launches
-    // k_live_finish instead of the ingest
+    // host-mapped stream while the adds ran; run_batch launches no ingest
     bool live = false;
     // a live batch that outgrew its capacities: its partial work is undone
     // (launch_live_reset) before the ingest of the whole stream
@@ -162,17 +161,18 @@ struct BatchBufs {
                          // small directory, engine.hip edges_read_check)
     bool rounds;         // the decision by rounds (k_decide_rounds, rounds_fit): no overlap pairs
     bool rc_fused;       // this batch's history read check ran in the sort's bucket launch
-    // live ingest: the write endpoints by 2w until k_live_finish places them
-    // at 2R + 2w
-    KeyArrays lv_wkeys;
-    uint64_t* lv_wkoff;
-    uint32_t* lv_wklen;
-    int64_t lv_wcap;
+    // live ingest: the slot of write 0's begin (0: 2R, the view's own
+    // layout).  k_live_ingest does not know R before the final word, so a live
+    // batch's writes sit at 2 caps.R + 2w -- a gap after the reads that every
+    // stage addresses through write_base() -- and job 1's bucket count is the
+    // one its scatter used (the capacities' 2W, lv_nb1)
+    int64_t lv_wbase;
+    int32_t lv_nb1;
     // rounds mode (kernels_batch.hip k_decide_rounds)
     int32_t* rq;         // [2R] sorted write endpoints <= each read's begin / < its end
     int32_t* plist;      // [R + W] candidate reads: some write of the batch may overlap them (duplicates)
     uint8_t* wnew;       // [2W + 64] sorted write endpoint p starts a new distinct key
-    int32_t* winv;       // [2W] sorted position of each write endpoint (by slot - 2R)
+    int32_t* winv;       // [2W] sorted position of each write endpoint (by slot - write_base)
     int32_t* wcov;       // [2W] write cover: begins minus ends among the sorted write endpoints up to each
     uint2* items;        // [R + W] the rounds' writes and reads when they do not fit in LDS
     int64_t list_cap;    // entries of plist (items: 2 * list_cap)
@@ -232,6 +232,11 @@ struct BatchBufs {
     uint8_t* verdict;
 };
 
+// the slot of write 0's begin in this batch's key arrays (BatchBufs::lv_wbase)
+inline int64_t write_base(const BatchBufs& b, const fdbcs_batch_view& v) {
+    return b.lv_wbase ? b.lv_wbase : 2 * (int64_t)v.read_count;
+}
+
 struct HistBufs {
     Pool pool;
     int32_t cap_pages;
@@ -267,16 +272,14 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // that encodes the per-transaction stream from host-mapped memory as the
 // host publishes it (prog: host-mapped progress words, stage.h), launched
 // when the batch begins; parity: the sort counters' (cs->sorts & 1).
-// launch_live_finish: after the host's final word, the write endpoints'
-// places and sort records, the per-batch resets and bmax2 (in place of
-// launch_ingest).  launch_live_reset: undo a failed live batch's partial work
+// After the host's final word nothing is left to place: the writes and
+// their sort records are at write_base (BatchBufs::lv_wbase), the per-batch
+// resets ran in the kernel's prologue.  launch_live_reset: undo a failed live batch's partial work
 // before the whole stream is ingested again.
 // gen: the live batch's generation (tags the progress words in Scalars)
 void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
                         const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
                         UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, hipStream_t s);
-void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity, const Dir& hd,
-                        uint32_t gen, hipStream_t s);
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s);
 // lm: an attached sample's load-metrics roll (staged batches only; null: none)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,

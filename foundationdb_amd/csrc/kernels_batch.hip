@@ -80,6 +80,7 @@ __device__ inline Key encode_key(const uint8_t* p, uint32_t L, uint8_t* btail, u
 
 struct IngestArgs {
     int T, R, W, prep_blocks, bmax2_blocks;
+    int64_t wbase;  // slot of write 0's begin (write_base: 2R, or a live batch's 2 caps.R)
     Dir hd;  // bmax2 blocks: the history directory of this batch's read check
     const int64_t* snap;
     const int32_t* ro;
@@ -691,12 +692,8 @@ struct StgShared {
         pre[STG_BLOCK / 64][STG_TPW];
 };
 
-// LIVE's destinations for the write endpoints (by 2w until k_live_finish
-// places them at 2R + 2w) and its capacities
+// LIVE's capacities and stream bounds
 struct LiveOut {
-    KeyArrays wkeys;
-    uint64_t* wkoff;
-    uint32_t* wklen;
     int32_t capT, capR, capW;
     // the window copy stays below this: the stream allocation's size, and in
     // the live kernel the bytes the host has written whole, rounded up to 16
@@ -743,9 +740,9 @@ struct LiveWin {
 
 // One wavefront's group of transactions [t0, t0 + nt) (nt <= STG_TPW) of a
 // per-transaction record stream.  LIVE (k_live_ingest): the stream is
-// host-mapped and the batch's read count is not known yet, so a write's keys
-// and view entries go to O by 2w and only the read begins are scattered; a
-// transaction past the live capacities marks lv_err (the host falls back).
+// host-mapped and the batch's read count is not known yet, so the writes sit
+// at A.wbase = 2 caps.R (BatchBufs::lv_wbase); a transaction past the live
+// capacities marks lv_err and fails the batch (the host cancels first).
 template <bool SCATTER, bool LIVE>
 __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, const StagedBatch& S, const LiveOut& O,
                                     int t0, int nt, StgShared& L, const uint64_t* sp0, const uint64_t* sp1,
@@ -816,6 +813,7 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         n = h.nr + h.nw;
         if (LIVE && (t >= O.capT || h.ro + h.nr > O.capR || h.wo + h.nw > O.capW)) {
             atomicOr(&A.sc->lv_err, 1);
+            atomicCAS(&A.sc->err, 0, FDBCS_E_STATE);
             n = 0;
         }
         L.base[wv][lane] = h.base;
@@ -848,16 +846,16 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         const uint64_t eo = base + sizeof(StageHdr) + sizeof(StageRange) * (uint64_t)q;
         const StageRange e = *reinterpret_cast<const StageRange*>(LIVE ? X.at(eo, sizeof(StageRange)) : S.stream + eo);
         const int nrj = L.nr[wv][j];
-        int64_t i;  // range index: reads first, then writes (the slot layout of fdbcs_batch_view)
-        int w = -1;
+        int64_t i;  // the range's begin slot: read r at 2r, write w at wbase + 2w (fdbcs_batch_view's layout)
+        int r = -1, w = -1;
         if (q < nrj) {
-            const int r = L.ro[wv][j] + q;
-            i = r;
+            r = L.ro[wv][j] + q;
+            i = 2 * (int64_t)r;
             A.read_txn[r] = t0 + j;
             A.read_snap[r] = L.snap[wv][j];
         } else {
             w = L.wo[wv][j] + q - nrj;
-            i = (int64_t)A.R + w;
+            i = A.wbase + 2 * (int64_t)w;
             A.write_txn[w] = t0 + j;
         }
         const uint64_t ob = base + e.kofs, oe = base + stage_end_ofs(e);
@@ -872,27 +870,18 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
             if (amt) lm_append(A.lm, A.sc, amt, b, pos);
         }
         if (kcmp(b, en) >= 0) atomicCAS(&A.sc->err, 0, FDBCS_E_RANGE);  // every range must be non-empty
-        if (LIVE && w >= 0) {  // (its slot 2R + 2w is not known yet)
-            O.wkoff[2 * w] = ob;
-            O.wklen[2 * w] = e.blen;
-            O.wkoff[2 * w + 1] = oe;
-            O.wklen[2 * w + 1] = el;
-            O.wkeys.put(2 * (int64_t)w, b);
-            O.wkeys.put(2 * (int64_t)w + 1, en);
-            continue;
-        }
-        S.view.koff[2 * i] = ob;
-        S.view.klen[2 * i] = e.blen;
-        S.view.koff[2 * i + 1] = oe;
-        S.view.klen[2 * i + 1] = el;
-        A.keys.put(2 * i, b);
-        A.keys.put(2 * i + 1, en);
+        S.view.koff[i] = ob;
+        S.view.klen[i] = e.blen;
+        S.view.koff[i + 1] = oe;
+        S.view.klen[i + 1] = el;
+        A.keys.put(i, b);
+        A.keys.put(i + 1, en);
         if constexpr (SCATTER) {
             if (w < 0) {
-                if (J.nb[0]) scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp0);
+                if (J.nb[0]) scatter_rec(J, 0, r, SRec{b.hi, b.lo, b.meta, (uint32_t)i, 0}, tails, sp0);
             } else {
-                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp1);
-                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(2 * i + 1), 0}, tails, sp1);
+                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)i, 0}, tails, sp1);
+                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(i + 1), 0}, tails, sp1);
             }
         }
     }
@@ -938,8 +927,10 @@ __global__ __launch_bounds__(STG_BLOCK) void k_ingest_staged(IngestArgs A, SortJ
 //                    device memory;
 //   other waves:     group g = wave, wave + waves, ... once published.
 // Every wave leaves when the host's final word says its groups are past the
-// batch, when the host cancels, or after LIVE_TIMEOUT (the poller's word
-// says LV_TIMEOUT, and k_live_finish then fails the batch).
+// batch, when the host cancels, or after LIVE_TIMEOUT (the poller fails the
+// batch).  Nothing is left for detectConflicts to place: the writes and their
+// sort records went to the gapped slots from A.wbase, and the per-batch resets
+// ran in the prologue.
 struct LiveArgs {
     IngestArgs A;      // T, R: the live capacities (the real counts come with the final word)
     SortJobs J;        // job 1's splitters (rounds mode: the read begins are not sorted)
@@ -977,12 +968,18 @@ __device__ inline void lv_store(T* p, T v) {
 
 __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
     __shared__ StgShared L;
-    __shared__ uint64_t sp0[SS_MAXB];
+    __shared__ uint64_t sp1[SS_MAXB];  // job 1's (live batches are in rounds mode: J.nb[0] = 0, no job 0)
     __shared__ __attribute__((aligned(16))) uint8_t win[STG_BLOCK / 64][LIVE_WIN];
     Scalars* sc = V.A.sc;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wid = (int)blockIdx.x * (STG_BLOCK / 64) + wv;
-    splitter_fill(V.J, 0, sp0);  // (every wave, the poller's too, before the barrier)
+    splitter_fill(V.J, 1, sp1);  // (every wave, the poller's too, before the barrier)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the per-batch resets (k_ingest_staged's)
+        sc->n_comb = 0;
+        sc->n_comb_own = 0;
+        sc->ss_resample = 0;
+        sc->ss_maxc = 0;
+    }
     __syncthreads();
     {  // bmax2 of the directory this batch's read check uses (the previous
        // batch's update ran before this kernel): off the path after the adds
@@ -1008,10 +1005,18 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                     PSET(sc, 10);
                     uint64_t w = lv_word(gen, LV_CANCEL, 0, 0);
                     if (st == LV_FINAL) {
-                        lv_store(&sc->lv_R, (int32_t)host_load(V.prog + 4));
-                        lv_store(&sc->lv_W, (int32_t)host_load(V.prog + 5));
-                        // (the final T and bytes: written before the state word)
-                        w = lv_word(gen, LV_FINAL, host_load(V.prog + 3), host_load(V.prog + 1));
+                        // (the final counts and bytes: written before the state word)
+                        const uint64_t T = host_load(V.prog + 3);
+                        const int32_t R = (int32_t)host_load(V.prog + 4), W = (int32_t)host_load(V.prog + 5);
+                        lv_store(&sc->lv_R, R);
+                        lv_store(&sc->lv_W, W);
+                        w = lv_word(gen, LV_FINAL, T, host_load(V.prog + 1));
+                        if (T <= (uint64_t)V.O.capT) {
+                            V.S.view.ro[T] = R;
+                            V.S.view.wo[T] = W;
+                        } else {
+                            atomicCAS(&sc->err, 0, FDBCS_E_STATE);
+                        }
                     }
                     lv_store(&sc->lv_pub, w);
                     break;
@@ -1021,6 +1026,7 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                     last = pub;
                 }
                 if (wall_clock64() - t_start > V.timeout) {
+                    atomicCAS(&sc->err, 0, FDBCS_E_STATE);
                     lv_store(&sc->lv_pub, lv_word(gen, LV_TIMEOUT, 0, 0));
                     break;
                 }
@@ -1064,55 +1070,12 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
         // `used`, so the window's last LIVE_WIN bytes are read together with
         // the offsets (one round trip instead of two)
         O.spec = FDBCS_LIVE_SPEC && tav - t0 <= 2 * STG_TPW;
-        staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp0, sp0, win[wv]);
+        staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp1, sp1, win[wv]);
         if (lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             PMAX(sc, 23);
         }
     }
-}
-
-// After the host's final word: every write's keys to slots 2R + 2w, 2R + 2w + 1
-// with its view entries and sort records (the read begins were scattered
-// live), the per-batch resets, bmax2; a cancelled / timed-out / overflowed
-// live batch fails here (the host only lets complete ones through).
-__global__ __launch_bounds__(256) void k_live_finish(IngestArgs A, SortJobs J, StagedBatch S, LiveOut O, int w_blocks,
-                                                     uint32_t gen) {
-    __shared__ uint64_t sp1[SS_MAXB];
-    if ((int)blockIdx.x >= w_blocks) {  // bmax2: one word per block
-        bmax2_block(A.hd, A.sc->D, (int)blockIdx.x - w_blocks);
-        return;
-    }
-    Scalars* sc = A.sc;
-    PHASE(sc, 12);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        sc->n_comb = 0;
-        sc->n_comb_own = 0;
-        sc->ss_resample = 0;
-        sc->ss_maxc = 0;
-        S.view.ro[A.T] = A.R;
-        S.view.wo[A.T] = A.W;
-        const uint64_t w = sc->lv_pub;
-        if (lv_gen(w) != (gen & 0x3FF) || lv_state(w) != LV_FINAL || lv_txns(w) != A.T || sc->lv_err ||
-            sc->lv_R != A.R || sc->lv_W != A.W)
-            atomicCAS(&sc->err, 0, FDBCS_E_STATE);
-        sc->lv_err = 0;
-    }
-    splitter_fill(J, 1, sp1);
-    __syncthreads();
-    const int w = (int)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= A.W) return;
-    const int64_t s = 2 * (int64_t)A.R + 2 * (int64_t)w;
-    const Key b = O.wkeys.get(2 * (int64_t)w), e = O.wkeys.get(2 * (int64_t)w + 1);
-    A.keys.put(s, b);
-    A.keys.put(s + 1, e);
-    S.view.koff[s] = O.wkoff[2 * w];
-    S.view.klen[s] = O.wklen[2 * w];
-    S.view.koff[s + 1] = O.wkoff[2 * w + 1];
-    S.view.klen[s + 1] = O.wklen[2 * w + 1];
-    const uint8_t* const* tails = A.keys.tail;
-    scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)s, 0}, tails, sp1);
-    scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(s + 1), 0}, tails, sp1);
 }
 
 // a failed live batch: its sort counters (this parity), load-metrics entries,
@@ -1753,7 +1716,7 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
     J.n[1] = 2 * W;
     J.sbase[0] = 0;
     J.sstride[0] = 2;
-    J.sbase[1] = 2 * (int64_t)R;
+    J.sbase[1] = write_base(b, v);
     J.sstride[1] = 1;
     J.out[0] = b.rec_r0;
     J.out[1] = b.rec_w0;
@@ -1776,6 +1739,7 @@ static SortJobs make_sort_jobs(const fdbcs_batch_view& v, BatchBufs& b, Scalars*
         J.wcov = b.wcov;
     }
     for (int j = 0; j < 2; j++) J.nb[j] = ss_buckets(J.n[j]);
+    if (b.lv_wbase && b.lv_nb1) J.nb[1] = b.lv_nb1;  // (a live batch: the buckets k_live_ingest scattered into)
     J.blocks0 = cdiv(J.n[0], 256);
     return J;
 }
@@ -1835,6 +1799,7 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
     IngestArgs A;
     A.lm = lm && b.staged.stream ? *lm : LmArgs{};  // (k_ingest, the view path, does not roll)
     A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
+    A.wbase = write_base(b, v);
     A.prep_blocks = std::max(1, cdiv(v.txn_count, IB));
     A.snap = v.snapshot; A.ro = v.read_off; A.wo = v.write_off;
     A.koff = v.key_off; A.klen = v.key_len; A.bytes = v.key_bytes;
@@ -1873,26 +1838,19 @@ void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t
     fdbcs_batch_view vc{};
     vc.read_count = caps.R;
     vc.write_count = caps.W;
+    b.lv_wbase = 2 * (int64_t)caps.R;  // (the writes' slots and job 1's buckets hold until the batch's detect)
+    b.lv_nb1 = 0;
+    A.wbase = b.lv_wbase;
     const SortJobs J = make_sort_jobs(vc, b, sc, parity);
+    b.lv_nb1 = J.nb[1];
     StagedBatch S;
     S.stream = stream;
     S.toff = toff;
     S.view = view;
     S.live = true;
-    const LiveOut O{b.lv_wkeys, b.lv_wkoff, b.lv_wklen, caps.T, caps.R, caps.W, stream_cap};
+    const LiveOut O{caps.T, caps.R, caps.W, stream_cap};
     const LiveArgs V{A, J, S, O, prog, LIVE_TIMEOUT_TICKS, gen};
     hipLaunchKernelGGL(k_live_ingest, dim3(LIVE_BLOCKS), dim3(STG_BLOCK), 0, s, V);
-}
-
-void launch_live_finish(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, int parity, const Dir& hd,
-                        uint32_t gen, hipStream_t s) {
-    IngestArgs A{};
-    A.T = v.txn_count; A.R = v.read_count; A.W = v.write_count;
-    A.keys = b.keys; A.sc = sc; A.hd = hd;
-    const SortJobs J = make_sort_jobs(v, b, sc, parity);
-    const LiveOut O{b.lv_wkeys, b.lv_wkoff, b.lv_wklen, 0, 0, 0, 0};
-    const int w_blocks = std::max(1, cdiv((int64_t)v.write_count, 256));  // (bmax2: k_live_ingest did it)
-    hipLaunchKernelGGL(k_live_finish, dim3(w_blocks), dim3(256), 0, s, A, J, b.staged, O, w_blocks, gen);
 }
 
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {
@@ -1987,11 +1945,12 @@ struct WriteSearchArgs {
     int64_t v0;
     WriteHits wh;
     const int32_t* qx;  // large batches: directory entry of every write endpoint (k_dir_join; index R + slot - 2R)
+    int64_t wbase;      // slot of write 0's begin (write_base)
 };
 
 __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<RC_G>& g, int w) {
     if (w >= A.W) return;
-    const int64_t s = 2 * (int64_t)A.R + 2 * (int64_t)w;
+    const int64_t s = A.wbase + 2 * (int64_t)w;
     const Key b = A.keys.get(s), e = A.keys.get(s + 1);
     const int D = A.sc->D;
     DirHit hb, he;
@@ -2049,6 +2008,7 @@ struct EdgesArgs {
     const int32_t* wcov;  // [2W] write cover at each sorted write endpoint (rounds mode)
     uint32_t* rstamp;  // [R] batch stamp of reads already on plist
     uint32_t rseq;     // this batch's stamp
+    int64_t wbase;     // slot of write 0's begin (write_base)
 };
 
 // The two searches of an edge lane: an LDS sample of the sorted array's first
@@ -2154,13 +2114,13 @@ __device__ inline void rounds_lane(const EdgesArgs& A, int i, const uint64_t* sm
         const int p = i - R;
         const SRec x = A.sw[p];
         A.wnew[p] = p == 0 || !rec_key_eq(A.sw[p - 1], x, tails);
-        A.winv[x.idx - 2 * (int64_t)R] = p;
+        A.winv[x.idx - A.wbase] = p;
     }
 }
 
 __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp_r, const uint64_t* smp_w) {
     const int R = A.R, W = A.W;
-    const int64_t wbase = 2 * (int64_t)R;
+    const int64_t wbase = A.wbase;
     const uint8_t* const* tails = A.keys.tail;
     if (A.rq) {
         rounds_lane(A, i, smp_w);
@@ -2326,7 +2286,7 @@ __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
     __shared__ uint64_t s_hi[MS_CHUNK], s_lo[MS_CHUNK], s_mi[MS_CHUNK];
     __shared__ int s_cut[2];
     const int R = A.R, nw = 2 * A.W;
-    const int64_t wbase = 2 * (int64_t)R;
+    const int64_t wbase = A.wbase;
     const uint8_t* const* tails = A.keys.tail;
     const SRec* sr = A.sr;
     const SRec* sw = A.sw;
@@ -2416,7 +2376,7 @@ void launch_write_search(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, i
     b.ws_deferred = false;
     const int R = v.read_count, W = v.write_count;
     if (W == 0) return;
-    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, nullptr};
+    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, nullptr, write_base(b, v)};
     hipLaunchKernelGGL(k_write_search, dim3(cdiv((int64_t)W * RC_G, 256)), dim3(256), 0, s, WA);
 }
 
@@ -2437,8 +2397,8 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
     EdgesArgs EA{R,     W,    b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
                  b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv,
-                 b.wcov, b.rstamp, b.rseq};
-    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx};
+                 b.wcov, b.rstamp, b.rseq, write_base(b, v)};
+    WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx, write_base(b, v)};
     // (rc_fused: the history read check already ran in the sort's bucket launch)
     const int rc_blocks = b.rc_fused ? 0 : cdiv((int64_t)R * RC_G, 256);
     b.rc_fused = false;
@@ -2519,6 +2479,7 @@ struct RoundArgs {
     // blocks 1.. of the launch: the merge's write searches (deferred by the
     // read check), beside the decision in block 0, which holds one CU
     WriteSearchArgs ws;
+    int64_t wbase;  // slot of write 0's begin (write_base)
 };
 
 static constexpr int DC_THREADS = 1024;
@@ -2601,7 +2562,7 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     uint16_t* r16 = reinterpret_cast<uint16_t*>(cwb + wwords);  // ranks: P u16 first, then val / stab
     uint2* litems = reinterpret_cast<uint2*>(r16 + ((rank_words16(P) + 3) & ~3));  // lcap items
     Scalars* sc = A.sc;
-    const int64_t wbase = 2 * (int64_t)R;
+    const int64_t wbase = A.wbase;
     int ncand = 0;
     PHASE(sc, 0);
 
@@ -3001,7 +2962,7 @@ __global__ __launch_bounds__(CB_THREADS) void k_comb_emit(CombArgs A) {
 static void launch_combine_grid(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, hipStream_t s) {
     const int P = 2 * v.write_count;
     const int nblk = cdiv(P, CB_BLOCK);
-    CombArgs C{P, 2 * (int64_t)v.read_count, b.sw_slot, b.write_txn, b.committed, b.comb_blk,
+    CombArgs C{P, write_base(b, v), b.sw_slot, b.write_txn, b.committed, b.comb_blk,
                b.comb_blk + nblk + 1, b.cb_pos, b.ce_pos, sc};
     hipLaunchKernelGGL(k_comb_sum, dim3(nblk), dim3(CB_THREADS), 0, s, C);
     hipLaunchKernelGGL(k_comb_open, dim3(nblk), dim3(CB_THREADS), 0, s, C);
@@ -3180,6 +3141,7 @@ bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     }
     RoundArgs A;
     A.T = T; A.R = v.read_count; A.W = v.write_count;
+    A.wbase = write_base(b, v);
     A.combine = multi ? 0 : 1;
     const size_t base = rounds_lds_base(T, v.write_count);
     A.lcap = (int)std::min<int64_t>((int64_t)(ROUNDS_LDS_MAX - base) / 8, (int64_t)v.read_count + v.write_count);
@@ -3195,7 +3157,8 @@ bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
     int wsb = 0;  // the deferred write searches ride in the same launch
     if (h && b.ws_deferred && v.write_count > 0) {
         b.ws_deferred = false;
-        A.ws = WriteSearchArgs{v.read_count, v.write_count, b.keys, h->pool, h->dir[cur], sc, v0, b.wh, nullptr};
+        A.ws = WriteSearchArgs{v.read_count, v.write_count, b.keys, h->pool, h->dir[cur], sc, v0, b.wh, nullptr,
+                               write_base(b, v)};
         wsb = cdiv((int64_t)v.write_count * RC_G, DC_THREADS);
     }
     hipLaunchKernelGGL(k_decide_rounds, dim3(1 + wsb), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);

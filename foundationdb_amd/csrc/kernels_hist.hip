@@ -1247,7 +1247,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
     if (W > 0) {
         hipLaunchKernelGGL(k_plan_ranges, dim3(cdiv(W, 256)), dim3(256), 0, s, (const int32_t*)b.cb_pos,
                            (const int32_t*)b.ce_pos, (const SRec*)b.sw, (const uint8_t* const*)b.keys.tail, b.wh,
-                           2 * (int64_t)v.read_count, v0, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
+                           write_base(b, v), v0, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
     hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
