@@ -1,5 +1,6 @@
 // stage.hip -- host staging of the per-transaction path (see stage.h).
 #include "stage.h"
+#include "stage_pack.h"
 
 #include <immintrin.h>
 
@@ -25,72 +26,7 @@ unsigned stream_flags(uint64_t bytes) {
 }
 #endif
 
-// ~70,000 short keys per config-2 batch: inline word compares and copies
-// instead of a libc call per key (measured: 185 -> ~110 us per batch).
-inline uint64_t ld64(const uint8_t* p) {
-    uint64_t x;
-    memcpy(&x, p, 8);
-    return x;
-}
-
-// the reference's key order (SkipList.cpp:113-120), eight bytes at a time;
-// -2: a is a proper prefix of b (so a < b)
-__attribute__((always_inline)) inline int key_cmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
-    const uint32_t n = std::min(al, bl);
-    uint32_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        const uint64_t x = ld64(a + i), y = ld64(b + i);
-        if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y) ? -1 : 1;
-    }
-    for (; i < n; i++)
-        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-    return al < bl ? -2 : (al > bl ? 1 : 0);
-}
-
-// copy n bytes; reads and writes stay inside the n bytes
-__attribute__((always_inline)) inline void copy_small(uint8_t* d, const uint8_t* s, uint32_t n) {
-    if (n >= 16 && n <= 32) {
-        uint8_t t0[16], t1[16];
-        memcpy(t0, s, 16);
-        memcpy(t1, s + n - 16, 16);
-        memcpy(d, t0, 16);
-        memcpy(d + n - 16, t1, 16);
-    } else if (n >= 8 && n < 16) {
-        const uint64_t x = ld64(s), y = ld64(s + n - 8);
-        memcpy(d, &x, 8);
-        memcpy(d + n - 8, &y, 8);
-    } else if (n > 32) {
-        memcpy(d, s, n);
-    } else {
-        for (uint32_t i = 0; i < n; i++) d[i] = s[i];
-    }
-}
-
-// check and copy ranges into the record at rec: entries (where the keys are,
-// their lengths) and the key bytes at kp (advanced); true if some range has
-// begin >= end.  A point range [k, k\x00) is written as k\x00 once
-// (kernels.h STAGE_SHARED): the begin < end compare already tells it.
-__attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int n, StageRange* ent,
-                                                      const uint8_t* rec, uint8_t*& kp) {
-    bool bad = false;
-    for (int i = 0; i < n; i++) {
-        const uint8_t *b = rg[i].begin, *e = rg[i].end;
-        const uint32_t bl = rg[i].begin_len, el = rg[i].end_len;
-        const int c = key_cmp(b, bl, e, el);
-        bad |= c >= 0;
-        copy_small(kp, b, bl);
-        if (c == -2 && el == bl + 1 && e[bl] == 0) {  // point range: k then one 0 byte
-            ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)(el | STAGE_SHARED)};
-            kp[bl] = 0;
-            kp += bl + 1;
-        } else {
-            ent[i] = StageRange{(uint32_t)(kp - rec), (uint16_t)bl, (uint16_t)el};
-            copy_small(kp + bl, e, el);
-            kp += bl + el;
-        }
-    }
-    return bad;
-}
+using fdbcs_pack::put_ranges;
 
 }  // namespace
 
@@ -285,8 +221,8 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     uint8_t* p = pin_ + used_;
     StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
     uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)n;
-    bool bad = put_ranges(reads, nr, ent, p, kp);
-    bad |= put_ranges(writes, nw, ent + nr, p, kp);
+    bool bad = put_ranges<StageRange, STAGE_SHARED>(reads, nr, ent, p, kp);
+    bad |= put_ranges<StageRange, STAGE_SHARED>(writes, nw, ent + nr, p, kp);
     if (bad) return FDBCS_E_RANGE;  // (the record is not committed: used_ stays)
     const uint64_t rec_used = ((uint64_t)(kp - p) + 7) & ~uint64_t(7);  // (<= rec: point ranges share bytes)
     const StageHdr h{snap, (int32_t)R_, (int32_t)W_, nr, nw};

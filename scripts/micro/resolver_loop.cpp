@@ -22,7 +22,9 @@ int main(int argc, char** argv) {
     if (fdbcs_create(&cs, 0, &c)) return 1;
     fdbwl* g = fdbwl_create(cfg, 0, 0);
     if (fdbwl_prefill(g, cs, 0, prefill)) return 2;
-    if (argc > 5 && atoi(argv[5]) == 2) {  // add_micro's synthetic point ranges through fdbcs_batch_add
+    if (argc > 5 && atoi(argv[5]) >= 2) {  // add_micro's synthetic point ranges through fdbcs_batch_add
+        // (mode 3: one read in five a short range [k, k + 1..16), as config 2's)
+        const bool mixed = atoi(argv[5]) == 3;
         const int T = 5000;
         std::vector<uint8_t> bytes((size_t)T * 7 * 34);
         std::vector<fdbcs_range> rd(T * 5), wr(T * 2);
@@ -35,7 +37,11 @@ int main(int argc, char** argv) {
             }
             memcpy(p + 17, p, 16);
             p[33] = 0;
-            const fdbcs_range rg{p, 16, p + 17, 17};
+            fdbcs_range rg{p, 16, p + 17, 17};
+            if (mixed && r < T * 5 && (x >> 40) % 5 == 0 && p[15] < 0xF0) {
+                p[17 + 15] = (uint8_t)(p[15] + 1 + (x >> 50) % 15);
+                rg.end_len = 16;
+            }
             if (r < T * 5) rd[r] = rg; else wr[r - T * 5] = rg;
         }
         double a = 0;
@@ -46,7 +52,7 @@ int main(int argc, char** argv) {
             if (st) return 4;
             if (i >= 5) a += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
-        printf("synthetic points via fdbcs_batch_add: %.1f us\n", a / (steps - 5));
+        printf("synthetic %s via fdbcs_batch_add: %.1f us\n", mixed ? "points + 1/5 short reads" : "points", a / (steps - 5));
         return 0;
     }
     if (argc > 5 && atoi(argv[5])) {  // the same batch over and over (warm caches and TLB)
