@@ -300,6 +300,7 @@ struct Scalars {
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;
+constexpr uint64_t LV_FINAL_BIT = 1ull << 63;  // in the host's published word (stage.h prog_[0])
 // gen: 10 bits (another batch's word reads as "nothing yet"), state: 2,
 // transactions: 20 (live batches have T <= LARGE_T), bytes: 32 (the live
 // stream stays below 4 GB)

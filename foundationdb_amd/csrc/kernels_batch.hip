@@ -1000,7 +1000,22 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                 const uint64_t st = host_load(V.prog + 2);
                 const uint64_t pw = host_load(V.prog);  // (one word: the count and the bytes stay consistent)
                 const int64_t pub = (int64_t)(pw & 0xFFFFF);
-                const uint64_t used = pw >> 20;
+                const uint64_t used = (pw & ~LV_FINAL_BIT) >> 20;
+                if (pw & LV_FINAL_BIT) {  // the batch is whole: its last T and bytes are this word's
+                    PSET(sc, 10);
+                    lv_store(&sc->lv_pub, lv_word(gen, LV_FINAL, (uint64_t)pub, used));
+                    // (then the read and write counts, a round trip later, off the workers' path)
+                    const int32_t R = (int32_t)host_load(V.prog + 4), W = (int32_t)host_load(V.prog + 5);
+                    lv_store(&sc->lv_R, R);
+                    lv_store(&sc->lv_W, W);
+                    if (pub <= (int64_t)V.O.capT) {
+                        V.S.view.ro[pub] = R;
+                        V.S.view.wo[pub] = W;
+                    } else {
+                        atomicCAS(&sc->err, 0, FDBCS_E_STATE);
+                    }
+                    break;
+                }
                 if (st != LV_RUNNING) {
                     PSET(sc, 10);
                     uint64_t w = lv_word(gen, LV_CANCEL, 0, 0);

@@ -127,8 +127,8 @@ class TxnStage {
     int64_t pub_every_ = 16;      // FDBCS_LIVE_PUB: transactions per progress word
     int64_t next_pub_ = 0;
     // host-mapped progress: [0] published bytes << 20 | published T (one
-    // word), [1] final stream bytes, [2] state (LV_RUNNING / LV_FINAL /
-    // LV_CANCEL), [3..5] final T, R, W
+    // word; LV_FINAL_BIT once the batch is whole), [1] final stream bytes,
+    // [2] state (LV_RUNNING / LV_FINAL / LV_CANCEL), [3..5] final T, R, W
     uint64_t* prog_ = nullptr;
     uint64_t* prog_dev_ = nullptr;
 };

@@ -366,6 +366,10 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
         prog_[5] = (uint64_t)W_;
         prog_[1] = used_;
         if (bar_) _mm_sfence();
+        // the published word itself says final (LV_FINAL_BIT): the kernel's
+        // poller sees the last T and bytes in the one word it polls, a PCIe
+        // round trip sooner than by reading [3] and [1] after the state
+        __atomic_store_n(&prog_[0], LV_FINAL_BIT | (uint64_t)used_ << 20 | (uint64_t)T_, __ATOMIC_RELEASE);
         __atomic_store_n(&prog_[2], (uint64_t)LV_FINAL, __ATOMIC_RELEASE);
         live_ = false;
         dv = fdbcs_batch_view{};
