@@ -530,6 +530,7 @@ __global__ __launch_bounds__(1024) void k_ss_sample(SortJobs J, KeyArrays keys, 
 // made even the usual immediate return cost ~4.6 us): the rare resample sorts
 // its sample in global scratch (3 * SS_S words per job).
 __global__ __launch_bounds__(1024) void k_ss_guard(SortJobs J, KeyArrays keys, uint64_t* scratch) {
+    PHASE(J.sc, 12);  // (FDBCS_PHASES builds: the first launch after the live kernel, scripts/diag_live.py)
     uint64_t* g = scratch + (int64_t)blockIdx.x * 3 * SS_S;
     ss_sample_job(J, keys, LdsRecs{g, g + SS_S, g + 2 * SS_S}, 1);
 }

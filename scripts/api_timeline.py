@@ -74,7 +74,7 @@ def main():
         agg["detect"].append(t1 - ta)
         ev = [e for e in dev if ta - 400_000 <= e[0] <= t1]
         ks = [e for e in ev if e[2].startswith("K ") and e[0] >= ta - 50_000]
-        ing = [e for e in ks if ("ingest" in e[2] or "live_finish" in e[2]) and e[0] >= ta]
+        ing = [e for e in ks if "ingest" in e[2] and e[0] >= ta]
         live = [e for e in ev if "k_live_ingest" in e[2] and e[0] <= ta]
         if live:  # (live ingest: the kernel began at fdbcs_batch_begin, before the adds ended)
             agg["live_ingest_end-adds_end"].append(live[-1][1] - ta)

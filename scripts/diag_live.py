@@ -44,14 +44,14 @@ def main():
                 us[j], add[j] = u[0], a_[0]
                 cs._lib.fdbcs_debug_phases(cs.handle, phases, 32)
                 p = np.array(phases[:32], np.int64)
-                # final seen -> last wave out, last wave out -> k_live_finish, poller start -> final seen;
+                # final seen -> last wave out, last wave out -> k_ss_guard's start, poller start -> final seen;
                 # the last group: final -> its start, its acquire, toff + window, its ranges
                 ph.append(((p[11] - p[10]) * 0.01, (p[12] - p[11]) * 0.01, (p[10] - p[13]) * 0.01,
                            (p[20] - p[10]) * 0.01, (p[21] - p[20]) * 0.01, (p[22] - p[21]) * 0.01,
                            (p[23] - p[22]) * 0.01, (p[11] - p[23]) * 0.01))
             ph = np.array(ph)
             m = ph.mean(axis=0)
-            print(f"   live phases (us, mean): final->last wave out {m[0]:.1f}, last wave out->finish start "
+            print(f"   live phases (us, mean): final->last wave out {m[0]:.1f}, last wave out->guard start "
                   f"{m[1]:.1f}, kernel start->final {m[2]:.1f}; last group: final->start {m[3]:.1f}, acquire "
                   f"{m[4]:.1f}, toff+window {m[5]:.1f}, ranges {m[6]:.1f}, end->last wave out {m[7]:.1f}")
         else:
