@@ -1177,25 +1177,143 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
                 s_r4[2 * e + 1] = make_uint4(x[q].meta, x[q].idx, 0, 0);
             }
         }
+        // Long-key buckets (config 4: a 64-byte tenant prefix): when every
+        // record ties on its first 17 bytes, each compare below would read two
+        // tails from global memory.  Instead the tail words all records share
+        // are skipped once -- W: the first tail word where some record differs
+        // from record 0 -- and the 16 bytes from there rank the records from
+        // LDS (zero past a key's end; equal words and both keys ending inside
+        // them: length, then the tie rule; a key longer than that: the full
+        // compare).
+        const uint64_t h0 = __shfl(x[0].hi, 0), l0 = __shfl(x[0].lo, 0);
+        const uint32_t m0 = (uint32_t)__shfl((int)x[0].meta, 0), i0 = (uint32_t)__shfl((int)x[0].idx, 0);
+        bool same = true;
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            if (lane + 64 * q < c)
+                same &= (x[q].hi == h0) & (x[q].lo == l0) & ((x[q].meta >> 24) == (m0 >> 24)) &
+                        (key_len(x[q].meta) > 17);
+        const bool longb = c > 1 && key_len(m0) > 17 && __ballot(!same) == 0;  // (wave-uniform)
+        uint64_t* s_t = s_buf + 4 * (SS_WAVE + 8);  // (after the records' 2 uint4 each, read 8 past c)
+        static_assert(4 * (SS_WAVE + 8) + 2 * (SS_WAVE + 8) <= 3 * SS_ROW, "long-key staging");
+        uint64_t xt[2][2] = {{0, 0}, {0, 0}};
+        uint32_t lim = 0;  // keys up to this long end inside the ranked 16 bytes
+        if (longb) {
+            auto tail_words = [](uint32_t meta) { return (key_len(meta) - 17 + 7) >> 3; };
+            const uint64_t* t0 = reinterpret_cast<const uint64_t*>(tails[i0]);
+            const uint32_t n0 = tail_words(m0);
+            uint32_t wmin = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                if (lane + 64 * q >= c) continue;
+                const uint64_t* t = reinterpret_cast<const uint64_t*>(tails[x[q].idx]);
+                const uint32_t nm = min(tail_words(x[q].meta), n0);
+                uint32_t w = 0;
+                while (w < nm) {  // (four independent loads a step)
+                    uint64_t a[4], z[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const bool ok = w + k < nm;
+                        a[k] = ok ? t[w + k] : 0;
+                        z[k] = ok ? t0[w + k] : 0;
+                    }
+                    int d = 4;
+#pragma unroll
+                    for (int k = 3; k >= 0; k--)
+                        if (a[k] != z[k]) d = k;
+                    if (d < 4) {
+                        w += d;
+                        break;
+                    }
+                    w += 4;
+                }
+                wmin = min(wmin, min(w, nm));
+            }
+            const uint32_t W = wave_reduce_min(wmin);
+            lim = 17 + 8 * (W + 2);
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int e = lane + 64 * q;
+                if (e >= c) continue;
+                const uint64_t* t = reinterpret_cast<const uint64_t*>(tails[x[q].idx]);
+                const uint32_t n = tail_words(x[q].meta);
+                xt[q][0] = W < n ? __builtin_bswap64(t[W]) : 0;
+                xt[q][1] = W + 1 < n ? __builtin_bswap64(t[W + 1]) : 0;
+                s_t[2 * e] = xt[q][0];
+                s_t[2 * e + 1] = xt[q][1];
+            }
+        }
         const int64_t c2 = PCLK();
         const int64_t c2b = c2;
         __syncthreads();
+        // (a long-key bucket's order from the ranked words: -1 / 1, or 0 when
+        // they tie and a key runs past them -- resolved after the loop, every
+        // lane's ties at once, instead of a wave-wide stall on each record a
+        // lane ties with: a point write's begin k and end k\x00 always do)
+        auto long_cmp = [&](uint64_t a0, uint64_t a1, const SRec& a, uint64_t b0, uint64_t b1, const SRec& bb) {
+            if (a0 != b0) return a0 < b0 ? -1 : 1;
+            if (a1 != b1) return a1 < b1 ? -1 : 1;
+            const uint32_t la = key_len(a.meta), lb = key_len(bb.meta);
+            if (la > lim || lb > lim) return 0;
+            if (la != lb) return la < lb ? -1 : 1;
+            const uint32_t pa = a.idx & 1, pb = bb.idx & 1;
+            return (pa != pb ? pa > pb : a.idx < bb.idx) ? -1 : 1;
+        };
         int rank[2] = {0, 0}, dsum[2] = {0, 0};
-        for (int j0 = 0; j0 < c; j0 += 8) {  // eight records per round: their LDS reads overlap
-            SRec y[8];
+        auto rec_at = [&](int j) {
+            const uint4 a = s_r4[2 * j], m = s_r4[2 * j + 1];
+            return SRec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), m.x, m.y, 0};
+        };
+        if (!longb) {
+            for (int j0 = 0; j0 < c; j0 += 8) {  // eight records per round: their LDS reads overlap
+                SRec y[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint4 a = s_r4[2 * (j0 + u)], m = s_r4[2 * (j0 + u) + 1];
-                y[u] = SRec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), m.x, m.y, 0};
+                for (int u = 0; u < 8; u++) y[u] = rec_at(j0 + u);
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < c)
+#pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            const bool lt = (lane + 64 * q < c) && rec_lt(y[u], x[q], tails);
+                            rank[q] += lt;
+                            dsum[q] += lt ? delta(y[u].idx) : 0;
+                        }
             }
+        } else {
+            constexpr int NPEND = 4;
+            int pend[2][NPEND], np[2] = {0, 0};
+            for (int j0 = 0; j0 < c; j0 += 8) {
+                SRec y[8];
+                uint64_t yt[8][2];
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (j0 + u < c)
+                for (int u = 0; u < 8; u++) {
+                    y[u] = rec_at(j0 + u);
+                    yt[u][0] = s_t[2 * (j0 + u)];
+                    yt[u][1] = s_t[2 * (j0 + u) + 1];
+                }
 #pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const bool lt = (lane + 64 * q < c) && rec_lt(y[u], x[q], tails);
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < c)
+#pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            bool lt = false;
+                            if (lane + 64 * q < c) {
+                                const int r = long_cmp(yt[u][0], yt[u][1], y[u], xt[q][0], xt[q][1], x[q]);
+                                if (r == 0 && np[q] < NPEND) pend[q][np[q]++] = j0 + u;
+                                else lt = r == 0 ? rec_lt(y[u], x[q], tails) : r < 0;
+                            }
+                            rank[q] += lt;
+                            dsum[q] += lt ? delta(y[u].idx) : 0;
+                        }
+            }
+            for (int k = 0; k < NPEND; k++)  // (the ties: full compares, all lanes together)
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    if (k < np[q]) {
+                        const SRec y = rec_at(pend[q][k]);
+                        const bool lt = rec_lt(y, x[q], tails);
                         rank[q] += lt;
-                        dsum[q] += lt ? delta(y[u].idx) : 0;
+                        dsum[q] += lt ? delta(y.idx) : 0;
                     }
         }
         const int64_t c3 = PCLK();

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/kt_ab
 for v in "$@"; do
   rm -rf /tmp/kt_$v
   LD_LIBRARY_PATH=$PWD/scripts/micro/var/$v timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d /tmp/kt_$v -o run -- ./scripts/micro/resolver_loop 2500 100 2 0 > gpurun_out/kt_ab/$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/kt_ab/$v.log; exit 1; }
+    -d /tmp/kt_$v -o run -- ./scripts/micro/resolver_loop ${PREFILL:-2500} 100 ${CFG:-2} 0 > gpurun_out/kt_ab/$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/kt_ab/$v.log; exit 1; }
   kt=$(find /tmp/kt_$v -name "*kernel_trace.csv" | head -1)
   # (the live batches only: dispatches from the first k_live_ingest on)
   echo "== $v"; python3 -c "
