@@ -2632,7 +2632,7 @@ __device__ __host__ inline int64_t rank_words16(int64_t P) {  // val + stab + th
 
 __host__ __device__ inline size_t rounds_lds_base(int64_t T, int64_t W) {
     const int64_t P = 2 * W;
-    const int64_t bits = 3 * ((T + 31) / 32) + (W + 31) / 32;
+    const int64_t bits = 4 * ((T + 31) / 32) + (W + 31) / 32;
     return (size_t)(4 * bits + 2 * rank_words16(P) + 64);
 }
 
@@ -2692,16 +2692,25 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     uint32_t* ubits = lds;              // U
     uint32_t* cbits = lds + nwords;     // the candidate committed set; C* at the end
     uint32_t* nbits = cbits + nwords;   // conflicts found this round
-    uint32_t* cwb = nbits + nwords;     // committed, per write (combine)
+    uint32_t* tbits = nbits + nwords;   // too old (the verdicts read it here, not from global memory)
+    uint32_t* cwb = tbits + nwords;     // committed, per write (combine)
     uint16_t* r16 = reinterpret_cast<uint16_t*>(cwb + wwords);  // ranks: P u16 first, then val / stab
     uint2* litems = reinterpret_cast<uint2*>(r16 + ((rank_words16(P) + 3) & ~3));  // lcap items
     Scalars* sc = A.sc;
     const int64_t wbase = A.wbase;
     int ncand = 0;
     PHASE(sc, 0);
+    // (the flag's error words, final before this launch: loaded now, off the
+    // way from the verdicts to the flag)
+    uint32_t eo_err = 0, eo_last = 0, eo_lm = 0;
+    if (A.eo.flag && tid == 0) {
+        eo_err = (uint32_t)sc->err;
+        eo_last = (uint32_t)sc->last_err;
+        eo_lm = (uint32_t)sc->lm_count;  // (the ingest's load-metrics entries, if a sample is attached)
+    }
 
     // ---- U: 4 transactions per lane from one 4-byte load of each flag array ----
-    for (int i = tid; i < nwords; i += nthr) nbits[i] = 0;
+    for (int i = tid; i < nwords; i += nthr) nbits[i] = tbits[i] = 0;
     if (tid == 0) s_nw = s_nr = 0;
     const bool wide = sc->dec_wide != 0;
     const int npot = wide ? R : (int)min((int64_t)sc->n_pot, A.lcap_list);
@@ -2709,10 +2718,14 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     for (int t4 = tid; 4 * t4 < T; t4 += nthr) {
         const uint32_t to = reinterpret_cast<const uint32_t*>(A.too_old)[t4];
         const uint32_t hs = reinterpret_cast<const uint32_t*>(A.hist)[t4];
-        uint32_t m = 0;
+        uint32_t m = 0, mt = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) m |= (uint32_t)(4 * t4 + k < T && !(((to | hs) >> (8 * k)) & 0xFF)) << k;
+        for (int k = 0; k < 4; k++) {
+            m |= (uint32_t)(4 * t4 + k < T && !(((to | hs) >> (8 * k)) & 0xFF)) << k;
+            mt |= (uint32_t)(4 * t4 + k < T && ((to >> (8 * k)) & 0xFF)) << k;
+        }
         if (m) atomicOr(&nbits[t4 >> 3], m << (4 * (t4 & 7)));
+        if (mt) atomicOr(&tbits[t4 >> 3], mt << (4 * (t4 & 7)));
     }
     __syncthreads();
     for (int i = tid; i < nwords; i += nthr) {
@@ -2872,13 +2885,12 @@ decided:
         const bool al16 = ((reinterpret_cast<uintptr_t>(A.verdict) | reinterpret_cast<uintptr_t>(A.committed)) & 15) == 0;
         for (int t0 = 16 * tid; t0 < T; t0 += 16 * nthr) {
             const uint32_t cw = cbits[t0 >> 5] >> (t0 & 31);  // (t0 % 32 is 0 or 16; bits past T are 0)
-            const uint4 to4 = *reinterpret_cast<const uint4*>(A.too_old + t0);  // (too_old is padded by 64 bytes)
-            const uint32_t tw[4] = {to4.x, to4.y, to4.z, to4.w};
+            const uint32_t tw = tbits[t0 >> 5] >> (t0 & 31);
             uint32_t vw[4] = {0, 0, 0, 0}, cm[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const uint32_t c = (cw >> k) & 1;
-                const uint32_t v = c ? FDBCS_COMMITTED : (((tw[k >> 2] >> (8 * (k & 3))) & 0xFF) ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
+                const uint32_t v = c ? FDBCS_COMMITTED : (((tw >> k) & 1) ? FDBCS_TOO_OLD : FDBCS_CONFLICT);
                 vw[k >> 2] |= v << (8 * (k & 3));
                 cm[k >> 2] |= c << (8 * (k & 3));
             }
@@ -2900,9 +2912,9 @@ decided:
         // workgroup ended (the host saw the flag ~19 us late, after the
         // combine below)
         if (tid == 0) {
-            A.eo.flag[1] = (uint32_t)sc->err;
-            A.eo.flag[2] = (uint32_t)sc->last_err;
-            A.eo.flag[3] = (uint32_t)sc->lm_count;  // (the ingest's load-metrics entries, if a sample is attached)
+            A.eo.flag[1] = eo_err;
+            A.eo.flag[2] = eo_last;
+            A.eo.flag[3] = eo_lm;
         }
         __threadfence_system();
         __syncthreads();
