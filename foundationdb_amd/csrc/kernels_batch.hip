@@ -2907,10 +2907,9 @@ decided:
     }
     if (A.eo.flag) {
         // host-mapped verdicts: every lane's stores and the error words, a
-        // system-scope fence, then the flag -- itself pushed out with a second
-        // fence: a plain store after the first fence stayed in L2 until the
-        // workgroup ended (the host saw the flag ~19 us late, after the
-        // combine below)
+        // system-scope fence, then the flag (a plain store after the fence
+        // stayed in L2 until the workgroup ended: the host saw the flag ~19 us
+        // late, after the combine below)
         if (tid == 0) {
             A.eo.flag[1] = eo_err;
             A.eo.flag[2] = eo_last;
@@ -2919,8 +2918,15 @@ decided:
         __threadfence_system();
         __syncthreads();
         if (tid == 0) {
+#ifndef FDBCS_FLAG_STORE
+            // the flag as a system-scope exchange: an atomic is performed at
+            // the host's memory, so nothing holds it back and no second fence
+            // is needed (flag 1.7 us sooner by the decision's own clock)
+            (void)__hip_atomic_exchange(A.eo.flag, A.eo.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else  // (A/B: the store and a second fence, round 4's first form)
             __hip_atomic_store(A.eo.flag, A.eo.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             __threadfence_system();
+#endif
         }
     }
     PHASE(sc, 1);
