@@ -836,6 +836,7 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
     const int ntot = __builtin_amdgcn_readlane(incl, STG_TPW - 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wavefront's LDS writes, read below)
     __builtin_amdgcn_wave_barrier();
+    if (LIVE && lane == 0) PMAX(A.sc, 14);
     const uint8_t* const* tails = A.keys.tail;
     // ---- the wavefront's ranges, one per lane
     for (int k = lane; k < ntot; k += 64) {
@@ -886,6 +887,7 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
             }
         }
     }
+    if (LIVE && lane == 0) PMAX(A.sc, 15);  // (the ranges issued; their stores drain before ph[23])
 }
 
 template <bool SCATTER>

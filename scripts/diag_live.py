@@ -48,12 +48,14 @@ def main():
                 # the last group: final -> its start, its acquire, toff + window, its ranges
                 ph.append(((p[11] - p[10]) * 0.01, (p[12] - p[11]) * 0.01, (p[10] - p[13]) * 0.01,
                            (p[20] - p[10]) * 0.01, (p[21] - p[20]) * 0.01, (p[22] - p[21]) * 0.01,
-                           (p[23] - p[22]) * 0.01, (p[11] - p[23]) * 0.01))
+                           (p[23] - p[22]) * 0.01, (p[11] - p[23]) * 0.01,
+                           (p[14] - p[22]) * 0.01, (p[15] - p[14]) * 0.01, (p[23] - p[15]) * 0.01))
             ph = np.array(ph)
             m = ph.mean(axis=0)
             print(f"   live phases (us, mean): final->last wave out {m[0]:.1f}, last wave out->guard start "
                   f"{m[1]:.1f}, kernel start->final {m[2]:.1f}; last group: final->start {m[3]:.1f}, acquire "
-                  f"{m[4]:.1f}, toff+window {m[5]:.1f}, ranges {m[6]:.1f}, end->last wave out {m[7]:.1f}")
+                  f"{m[4]:.1f}, toff+window {m[5]:.1f}, ranges {m[6]:.1f} (headers {m[8]:.1f}, range issue "
+                  f"{m[9]:.1f}, store drain {m[10]:.1f}), end->last wave out {m[7]:.1f}")
         else:
             us, add, _ = r.run(cs, verdicts=False)
         nxt += per
