@@ -192,3 +192,54 @@ def test_live_resolver_loop(gpu):
     st = g.batch_stats()
     assert st["live_batches"] >= nb - 2, st
     g.close()
+
+
+def test_last_device_batch_after_live(gpu):
+    """A live batch lays its writes out after a gap (slot 2 caps.R + 2w,
+    BatchBufs::lv_wbase); fdbcs_last_device_batch hands out the view's own
+    layout (writes from 2R), moving the write entries down on the call.  The
+    exported view, read back from the device, holds every range of the batch
+    in order: reads at 2r, 2r + 1, writes at 2R + 2w, 2R + 2w + 1."""
+    import ctypes as C
+
+    from foundationdb_amd import _abi
+
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+
+    def d2h(ptr, nbytes, dtype):
+        out = np.empty(max(nbytes, 1), np.uint8)
+        if nbytes:
+            assert hip.hipMemcpy(out.ctypes.data, ptr, nbytes, 4) == 0  # (hipMemcpyDefault)
+        return out[:nbytes].view(dtype)
+
+    g = live_cs()
+    lib = _abi.lib()
+    checked, live_before = 0, 0
+    for batch, now, nold in mixed_stream(23, n_batches=10, max_txns=400, keyspace=3000):
+        run_batch(g, batch, now, nold)
+        live_now = g.batch_stats()["live_batches"]
+        was_live, live_before = live_now > live_before, live_now
+        if not was_live:
+            continue
+        v = _abi.BatchView()
+        _abi.check(lib.fdbcs_last_device_batch(g.handle, C.byref(v)), "fdbcs_last_device_batch")
+        R, W = v.read_count, v.write_count
+        slots = 2 * (R + W)
+        koff = d2h(v.key_off, 8 * slots, np.uint64)
+        klen = d2h(v.key_len, 4 * slots, np.uint32)
+        kb = d2h(v.key_bytes, int(v.key_bytes_len), np.uint8)
+        reads = [r for _, rs, _ in batch.txns() for r in rs]
+        writes = [w for _, _, ws in batch.txns() for w in ws]
+        assert (len(reads), len(writes)) == (R, W)
+
+        def key(s):
+            return kb[int(koff[s]):int(koff[s]) + int(klen[s])].tobytes()
+
+        for r, (b, e) in enumerate(reads):
+            assert (key(2 * r), key(2 * r + 1)) == (bytes(b), bytes(e)), ("read", r)
+        for w, (b, e) in enumerate(writes):
+            assert (key(2 * R + 2 * w), key(2 * R + 2 * w + 1)) == (bytes(b), bytes(e)), ("write", w)
+        checked += 1
+    assert checked >= 1, g.batch_stats()
+    g.close()
