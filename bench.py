@@ -343,17 +343,22 @@ def shim_skiplisttest():
     out = r.stdout
     m = re.search(r"New conflict set:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
     d = re.search(r"Detect only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
+    vo = re.search(r"Verdicts only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
     sk = re.search(r"Skiplist only:\s*([0-9.]+) sec\s*\n\s*([0-9.]+) Mtransactions/sec", out)
     h = re.search(r"(\d+) entries in version history", out)
     if r.returncode != 0 or not m:
         return {"error": f"rc={r.returncode}", "tail": out[-300:] + r.stderr[-300:]}
     return {"new_conflict_set_mtxn_s": float(m.group(2)), "detect_only_mtxn_s": float(d.group(2)) if d else None,
+            "verdicts_only_mtxn_s": float(vo.group(2)) if vo else None,
             "skiplist_only_mtxn_s": float(sk.group(2)) if sk else None,
             "history_entries": int(h.group(1)) if h else None,
             "reference_here_mtxn_s": 0.155,
             "path": "tests/shim/shim_smoke skiplisttest: ConflictSetShim.cpp skipListTest() (config 1: 500 x 2,500 "
                     "txns) -> addTransaction / detectConflicts -> libfdbcs; 'New conflict set' includes building the "
-                    "transactions (g_buildTest) as SkipList.cpp:1456-1489 does; 'Skiplist only' = device D.CheckRead + "
+                    "transactions (g_buildTest) as SkipList.cpp:1456-1489 does; 'Detect only' = detectConflicts with its history "
+                    "update (merge + removeBefore, the reference's SkipList.cpp:1485-1487 quantity) from a stage-timed "
+                    "run; 'Verdicts only' = detectConflicts returning at the verdicts (the Resolver's wait); "
+                    "'Skiplist only' = device D.CheckRead + "
                     "D.MergeWrite from a stage-timed second run"}
 
 
@@ -413,6 +418,7 @@ def run_single(args):
           f"{time.time() - t_w:.1f}s", file=sys.stderr, flush=True)
     key_bytes = None
     seq_batches = None
+    lv0 = cs.batch_stats()  # (synchronizes: before the clock)
     if seq:
         # ---- timed: K windows, each batch generated (untimed) from the history before it ----
         us, add_us, verdicts, seq_batches = [], [], [], []
@@ -438,6 +444,11 @@ def run_single(args):
         elapsed = time.perf_counter() - t0
         del run
     H_post = cs.history_size()
+    lv1 = cs.batch_stats()
+    # how the timed batches were ingested: live (encoded during the adds,
+    # DESIGN.md §2.1), cancelled on the way, or by a timed-out live kernel
+    live = {k: lv1[f"live_{k}"] - lv0[f"live_{k}"] for k in ("batches", "cancelled", "timeouts")}
+    live["not_live"] = args.steps - live["batches"]
     value = T * args.steps / elapsed
     lat_ms = us / 1e3
     next_i = first + args.steps
@@ -644,6 +655,7 @@ def run_single(args):
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         **p99_fields(lat_ms, latency),
         "add_us_mean": round(float(np.mean(add_us)), 2),
+        "live_ingest": live,
         "latency": latency,
         "higher_is_better": True,
         "scaling": "weak",

@@ -132,7 +132,8 @@ class ConflictSet:
     # --- whole-batch entry points -------------------------------------------------
     STAT_NAMES = ("txns", "reads", "writes", "combined", "pages_merged", "dir_entries", "history", "window_pages",
                   "window_survivors", "dependents", "decision_rounds", "sort_rebucketed", "sort_max_bucket",
-                  "tail_arena_bytes", "tail_used", "tail_half", "live_batches", "live_cancelled")
+                  "tail_arena_bytes", "tail_used", "tail_half", "live_batches", "live_cancelled",
+                  "live_timeouts")
 
     def batch_stats(self):
         """Shape and outcome of the last synchronized batch (fdbcs_batch_stats)."""

@@ -222,6 +222,8 @@ struct fdbcs {
     int64_t lv_prev_T = 0, lv_prev_R = 0, lv_prev_W = 0;  // shape of the last per-transaction batch
     uint64_t lv_prev_K = 0;
     int64_t lv_done = 0, lv_cancelled = 0;  // batches ingested live / cancelled on the way (stats)
+    LiveTune lv_tune;      // the live kernel's shape (FDBCS_LIVE_BLOCKS / _SPEC / _TIMEOUT_US)
+    uint64_t lv_kb = 0;    // the key bytes the open live batch's buffers were sized for (live_begin)
 };
 
 namespace {
@@ -405,6 +407,9 @@ int grow_pool(fdbcs* cs, int64_t pages) {
         HIPOK(hipMemcpyAsync(h.dir[d].fmeta, old.dir[d].fmeta, od * 4, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].ftail, old.dir[d].ftail, od * 8, hipMemcpyDeviceToDevice, s));
         HIPOK(hipMemcpyAsync(h.dir[d].bmax, old.dir[d].bmax, (od / 64 + 2) * 8, hipMemcpyDeviceToDevice, s));
+        // (bmax2 is rebuilt by every ingest, but a live batch's was built by
+        // its kernel during the adds: run_batch may grow the pool after that)
+        HIPOK(hipMemcpyAsync(h.dir[d].bmax2, old.dir[d].bmax2, (od / BMAX2_SPAN + 2) * 8, hipMemcpyDeviceToDevice, s));
     }
     launch_sidx_build(h, cs->cur, cs->sc, s);  // index levels are laid out by capacity
     launch_push_free(h, (int32_t)cs->known_free, old.cap_pages, (int32_t)(np - old.cap_pages), s);
@@ -759,8 +764,22 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     cs->last_wbase = 0;
     // (a staged batch's keys can outnumber its stream's bytes: point ranges
     // share theirs, stage.hip)
-    const uint64_t kb = std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total);
+    const bool live = cs->b.staged.live;
+    uint64_t kb = std::max<uint64_t>(v.key_bytes_len, cs->stage_key_total);
+    if (live) {
+        // k_live_ingest wrote this batch's keys, tails and sort records during
+        // the adds: ensure_batch must not move any buffer (a moved btail left
+        // keys.tail pointing into freed memory).  live_begin sized them for
+        // the capacities the batch stayed within, stream padding included.
+        if (kb > cs->lv_kb) return FDBCS_E_STATE;
+        kb = cs->lv_kb;
+    }
+    const BatchBufs held = cs->b;
     if ((r = ensure_batch(cs, T, R, W, kb))) return r;
+    if (live && (held.btail != cs->b.btail || held.keys.hi != cs->b.keys.hi || held.keys.tail != cs->b.keys.tail ||
+                 held.ss_tmp != cs->b.ss_tmp || held.ss_bkt != cs->b.ss_bkt || held.read_txn != cs->b.read_txn ||
+                 held.write_txn != cs->b.write_txn || held.too_old != cs->b.too_old || held.wcov != cs->b.wcov))
+        return FDBCS_E_STATE;  // (cannot happen: the capacities bound every size; never compute on moved buffers)
     if ((r = ensure_history(cs, W, kb))) return r;
     if (early && (r = ensure_pinned(cs->vpin, cs->vpin_cap, vpin_scalars_off(T) + sizeof(Scalars)))) return r;
     if (early && (size_t)T + 64 > cs->vmap_cap) {
@@ -786,7 +805,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     static const bool no_fuse = getenv("FDBCS_SEPARATE_SCATTER") != nullptr;  // (A/B measurements)
     // steady state: the ingest scatters the sort records (large batches merge-sort instead)
     const bool scatter = cs->have_quantiles && !no_fuse && !b.large;
-    if (b.staged.live) {  // k_live_ingest encoded the batch during the adds (writes from b.lv_wbase)
+    if (live) {  // k_live_ingest encoded the batch during the adds (writes from b.lv_wbase)
         cs->lv_done++;
     } else {
         b.lv_wbase = 0;  // (the view's own layout: writes from 2R)
@@ -950,16 +969,19 @@ void live_begin(fdbcs* cs) {
     if (large_batch_mode(c.T) || large_batch_mode(cs->lv_prev_T)) return;
     // the batch buffers at their final size before the kernel writes them (the
     // detect's ensure_batch must not move them): keys and the stream's bytes
-    const uint64_t kb = c.key_bytes + 32 * (uint64_t)c.T + 8 * ((uint64_t)c.R + c.W) + 64;
+    // (run_batch asks max(stream bytes, key bytes): the stream's bound
+    // counts the publishes' padding, TxnStage::live_stream_bound)
+    const uint64_t kb = std::max<uint64_t>(c.key_bytes, cs->st.live_stream_bound(c));
     BatchBufs& b = cs->b;
     if (ensure_batch(cs, c.T, c.R, c.W, kb) || !b.rounds) return;  // (the live kernel leaves the reads unsorted)
     if (cs->st.begin_live(c)) return;
+    cs->lv_kb = kb;
     LmArgs la{};
     cs->lv_lm = cs->lm.owner && lm_arm(cs, (uint64_t)c.R + c.W, c.key_bytes, la) == FDBCS_OK;
     if (++cs->lv_gen == 0) cs->lv_gen = 1;
     launch_live_ingest(b, cs->sc, c, cs->oldest, (int)(cs->sorts & 1), cs->st.stream_dev(), cs->st.stream_cap(),
                        cs->st.toff_dev(), cs->st.prog_dev(), cs->st.live_view(), cs->lv_lm ? &la : nullptr,
-                       cs->lv_gen, cs->h.dir[cs->cur], cs->stream);
+                       cs->lv_gen, cs->h.dir[cs->cur], cs->lv_tune, cs->stream);
 }
 
 void lm_release(fdbcs::Lm& L) {
@@ -1345,6 +1367,11 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     {
         const char* c = getenv("FDBCS_STAGE_CHUNK");  // bytes per streamed H2D chunk of the per-transaction path
         if ((r = cs->st.configure(cs->stream, cs->copy_stream, c ? strtoull(c, nullptr, 0) : 512 << 10))) return fail(r);
+        // the live kernel's shape (kernels.h LiveTune; tests run each)
+        if (const char* e = getenv("FDBCS_LIVE_BLOCKS")) cs->lv_tune.blocks = std::min(1024, std::max(2, atoi(e)));
+        if (const char* e = getenv("FDBCS_LIVE_SPEC")) cs->lv_tune.spec = atoi(e) != 0;
+        if (const char* e = getenv("FDBCS_LIVE_TIMEOUT_US"))
+            cs->lv_tune.timeout_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 0)) * 100;  // (100 MHz)
     }
 
     *out = cs;
@@ -1739,7 +1766,7 @@ int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
     const int64_t v[FDBCS_STATS] = {cs->last_T, cs->last_R, cs->last_W, h.n_comb, h.n_aff, h.D, h.H, h.win_np,
                                     h.win_surv, h.n_dep, h.jac_iters, h.ss_resample, h.ss_maxc,
                                     (int64_t)cs->h.tail_cap, (int64_t)h.tail_used, h.tail_half, cs->lv_done,
-                                    cs->lv_cancelled};
+                                    cs->lv_cancelled, cs->st.live_timeouts()};
     const int n = std::min(cap, (int)FDBCS_STATS);
     for (int i = 0; i < n; i++) out[i] = v[i];
     return n;

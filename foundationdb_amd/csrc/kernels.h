@@ -118,6 +118,16 @@ struct LiveCaps {
     int32_t T, R, W;
     uint64_t key_bytes;
 };
+// Live kernel shape, read from the environment when the conflict set is made
+// (tests run every shape; the defaults are the measured best):
+// FDBCS_LIVE_BLOCKS workgroups (128), FDBCS_LIVE_SPEC the speculative record
+// window of the last groups (1), FDBCS_LIVE_TIMEOUT_US the poller's limit
+// (8 s; the batch then falls back to the whole-stream ingest, stage.h).
+struct LiveTune {
+    int blocks = 128;
+    bool spec = true;
+    uint64_t timeout_ticks = 8ull * 100000000ull;  // (100 MHz wall clock)
+};
 
 struct BatchBufs {
     StagedBatch staged;  // per-transaction path: set for one run_batch (stage.h)
@@ -279,7 +289,8 @@ void scan_i64_from_i32(const int32_t* in, int64_t* out, const int32_t* n_ptr, in
 // gen: the live batch's generation (tags the progress words in Scalars)
 void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
                         const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
-                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, hipStream_t s);
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, const LiveTune& tune,
+                        hipStream_t s);
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s);
 // lm: an attached sample's load-metrics roll (staged batches only; null: none)
 void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scalars* sc, bool scatter, int parity,

@@ -939,18 +939,14 @@ struct LiveArgs {
     SortJobs J;        // job 1's splitters (rounds mode: the read begins are not sorted)
     StagedBatch S;     // stream, toff: host-mapped; view: the batch view's arrays (capacity layout)
     LiveOut O;
-    const uint64_t* prog;  // host-mapped: [0] published T, [2] state, [3..5] final T, R, W (stage.h)
+    // host-mapped: [0] published T, [2] state, [3..5] final T, R, W (stage.h);
+    // [6] the poller's timeout mark (written here, read by TxnStage::finish)
+    uint64_t* prog;
     uint64_t timeout;      // wall_clock64 ticks (100 MHz)
     uint32_t gen;          // this live batch's generation (tags lv_pub)
+    bool spec;             // the speculative window of the last groups (LiveTune)
 };
-#ifndef FDBCS_LIVE_SPEC
-#define FDBCS_LIVE_SPEC 1
-#endif
-#ifndef FDBCS_LIVE_BLOCKS
-#define FDBCS_LIVE_BLOCKS 128  // (511 worker waves; 64: 1-2 us slower per window, 32: 12 us)
-#endif
-constexpr int LIVE_BLOCKS = FDBCS_LIVE_BLOCKS;
-constexpr uint64_t LIVE_TIMEOUT_TICKS = 8ull * 100000000ull;  // 8 s of the 100 MHz wall clock
+// (LiveTune::blocks: 128 = 511 worker waves; 64: 1-2 us slower per window, 32: 12 us)
 
 // Polling (MI355X_MICROARCH.md, inter-workgroup visibility): relaxed
 // agent-scope loads and stores (sc1: past this CU's L1) for the mirrored
@@ -1044,6 +1040,16 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
                     last = pub;
                 }
                 if (wall_clock64() - t_start > V.timeout) {
+                    // Give up, unless the batch became whole meanwhile.  Dekker
+                    // with TxnStage::finish (which stores its final word, fences,
+                    // then loads this mark): mark, fence, look again.  Either
+                    // this look sees the final word (finish the batch as usual;
+                    // should the host have seen the mark too, it falls back to
+                    // the whole-stream ingest, which resets this kernel's work
+                    // after it) or the host sees the mark and falls back.
+                    __hip_atomic_store(V.prog + 6, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                    if ((host_load(V.prog) & LV_FINAL_BIT) || host_load(V.prog + 2) != LV_RUNNING) continue;
                     atomicCAS(&sc->err, 0, FDBCS_E_STATE);
                     lv_store(&sc->lv_pub, lv_word(gen, LV_TIMEOUT, 0, 0));
                     break;
@@ -1087,7 +1093,7 @@ __global__ __launch_bounds__(STG_BLOCK) void k_live_ingest(LiveArgs V) {
         // a group among the last published ones: its records end at most
         // `used`, so the window's last LIVE_WIN bytes are read together with
         // the offsets (one round trip instead of two)
-        O.spec = FDBCS_LIVE_SPEC && tav - t0 <= 2 * STG_TPW;
+        O.spec = V.spec && tav - t0 <= 2 * STG_TPW;
         staged_group<true, true>(V.A, V.J, V.S, O, t0, min(STG_TPW, tav - t0), L, sp1, sp1, win[wv]);
         if (lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1963,7 +1969,8 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
 
 void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t oldest, int parity,
                         const uint8_t* stream, uint64_t stream_cap, const uint64_t* toff, const uint64_t* prog,
-                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, hipStream_t s) {
+                        UnpackOut view, const LmArgs* lm, uint32_t gen, const Dir& hd, const LiveTune& tune,
+                        hipStream_t s) {
     IngestArgs A{};
     A.hd = hd;
     A.T = caps.T; A.R = caps.R; A.W = caps.W;
@@ -1985,8 +1992,8 @@ void launch_live_ingest(BatchBufs& b, Scalars* sc, const LiveCaps& caps, int64_t
     S.view = view;
     S.live = true;
     const LiveOut O{caps.T, caps.R, caps.W, stream_cap};
-    const LiveArgs V{A, J, S, O, prog, LIVE_TIMEOUT_TICKS, gen};
-    hipLaunchKernelGGL(k_live_ingest, dim3(LIVE_BLOCKS), dim3(STG_BLOCK), 0, s, V);
+    const LiveArgs V{A, J, S, O, const_cast<uint64_t*>(prog), tune.timeout_ticks, gen, tune.spec};
+    hipLaunchKernelGGL(k_live_ingest, dim3(std::max(2, tune.blocks)), dim3(STG_BLOCK), 0, s, V);
 }
 
 void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {

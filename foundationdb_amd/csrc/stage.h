@@ -52,6 +52,14 @@ class TxnStage {
     // `caps` (or a buffer that must grow) is cancelled and ingested at
     // finish() as usual.
     int begin_live(const LiveCaps& caps);
+    // The most stream bytes a live batch within `caps` can reach (records,
+    // the padding of every publish and of the final word): the batch tail
+    // buffers are sized by it before the live kernel writes them
+    // (engine.hip live_begin), so detectConflicts never has to move them.
+    uint64_t live_stream_bound(const LiveCaps& caps) const;
+    // live batches whose kernel gave up (LiveTune::timeout_ticks) and that
+    // finish() sent to the whole-stream ingest instead
+    int64_t live_timeouts() const { return timeouts_; }
     // the live kernel's inputs (device pointers of the host-mapped buffers)
     const uint8_t* stream_dev() const { return pin_dev_; }
     uint64_t stream_cap() const { return cap_; }
@@ -125,10 +133,12 @@ class TxnStage {
     LiveCaps lcaps_{};
     UnpackOut lview_{};           // the view's arrays in the live layout (sized by lcaps_)
     int64_t pub_every_ = 16;      // FDBCS_LIVE_PUB: transactions per progress word
+    int64_t timeouts_ = 0;
     int64_t next_pub_ = 0;
     // host-mapped progress: [0] published bytes << 20 | published T (one
     // word; LV_FINAL_BIT once the batch is whole), [1] final stream bytes,
-    // [2] state (LV_RUNNING / LV_FINAL / LV_CANCEL), [3..5] final T, R, W
+    // [2] state (LV_RUNNING / LV_FINAL / LV_CANCEL), [3..5] final T, R, W,
+    // [6] set by the live kernel's poller when it gave up (timeout)
     uint64_t* prog_ = nullptr;
     uint64_t* prog_dev_ = nullptr;
 };

@@ -318,14 +318,20 @@ void TxnStage::live_cancel() {
     __atomic_store_n(&prog_[2], (uint64_t)LV_CANCEL, __ATOMIC_RELEASE);
 }
 
+// records (header <= 24 B + 7 B of alignment, 8 B range entries, keys) and
+// the padding of every publish (< 144 B each: one per pub_every_
+// transactions, one more at the final word, pad_published)
+uint64_t TxnStage::live_stream_bound(const LiveCaps& caps) const {
+    const uint64_t slots = 2 * ((uint64_t)caps.R + (uint64_t)caps.W);
+    return 32 * (uint64_t)caps.T + 4 * slots + caps.key_bytes + 64 +
+           160 * ((uint64_t)caps.T / (uint64_t)pub_every_ + 2);
+}
+
 int TxnStage::begin_live(const LiveCaps& caps) {
     if (!open_ || T_ || live_) return FDBCS_E_STATE;
-    // records (header, range entries, keys, padding) and, should the batch
-    // fall back, the offsets appended at finish
+    // the records and, should the batch fall back, the offsets appended at finish
+    const uint64_t need = live_stream_bound(caps) + 8 * ((uint64_t)caps.T + 1);
     const uint64_t slots = 2 * ((uint64_t)caps.R + (uint64_t)caps.W);
-    // (+ the padding of every publish, TxnStage::publish)
-    const uint64_t need = 32 * (uint64_t)caps.T + 4 * slots + caps.key_bytes + 8 * ((uint64_t)caps.T + 1) + 64 +
-                          160 * ((uint64_t)caps.T / (uint64_t)pub_every_ + 2);
     int r;
     if ((r = grow(caps.T + 1, need))) return r;
     if (!pin_live_ || !toff_live_) return FDBCS_E_STATE;  // (grown past the live size: not coherent)
@@ -359,6 +365,7 @@ int TxnStage::begin_live(const LiveCaps& caps) {
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
+    bool go_live = false;
     if (live_ && !live_broken_ && staged && pad_published()) {
         // the final word: the kernel finishes the last groups and leaves
         prog_[3] = (uint64_t)T_;
@@ -371,6 +378,20 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
         // round trip sooner than by reading [3] and [1] after the state
         __atomic_store_n(&prog_[0], LV_FINAL_BIT | (uint64_t)used_ << 20 | (uint64_t)T_, __ATOMIC_RELEASE);
         __atomic_store_n(&prog_[2], (uint64_t)LV_FINAL, __ATOMIC_RELEASE);
+        // Did the kernel give up first (its timeout: e.g. an add phase stalled
+        // for seconds behind another engine's hipFree)?  Store, full fence,
+        // load here; mark, fence, load in the poller (k_live_ingest): one of
+        // the two sees the other.  Marked: ingest the whole stream below (its
+        // k_live_reset undoes whatever the kernel did).
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        if (__atomic_load_n(&prog_[6], __ATOMIC_ACQUIRE)) {
+            timeouts_++;
+            live_broken_ = true;
+        } else {
+            go_live = true;
+        }
+    }
+    if (go_live) {
         live_ = false;
         dv = fdbcs_batch_view{};
         dv.txn_count = (int32_t)T_;

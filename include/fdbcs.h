@@ -325,9 +325,11 @@ int  fdbcs_stage_times(fdbcs* cs, double* out_us, int cap);
  * [15] current half (flips when a compaction sweep freed the other)
  * [16] per-transaction batches ingested live (during their adds) so far
  * [17] live batches cancelled on the way (outgrew the live capacities, or
- * another call needed the stream) and ingested whole at detect.
+ * another call needed the stream) and ingested whole at detect  [18] of
+ * those, batches whose live kernel gave up waiting for the adds (its
+ * timeout, FDBCS_LIVE_TIMEOUT_US, default 8 s).
  * Returns the count written. */
-#define FDBCS_STATS 18
+#define FDBCS_STATS 19
 int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
 
 /* Profiling builds only (-DFDBCS_PHASES): the 100 MHz device timestamps the
@@ -393,6 +395,12 @@ int  fdbcs_sample_add_metric(fdbcs_sample* s, const uint8_t* key, uint32_t len, 
  * (Resolver.actor.cpp:286-289, every SAMPLE_POLL_TIME). */
 int  fdbcs_sample_poll(fdbcs_sample* s, double now);
 
+/* Threading of the queries below: they take a const handle, but each first
+ * inserts the batches an attached engine rolled and fdbcs_sample_add_batch
+ * queued (in batch order, so nothing observable moves) -- they MUTATE the
+ * sample.  Like every other call on a sample, they are not thread-safe: one
+ * thread at a time per sample, queries included (the Resolver's actor runs
+ * them on its one network thread, Resolver.actor.cpp:276-289). */
 /* getEstimate(KeyRangeRef(b, e)) (StorageMetrics.actor.h:35-37): the sum of
  * the sampled metrics of keys in [b, e).  ResolutionMetricsRequest answers
  * getEstimate(allKeys) (Resolver.actor.cpp:276-277). */

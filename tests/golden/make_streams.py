@@ -40,6 +40,11 @@ def make(name):
         wl.set_successor(cs)
     out = []
     t0 = time.time()
+    for i in range(spec.get("prefill", 0)):  # unrecorded batches [0, prefill) from an empty history
+        b, now, nold = wl.batch(i)
+        cs.detect_packed(b, now, nold)
+        if i % 250 == 0:
+            print(f"{name}: prefill batch {i}, {time.time() - t0:.0f}s", flush=True)
     for i in range(spec["first"], spec["first"] + spec["batches"]):
         b, now, nold = wl.batch(i)
         v = cs.detect_packed(b, now, nold)

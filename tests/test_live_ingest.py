@@ -35,18 +35,25 @@ def same_history(g, c):
         assert np.array_equal(gk[:n], ck[:n]), "key bytes differ"
 
 
-def live_cs(pub=None):
-    old = os.environ.get("FDBCS_LIVE_PUB")
-    if pub is not None:
-        os.environ["FDBCS_LIVE_PUB"] = str(pub)
+def live_cs(pub=None, blocks=None, spec=None, timeout_us=None):
+    """A conflict set whose live kernel has the given shape: FDBCS_LIVE_PUB
+    (transactions per progress word), FDBCS_LIVE_BLOCKS (workgroups),
+    FDBCS_LIVE_SPEC (the speculative record window), FDBCS_LIVE_TIMEOUT_US --
+    read when the conflict set is made (None: the default)."""
+    env = {"FDBCS_LIVE_PUB": pub, "FDBCS_LIVE_BLOCKS": blocks, "FDBCS_LIVE_SPEC": spec,
+           "FDBCS_LIVE_TIMEOUT_US": timeout_us}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is not None:
+            os.environ[k] = str(v)
     try:
         return ConflictSet()
     finally:
-        if pub is not None:
-            if old is None:
-                del os.environ["FDBCS_LIVE_PUB"]
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["FDBCS_LIVE_PUB"] = old
+                os.environ[k] = v
 
 
 def run_batch(g, batch, now, nold):
@@ -56,9 +63,16 @@ def run_batch(g, batch, now, nold):
     return b.detect_conflicts(now, nold)
 
 
-@pytest.mark.parametrize("pub", [None, 8, 1000])
-def test_live_steady_state(gpu, pub):
-    g = live_cs(pub)
+# (blocks, speculative window, publish cadence): the default and the shapes a
+# round-4 variant build failed on (64 blocks, no speculative window: wrong
+# statuses on valid input from stale host lines, fixed in f05d87a -- DESIGN §8)
+LIVE_SHAPES = [(None, None, None), (64, 0, None), (64, 1, 8), (32, 1, None), (32, 0, 1000), (128, 0, 8),
+               (128, 1, 1000), (2, 1, 16)]
+
+
+@pytest.mark.parametrize("blocks,spec,pub", LIVE_SHAPES)
+def test_live_steady_state(gpu, blocks, spec, pub):
+    g = live_cs(pub, blocks, spec)
     c = CpuSpec()
     n = 0
     for batch, now, nold in mixed_stream(11, n_batches=14, max_txns=700, keyspace=4000):
@@ -242,4 +256,123 @@ def test_last_device_batch_after_live(gpu):
             assert (key(2 * R + 2 * w), key(2 * R + 2 * w + 1)) == (bytes(b), bytes(e)), ("write", w)
         checked += 1
     assert checked >= 1, g.batch_stats()
+    g.close()
+
+
+@pytest.mark.parametrize("blocks,spec,pub", LIVE_SHAPES)
+def test_live_skip_runs(gpu, blocks, spec, pub):
+    """tests/test_gpu_parity.py::test_per_transaction_skip_runs on a live
+    conflict set of each shape: runs of range-less transactions in one
+    fdbcs_batch_skip call between the adds, verdicts and the whole history
+    against the oracle after every batch."""
+    import random
+    g = live_cs(pub, blocks, spec)
+    for seed in range(3):
+        g.load_history([], [], v0=0, oldest=0, removal_key=b"")
+        c = CpuSpec()
+        rng = random.Random(seed)
+        for batch, now, nold in mixed_stream(seed, n_batches=8, max_txns=400, keyspace=3000):
+            txns = []
+            for t in batch.txns():
+                if rng.random() < 0.3:
+                    txns += [(rng.randrange(0, now), [], [])] * rng.randint(1, 5)
+                txns.append(t)
+            txns += [(0, [], [])] * rng.randint(0, 3)
+            vc = c.detect_packed(PackedBatch.from_txns(txns), now, nold)
+            b = ConflictBatch(g)
+            pending = 0
+            for snap, r, w in txns:
+                if not r and not w:
+                    pending += 1
+                    continue
+                if pending:
+                    b.skip(pending)
+                    pending = 0
+                b.add_transaction(r, w, snap)
+            if pending:
+                b.skip(pending)
+            assert np.array_equal(b.detect_conflicts(now, nold), vc), (seed, now)
+        same_history(g, c)
+        c.close()
+    assert g.batch_stats()["live_batches"] >= 1, g.batch_stats()
+    g.close()
+
+
+@pytest.mark.parametrize("pub", [8, None])
+def test_live_batch_at_its_caps(gpu, pub):
+    """a live batch that ends just under all four of its
+    capacities (T, R, W and key bytes: the previous batch's plus a quarter,
+    engine.hip live_begin) with keys longer than 17 bytes, so every key has a
+    tail in the batch's tail buffer.  The buffers were sized without the
+    stream's publish padding, so detectConflicts reallocated the tail buffer
+    after the live kernel had written into it (keys.tail left dangling).  Now
+    live_begin sizes them for the padded stream and run_batch refuses to move
+    any of them."""
+    g = live_cs(pub)
+    c = CpuSpec()
+    now = 100
+
+    def txn(k, wlen, snap):
+        key = b"key-%012d" % k + b"." * (wlen - 16)  # wlen bytes, > 17
+        rk = b"key-%012d" % (k + 1) + b"r" * 8
+        return (snap, [(rk, rk + b"\x00")], [(key, key + b"\x00")])
+
+    T0 = 2000
+    first = [txn(4 * t, 24, now - 5) for t in range(T0)]
+    kb0 = sum(len(b) + len(e) for _, rs, ws in first for b, e in rs + ws)
+    cap_t = T0 + T0 // 4 + 256  # (R = W = T here)
+    cap_k = kb0 + kb0 // 4 + 65536
+    T1 = cap_t - 1
+    second = [txn(4 * t + 100_000, 24, now + 5) for t in range(T1)]
+    kb1 = sum(len(b) + len(e) for _, rs, ws in second for b, e in rs + ws)
+    extra = cap_k - 1 - kb1  # grow write keys (2 bytes of key per byte of length) up to the key cap
+    i = 0
+    while extra >= 2:
+        snap, rs, ws = second[i]
+        grow = min(extra // 2, 32 - len(ws[0][0]))  # (keys up to 32 bytes are staged whole: the most stream bytes)
+        k = ws[0][0] + b"+" * grow
+        second[i] = (snap, rs, [(k, k + b"\x00")])
+        extra -= 2 * grow
+        i += 1
+    kb1 = sum(len(b) + len(e) for _, rs, ws in second for b, e in rs + ws)
+    assert cap_k - 2 <= kb1 < cap_k and T1 < cap_t
+    for i, txns in enumerate([first, second, first[:500]]):
+        b = ConflictBatch(g)
+        for snap, r, w in txns:
+            b.add_transaction(r, w, snap)
+        v = b.detect_conflicts(now, 0)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, 0)), i
+        if i == 1:
+            st = g.batch_stats()
+            assert st["live_batches"] == 1 and st["live_cancelled"] == 0, st
+        now += 10
+    same_history(g, c)
+    g.close()
+
+
+def test_live_timeout_falls_back(gpu):
+    """a live kernel whose adds stall past its timeout
+    (here 20 ms; 8 s by default) gives up and marks the progress words; the
+    batch's detectConflicts sees the mark and ingests the whole stream, so its
+    verdicts and history are still exact, and the next batch goes live again."""
+    import time
+    g = live_cs(timeout_us=20_000)
+    c = CpuSpec()
+    now = 10
+    for i in range(4):
+        txns = txns_for(300, 1000 * i, now - 5, 20)
+        b = ConflictBatch(g)
+        for j, (snap, r, w) in enumerate(txns):
+            if i == 2 and j == 150:
+                time.sleep(0.25)  # (the kernel gives up here)
+            b.add_transaction(r, w, snap)
+        v = b.detect_conflicts(now, 0)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, 0)), i
+        st = g.batch_stats()
+        if i == 2:
+            assert st["live_timeouts"] == 1 and st["live_cancelled"] >= 1, st
+        now += 10
+    st = g.batch_stats()
+    assert st["live_timeouts"] == 1 and st["live_batches"] >= 2, st
+    same_history(g, c)
     g.close()

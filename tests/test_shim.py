@@ -75,7 +75,7 @@ def test_shim_skiplisttest_entry(gpu):
         pytest.skip("shim driver not built")
     r = subprocess.run([B.SHIM_CHECK, "skiplisttest"], capture_output=True, text=True, timeout=120, check=True)
     out = r.stdout
-    assert "New conflict set:" in out and "Detect only:" in out
+    assert "New conflict set:" in out and "Detect only:" in out and "Verdicts only:" in out
     rate = float(re.search(r"New conflict set:.*?\n\s+([0-9.]+) Mtransactions/sec", out, re.S).group(1))
     hist = int(re.search(r"(\d+) entries in version history", out).group(1))
     # the reference's run of the same shape ends with 428,868 entries (a different RNG)
