@@ -296,7 +296,9 @@ struct Scalars {
     uint64_t lv_pub;
     int32_t lv_R, lv_W;     // the final read / write counts (diagnostics)
     int32_t lv_err;         // a transaction past the live capacities (the host falls back)
-    int32_t lv_pad;
+    // rounds mode, edge lanes fused into the decision launch (k_decide_rounds):
+    // edge blocks done; block 0 waits for all of them, then zeroes it
+    int32_t e_done;
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;

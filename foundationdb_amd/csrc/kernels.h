@@ -187,6 +187,7 @@ struct BatchBufs {
     uint2* items;        // [R + W] the rounds' writes and reads when they do not fit in LDS
     int64_t list_cap;    // entries of plist (items: 2 * list_cap)
     bool ws_deferred;    // this batch's write searches wait for launch_write_search
+    bool edges_fused;    // rounds mode: the edge lanes wait for launch_decide (blocks of the decision launch)
     uint64_t* ss_gsamp;  // [2 * 3 * 4096] global sample scratch of the sort's overflow guard
     uint32_t* rstamp;    // [R] per read: the batch (rseq) that put it on plist
     uint32_t rseq;

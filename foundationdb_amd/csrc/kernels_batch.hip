@@ -15,6 +15,19 @@
 
 namespace fdbcs_dev {
 
+// Write-through (sc1) stores and loads of values handed between workgroups
+// inside one launch (MI355X_MICROARCH.md, inter-workgroup visibility): the
+// fused edge lanes (k_decide_rounds) and the sort-overflow flag the live
+// kernel's poller watches.
+template <class T>
+__device__ inline void st1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ inline T ld1(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 
 // -------------------------------------------------------------- ingest ----
 // One launch, two kinds of blocks:
@@ -2299,6 +2312,72 @@ __device__ inline void edges_lane(const EdgesArgs& A, int i, const uint64_t* smp
     }
 }
 
+// ---- rounds-mode edge lanes as blocks of the decision's launch ----------
+// (launch_decide with b.edges_fused).  Block 0 of k_decide_rounds, the
+// decision, waits for these blocks inside the launch instead of a kernel
+// boundary: every handed-off value (rq, plist, n_pot, dec_wide, wnew, winv)
+// is stored write-through (sc1) and drained (s_waitcnt vmcnt(0)) by every
+// storing wave, then one lane per block adds to Scalars::e_done; block 0
+// polls that counter and reads the values with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the write-through form,
+// no L2 writeback or invalidate).  No deadlock: only block 0 waits, on one
+// CU, and the blocks it waits for wait on nothing.
+// read i (as rounds_lane), its outputs write-through
+__device__ inline void fused_read_lane(const EdgesArgs& A, int i, const uint64_t* smp_w) {
+    const int P = 2 * A.W;
+    const uint8_t* const* tails = A.keys.tail;
+    if (A.too_old[A.read_txn[i]]) return;
+    const Key b = A.keys.get(2 * (int64_t)i), e = A.keys.get(2 * (int64_t)i + 1);
+    int lb, hb, le, he, pb, pe;
+    sample_narrow(smp_w, P, b.hi, lb, hb);
+    sample_narrow(smp_w, P, e.hi, le, he);
+    bsearch2(A.sw, b, true, lb, hb, e, le, he, tails, pb, pe);
+    st1(reinterpret_cast<uint64_t*>(A.rq) + i, (uint64_t)(uint32_t)pb | (uint64_t)(uint32_t)pe << 32);
+    if (pe > pb || (pb > 0 && (A.wcov[pb - 1] > 0 || rec_vs_key(A.sw[pb - 1], b, tails) == 0))) {
+        const int j = atomicAdd(&A.sc->n_pot, 1);  // (one lane per read: no stamp needed)
+        if (j < A.plist_cap) st1(A.plist + j, i);
+        else st1(&A.sc->dec_wide, 1);  // (overflow: every read is a candidate)
+    }
+}
+
+// sorted write endpoints 4q .. 4q + 3: new-key flags (one 4-byte word) and
+// their sorted positions
+__device__ inline void fused_quad_lane(const EdgesArgs& A, int q) {
+    const int P = 2 * A.W, p0 = 4 * q;
+    const uint8_t* const* tails = A.keys.tail;
+    SRec x[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {  // (sw[p0 - 1 .. p0 + 3], loads issued together)
+        const int p = p0 - 1 + k;
+        if (p >= 0 && p < P) x[k] = A.sw[p];
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 1; k < 5; k++) {
+        const int p = p0 - 1 + k;
+        if (p >= P) break;
+        const bool nw = p == 0 || !rec_key_eq(x[k - 1], x[k], tails);
+        word |= (uint32_t)nw << (8 * (k - 1));
+        st1(A.winv + (x[k].idx - A.wbase), p);
+    }
+    st1(reinterpret_cast<uint32_t*>(A.wnew) + q, word);
+}
+
+__host__ __device__ inline int fused_edge_quads(int W) { return (2 * W + 3) / 4; }
+
+// one edge block of the decision's launch: lanes [0, R) reads, then quads
+__device__ void fused_edge_block(const EdgesArgs& A, int eb, uint64_t* smp_w) {
+    const int i0 = eb * (int)blockDim.x;
+    if (i0 < A.R) sample_fill(smp_w, A.sw, 2 * A.W);
+    __syncthreads();
+    const int i = i0 + (int)threadIdx.x;
+    if (i < A.R) fused_read_lane(A, i, smp_w);
+    else if (i < A.R + fused_edge_quads(A.W)) fused_quad_lane(A, i - A.R);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every wave drains its sc1 stores)
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&A.sc->e_done, 1);
+}
+
 // One launch, three kinds of blocks: read-check groups and write-search
 // groups (history), then edge lanes (intra-batch) -- all latency-bound
 // searches, so they overlap.
@@ -2523,6 +2602,12 @@ void launch_write_search(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, i
     hipLaunchKernelGGL(k_write_search, dim3(cdiv((int64_t)W * RC_G, 256)), dim3(256), 0, s, WA);
 }
 
+static EdgesArgs make_edges_args(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc) {
+    return EdgesArgs{v.read_count, v.write_count, b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn,
+                     b.write_txn, b.too_old, b.et, b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew,
+                     b.plist, b.list_cap, b.winv, b.wcov, b.rstamp, b.rseq, write_base(b, v)};
+}
+
 void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t v0,
                              hipStream_t s, bool defer_ws) {
     const int R = v.read_count, W = v.write_count;
@@ -2538,9 +2623,7 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     }
     const int32_t* qx = dj ? b.ss_bkt : nullptr;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
-    EdgesArgs EA{R,     W,    b.keys, (const SRec*)b.sr, (const SRec*)b.sw, b.read_txn, b.write_txn, b.too_old,
-                 b.et,  b.eu, b.edge_cap, sc, b.deg, b.rounds ? b.rq : nullptr, b.wnew, b.plist, b.list_cap, b.winv,
-                 b.wcov, b.rstamp, b.rseq, write_base(b, v)};
+    const EdgesArgs EA = make_edges_args(v, b, sc);
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx, write_base(b, v)};
     // (rc_fused: the history read check already ran in the sort's bucket launch)
     const int rc_blocks = b.rc_fused ? 0 : cdiv((int64_t)R * RC_G, 256);
@@ -2551,7 +2634,19 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 2 * W : W), 256) : 0;
     const bool wide = FDBCS_RC_WIDE;  // (WIDE = false: the two-level range maximum, kept for A/B)
-    if (rc_blocks + ws_blocks + e_blocks > 0) {
+    // rounds mode with nothing else in this launch (the read check fused into
+    // the sort's buckets, the write searches deferred): the edge lanes become
+    // blocks of the decision's launch instead, one dependent launch fewer
+    // before the verdicts (k_decide_rounds, "fused edge lanes")
+    // Measured and off by default (FDBCS_FUSE_EDGES=1 turns it on): config 2,
+    // alternating runs on one box, HBM-resident batch 0.1996 / 0.1979 ms fused
+    // against 0.1957 / 0.1962 separate -- the decision launch's blocks carry
+    // its ~150 KB of LDS, so its edge blocks run one per CU (44 CUs of 16
+    // waves instead of 176 of 4) and the searches lose more than the launch
+    // boundary saves
+    static const bool fuse = getenv("FDBCS_FUSE_EDGES") && atoi(getenv("FDBCS_FUSE_EDGES"));
+    b.edges_fused = b.rounds && defer_ws && fuse && rc_blocks == 0 && ws_blocks == 0 && e_blocks > 0 && !join;
+    if (!b.edges_fused && rc_blocks + ws_blocks + e_blocks > 0) {
         if (wide)
             hipLaunchKernelGGL(k_edges_read_check<true>, dim3(rc_blocks + ws_blocks + e_blocks), dim3(256), 0, s, RA,
                                rc_blocks, WA, ws_blocks, EA);
@@ -2623,6 +2718,10 @@ struct RoundArgs {
     // read check), beside the decision in block 0, which holds one CU
     WriteSearchArgs ws;
     int64_t wbase;  // slot of write 0's begin (write_base)
+    // blocks 1 .. eblocks: the fused edge lanes (b.edges_fused), before the
+    // write-search blocks; 0: k_edges_read_check ran them
+    EdgesArgs ea;
+    int eblocks;
 };
 
 static constexpr int DC_THREADS = 1024;
@@ -2687,12 +2786,17 @@ __device__ inline void blocks_of(int a, int b, F1 pos, F2 blk1, F3 blk2) {
 __device__ inline bool bit_of(const uint32_t* bits, int t) { return (bits[t >> 5] >> (t & 31)) & 1; }
 
 __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
-    if (blockIdx.x > 0) {  // a write-search block: 64 groups of RC_G lanes
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (blockIdx.x > 0) {
+        if ((int)blockIdx.x <= A.eblocks) {  // a fused edge block (its sample of the sorted writes in LDS)
+            fused_edge_block(A.ea, (int)blockIdx.x - 1, reinterpret_cast<uint64_t*>(lds));
+            return;
+        }
+        // a write-search block: 64 groups of RC_G lanes
         const Group<RC_G> g;
-        write_search_group(A.ws, g, (int)(((blockIdx.x - 1) * blockDim.x + threadIdx.x) / RC_G));
+        write_search_group(A.ws, g, (int)(((blockIdx.x - 1 - A.eblocks) * blockDim.x + threadIdx.x) / RC_G));
         return;
     }
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ int32_t red32[DC_THREADS / 64 + 1];
     __shared__ int32_t s_nw, s_nr;
     const int T = A.T, R = A.R, W = A.W, P = 2 * A.W;
@@ -2721,8 +2825,6 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     // ---- U: 4 transactions per lane from one 4-byte load of each flag array ----
     for (int i = tid; i < nwords; i += nthr) nbits[i] = tbits[i] = 0;
     if (tid == 0) s_nw = s_nr = 0;
-    const bool wide = sc->dec_wide != 0;
-    const int npot = wide ? R : (int)min((int64_t)sc->n_pot, A.lcap_list);
     __syncthreads();
     for (int t4 = tid; 4 * t4 < T; t4 += nthr) {
         const uint32_t to = reinterpret_cast<const uint32_t*>(A.too_old)[t4];
@@ -2741,7 +2843,13 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
         ubits[i] = cbits[i] = nbits[i];
         nbits[i] = 0;
     }
+    if (A.eblocks && tid == 0) {  // the fused edge blocks of this launch (U above overlapped them)
+        while (ld1(&sc->e_done) < A.eblocks) __builtin_amdgcn_s_sleep(1);
+        st1(&sc->e_done, 0);  // (every edge block has added: zero for the next batch)
+    }
     __syncthreads();
+    const bool wide = ld1(&sc->dec_wide) != 0;
+    const int npot = wide ? R : (int)min((int64_t)ld1(&sc->n_pot), A.lcap_list);
     if (npot == 0) goto decided;  // no read can meet a write of the batch: C* = U
     PHASE(sc, 2);
     {
@@ -2752,7 +2860,7 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
         int nnew = 0;
 #pragma unroll
         for (int k = 0; k < CPMAX / 4 + 1; k++) {
-            fl[k] = p0 + 4 * k < p1 ? reinterpret_cast<const uint32_t*>(A.wnew)[(p0 >> 2) + k] : 0;
+            fl[k] = p0 + 4 * k < p1 ? ld1(reinterpret_cast<const uint32_t*>(A.wnew) + (p0 >> 2) + k) : 0;
             nnew += __popc(fl[k] & 0x01010101u & (p0 + 4 * k + 4 <= p1 ? ~0u : (1u << (8 * (p1 - p0 - 4 * k))) - 1));
         }
         int tot;
@@ -2771,8 +2879,8 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
             for (int k = 0; k < DG; k++) {
                 const int w = w0 + k * nthr;
                 if (u[k] >= 0 && bit_of(ubits, u[k])) {
-                    pb[k] = A.winv[2 * w];
-                    pe[k] = A.winv[2 * w + 1];
+                    pb[k] = ld1(A.winv + 2 * w);
+                    pe[k] = ld1(A.winv + 2 * w + 1);
                 } else {
                     u[k] = -1;
                 }
@@ -2791,7 +2899,7 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
         for (int i0 = tid; i0 < npot; i0 += DG * nthr) {
             int r[DG], t[DG], pb[DG], pe[DG];
 #pragma unroll
-            for (int k = 0; k < DG; k++) r[k] = i0 + k * nthr < npot ? (wide ? i0 + k * nthr : A.plist[i0 + k * nthr]) : -1;
+            for (int k = 0; k < DG; k++) r[k] = i0 + k * nthr < npot ? (wide ? i0 + k * nthr : ld1(A.plist + i0 + k * nthr)) : -1;
 #pragma unroll
             for (int k = 0; k < DG; k++) r[k] = r[k] < R ? r[k] : -1;
 #pragma unroll
@@ -2799,8 +2907,9 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
 #pragma unroll
             for (int k = 0; k < DG; k++) {
                 if (t[k] >= 0 && bit_of(ubits, t[k]) && !A.too_old[t[k]]) {
-                    pb[k] = A.rq[2 * r[k]];
-                    pe[k] = A.rq[2 * r[k] + 1];
+                    const uint64_t q = ld1(reinterpret_cast<const uint64_t*>(A.rq) + r[k]);  // (pb, pe)
+                    pb[k] = (int32_t)(uint32_t)q;
+                    pe[k] = (int32_t)(uint32_t)(q >> 32);
                 } else {
                     t[k] = -1;
                 }
@@ -3322,7 +3431,15 @@ bool launch_decide(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, uint8_t
                                write_base(b, v)};
         wsb = cdiv((int64_t)v.write_count * RC_G, DC_THREADS);
     }
-    hipLaunchKernelGGL(k_decide_rounds, dim3(1 + wsb), dim3(DC_THREADS), base + 8 * (size_t)A.lcap, s, A);
+    A.eblocks = 0;  // the edge lanes too, when launch_edges_read_check left them (b.edges_fused)
+    size_t shm = base + 8 * (size_t)A.lcap;
+    if (b.edges_fused) {
+        b.edges_fused = false;
+        A.ea = make_edges_args(v, b, sc);
+        A.eblocks = cdiv((int64_t)v.read_count + fused_edge_quads(v.write_count), DC_THREADS);
+        shm = std::max<size_t>(shm, EQ * sizeof(uint64_t));  // (an edge block's sample of the sorted writes)
+    }
+    hipLaunchKernelGGL(k_decide_rounds, dim3(1 + A.eblocks + wsb), dim3(DC_THREADS), shm, s, A);
     if (multi && !split) launch_combine_grid(v, b, sc, s);
     return eo != nullptr;
 }

@@ -376,3 +376,27 @@ def test_live_timeout_falls_back(gpu):
     assert st["live_timeouts"] == 1 and st["live_batches"] >= 2, st
     same_history(g, c)
     g.close()
+
+
+def test_live_sort_overflow_falls_back(gpu):
+    """Live batches whose keys moved away from the last batch's quantiles (a
+    sort bucket overflows its staging row while the live kernel scatters):
+    the overflow guard after the live kernel re-buckets them, as after the
+    whole-stream ingest; verdicts and history stay exact and every batch
+    after the first stays live."""
+    g = live_cs(8)
+    c = CpuSpec()
+    now = 10
+    plan = [(400, 1000), (400, 5000), (400, 9_000_000), (400, 9_001_000), (400, 20_000)]
+    for i, (T, base) in enumerate(plan):
+        txns = txns_for(T, base, now - 5, 14)  # (base 9 M: every key above the last batch's splitters)
+        b = ConflictBatch(g)
+        for snap, r, w in txns:
+            b.add_transaction(r, w, snap)
+        v = b.detect_conflicts(now, 0)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, 0)), i
+        now += 10
+    st = g.batch_stats()
+    assert st["live_batches"] == len(plan) - 1 and st["sort_rebucketed"] in (0, 1), st
+    same_history(g, c)
+    g.close()
