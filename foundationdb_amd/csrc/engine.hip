@@ -214,6 +214,11 @@ struct fdbcs {
         uint64_t rolled_seq = 0;  // ... with this draw counter
         int64_t count = 0;        // ... into this many entries
         uint64_t batch = 0;       // ... and it was batch number `batch`
+        // ... on the host instead (a protocol-B shard's adds, fdbcs_sharded:
+        // lm_ent / lm_bytes): the entries' home; null: the pinned buffers above
+        const LmEntry* host_ent = nullptr;
+        const uint8_t* host_bytes = nullptr;
+        size_t host_nb = 0;
     } lm;
     uint64_t batches = 0;  // batches run (run_batch / sh_run)
     // live ingest (k_live_ingest)
@@ -1203,6 +1208,7 @@ int finish_detect(fdbcs* cs, const fdbcs_batch_view& dv, int64_t now, int64_t ne
                       (live ? cs->lv_lm
                             : lm_arm(cs, (uint64_t)dv.read_count + dv.write_count, dv.key_bytes_len, la) == FDBCS_OK);
     cs->lm.rolled = false;
+    cs->lm.host_ent = nullptr;
     if ((r = run_batch(cs, dv, now, new_oldest, nullptr, false, early, roll && !live ? &la : nullptr))) return r;
     int64_t count = 0;
     if (early) {
@@ -1293,7 +1299,8 @@ void engine_lm_attach(fdbcs* cs, const void* owner, const uint64_t* seq, uint64_
 bool engine_lm_take(fdbcs* cs, const void* owner, uint64_t seq, int64_t opk, LmTake& out) {
     const fdbcs::Lm& L = cs->lm;
     if (!L.rolled || L.owner != owner || L.batch != cs->batches || L.rolled_seq != seq || L.opk != opk) return false;
-    out = LmTake{L.count, L.ent, L.bytes, L.cap_n, L.cap_b};
+    if (L.host_ent) out = LmTake{L.count, L.host_ent, L.host_bytes, (size_t)L.count, L.host_nb};  // (the shard's host roll)
+    else out = LmTake{L.count, L.ent, L.bytes, L.cap_n, L.cap_b};
     return true;
 }
 }  // namespace fdbcs_dev
@@ -2101,6 +2108,20 @@ struct fdbcs_sharded {
     // marked dead instead of being cleared under the owner's feet.
     std::mutex comm_mu;
     bool comm_dead = false;                // (guarded by comm_mu)
+    // A load sample attached to this rank's engine (the Resolver attaches to
+    // conflictSetDevice = rank 0's): under protocol B the rank keeps only the
+    // ranges on its keys, so its ingest cannot roll the batch as one resolver
+    // would (and sh_run's ingest does not roll under A either).  The adds roll
+    // every range of every transaction on the host instead -- the Resolver's
+    // order (writes, then reads), positions over the whole batch
+    // (Resolver.actor.cpp:146-151) -- so the sample is the one-GPU sample
+    // exactly (fdbcs_sharded_batch_add).  Not with FDBCS_SHARD_PRESPLIT (the
+    // adds never see the whole transaction): the sample then covers the
+    // rank's share.
+    bool lm_host = false;
+    uint64_t lm_seq = 0, lm_pos = 0;
+    std::vector<LmEntry> lm_ent;
+    std::vector<uint8_t> lm_bytes;
 };
 
 namespace {
@@ -2472,12 +2493,36 @@ int fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_b
     return sh_run(sh, *dev_batch, now, new_oldest, verdict);
 }
 
+// iopsSample.addAndExpire of every range's begin of one added transaction,
+// writes then reads (fdbcs_sharded::lm_host)
+static void sh_roll_host(fdbcs_sharded* sh, const fdbcs_range* reads, int32_t nreads, const fdbcs_range* writes,
+                         int32_t nwrites) {
+    const fdbcs::Lm& L = sh->cs->lm;
+    for (int32_t i = 0; i < nwrites + nreads; i++) {
+        const fdbcs_range& x = i < nwrites ? writes[i] : reads[i - nwrites];
+        const uint64_t pos = sh->lm_pos++;
+        const int64_t amt = roll_amount(roll_hash(L.seed, sh->lm_seq, pos), L.opk + (int64_t)x.begin_len, L.units);
+        if (!amt) continue;
+        const uint64_t off = sh->lm_bytes.size();
+        sh->lm_bytes.insert(sh->lm_bytes.end(), x.begin, x.begin + x.begin_len);
+        sh->lm_ent.push_back(LmEntry{amt, (uint32_t)pos, x.begin_len, off, 0});
+    }
+}
+
 int fdbcs_sharded_batch_begin(fdbcs_sharded* sh) {
     if (!sh) return FDBCS_E_ARG;
     int r;
     sh->cs->lv_prev_T = 0;  // (no live ingest: sh_run ingests the whole batch)
     if ((r = fdbcs_batch_begin(sh->cs))) return r;
     sh->in_batch = true;
+    const fdbcs::Lm& L = sh->cs->lm;
+    sh->lm_host = !sh->presplit && sh->world > 1 && L.owner && L.seq;
+    if (sh->lm_host) {
+        sh->lm_seq = *L.seq;  // (the draws of the batch the sample takes next)
+        sh->lm_pos = 0;
+        sh->lm_ent.clear();
+        sh->lm_bytes.clear();
+    }
     return FDBCS_OK;
 }
 
@@ -2495,6 +2540,11 @@ int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbc
                             const fdbcs_range* writes, int32_t nwrites) {
     if (!sh) return FDBCS_E_ARG;
     if (!sh->in_batch) return FDBCS_E_STATE;
+    if (sh->lm_host && sh->proto == FDBCS_PROTOCOL_A) {  // (B rolls below, after its checks)
+        const int r = fdbcs_batch_add(sh->cs, read_snapshot, reads, nreads, writes, nwrites);
+        if (r == FDBCS_OK) sh_roll_host(sh, reads, nreads, writes, nwrites);
+        return r;
+    }
     if (sh->proto == FDBCS_PROTOCOL_A || sh->presplit || sh->world == 1)
         return fdbcs_batch_add(sh->cs, read_snapshot, reads, nreads, writes, nwrites);
     // protocol B: only the ranges that intersect this rank's keys, and the
@@ -2520,6 +2570,7 @@ int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbc
         return (!sh->has_lo || keycmp(x.end, x.end_len, lo, ll) > 0) &&
                (!sh->has_hi || keycmp(x.begin, x.begin_len, hi, hl) < 0);
     };
+    if (sh->lm_host) sh_roll_host(sh, reads, nreads, writes, nwrites);
     std::vector<fdbcs_range>& k = sh->keep;
     k.clear();
     for (int32_t i = 0; i < nreads; i++)
@@ -2552,6 +2603,19 @@ int fdbcs_sharded_batch_detect(fdbcs_sharded* sh, int64_t now, int64_t new_oldes
     r = sh_run(sh, dv, now, new_oldest, verdict);
     cs->stage_key_total = 0;
     cs->b.staged = StagedBatch{};
+    fdbcs::Lm& L = cs->lm;
+    L.rolled = false;
+    L.host_ent = nullptr;
+    if (r == FDBCS_OK && sh->lm_host && L.owner && L.seq) {  // this batch's host roll, for fdbcs_sample_add_batch
+        L.rolled = true;
+        L.rolled_seq = sh->lm_seq;
+        L.count = (int64_t)sh->lm_ent.size();
+        L.batch = cs->batches;
+        L.host_ent = sh->lm_ent.data();
+        L.host_bytes = sh->lm_bytes.data();
+        L.host_nb = sh->lm_bytes.size();
+    }
+    sh->lm_host = false;
     return r;
 }
 

@@ -13,8 +13,10 @@
 #include <vector>
 
 #include "fdbserver/ConflictSet.h"
+#include "fdbcs.h"
 
 void skipListTest();
+fdbcs* conflictSetDevice(ConflictSet* cs);  // ConflictSetShim.cpp (the Resolver's load-metrics binding)
 
 template <class T>
 static T rd(FILE* f) {
@@ -98,7 +100,76 @@ static int rankfail_mode() {
     return 0;
 }
 
+// "sample IN OUT UNITS SEED": the resolve loop of main() with the Resolver's
+// iopsSample bound as INTEGRATION.md §4.3 binds it (fdbcs_sample_attach to
+// conflictSetDevice once, fdbcs_sample_add_batch after each detectConflicts,
+// a poll every third batch); OUT (text): every sample entry (hex key,
+// metric), the queue size, getEstimate(allKeys) and two splitEstimates
+static int sample_mode(const char* inp, const char* outp, long units, unsigned long seed) {
+    FILE* in = fopen(inp, "rb");
+    FILE* out = fopen(outp, "w");
+    if (!in || !out) return 2;
+    ConflictSet* cs = newConflictSet();
+    fdbcs_sample* s = nullptr;
+    if (fdbcs_sample_create(&s, units, seed) || fdbcs_sample_attach(s, conflictSetDevice(cs), 100)) return 4;
+    const int nb = rd<int32_t>(in);
+    for (int b = 0; b < nb; b++) {
+        const int64_t now = rd<int64_t>(in), nold = rd<int64_t>(in);
+        const int T = rd<int32_t>(in);
+        std::vector<std::vector<uint8_t>> keep;
+        std::vector<CommitTransactionRef> trs(T);
+        for (int t = 0; t < T; t++) {
+            trs[t].read_snapshot = rd<int64_t>(in);
+            const int nr = rd<int32_t>(in), nw = rd<int32_t>(in);
+            for (int k = 0; k < nr + nw; k++) {
+                KeyRef ends[2];
+                for (int q = 0; q < 2; q++) {
+                    const uint32_t n = rd<uint32_t>(in);
+                    keep.emplace_back(n + 1);
+                    if (n && fread(keep.back().data(), 1, n, in) != n) return 3;
+                    ends[q] = KeyRef(keep.back().data(), (int)n);
+                }
+                (k < nr ? trs[t].read_conflict_ranges : trs[t].write_conflict_ranges)
+                    .push_back(KeyRangeRef(ends[0], ends[1]));
+            }
+        }
+        std::vector<int> commitList, tooOldList;
+        {
+            ConflictBatch batch(cs);
+            for (int t = 0; t < T; t++) batch.addTransaction(trs[t]);
+            batch.detectConflicts(now, nold, commitList, &tooOldList);
+        }
+        if (fdbcs_sample_add_batch(s, conflictSetDevice(cs), nullptr, 100, 0.5 * b + 1.0, nullptr)) return 5;
+        if (b % 3 == 2 && fdbcs_sample_poll(s, 0.5 * b)) return 6;
+    }
+    std::vector<uint8_t> k(70000);
+    const int64_t n = fdbcs_sample_size(s);
+    for (int64_t i = 0; i < n; i++) {
+        int64_t m = 0;
+        const int32_t len = fdbcs_sample_entry(s, i, k.data(), (uint32_t)k.size(), &m);
+        if (len < 0) return 7;
+        for (int32_t j = 0; j < len; j++) fprintf(out, "%02x", k[j]);
+        fprintf(out, " %lld\n", (long long)m);
+    }
+    const uint8_t hi[2] = {0xff, 0xff};
+    const int64_t total = fdbcs_sample_estimate(s, nullptr, 0, hi, 2);
+    fprintf(out, "queue %lld\nestimate %lld\n", (long long)fdbcs_sample_queue_size(s), (long long)total);
+    for (int front = 0; front < 2; front++) {
+        const int32_t len = fdbcs_sample_split(s, nullptr, 0, hi, 2, total / 3, front, k.data(), (uint32_t)k.size());
+        if (len < 0) return 8;
+        fprintf(out, "split%d ", front);
+        for (int32_t j = 0; j < len; j++) fprintf(out, "%02x", k[j]);
+        fprintf(out, "\n");
+    }
+    destroyConflictSet(cs);  // (before its sample, as ~Resolver does)
+    fdbcs_sample_destroy(s);
+    fclose(out);
+    fclose(in);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 6 && std::string(argv[1]) == "sample") return sample_mode(argv[2], argv[3], atol(argv[4]), strtoul(argv[5], nullptr, 0));
     if (argc == 2 && std::string(argv[1]) == "skiplisttest") {
         skipListTest();
         return 0;

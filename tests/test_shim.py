@@ -160,3 +160,40 @@ def test_shim_rank_failure_throws_not_hangs(gpu, protocol):
     r = subprocess.run([B.SHIM_CHECK, "rankfail"], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stderr
     assert "batch 0 ok" in r.stdout and "threw at batch 1" in r.stdout and "unusable" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,protocol", [(1, "b"), (2, "b"), (3, "b"), (2, "a")])
+def test_shim_load_sample_across_ranks(gpu, tmp_path, shards, protocol):
+    """The Resolver's iopsSample through the drop-in (INTEGRATION.md §4.3:
+    attached to conflictSetDevice, fdbcs_sample_add_batch after each
+    detectConflicts, polls) with G GPUs as one resolver.  Under protocol B a
+    rank keeps only the ranges on its keys, so the sample is rolled on the host
+    by the adds of the rank whose engine holds it -- every range of the global
+    batch, in the Resolver's order.  The sample, its
+    queue, getEstimate(allKeys) and splitEstimate equal one resolver's, as the
+    oracle rolls them."""
+    if not os.path.exists(B.SHIM_CHECK):
+        pytest.skip("shim driver not built")
+    from oracle.load_sample import SpecSample
+    batches = list(tiny_stream(31, n_batches=18, max_txns=40, maxlen=11)) + list(mixed_stream(32, n_batches=4))
+    units, seed = 110, 7
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.txt"
+    write_batches(fin, batches)
+    env = dict(os.environ, FDBCS_SHARDS=str(shards), FDBCS_SHARD_COMM="host", FDBCS_SHARD_DEVICES="0",
+               FDBCS_SHARD_PROTOCOL=protocol, FDBCS_SHARD_BOUNDS="61,62"[:2 if shards == 2 else 5])
+    subprocess.run([B.SHIM_CHECK, "sample", str(fin), str(fout), str(units), str(seed)], check=True, timeout=120,
+                   env=env)
+    o = SpecSample(units, seed=seed)
+    for b, (batch, now, nold) in enumerate(batches):
+        o.add_batch(batch, 0.5 * b + 1.0, offset_per_key=100)
+        if b % 3 == 2:
+            o.poll(0.5 * b)
+    hi = b"\xff\xff"
+    total = o.get_estimate(b"", hi)
+    want = [f"{k.hex()} {m}" for k, m in o.items()]
+    want += [f"queue {len(o.queue)}", f"estimate {total}"]
+    want += ["split%d %s" % (f, o.split_estimate(b"", hi, total // 3, bool(f)).hex()) for f in (0, 1)]
+    got = fout.read_text().split("\n")[:-1]
+    assert len(o.items()) > 20, "too few sampled keys to mean anything"
+    assert got == want
