@@ -299,6 +299,11 @@ struct Scalars {
     // rounds mode, edge lanes fused into the decision launch (k_decide_rounds):
     // edge blocks done; block 0 waits for all of them, then zeroes it
     int32_t e_done;
+    // large batches (k_page_join): reads whose end lies past their begin's page
+    int32_t n_fall;
+    // protocol B's edge exchange at a fixed capacity (k_sh_edges_cat_fixed):
+    // the largest shard count when some shard's did not fit (0: they did)
+    int32_t sh_need;
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;
@@ -354,6 +359,12 @@ struct LmArgs {
     uint32_t cap_n;
     uint64_t cap_b;
 };
+
+// Internal status of a sharded batch whose fixed-capacity edge exchange was
+// short (k_sh_edges_cat_fixed): every history stage after it leaves the
+// history as it was, and the host runs the batch's exchange onward again
+// with a larger capacity (engine.hip sh_run).  Never returned to a caller.
+constexpr int32_t E_SH_RETRY = -100;
 
 constexpr int32_t TF_NOGC = 1;        // a survivor's tail could not be moved this sweep: no swap
 constexpr int32_t TF_FROM_START = 2;  // this sweep's first window started at boundary 0

@@ -475,6 +475,7 @@ void free_batch(BatchBufs& b) {
     dfree(b.ss_cnt); dfree(b.ss_gsamp); dfree(b.ss_q); dfree(b.ss_qt); dfree(b.ss_bkt); dfree(b.ss_tmp); dfree(b.lb_meta); dfree(b.lb_hist);
     dfree(b.et); dfree(b.eu); dfree(b.csr);
     dfree(b.rq); dfree(b.rstamp); dfree(b.plist); dfree(b.items); dfree(b.wnew); dfree(b.winv); dfree(b.wcov);
+    dfree(b.pj_fall);
     dfree(b.cb_pos); dfree(b.ce_pos); dfree(b.comb_blk); free_keys(b.rkb); free_keys(b.rke);
     dfree(b.pb); dfree(b.ib); dfree(b.pe); dfree(b.ie); dfree(b.need_e); dfree(b.vb);
     dfree(b.wh.b); dfree(b.wh.e);
@@ -579,6 +580,13 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         HIPOK(hipMemsetAsync(b.ss_q, 0, 2 * 1024 * sizeof(SRec), s));  // equal records: valid (sorted) splitters
     }
     if (!b.lb_meta && (r = dalloc(b.lb_meta, lb_meta_words()))) return r;
+    if (b.large && R + 2 * W + 64 > b.pj_cap) {  // (k_page_join's lists)
+        const int64_t n = R + 2 * W + 64;
+        dfree(b.pj_fall);
+        b.pj_cap = 0;
+        if ((r = dalloc(b.pj_fall, n))) return r;
+        b.pj_cap = n;
+    }
     if (b.large && lb_hist_words((int)R, (int)W) + 1 > b.lb_hist_cap) {
         const int64_t n = lb_hist_words((int)R, (int)W) + 1;
         dfree(b.lb_hist);
@@ -2097,10 +2105,8 @@ struct fdbcs_sharded {
     std::vector<fdbcs_range> keep;         // the add filter's output
     int32_t* ebuf = nullptr;               // device: [send 2M | recv G x 2M | readers E | writers E]
     int64_t ebuf_cap = 0;                  // (int32 elements)
-    uint64_t* emap = nullptr;              // host-mapped: k_sh_edges_plan's {seq, max, total, overflow, own}
-    uint64_t* emap_dev = nullptr;
-    uint64_t eseq = 0;
-    hipEvent_t ev_edges = nullptr;
+    int64_t ecap = 4096;                   // edge pairs per shard in the exchange (grows on a short batch)
+    int64_t retries = 0;                   // batches whose exchange was short and ran again (stats)
     std::atomic<bool> aborted{false};      // fdbcs_sharded_abort (any thread)
     // The communicator is touched by the rank's own thread (init, enqueues,
     // progress polls) and by fdbcs_sharded_abort from another one: every use
@@ -2205,10 +2211,15 @@ int sh_allgather(fdbcs_sharded* sh, const void* dev_send, void* dev_recv, size_t
 
 // Protocol B, after the check: exchange 1 (the abort flags and slots, which
 // carry every shard's edge count) and then the union of the shards' overlap
-// edges as this shard's list.  The host reads the counts once (mapped
-// memory, ~2 ms of polling before it blocks on an event) to size the edge
-// all-gather; when any shard's list overflowed, every shard searches again
-// into a larger one and exchange 1 repeats (the read check is idempotent).
+// edges as this shard's list -- at a fixed capacity of sh->ecap pairs per
+// shard, so the host enqueues the whole batch without reading anything
+// (the counts used to be polled from host-mapped memory
+// mid-batch to size the all-gather).  When some shard's list does not fit
+// (or overflowed its own buffer) k_sh_edges_cat_fixed marks the batch
+// E_SH_RETRY: the decision's verdicts say so, every history stage after it
+// leaves the history as it was, and sh_run searches again and repeats the
+// exchange with a larger capacity -- on every rank alike, since all of them
+// see the same gathered counts.
 int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, uint8_t* flags) {
     fdbcs* cs = sh->cs;
     BatchBufs& b = cs->b;
@@ -2216,55 +2227,30 @@ int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, ui
     const int64_t T = v.txn_count;
     int64_t* sl = reinterpret_cast<int64_t*>(sh->x1);
     int r;
-    for (int attempt = 0;; attempt++) {
-        launch_sh_edges_count(cs->sc, sl, sh->rank, sh->world, b.edge_cap, s);
-        if (T) launch_flags_out(b, (int)T, flags, s);
-        if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
-        if (++sh->eseq == 0) sh->eseq = 1;
-        launch_sh_edges_plan(sl, sh->world, sh->rank, sh->emap_dev, sh->eseq, s);
-        HIPOK(hipEventRecord(sh->ev_edges, s));
-        const auto t0 = std::chrono::steady_clock::now();
-        for (int it = 1; __atomic_load_n(sh->emap, __ATOMIC_ACQUIRE) != sh->eseq; it++) {
-            _mm_pause();
-            if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-                if ((r = wait_event(sh->ev_edges))) return r;
-                if (__atomic_load_n(sh->emap, __ATOMIC_ACQUIRE) != sh->eseq) return FDBCS_E_HIP;
-                break;
-            }
-        }
-        const int64_t mx = (int64_t)sh->emap[1], tot = (int64_t)sh->emap[2], own = (int64_t)sh->emap[4];
-        if (!sh->emap[3]) {
-            if (mx == 0) return FDBCS_OK;  // no overlap anywhere: this shard's empty list is the union
-            if (tot > INT32_MAX) return FDBCS_E_CAPACITY;
-            const int64_t need = 2 * mx * (sh->world + 1) + 2 * tot;
-            if (need > sh->ebuf_cap) {
-                HIPOK(hipStreamSynchronize(s));  // (the previous batch's exchange may still read it)
-                if (sh->ebuf) hipFree(sh->ebuf);
-                sh->ebuf = nullptr;
-                sh->ebuf_cap = 0;
-                const int64_t n = need + need / 2 + 4096;
-                if ((r = dalloc(sh->ebuf, n))) return r;
-                sh->ebuf_cap = n;
-            }
-            int32_t* send = sh->ebuf;
-            int32_t* recv = send + 2 * mx;
-            int32_t* cat = recv + 2 * mx * sh->world;
-            launch_sh_edges_pack(b, cs->sc, mx, send, s);
-            if ((r = sh_allgather(sh, send, recv, (size_t)(2 * mx) * 4))) return r;
-            if (tot > b.edge_cap && (r = grow_edges(b, tot + tot / 4 + 1024))) return r;
-            launch_sh_edges_cat(recv, sl, sh->world, mx, cat, cat + tot, s);
-            launch_set_edges(b, cs->sc, (int)T, cat, cat + tot, tot, s);
-            return FDBCS_OK;
-        }
-        // some shard's list overflowed: every shard searches again (into a
-        // larger list where its own overflowed)
-        if (attempt >= 3) return FDBCS_E_CAPACITY;
-        GROWLOG("sharded edges: own %lld cap %lld\n", (long long)own, (long long)b.edge_cap);
-        if (own > b.edge_cap && (r = grow_edges(b, own + own / 4 + 1024))) return r;
-        if (T) HIPOK(hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s));
-        HIPOK(hipMemsetAsync(&cs->sc->edges_total, 0, sizeof(int32_t), s));
-        launch_edges_read_check(v, b, cs->h, cs->cur, cs->sc, sh->v0, s);
+    const int64_t M = sh->ecap, G = sh->world;
+    const int64_t need = 2 * M * (2 * G + 1);  // send | recv G x | concatenated G x, int32 pairs
+    if (need > sh->ebuf_cap) {
+        HIPOK(hipStreamSynchronize(s));  // (the previous batch's exchange may still read it)
+        if (sh->ebuf) hipFree(sh->ebuf);
+        sh->ebuf = nullptr;
+        sh->ebuf_cap = 0;
+        if ((r = dalloc(sh->ebuf, need))) return r;
+        sh->ebuf_cap = need;
     }
+    // (the gathered list's home is this shard's list: sized before its search,
+    // sh_run -- growing it here would drop the edges just found)
+    if (M * G > b.edge_cap) return FDBCS_E_STATE;
+    launch_sh_edges_count(cs->sc, sl, sh->rank, sh->world, b.edge_cap, s);
+    if (T) launch_flags_out(b, (int)T, flags, s);
+    if ((r = sh_allreduce_max(sh, sh->x1, slots + (size_t)T))) return r;
+    int32_t* send = sh->ebuf;
+    int32_t* recv = send + 2 * M;
+    int32_t* cat = recv + 2 * M * G;
+    launch_sh_edges_pack(b, cs->sc, M, send, s);
+    if ((r = sh_allgather(sh, send, recv, (size_t)(2 * M) * 4))) return r;
+    launch_sh_edges_cat_fixed(recv, sl, (int)G, M, cat, cat + M * G, cs->sc, s);
+    launch_set_edges(b, cs->sc, (int)T, cat, cat + M * G, -(M * G), s);
+    return FDBCS_OK;
 }
 
 // one batch of the sharded resolver on the device-resident view v
@@ -2322,9 +2308,15 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
         cs->sorts++;
         cs->have_quantiles = true;
     }
+    const int64_t oldest0 = cs->oldest;
+    if (sh->proto == FDBCS_PROTOCOL_B) {
+        // (the list the search fills also receives the gathered edges: sized first)
+        if (sh->ecap * sh->world > b.edge_cap && (r = grow_edges(b, sh->ecap * sh->world))) return r;
+        launch_edges_read_check(v, b, cs->h, cs->cur, sc, sh->v0, s);
+    }
+    for (int attempt = 0;; attempt++) {  // (protocol B: again after a short edge exchange)
     if (sh->proto == FDBCS_PROTOCOL_B) {
         // 3 (protocol B): exchange 1 with the edge counts, then the edges
-        launch_edges_read_check(v, b, cs->h, cs->cur, sc, sh->v0, s);
         if ((r = sh_exchange_b(sh, v, slots, flags))) return r;
     } else {
         if ((r = edges_read_check(cs, v, sh->v0))) return r;
@@ -2363,7 +2355,33 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     launch_sh_slot_out(sc, reinterpret_cast<int64_t*>(sh->x1), sh->rank, sh->world, s);
     // the one wait: the verdicts
     if (!T) return FDBCS_OK;
-    if ((r = verdict_wait(cs, T, verdict))) return r;
+    r = verdict_wait(cs, T, verdict);
+    if (r != E_SH_RETRY) {
+        if (r) return r;
+        break;
+    }
+    // Some shard's edge list did not fit the exchange (every rank sees it
+    // alike): this attempt's merge, plan and compaction left the history as
+    // it was (k_plan_ranges / k_page_merge skip on the error, the directory
+    // is copied to the other buffer, k_sh_plan opens no window).  Grow the
+    // capacity, search the edges again (the gathered list overwrote this
+    // shard's own), and run the batch from exchange 1 on once more.
+    if (attempt >= 4) return FDBCS_E_CAPACITY;
+    if ((r = sync_state(cs))) return r;
+    const int64_t need = cs->sc_host->sh_need;
+    sh->retries++;
+    GROWLOG("sharded edge exchange short: need %lld, capacity %lld\n", (long long)need, (long long)sh->ecap);
+    sh->ecap = std::max<int64_t>(2 * sh->ecap, need + need / 4 + 1024);
+    cs->oldest = oldest0;
+    HIPOK(hipMemsetAsync(&sc->err, 0, sizeof(int32_t), s));
+    HIPOK(hipMemsetAsync(&sc->last_err, 0, sizeof(int32_t), s));
+    HIPOK(hipMemsetAsync(&sc->sh_need, 0, sizeof(int32_t), s));
+    const int64_t cap = std::max<int64_t>(need + need / 4 + 1024, sh->ecap * sh->world);
+    if (cap > b.edge_cap && (r = grow_edges(b, cap))) return r;
+    if (T) HIPOK(hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s));
+    HIPOK(hipMemsetAsync(&sc->edges_total, 0, sizeof(int32_t), s));
+    launch_edges_read_check(v, b, cs->h, cs->cur, sc, sh->v0, s);
+    }
     cs->last_dv = v;
     cs->have_last_dv = true;
     return FDBCS_OK;
@@ -2395,6 +2413,7 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     sh->rank = rank;
     sh->world = world;
     sh->v0 = v0;
+    if (const char* e = getenv("FDBCS_TEST_SH_ECAP")) sh->ecap = std::max(1, atoi(e));  // (tests: short exchanges)
     auto fail = [&](int code) {
         fdbcs_sharded_destroy(sh);
         return code;
@@ -2415,11 +2434,6 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     sh->has_hi = rank < world - 1;
     if (sh->has_lo) sh->lo.assign(lo, lo + bound_len[rank - 1]);
     if (sh->has_hi) sh->hi.assign(hi, hi + bound_len[rank]);
-    if (hipHostMalloc((void**)&sh->emap, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-        return fail(FDBCS_E_NOMEM);
-    memset(sh->emap, 0, 64);
-    HIPOK(hipHostGetDevicePointer((void**)&sh->emap_dev, sh->emap, 0));
-    HIPOK(hipEventCreateWithFlags(&sh->ev_edges, hipEventDisableTiming));
     if (hipMalloc((void**)&sh->x2, (size_t)(world + 1) * SH_WORDS * 8) != hipSuccess) return fail(FDBCS_E_NOMEM);
     launch_sh_init(cs->sc, v0, true, cs->stream);
     if (ops) {
@@ -2469,8 +2483,6 @@ void fdbcs_sharded_destroy(fdbcs_sharded* sh) {
     if (sh->x2) hipFree(sh->x2);
     if (sh->hx) hipHostFree(sh->hx);
     if (sh->ebuf) hipFree(sh->ebuf);
-    if (sh->emap) hipHostFree(sh->emap);
-    if (sh->ev_edges) hipEventDestroy(sh->ev_edges);
     if (sh->cs) fdbcs_destroy(sh->cs);
     delete sh;
 }

@@ -226,6 +226,10 @@ struct BatchBufs {
     int32_t* aff_cnt;
     int32_t* freed_list; // pages the merge frees, pushed after its pops
     int32_t* full_list;  // affected pages the merge rewrites (not in place)
+    // large batches (k_page_join): the reads whose end lies past their
+    // begin's page [R + 2W + 64]
+    int32_t* pj_fall;
+    int64_t pj_cap;
     // new-entry scratch [2W]
     Pool ne;             // key + version of new entries in page order
     int32_t* ne_ins;     // insertion index in the old page
@@ -400,10 +404,9 @@ bool engine_lm_take(fdbcs* cs, const void* owner, uint64_t seq, int64_t offset_p
 void sample_unlink(const void* owner, const fdbcs* cs);
 // protocol B's edge exchange (kernels_hist.hip)
 void launch_sh_edges_count(const Scalars* sc, int64_t* slots, int rank, int G, int64_t edge_cap, hipStream_t s);
-void launch_sh_edges_plan(const int64_t* slots, int G, int rank, uint64_t* map, uint64_t seq, hipStream_t s);
 void launch_sh_edges_pack(const BatchBufs& b, const Scalars* sc, int64_t M, int32_t* send, hipStream_t s);
-void launch_sh_edges_cat(const int32_t* recv, const int64_t* slots, int G, int64_t M, int32_t* cat_et,
-                         int32_t* cat_eu, hipStream_t s);
+void launch_sh_edges_cat_fixed(const int32_t* recv, const int64_t* slots, int G, int64_t M, int32_t* cat_et,
+                               int32_t* cat_eu, Scalars* sc, hipStream_t s);
 
 // fdbcs_nth_after (kernels_hist.hip): query keys (encoded; tails 8-byte
 // aligned, zero padded, in device memory) -> out[3q] = hi, lo, meta (~0: past

@@ -2416,6 +2416,9 @@ struct DirJoinArgs {
     KeyArrays keys;
     int R;
     int32_t* qx;
+    // by_pos: qx by sorted position instead -- [0, R) job 0, [R, R + 2W) job 1
+    // (k_page_join's runs)
+    int by_pos;
 };
 
 __global__ __launch_bounds__(MS_THREADS) void k_dir_join(DirJoinArgs A) {
@@ -2485,10 +2488,170 @@ __global__ __launch_bounds__(MS_THREADS) void k_dir_join(DirJoinArgs A) {
             const uint32_t slot = L.get(na + ib).idx;
             ib++;
             const int x = m - i;
-            if (job == 0) A.qx[slot >> 1] = x;
+            if (A.by_pos) A.qx[(job ? A.R : 0) + i] = x;
+            else if (job == 0) A.qx[slot >> 1] = x;
             else A.qx[A.R + (int)(slot - 2 * (uint32_t)A.R)] = x;
         }
     }
+}
+
+// ---- large batches: read checks and write searches, a lane per query ------
+// (config 5: 5 M reads and 4 M write endpoints over a 10^8-boundary history.)
+// The queries are sorted and k_dir_join gave each its directory entry (by
+// sorted position), so one lane answers one query with wide loads instead of
+// a 16-lane group probing 8 bytes a lane: the page's index line (hi of slots
+// 0, 16, ..., 240: 128 bytes), then the 16 slots of its window (128 bytes),
+// compared in registers; the full key only on a tie of the first 8 bytes.
+// A read whose end lies in the same page (the reads are short) searches the
+// same index line again and covers the versions between; one whose end lies
+// past the page goes to a list the 16-lane search then checks.  A write
+// endpoint gets its WriteHits record (slot, real boundaries before it,
+// valueBefore).  Measured first as a wavefront per page run, the page's keys
+// staged in LDS: slower (4.35 ms against 2.12 ms for the read-check stage at
+// config 5: ~10 queries per page left most lanes idle and every page was
+// read whole).
+struct PageJoinArgs {
+    int R, P;             // sorted read begins (job 0), sorted write endpoints (job 1)
+    const int32_t* xs;    // [R + P] directory entry of each sorted query (k_dir_join, by_pos)
+    int32_t* fall;        // reads whose end lies past their begin's page; Scalars::n_fall
+    const SRec* sr;
+    const SRec* sw;
+    KeyArrays keys;
+    const int32_t* read_txn;
+    const int64_t* read_snap;
+    uint8_t* hist;
+    Pool pool;
+    Dir dir;
+    Scalars* sc;
+    int64_t v0;
+    WriteHits wh;
+    int64_t wbase;
+};
+
+// slot s of a page (base) against k: the 8-byte word v already loaded
+__device__ inline int slot_vs(const Pool& p, int64_t base, int s, uint64_t v, const Key& k) {
+    if (v != k.hi) return v < k.hi ? -1 : 1;
+    return kcmp(pool_key(p, base + s), k);
+}
+
+// lower bound of k among the cnt slots of a page by one lane: idx = the
+// page's 16 index words (Pool::pidx), then one 16-slot window
+__device__ inline int lane_page_lb(const Pool& p, int64_t base, int cnt, const uint64_t (&idx)[16], const Key& k,
+                                   bool& eq) {
+    int n = 0;
+    bool eq_n = false;  // slot 16n holds k (when 16n < cnt)
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (16 * j < cnt) {
+            const int c = slot_vs(p, base, 16 * j, idx[j], k);
+            n += c < 0;
+            if (j == n && c == 0) eq_n = true;  // (the first slot not below k, when it equals k)
+        }
+    }
+    if (n == 0) {
+        eq = cnt > 0 && eq_n;
+        return 0;
+    }
+    const int w = 16 * (n - 1), e = min(cnt, 16 * n);
+    uint64_t v[16];
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(p.hi + base + w);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const ulonglong2 x = src[j];  // (a page's slots are 16-aligned: 128 bytes, whole line)
+        v[2 * j] = x.x;
+        v[2 * j + 1] = x.y;
+    }
+    int m = 0;  // slots of the window below k (slot w is)
+    bool eq_m = false;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (w + j < e) {
+            const int c = slot_vs(p, base, w + j, v[j], k);
+            m += c < 0;
+            if (j == m && c == 0) eq_m = true;
+        }
+    }
+    const int i = w + m;
+    eq = i < e ? eq_m : (e < cnt && eq_n);
+    return i;
+}
+
+__device__ inline void lane_index(const Pool& p, int pg, uint64_t (&idx)[16]) {
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(p.pidx + (int64_t)pg * (PAGE / PIDX_STRIDE));
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const ulonglong2 x = src[j];
+        idx[2 * j] = x.x;
+        idx[2 * j + 1] = x.y;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_page_join(PageJoinArgs A) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.R + A.P) return;
+    const Dir& d = A.dir;
+    const int x = A.xs[k];
+    const int pg = d.page[x], cnt = d.cnt[x];
+    const int64_t base = (int64_t)pg * PAGE;
+    uint64_t idx[16];
+    if (k < A.R) {  // the history check of read r
+        const SRec rec = A.sr[k];
+        const int r = (int)(rec.idx >> 1);
+        const int64_t s = A.read_snap[r];
+        if (s == INT64_MAX) return;
+        const Key b{rec.hi, rec.lo, rec.meta, key_len(rec.meta) > 17 ? A.keys.tail[2 * (int64_t)r] : nullptr};
+        const Key e = A.keys.get(2 * (int64_t)r + 1);
+        bool past = false;  // e > the next page's first key: e lies past this page
+        if (x + 1 < A.sc->D) {
+            const uint64_t fh = d.fhi[x + 1];
+            past = fh != e.hi ? fh < e.hi : kcmp(dir_first(d, x + 1), e) < 0;
+        }
+        if (past) {
+            A.fall[atomicAdd(&A.sc->n_fall, 1)] = r;  // (past this page: the 16-lane search)
+            return;
+        }
+        lane_index(A.pool, pg, idx);
+        bool eqb, eqe;
+        const int ib = lane_page_lb(A.pool, base, cnt, idx, b, eqb);
+        const int ie = lane_page_lb(A.pool, base, cnt, idx, e, eqe);
+        const int i0 = eqb ? ib : ib - 1;  // the slot whose version covers b
+        bool c = i0 < 0 && A.v0 > s;
+        for (int i = max(i0, 0); i < ie; i++) c |= A.pool.ver[base + i] > s;
+        if (c) A.hist[A.read_txn[r]] = 1;
+        return;
+    }
+    // where write endpoint (slot) falls (write_search_group)
+    const SRec rec = A.sw[k - A.R];
+    const uint32_t slot = rec.idx;
+    const int w = (int)(((int64_t)slot - A.wbase) >> 1);
+    const Key key{rec.hi, rec.lo, rec.meta, key_len(rec.meta) > 17 ? A.keys.tail[slot] : nullptr};
+    uint64_t hm[HM_WORDS];
+    load_hmask(A.pool, pg, hm);
+    lane_index(A.pool, pg, idx);
+    bool eq;
+    const int i = lane_page_lb(A.pool, base, cnt, idx, key, eq);
+    const int rb = real_before(hm, i);
+    if (!(slot & 1)) {
+        A.wh.b[w] = WHitB{x, i, d.nr[x], rb};
+        return;
+    }
+    int64_t vb;
+    bool from_v0 = false;  // no boundary below e: the header version
+    if (i > 0) vb = A.pool.ver[base + i - 1];
+    else if (x > 0 && d.cnt[x - 1] > 0) vb = A.pool.ver[(int64_t)d.page[x - 1] * PAGE + d.cnt[x - 1] - 1];
+    else vb = A.v0, from_v0 = true;  // (only entry 0 can be an empty page)
+    A.wh.e[w] = WHitE{vb, x, i, rb, (int32_t)((int)eq | (int)from_v0 << 1), 0};
+}
+
+// the reads k_page_join listed (their end lies past their begin's page): the
+// 16-lane history check with the directory search
+template <bool WIDE>
+__global__ __launch_bounds__(256) void k_read_check_list(ReadCheckArgs RA, const int32_t* list) {
+    const Group<RC_G> g;
+    const int n = RA.sc->n_fall;
+    const int ng = gridDim.x * blockDim.x / RC_G;
+    for (int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) / RC_G); q < n; q += ng)
+        read_check_group<WIDE>(RA, g, list[q]);
 }
 
 // Large batches: the overlap edges by one merge-join of the sorted read
@@ -2614,22 +2777,38 @@ void launch_edges_read_check(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& 
     // unsharded batches with b.dir_join: directory entries by merge-join (ss_bkt is free once the sort is done)
     static const bool dir_search = getenv("FDBCS_LARGE_DIR_SEARCH") != nullptr;  // (A/B measurements)
     const bool dj = b.dir_join && !(h.shard.has_lo | h.shard.has_hi) && !dir_search && R + W > 0;
+    // ... and then the read checks and write searches by page runs
+    // (k_page_join; FDBCS_LARGE_PAGE_JOIN=0: the 16-lane searches from the
+    // join's entries, A/B)
+    static const bool no_pj = getenv("FDBCS_LARGE_PAGE_JOIN") && !atoi(getenv("FDBCS_LARGE_PAGE_JOIN"));
+    const bool pj = dj && !no_pj && b.pj_fall && R + 2 * (int64_t)W + 64 <= b.pj_cap;
     if (dj) {
-        DirJoinArgs J{{b.sr, b.sw}, {R, 2 * W}, 0, h.dir[cur], sc, b.keys, R, b.ss_bkt};
+        DirJoinArgs J{{b.sr, b.sw}, {R, 2 * W}, 0, h.dir[cur], sc, b.keys, R, b.ss_bkt, pj ? 1 : 0};
         const int64_t cap_f = h.cap_dir;  // (an upper bound on D: blocks past the merged length exit)
         J.blocks0 = cdiv(cap_f + R, MS_CHUNK);
         const int blocks = J.blocks0 + cdiv(cap_f + 2 * (int64_t)W, MS_CHUNK);
         hipLaunchKernelGGL(k_dir_join, dim3(blocks), dim3(MS_THREADS), 0, s, J);
     }
-    const int32_t* qx = dj ? b.ss_bkt : nullptr;
+    const int32_t* qx = dj && !pj ? b.ss_bkt : nullptr;
     ReadCheckArgs RA{R, b.keys, b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, h.shard, qx};
+    if (pj && R + W > 0) {
+        (void)hipMemsetAsync(&sc->n_fall, 0, sizeof(int32_t), s);
+        const PageJoinArgs PJ{R, 2 * W, b.ss_bkt, b.pj_fall, (const SRec*)b.sr, (const SRec*)b.sw, b.keys,
+                              b.read_txn, b.read_snap, b.hist, h.pool, h.dir[cur], sc, v0, b.wh, write_base(b, v)};
+        const int64_t nq = R + 2 * (int64_t)W;
+        hipLaunchKernelGGL(k_page_join, dim3(cdiv(nq, 256)), dim3(256), 0, s, PJ);
+        if (R > 0) {
+            if (FDBCS_RC_WIDE) hipLaunchKernelGGL(k_read_check_list<true>, dim3(1024), dim3(256), 0, s, RA, b.pj_fall);
+            else hipLaunchKernelGGL(k_read_check_list<false>, dim3(1024), dim3(256), 0, s, RA, b.pj_fall);
+        }
+    }
     const EdgesArgs EA = make_edges_args(v, b, sc);
     WriteSearchArgs WA{R, W, b.keys, h.pool, h.dir[cur], sc, v0, b.wh, qx, write_base(b, v)};
     // (rc_fused: the history read check already ran in the sort's bucket launch)
-    const int rc_blocks = b.rc_fused ? 0 : cdiv((int64_t)R * RC_G, 256);
+    const int rc_blocks = b.rc_fused || pj ? 0 : cdiv((int64_t)R * RC_G, 256);
     b.rc_fused = false;
     b.ws_deferred = defer_ws && !dj;
-    const int ws_blocks = b.ws_deferred ? 0 : cdiv((int64_t)W * RC_G, 256);
+    const int ws_blocks = b.ws_deferred || pj ? 0 : cdiv((int64_t)W * RC_G, 256);
     static const bool search_edges = getenv("FDBCS_LARGE_EDGES_SEARCH") != nullptr;  // (A/B measurements)
     const bool join = b.large && !search_edges;
     const int e_blocks = R > 0 && W > 0 && !join ? cdiv(R + (b.rounds ? 2 * W : W), 256) : 0;
@@ -3488,8 +3667,26 @@ void launch_flags_in(BatchBufs& b, int T, const uint8_t* flags, hipStream_t s) {
     if (T > 0) hipLaunchKernelGGL(k_flags_in, dim3(cdiv(T, 256)), dim3(256), 0, s, T, flags, b.too_old, b.hist);
 }
 
+// n < 0: the count is sc->edges_total (set on the device), at most -n
+__global__ __launch_bounds__(256) void k_set_edges_dev(const int32_t* __restrict__ et, const int32_t* __restrict__ eu,
+                                                       int32_t* __restrict__ det, int32_t* __restrict__ deu,
+                                                       int32_t* __restrict__ deg, const Scalars* sc) {
+    const int64_t n = sc->edges_total;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t t = et[i];
+        det[i] = t;
+        deu[i] = eu[i];
+        atomicAdd(&deg[t], 1);
+    }
+}
 void launch_set_edges(BatchBufs& b, Scalars* sc, int T, const int32_t* et, const int32_t* eu, int64_t n,
                       hipStream_t s) {
+    if (n < 0) {  // (the device's count, sh_exchange_b)
+        if (T > 0) hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s);
+        hipLaunchKernelGGL(k_set_edges_dev, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, cdiv(-n, 256)))),
+                           dim3(256), 0, s, et, eu, b.et, b.eu, b.deg, (const Scalars*)sc);
+        return;
+    }
     if (T > 0) hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s);
     hipLaunchKernelGGL(k_set_edges, dim3(std::max(1, cdiv(n, 256))), dim3(256), 0, s, et, eu, n, b.et, b.eu, b.deg,
                        sc);

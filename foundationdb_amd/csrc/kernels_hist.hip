@@ -1653,6 +1653,10 @@ __global__ __launch_bounds__(64) void k_sh_plan(Pool pool, Dir dir, Scalars* sc,
                                                 int G, int64_t v0, int compact, RemovalKey rk) {
     __shared__ int64_t s_part[4];
     __shared__ int64_t s_owner[2];
+    if (sc->err == E_SH_RETRY) {  // (a short edge exchange: this attempt changes nothing; no window)
+        if (threadIdx.x == 0) sc->win_np = 0;
+        return;
+    }
     if (threadIdx.x == 0) {
         int64_t tot = 0, carry = v0, cur = v0;
         for (int g = 0; g < G; g++) {
@@ -1767,29 +1771,6 @@ __global__ __launch_bounds__(64) void k_sh_edges_count(const Scalars* sc, int64_
     }
 }
 
-// After exchange 1: the largest count, the total and any overflow, for the
-// host (mapped memory; the sequence word last, pushed to system scope): it
-// sizes the edge all-gather, or has every shard search again into a larger
-// list.
-__global__ __launch_bounds__(64) void k_sh_edges_plan(const int64_t* slots, int G, int rank, uint64_t* map,
-                                                      uint64_t seq) {
-    if (threadIdx.x != 0) return;
-    int64_t mx = 0, tot = 0, ovf = 0;
-    for (int g = 0; g < G; g++) {
-        const int64_t n = slots[g * SH_WORDS + 2];
-        mx = max(mx, n);
-        tot += n;
-        ovf |= slots[g * SH_WORDS + 3];
-    }
-    map[1] = (uint64_t)mx;
-    map[2] = (uint64_t)tot;
-    map[3] = (uint64_t)ovf;
-    map[4] = (uint64_t)slots[rank * SH_WORDS + 2];
-    __threadfence_system();
-    __hip_atomic_store(map, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-}
-
 // this shard's list, zero padded to M pairs: [readers M | writers M]
 __global__ __launch_bounds__(256) void k_sh_edges_pack(const int32_t* __restrict__ et, const int32_t* __restrict__ eu,
                                                        const Scalars* sc, int64_t M, int32_t* __restrict__ send) {
@@ -1800,36 +1781,48 @@ __global__ __launch_bounds__(256) void k_sh_edges_pack(const int32_t* __restrict
     }
 }
 
-// the gathered lists (shard g's at recv + 2 M g) concatenated in shard order
-__global__ __launch_bounds__(256) void k_sh_edges_cat(const int32_t* __restrict__ recv, const int64_t* slots, int64_t M,
-                                                      int32_t* __restrict__ cat_et, int32_t* __restrict__ cat_eu) {
-    const int g = blockIdx.y;
-    int64_t off = 0;
-    for (int q = 0; q < g; q++) off += slots[q * SH_WORDS + 2];
-    const int64_t n = slots[g * SH_WORDS + 2];
-    const int32_t* src = recv + 2 * M * g;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        cat_et[off + i] = src[i];
-        cat_eu[off + i] = src[M + i];
+// The fixed-capacity form (one host wait per batch, sh_exchange_b): every
+// shard sent min(count, M) pairs; one block concatenates the gathered lists
+// in shard order into (cat_et, cat_eu) and sets edges_total.  If some shard's
+// count exceeded M, or some shard's own list overflowed, the batch cannot be
+// decided from these: err = E_SH_RETRY (the history stages then change
+// nothing) and sh_need = the largest count.
+__global__ __launch_bounds__(1024) void k_sh_edges_cat_fixed(const int32_t* __restrict__ recv, const int64_t* slots,
+                                                             int G, int64_t M, int32_t* __restrict__ cat_et,
+                                                             int32_t* __restrict__ cat_eu, Scalars* sc) {
+    int64_t off = 0, mx = 0;
+    int64_t ovf = 0;
+    for (int g = 0; g < G; g++) {
+        const int64_t c = slots[g * SH_WORDS + 2], n = min(c, M);
+        mx = max(mx, c);
+        ovf |= slots[g * SH_WORDS + 3];
+        const int32_t* src = recv + 2 * M * g;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            cat_et[off + i] = src[i];
+            cat_eu[off + i] = src[M + i];
+        }
+        off += n;
+    }
+    if (threadIdx.x == 0) {
+        sc->edges_total = (int32_t)off;
+        if (mx > M || ovf) {
+            sc->sh_need = (int32_t)min<int64_t>(mx, INT32_MAX);
+            atomicCAS(&sc->err, 0, E_SH_RETRY);
+        }
     }
 }
 
 void launch_sh_edges_count(const Scalars* sc, int64_t* slots, int rank, int G, int64_t edge_cap, hipStream_t s) {
     hipLaunchKernelGGL(k_sh_edges_count, dim3(1), dim3(64), 0, s, sc, slots, rank, G, edge_cap);
 }
-void launch_sh_edges_plan(const int64_t* slots, int G, int rank, uint64_t* map, uint64_t seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_sh_edges_plan, dim3(1), dim3(64), 0, s, slots, G, rank, map, seq);
-}
 void launch_sh_edges_pack(const BatchBufs& b, const Scalars* sc, int64_t M, int32_t* send, hipStream_t s) {
     const int nb = (int)std::min<int64_t>(1024, (M + 255) / 256);
     hipLaunchKernelGGL(k_sh_edges_pack, dim3(std::max(1, nb)), dim3(256), 0, s, b.et, b.eu, sc, M, send);
 }
-void launch_sh_edges_cat(const int32_t* recv, const int64_t* slots, int G, int64_t M, int32_t* cat_et,
-                         int32_t* cat_eu, hipStream_t s) {
-    const int nb = (int)std::min<int64_t>(256, (M + 255) / 256);
-    hipLaunchKernelGGL(k_sh_edges_cat, dim3(std::max(1, nb), G), dim3(256), 0, s, recv, slots, M, cat_et, cat_eu);
+void launch_sh_edges_cat_fixed(const int32_t* recv, const int64_t* slots, int G, int64_t M, int32_t* cat_et,
+                               int32_t* cat_eu, Scalars* sc, hipStream_t s) {
+    hipLaunchKernelGGL(k_sh_edges_cat_fixed, dim3(1), dim3(1024), 0, s, recv, slots, G, M, cat_et, cat_eu, sc);
 }
-
 // ------------------------------------------------------------------ reset ----
 __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int cap_pages, Scalars* sc,
                                               uint64_t* hmask) {

@@ -34,9 +34,11 @@ def _streams(kind, seed):
     return list(mixed_stream(seed, n_batches=8, max_txns=400, keyspace=3000))
 
 
-def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None):
+def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None, sh_ecap=None):
     if edge_cap:  # (a tiny first edge list: every shard searches again into a larger one)
         os.environ["FDBCS_TEST_EDGE_CAP"] = str(edge_cap)
+    if sh_ecap:  # (a tiny edge exchange: the batch runs from exchange 1 again with a larger one)
+        os.environ["FDBCS_TEST_SH_ECAP"] = str(sh_ecap)
     import torch
     import torch.distributed as dist
 
@@ -80,7 +82,7 @@ def _rank(rank, world, port, bounds, kind, seed, q, protocol="a", edge_cap=None)
 @pytest.mark.gpu
 @pytest.mark.parametrize("protocol", ["a", "b"])
 @pytest.mark.parametrize("world,kind", [(2, "tiny"), (3, "tiny"), (2, "long"), (2, "mixed"), (3, "mixed")])
-def test_sharded_abi_equals_one_conflict_set(gpu, world, kind, protocol, edge_cap=None):
+def test_sharded_abi_equals_one_conflict_set(gpu, world, kind, protocol, edge_cap=None, sh_ecap=None):
     rng = random.Random(world * 31 + len(kind))
     if kind == "mixed":
         bounds = sorted({b"k%06d" % rng.randrange(1, 3000) for _ in range(world - 1)})
@@ -95,7 +97,7 @@ def test_sharded_abi_equals_one_conflict_set(gpu, world, kind, protocol, edge_ca
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.Random(os.getpid() * 13 + world + len(kind) + 7 * ord(protocol[0])).randint(0, 3000)
-    procs = [ctx.Process(target=_rank, args=(r, world, port, bounds, kind, seed, q, protocol, edge_cap))
+    procs = [ctx.Process(target=_rank, args=(r, world, port, bounds, kind, seed, q, protocol, edge_cap, sh_ecap))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -166,6 +168,18 @@ def test_sharded_abi_protocol_b_edge_overflow(gpu):
     overflows it on some rank, every rank searches again (exchange 1
     repeats) and the edges travel in the all-gather."""
     test_sharded_abi_equals_one_conflict_set(gpu, 3, "mixed", "b", edge_cap=3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,kind", [(3, "mixed"), (2, "tiny")])
+def test_sharded_abi_protocol_b_short_exchange(gpu, world, kind):
+    """Protocol B enqueues a whole batch without a host read: the edge
+    all-gather has a fixed capacity per shard (here 2 pairs).  A batch whose
+    lists do not fit is marked on every rank; its merge, plan and compaction
+    leave the history as it was, and the batch runs from exchange 1 again with
+    a larger capacity.  Verdicts, histories, removalKey
+    and oldestVersion as one conflict set's after every batch."""
+    test_sharded_abi_equals_one_conflict_set(gpu, world, kind, "b", sh_ecap=2)
 
 
 @pytest.mark.gpu
