@@ -764,6 +764,9 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
 // from the register-heavy rewrite.  UNIFIED (FDBCS_PM_UNIFIED builds): a page
 // the in-place pass cannot do is rewritten by the same wavefront at once (one
 // launch; both paths fit 3 waves per SIMD).
+#ifndef FDBCS_PM_REWRITE_AT  // (A/B: pages receiving this many new boundaries are rewritten, not shifted in place)
+#define FDBCS_PM_REWRITE_AT (PAGE + 1)
+#endif
 template <bool INPLACE, bool UNIFIED = false>
 __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
@@ -814,7 +817,8 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     }
     wave_lds_sync();
     if (INPLACE) {
-        if (parts == 1 && !__ballot(erases) && merge_in_place(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
+        if (parts == 1 && !__ballot(erases) && nn < FDBCS_PM_REWRITE_AT &&
+            merge_in_place(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
             return;
         if (!UNIFIED) {
             if (lane == 0) A.full_list[atomicAdd(&sc->n_full, 1)] = a;
