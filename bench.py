@@ -472,10 +472,23 @@ def run_single(args):
             done += n1
         next_i += done
         la = np.array(lus) / 1e3
+        # the window split into the caller's adds and detectConflicts (window - adds), per batch
+        ad = np.array(ladd, np.float64)
+        de = np.array(lus, np.float64) - ad
+
+        def pct(x):
+            return {q: round(float(np.percentile(x, v)), 1) for q, v in (("p50", 50), ("p99", 99), ("p999", 99.9))} | \
+                {"max": round(float(x.max()), 1)}
+
+        slow = np.argsort(-np.array(lus))[:5]
         latency = {"batches": done, "mean_ms": round(float(la.mean()), 4),
                    "p50_ms": round(float(np.percentile(la, 50)), 4), "p99_ms": round(float(np.percentile(la, 99)), 4),
                    "p999_ms": round(float(np.percentile(la, 99.9)), 4), "max_ms": round(float(la.max()), 4),
-                   "add_us_mean": round(float(np.mean(ladd)), 2), "history_post": cs.history_size(),
+                   "add_us_mean": round(float(np.mean(ladd)), 2),
+                   "adds_us": pct(ad), "detect_us": pct(de),
+                   "slowest": [{"window_us": round(float(lus[k]), 1), "adds_us": round(float(ad[k]), 1),
+                                "detect_us": round(float(de[k]), 1)} for k in slow],
+                   "history_post": cs.history_size(),
                    "window": "the timed region's window (fdbcs_batch_begin + T x fdbcs_batch_add + fdbcs_batch_detect), "
                              "per batch, right after the timed region"}
 

@@ -87,6 +87,7 @@ FDBCS_FUNCS = [
     ("fdbcs_stream", C.c_void_p, [C.c_void_p]),
     ("fdbcs_batch_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_debug_phases", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
+    ("fdbcs_debug_prefix_skips", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_split_batch", C.c_int,
      [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(BatchView), C.c_void_p,
       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),

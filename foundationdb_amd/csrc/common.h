@@ -165,6 +165,16 @@ struct Pool {
     // holes: bit i of hmask[4 * page + i / 64] marks slot i of the page as a
     // hole (below).  Bits at or above the page's slot count are zero.
     uint64_t* hmask;
+    // Long shared prefixes (config 4): px[s] = 8 bytes of slot s's key from
+    // byte pskip[page] (common.h key_bytes_at), pxidx = px of slots 0, 16,
+    // ..., 240 (one line per page, as pidx).  A search in a page uses them
+    // when 0 < pskip <= the skip of the page's directory window (Dir::wsk):
+    // then every key of the page and every query reaching it share their
+    // first pskip bytes.  pskip < 0: the page was rewritten and k_page_px
+    // sets it anew after the batch; 0: not used.
+    uint64_t* px;
+    uint64_t* pxidx;
+    int32_t* pskip;
 };
 constexpr int PIDX_STRIDE = 16;
 constexpr int HM_WORDS = PAGE / 64;
@@ -215,6 +225,16 @@ struct Dir {
     // 16-entry (128-byte) boundaries, so a 16-wide probe window is one cache
     // line (hist_search.h).  Rebuilt by k_bmax_commit with the directory.
     uint64_t* sidx;
+    // Long shared prefixes (config 4: tenant + path, 64 bytes): a search
+    // window of 16 entries at level l (aligned, as the searches take them) is
+    // only ever searched by keys between the window's first key and the next
+    // window's first key, so query and window share their common prefix
+    // (wsk, when > 17 bytes); then 8 bytes of each key from there (fpx for
+    // level 0, spx beside sidx for levels >= 1) order them without the tails.
+    // Rebuilt with the directory (k_dir_px); wsk 0: not used.
+    uint64_t* fpx;
+    uint64_t* spx;
+    int32_t* wsk;
     int32_t cap;        // entries allocated (levels are sized from it)
 };
 
@@ -232,6 +252,53 @@ __host__ __device__ inline int64_t sidx_off(int64_t cap, int l) {
         o += (n + SIDX_B - 1) & ~(int64_t)(SIDX_B - 1);
     }
     return o;
+}
+
+#ifndef FDBCS_DIR_PX  // (A/B: 0 leaves Dir::wsk at 0 -- the tails decide every tie)
+#define FDBCS_DIR_PX 1
+#endif
+constexpr int PX_MIN_SKIP = 18;           // (a shorter common prefix: the fixed 17 bytes order the keys)
+constexpr int PX_MAX_SKIP = 17 + 8 * 14;  // (the searches hold 16 tail words of the query)
+
+// offset of level l (0-based) in Dir::wsk: one skip per 16-entry window
+__host__ __device__ inline int64_t wsk_off(int64_t cap, int l) {
+    int64_t o = 0;
+    for (int q = 0; q < l; q++) {
+        const int64_t n = (cap + (1ll << (SIDX_LOG * q)) - 1) >> (SIDX_LOG * q);
+        o += (n + SIDX_B - 1) / SIDX_B;
+    }
+    return o;
+}
+
+// Common prefix length of two keys in bytes (at most the shorter length).
+__device__ inline int key_lcp(const Key& a, const Key& b) {
+    const int la = (int)key_len(a.meta), lb = (int)key_len(b.meta);
+    const int m = la < lb ? la : lb;
+    uint64_t x = a.hi ^ b.hi;
+    if (x) return min(m, __clzll((long long)x) >> 3);
+    x = a.lo ^ b.lo;
+    if (x) return min(m, 8 + (__clzll((long long)x) >> 3));
+    if ((a.meta >> 24) != (b.meta >> 24) || m <= 17) return min(m, 16);
+    const uint64_t* ta = reinterpret_cast<const uint64_t*>(a.tail);
+    const uint64_t* tb = reinterpret_cast<const uint64_t*>(b.tail);
+    const int words = (m - 17 + 7) >> 3;
+    for (int w = 0; w < words; w++) {
+        const uint64_t d = ta[w] ^ tb[w];  // (little-endian words: the first byte is the lowest)
+        if (d) return min(m, 17 + 8 * w + (__ffsll((unsigned long long)d) - 1) / 8);
+    }
+    return m;
+}
+
+// The 8 bytes of a key at byte s >= 17 (big-endian, zero past its end).
+__device__ inline uint64_t key_bytes_at(const Key& k, int s) {
+    const int len = (int)key_len(k.meta);
+    if (s >= len) return 0;
+    const int t = s - 17, w = t >> 3, sh = t & 7;
+    const int words = (len - 17 + 7) >> 3;
+    const uint64_t* tw = reinterpret_cast<const uint64_t*>(k.tail);
+    const uint64_t x0 = __builtin_bswap64(tw[w]);
+    const uint64_t x1 = w + 1 < words ? __builtin_bswap64(tw[w + 1]) : 0;
+    return sh ? (x0 << (8 * sh)) | (x1 >> (64 - 8 * sh)) : x0;
 }
 
 // Device-resident scalars shared between the kernels of one batch.
@@ -304,6 +371,7 @@ struct Scalars {
     // protocol B's edge exchange at a fixed capacity (k_sh_edges_cat_fixed):
     // the largest shard count when some shard's did not fit (0: they did)
     int32_t sh_need;
+    int32_t n_pxd;          // rewritten pages listed for k_page_px (pskip < 0)
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;

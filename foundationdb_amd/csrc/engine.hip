@@ -240,8 +240,11 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
     const int64_t slots = (int64_t)pages * PAGE;
     if ((r = dalloc(h.pool.hi, slots)) || (r = dalloc(h.pool.lo, slots)) || (r = dalloc(h.pool.meta, slots)) ||
         (r = dalloc(h.pool.ver, slots)) || (r = dalloc(h.pool.tail, slots)) || (r = dalloc(h.pool.pidx, slots / PIDX_STRIDE)) ||
-        (r = dalloc(h.pool.hmask, (int64_t)pages * HM_WORDS)) || (r = dalloc(h.free_stack, pages)))
+        (r = dalloc(h.pool.hmask, (int64_t)pages * HM_WORDS)) || (r = dalloc(h.free_stack, pages)) ||
+        (r = dalloc(h.pool.px, slots)) || (r = dalloc(h.pool.pxidx, slots / PIDX_STRIDE)) ||
+        (r = dalloc(h.pool.pskip, pages)) || (r = dalloc(h.px_list, (int64_t)pages + 1)))
         return r;
+    HIPOK(hipMemset(h.pool.pskip, 0, (size_t)pages * sizeof(int32_t)));
     h.cap_dir = pages + 1;
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
@@ -250,8 +253,11 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
             (r = dalloc(x.start, h.cap_dir + 1)) || (r = dalloc(x.fhi, h.cap_dir)) || (r = dalloc(x.flo, h.cap_dir)) ||
             (r = dalloc(x.fmeta, h.cap_dir)) || (r = dalloc(x.ftail, h.cap_dir)) ||
             (r = dalloc(x.bmax, h.cap_dir / 64 + 2)) || (r = dalloc(x.bmax2, h.cap_dir / BMAX2_SPAN + 2)) ||
-            (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))))
+            (r = dalloc(x.sidx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))) || (r = dalloc(x.fpx, h.cap_dir)) ||
+            (r = dalloc(x.spx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))) ||
+            (r = dalloc(x.wsk, wsk_off(h.cap_dir, SIDX_LEVELS + 1))))
             return r;
+        HIPOK(hipMemset(x.wsk, 0, wsk_off(h.cap_dir, SIDX_LEVELS + 1) * sizeof(int32_t)));
         x.cap = h.cap_dir;
     }
     return FDBCS_OK;
@@ -260,10 +266,11 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
 void free_pool(HistBufs& h) {
     dfree(h.pool.hi); dfree(h.pool.lo); dfree(h.pool.meta); dfree(h.pool.ver); dfree(h.pool.tail);
     dfree(h.pool.pidx); dfree(h.pool.hmask); dfree(h.free_stack);
+    dfree(h.pool.px); dfree(h.pool.pxidx); dfree(h.pool.pskip); dfree(h.px_list);
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
         dfree(x.page); dfree(x.cnt); dfree(x.nr); dfree(x.maxv); dfree(x.start); dfree(x.fhi); dfree(x.flo); dfree(x.fmeta);
-        dfree(x.ftail); dfree(x.bmax); dfree(x.bmax2); dfree(x.sidx);
+        dfree(x.ftail); dfree(x.bmax); dfree(x.bmax2); dfree(x.sidx); dfree(x.fpx); dfree(x.spx); dfree(x.wsk);
     }
 }
 
@@ -399,6 +406,9 @@ int grow_pool(fdbcs* cs, int64_t pages) {
     HIPOK(hipMemcpyAsync(h.pool.tail, old.pool.tail, os * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.pidx, old.pool.pidx, os / PIDX_STRIDE * 8, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.hmask, old.pool.hmask, (size_t)old.cap_pages * HM_WORDS * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.px, old.pool.px, os * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.pxidx, old.pool.pxidx, os / PIDX_STRIDE * 8, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(h.pool.pskip, old.pool.pskip, (size_t)old.cap_pages * 4, hipMemcpyDeviceToDevice, s));
     HIPOK(hipMemcpyAsync(h.free_stack, old.free_stack, (size_t)old.cap_pages * 4, hipMemcpyDeviceToDevice, s));
     const size_t od = (size_t)old.cap_dir;
     for (int d = 0; d < 2; d++) {
@@ -1710,6 +1720,7 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     HIPOK(hipMemcpyAsync(d.cnt, dcnt.data(), np * 4, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.nr, dnr.data(), np * 4, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(h.pool.hmask, hmask.data(), hmask.size() * 8, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemsetAsync(h.pool.pskip, 0xFF, (size_t)np * sizeof(int32_t), s));  // (k_page_px after the directory)
     HIPOK(hipMemcpyAsync(d.maxv, dmax.data(), np * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.fhi, dfhi.data(), np * 8, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d.flo, dflo.data(), np * 8, hipMemcpyHostToDevice, s));
@@ -1783,6 +1794,28 @@ int fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap) {
                                     (int64_t)cs->h.tail_cap, (int64_t)h.tail_used, h.tail_half, cs->lv_done,
                                     cs->lv_cancelled, cs->st.live_timeouts()};
     const int n = std::min(cap, (int)FDBCS_STATS);
+    for (int i = 0; i < n; i++) out[i] = v[i];
+    return n;
+}
+
+int fdbcs_debug_prefix_skips(fdbcs* cs, int64_t* out, int cap) {
+    if (!cs || !out) return FDBCS_E_ARG;
+    int r;
+    if ((r = sync_state(cs))) return r;
+    const HistBufs& h = cs->h;
+    const Dir& d = h.dir[cs->cur];
+    const int D = cs->sc_host->D;
+    std::vector<int32_t> wsk((size_t)(D + 15) / 16), page(D), pskip(h.cap_pages);
+    HIPOK(hipMemcpy(wsk.data(), d.wsk, wsk.size() * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(page.data(), d.page, (size_t)D * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(pskip.data(), h.pool.pskip, (size_t)h.cap_pages * 4, hipMemcpyDeviceToHost));
+    int64_t v[3] = {0, 0, 0};
+    for (int32_t x : wsk) v[0] += x > 0;
+    for (int32_t p : page) {
+        v[1] += pskip[p] > 0;
+        v[2] += pskip[p] < 0;
+    }
+    const int n = std::min(cap, 3);
     for (int i = 0; i < n; i++) out[i] = v[i];
     return n;
 }

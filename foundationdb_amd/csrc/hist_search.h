@@ -128,18 +128,83 @@ struct DirHit {
     int x, page, cnt;  // directory entry, its pool page and boundary count
 };
 
+// A query's tail words across its group: lane j holds word j (0 past the end).
+template <int G>
+__device__ inline uint64_t q_tail_word(const Group<G>& g, const Key& k) {
+    const int len = (int)key_len(k.meta);
+    const int words = len > 17 ? (len - 17 + 7) >> 3 : 0;
+    return g.lane < words ? reinterpret_cast<const uint64_t*>(k.tail)[g.lane] : 0;
+}
+
+// key_bytes_at(k, s) from the group's tail words (PX_MIN_SKIP <= s <= PX_MAX_SKIP)
+template <int G>
+__device__ inline uint64_t q_bytes_at(const Group<G>& g, uint64_t qtw, const Key& k, int s) {
+    const int t = s - 17, w = t >> 3, sh = t & 7;
+    const uint64_t x0 = __builtin_bswap64((uint64_t)__shfl((long long)qtw, g.shift + w));
+    const uint64_t x1 = __builtin_bswap64((uint64_t)__shfl((long long)qtw, g.shift + w + 1));
+    if (s >= (int)key_len(k.meta)) return 0;
+    return sh ? (x0 << (8 * sh)) | (x1 >> (64 - 8 * sh)) : x0;
+}
+
+// Probes of level l's window w (entry values v) not above k: the count.  A
+// tie of the first 8 bytes is decided by the window's skip and 8 bytes of
+// each key from there (common.h Dir::wsk) when it has one, else by the keys.
+// spec: the level above tied, so this level's skip and 8-byte words (s0, x0)
+// were loaded with v (one round trip instead of two); returns whether any
+// probe tied here.
+#ifndef FDBCS_PX_SPEC
+#define FDBCS_PX_SPEC 1
+#endif
+__device__ inline const uint64_t* dir_px(const Dir& d, int l) { return l == 0 ? d.fpx : d.spx + sidx_off(d.cap, l); }
+__device__ inline int dir_count(const Group<SIDX_B>& g, const Dir& d, int l, int n, int w, uint64_t v, const Key& k,
+                                uint64_t qtw, bool& spec, int s0, uint64_t x0) {
+    const int i = w + g.lane;
+    const bool in = i < n;
+    const bool tie = in && i != 0 && v == k.hi;
+    bool le = in && (i == 0 || v < k.hi);
+    const bool any = g.ballot(tie) != 0;
+    if (any) {
+        const int s = !FDBCS_DIR_PX ? 0 : spec ? s0 : d.wsk[wsk_off(d.cap, l) + (w >> SIDX_LOG)];
+        if (s) {
+            const uint64_t x = !tie ? 0 : spec ? x0 : dir_px(d, l)[i];
+            const uint64_t qx = q_bytes_at(g, qtw, k, s);
+            if (tie) le = x != qx ? x < qx : kcmp(dir_first(d, (int)((int64_t)i << (SIDX_LOG * l))), k) <= 0;
+        } else if (tie) {
+            le = kcmp(dir_first(d, (int)((int64_t)i << (SIDX_LOG * l))), k) <= 0;
+        }
+    }
+    spec = FDBCS_DIR_PX && FDBCS_PX_SPEC && any;
+    return __popc(g.ballot(le));
+}
+// (the speculative loads of a level: its window skip and the lane's word)
+__device__ inline void dir_spec(const Group<SIDX_B>& g, const Dir& d, int l, int n, int w, bool spec, int& s0,
+                                uint64_t& x0) {
+    s0 = 0;
+    x0 = 0;
+    if (spec) {
+        s0 = d.wsk[wsk_off(d.cap, l) + (w >> SIDX_LOG)];
+        if (w + g.lane < n) x0 = dir_px(d, l)[w + g.lane];
+    }
+}
+
 // dir_search(d, D, k, 1) for two keys by a group of 16 lanes
 __device__ inline void grp_dir_find2(const Group<SIDX_B>& g, const Dir& d, int D, const Key& k1, const Key& k2,
                                      DirHit& h1, DirHit& h2) {
     int w1 = 0, w2 = 0;  // window starts (entry index at the current level)
+    const uint64_t q1 = q_tail_word(g, k1), q2 = q_tail_word(g, k2);  // (long keys only)
+    bool sp1 = false, sp2 = false;
+    int s1, s2;
+    uint64_t x1, x2;
     for (int l = sidx_top(D); l >= 1; l--) {
         const int n = sidx_n(D, l);
         const uint64_t* arr = d.sidx + sidx_off(d.cap, l);
         const int i1 = w1 + g.lane, i2 = w2 + g.lane;
         const uint64_t v1 = i1 < n ? arr[i1] : 0;
         const uint64_t v2 = w2 == w1 ? v1 : (i2 < n ? arr[i2] : 0);
-        const int c1 = __popc(g.ballot(i1 < n && sidx_le(d, i1, l, v1, k1)));  // >= 1: slot w is <= k
-        const int c2 = __popc(g.ballot(i2 < n && sidx_le(d, i2, l, v2, k2)));
+        dir_spec(g, d, l, n, w1, sp1, s1, x1);
+        dir_spec(g, d, l, n, w2, sp2, s2, x2);
+        const int c1 = dir_count(g, d, l, n, w1, v1, k1, q1, sp1, s1, x1);  // >= 1: slot w is <= k
+        const int c2 = dir_count(g, d, l, n, w2, v2, k2, q2, sp2, s2, x2);
         w1 = (w1 + c1 - 1) << SIDX_LOG;
         w2 = (w2 + c2 - 1) << SIDX_LOG;
     }
@@ -159,8 +224,10 @@ __device__ inline void grp_dir_find2(const Group<SIDX_B>& g, const Dir& d, int D
         pg2 = d.page[i2];
         cn2 = d.cnt[i2];
     }
-    const int c1 = __popc(g.ballot(i1 < D && sidx_le(d, i1, 0, v1, k1)));
-    const int c2 = __popc(g.ballot(i2 < D && sidx_le(d, i2, 0, v2, k2)));
+    dir_spec(g, d, 0, D, w1, sp1, s1, x1);
+    dir_spec(g, d, 0, D, w2, sp2, s2, x2);
+    const int c1 = dir_count(g, d, 0, D, w1, v1, k1, q1, sp1, s1, x1);
+    const int c2 = dir_count(g, d, 0, D, w2, v2, k2, q2, sp2, s2, x2);
     h1.x = w1 + c1 - 1;
     h2.x = w2 + c2 - 1;
     h1.page = __shfl(pg1, g.shift + c1 - 1);
@@ -231,11 +298,32 @@ struct PageWin {
     bool eq;
 };
 
-__device__ inline void pwin_step1(const Group<PIDX_STRIDE>& g, const Pool& p, int64_t base, int cnt, const Key& k,
-                                  uint64_t v, PageWin& W) {
+// Step 1: the 16 indexed slots.  A tie of their first 8 bytes with k (all
+// of them, in a page whose keys share a long prefix) is decided by the
+// page's skip and 8 bytes of each key from there (common.h Pool::pskip) when
+// the page's directory window vouches for the skip (Dir::wsk of entry x):
+// *ps and *qx return the skip (0: none) and k's 8 bytes for step 2.
+__device__ inline void pwin_step1(const Group<PIDX_STRIDE>& g, const Pool& p, const Dir& d, int x, int page,
+                                  int64_t base, int cnt, const Key& k, uint64_t v, uint64_t qtw, PageWin& W, int& ps,
+                                  uint64_t& qx) {
     const int slot = g.lane * PIDX_STRIDE;
-    int c = 1;
-    if (slot < cnt) c = v != k.hi ? (v < k.hi ? -1 : 1) : kcmp(pool_key(p, base + slot), k);
+    const bool tie = slot < cnt && v == k.hi;
+    int c = slot < cnt ? (v < k.hi ? -1 : 1) : 1;
+    ps = 0;
+    qx = 0;
+    if (g.ballot(tie)) {
+        if (FDBCS_DIR_PX) {
+            const int s = p.pskip[page];
+            if (s > 0 && s <= d.wsk[x >> SIDX_LOG]) ps = s;
+        }
+        if (ps) {
+            const uint64_t u = tie ? p.pxidx[(int64_t)page * (PAGE / PIDX_STRIDE) + g.lane] : 0;
+            qx = q_bytes_at(g, qtw, k, ps);
+            if (tie) c = u != qx ? (u < qx ? -1 : 1) : kcmp(pool_key(p, base + slot), k);
+        } else if (tie) {
+            c = kcmp(pool_key(p, base + slot), k);
+        }
+    }
     const uint32_t lt = g.ballot(c < 0), eq = g.ballot(c == 0);
     const int n = __popc(lt);
     if (n == 0) {  // k <= key(0) (or empty page)
@@ -250,32 +338,44 @@ __device__ inline void pwin_step1(const Group<PIDX_STRIDE>& g, const Pool& p, in
     }
 }
 
+// Step 2: the 16 slots of the window; v: their first words, or with a skip
+// (ps > 0) their 8 bytes from it, against qx
 __device__ inline void pwin_step2(const Group<PIDX_STRIDE>& g, const Pool& p, int64_t base, const Key& k, uint64_t v,
-                                  PageWin& W) {
+                                  int ps, uint64_t qx, PageWin& W) {
     const int slot = W.w + g.lane;
     int c = 1;
-    if (slot < W.e) c = v != k.hi ? (v < k.hi ? -1 : 1) : kcmp(pool_key(p, base + slot), k);
+    if (slot < W.e) {
+        const uint64_t kv = ps ? qx : k.hi;
+        c = v != kv ? (v < kv ? -1 : 1) : kcmp(pool_key(p, base + slot), k);
+    }
     const uint32_t lt = g.ballot(c < 0), eq = g.ballot(c == 0);
     const int n = __popc(lt);  // >= 1: slot w < k
     W.i = W.w + n;
     W.eq = W.i < W.e ? ((eq >> n) & 1) : W.e_eq;
 }
 
-__device__ inline void grp_page_find2(const Group<PIDX_STRIDE>& g, const Pool& p, int page1, int cnt1, const Key& k1,
-                                      int page2, int cnt2, const Key& k2, int& i1, bool& eq1, int& i2, bool& eq2) {
+// x1, x2: the pages' directory entries (their window's skip, Dir::wsk)
+__device__ inline void grp_page_find2(const Group<PIDX_STRIDE>& g, const Pool& p, const Dir& d, int x1, int page1,
+                                      int cnt1, const Key& k1, int x2, int page2, int cnt2, const Key& k2, int& i1,
+                                      bool& eq1, int& i2, bool& eq2) {
     const int64_t b1 = (int64_t)page1 * PAGE, b2 = (int64_t)page2 * PAGE;
     const uint64_t u1 = p.pidx[(int64_t)page1 * (PAGE / PIDX_STRIDE) + g.lane];
     const uint64_t u2 = page2 == page1 ? u1 : p.pidx[(int64_t)page2 * (PAGE / PIDX_STRIDE) + g.lane];
+    const uint64_t q1 = q_tail_word(g, k1), q2 = q_tail_word(g, k2);  // (long keys only)
     PageWin W1, W2;
-    pwin_step1(g, p, b1, cnt1, k1, u1, W1);
-    pwin_step1(g, p, b2, cnt2, k2, u2, W2);
+    int ps1, ps2;
+    uint64_t qx1, qx2;
+    pwin_step1(g, p, d, x1, page1, b1, cnt1, k1, u1, q1, W1, ps1, qx1);
+    pwin_step1(g, p, d, x2, page2, b2, cnt2, k2, u2, q2, W2, ps2, qx2);
     const bool s1 = !W1.done, s2 = !W2.done;
+    const uint64_t* a1 = ps1 ? p.px : p.hi;
+    const uint64_t* a2 = ps2 ? p.px : p.hi;
     uint64_t v1 = 0, v2 = 0;
-    if (s1 && W1.w + g.lane < W1.e) v1 = p.hi[b1 + W1.w + g.lane];
+    if (s1 && W1.w + g.lane < W1.e) v1 = a1[b1 + W1.w + g.lane];
     if (s2 && W2.w + g.lane < W2.e)
-        v2 = (s1 && page2 == page1 && W2.w == W1.w) ? v1 : p.hi[b2 + W2.w + g.lane];
-    if (s1) pwin_step2(g, p, b1, k1, v1, W1);
-    if (s2) pwin_step2(g, p, b2, k2, v2, W2);
+        v2 = (s1 && page2 == page1 && W2.w == W1.w && ps2 == ps1) ? v1 : a2[b2 + W2.w + g.lane];
+    if (s1) pwin_step2(g, p, b1, k1, v1, ps1, qx1, W1);
+    if (s2) pwin_step2(g, p, b2, k2, v2, ps2, qx2, W2);
     i1 = W1.i; eq1 = W1.eq;
     i2 = W2.i; eq2 = W2.eq;
 }

@@ -256,6 +256,7 @@ struct HistBufs {
     Pool pool;
     int32_t cap_pages;
     int32_t* free_stack;
+    int32_t* px_list;  // [cap_pages] directory entries of rewritten pages (k_dir_px -> k_page_px)
     Dir dir[2];
     int32_t cap_dir;
     uint8_t* tail_arena;

@@ -227,7 +227,7 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
     const int pb = hb.x, pe = he.x, cb = hb.cnt;
     int ib, ie;
     bool eqb, eqe;
-    grp_page_find2(g, pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    grp_page_find2(g, pool, dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
     const int64_t baseb = (int64_t)hb.page * PAGE, basee = (int64_t)he.page * PAGE;
     const int i0 = eqb ? ib : ib - 1;  // the slot whose version covers b
     bool c = i0 < 0 && v0 > s;
@@ -2119,7 +2119,7 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
     }
     int ib, ie;
     bool eqb, eqe;
-    grp_page_find2(g, A.pool, hb.page, hb.cnt, b, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    grp_page_find2(g, A.pool, A.dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
     if (g.lane != 0) return;
     uint64_t hmb[HM_WORDS], hme[HM_WORDS];  // real positions for the merge plan's counts (holes, common.h)
     load_hmask(A.pool, hb.page, hmb);

@@ -505,9 +505,13 @@ struct MergeArgs {
 };
 
 __device__ inline void put_entry(const Pool& pool, int64_t d, uint64_t hi, uint64_t lo, uint32_t meta, int64_t ver,
-                                 const uint8_t* tail) {
+                                 const uint8_t* tail, uint64_t px = 0) {
     pool.hi[d] = hi; pool.lo[d] = lo; pool.meta[d] = meta; pool.ver[d] = ver; pool.tail[d] = tail;
     if ((d & (PIDX_STRIDE - 1)) == 0) pool.pidx[d / PIDX_STRIDE] = hi;
+    if (FDBCS_DIR_PX) {
+        pool.px[d] = px;
+        if ((d & (PIDX_STRIDE - 1)) == 0) pool.pxidx[d / PIDX_STRIDE] = px;
+    }
 }
 
 __device__ inline void put_desc(const DescArrays& D, int x, int page, int n, uint64_t hi, uint64_t lo,
@@ -687,22 +691,25 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
     }
     wave_lds_sync();
     // ---- read the boundaries that move, then write them
-    uint64_t ohi[4], olo[4];
+    uint64_t ohi[4], olo[4], opx[4];
     uint32_t ometa[4];
     int64_t over[4];
     const uint8_t* otail[4];
+    const int pskip = FDBCS_DIR_PX ? A.pool.pskip[pg] : 0;  // (< 0: rewritten this batch -- not here)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if (!((movem >> q) & 1)) continue;
         const int64_t sl = pbase + i0 + q;
         ohi[q] = A.pool.hi[sl]; olo[q] = A.pool.lo[sl]; ometa[q] = A.pool.meta[sl];
         over[q] = A.pool.ver[sl]; otail[q] = A.pool.tail[sl];
+        opx[q] = pskip > 0 ? A.pool.px[sl] : 0;
     }
     wave_loads_done();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int i = i0 + q;
-        if ((movem >> q) & 1) put_entry(A.pool, pbase + i + cb[q] + av[q], ohi[q], olo[q], ometa[q], over[q], otail[q]);
+        if ((movem >> q) & 1)
+            put_entry(A.pool, pbase + i + cb[q] + av[q], ohi[q], olo[q], ometa[q], over[q], otail[q], opx[q]);
         if ((usem >> q) & 1) atomicAnd(&S.hm[i >> 6], ~(1ull << (i & 63)));
     }
     // ---- the new entries, by the plan lanes: b_j (version now), then e_j
@@ -727,7 +734,7 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
             const int out = at + S.er[at] + (k - S.ins[at]);
             const uint8_t* tl;
             copy_tail(kk, A.arena, A.arena_cap, A.sc, &tl);
-            put_entry(A.pool, pbase + out, kk.hi, kk.lo, kk.meta, ver, tl);
+            put_entry(A.pool, pbase + out, kk.hi, kk.lo, kk.meta, ver, tl, pskip > 0 ? key_bytes_at(kk, pskip) : 0);
             vmax = max(vmax, ver);
             maxout = max(maxout, out);
             if (out == 0) part_first(S, A.dst, A, a, doff, 0, 1, 1, pg, kk.hi, kk.lo, kk.meta, tl);
@@ -937,6 +944,8 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
         const int q = x / HM_WORDS;
         A.pool.hmask[(int64_t)dest(q) * HM_WORDS + x % HM_WORDS] = spread_mask_word(min(per, nout - q * per), x % HM_WORDS);
     }
+    if (FDBCS_DIR_PX)  // (the parts' key-prefix skips: k_page_px, after the batch)
+        for (int q = lane; q < parts; q += 64) A.pool.pskip[dest(q)] = -1;
     if (parts == 1) {
         if (lane == 0) D.maxv[doff] = vmax;
         return;
@@ -1156,8 +1165,93 @@ __global__ __launch_bounds__(256) void k_sidx_build(Dir d, const int32_t* D) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) sidx_build(d, i);
 }
 
+// Dir::wsk / fpx / spx of a finished directory (common.h): a thread per
+// entry of each level.  Window w of level l holds entries x = (16w + t) <<
+// 4l; the searches reach it only with keys in [first(16w << 4l),
+// first((16w + 16) << 4l)) -- except window 0, whose entry 0 is the default
+// target of keys below every first key, and the last window -- so those two
+// keys' common prefix is the query's too.  (Every thread of a window works
+// its skip out from the same two keys.)  Level-0 threads also list the
+// entries whose page was rewritten (Pool::pskip < 0) for k_page_px, where
+// their window has a skip.
+__device__ inline int window_skip(const Dir& d, int D, int l, int w) {
+    const int64_t x0 = (int64_t)(SIDX_B * w) << (SIDX_LOG * l);
+    const int64_t x1 = (int64_t)(SIDX_B * w + SIDX_B) << (SIDX_LOG * l);
+    if (w == 0 || x1 >= D) return 0;
+    const uint64_t h0 = d.fhi[x0], h1 = d.fhi[x1], l0 = d.flo[x0], l1 = d.flo[x1];
+    const uint32_t m0 = d.fmeta[x0], m1 = d.fmeta[x1];
+    if (h0 != h1 || l0 != l1 || (m0 >> 24) != (m1 >> 24) || key_len(m0) <= 17 || key_len(m1) <= 17) return 0;
+    const int skip = key_lcp(Key{h0, l0, m0, d.ftail[x0]}, Key{h1, l1, m1, d.ftail[x1]});
+    return skip < PX_MIN_SKIP ? 0 : min(skip, PX_MAX_SKIP);  // (a shorter skip is as valid)
+}
+
+__global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool pool, int32_t* list, Scalars* sc) {
+    const int D = *Dp;
+    const int64_t cap = d.cap;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (int l = 0; l <= SIDX_LEVELS; l++) {
+        const int n = sidx_n(D, l);  // entries of level l
+        if (l > 0 && n <= 1) break;
+        for (int i = tid; i < n; i += nth) {
+            const int w = i >> SIDX_LOG;
+            const int skip = window_skip(d, D, l, w);
+            if ((i & (SIDX_B - 1)) == 0) d.wsk[wsk_off(cap, l) + w] = skip;
+            const int x = (int)((int64_t)i << (SIDX_LOG * l));
+            if (skip) (l == 0 ? d.fpx : d.spx + sidx_off(cap, l))[i] = key_bytes_at(dir_first(d, x), skip);
+            // (a page's skip counts only under a window skip: pages elsewhere
+            // stay listed as rewritten until their window has one)
+            if (l == 0 && skip && pool.pskip[d.page[x]] < 0) {
+                const int k = atomicAdd(&sc->n_pxd, 1);
+                if (k < d.cap) list[k] = x;
+            }
+        }
+    }
+}
+
+// Pool::pskip / px / pxidx of the pages k_dir_px listed, a wavefront each:
+// the skip is the common prefix of the page's first and last keys (so of
+// all of them), used by the searches only where the page's directory window
+// vouches for it (common.h Pool).
+__global__ __launch_bounds__(256) void k_page_px(Dir d, Pool pool, const int32_t* list, Scalars* sc) {
+    const int n = min(sc->n_pxd, d.cap);
+    const int lane = threadIdx.x & 63;
+    for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
+        const int x = list[k];
+        const int pg = d.page[x], c = d.cnt[x];
+        const int64_t b = (int64_t)pg * PAGE;
+        int skip = 0;
+        if (c > 1) {
+            const Key a = pool_key(pool, b), z = pool_key(pool, b + c - 1);  // (the last used slot is real)
+            if (a.hi == z.hi && a.lo == z.lo && (a.meta >> 24) == (z.meta >> 24) && key_len(a.meta) > 17 &&
+                key_len(z.meta) > 17) {
+                // (rounded down to 8 bytes: a page spans a sliver of its
+                // window, so its own common prefix often runs a byte or two
+                // past the window's -- then the window could not vouch for it)
+                skip = min(key_lcp(a, z), PX_MAX_SKIP) & ~7;
+                if (skip < PX_MIN_SKIP) skip = 0;
+            }
+        }
+        if (skip)
+            for (int i = lane; i < c; i += 64) {
+                const uint64_t v = key_bytes_at(pool_key(pool, b + i), skip);
+                pool.px[b + i] = v;
+                if ((i & (PIDX_STRIDE - 1)) == 0) pool.pxidx[(b + i) / PIDX_STRIDE] = v;
+            }
+        if (lane == 0) pool.pskip[pg] = skip;
+    }
+}
+
+void launch_dir_px(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
+    if (!FDBCS_DIR_PX) return;
+    (void)hipMemsetAsync(&sc->n_pxd, 0, sizeof(int32_t), s);
+    hipLaunchKernelGGL(k_dir_px, dim3(std::max(1, std::min(2048, cdiv(h.cap_dir, 256)))), dim3(256), 0, s,
+                       h.dir[which], &sc->D, h.pool, h.px_list, sc);
+    hipLaunchKernelGGL(k_page_px, dim3(256), dim3(256), 0, s, h.dir[which], h.pool, (const int32_t*)h.px_list, sc);
+}
+
 void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
     hipLaunchKernelGGL(k_sidx_build, dim3(cdiv(cdiv(h.cap_dir, SIDX_B), 256)), dim3(256), 0, s, h.dir[which], &sc->D);
+    launch_dir_px(h, which, sc, s);
 }
 
 // the batch's load-metrics roll counters (common.h LmArgs) become the
@@ -1230,6 +1324,7 @@ static void launch_bmax_commit(HistBufs& h, int which, Scalars* sc, hipStream_t 
     hipLaunchKernelGGL(k_bmax_commit, dim3(cdiv(groups, 4)), dim3(256), 0, s, h.dir[which], sc, freed_list,
                        h.free_stack, (int)end_of_batch, h.pool, rk, h.mirror,
                        (int)(h.shard.has_lo | h.shard.has_hi));
+    if (end_of_batch) launch_dir_px(h, which, sc, s);  // (else the compaction's k_win_dir builds the final directory)
 }
 
 void launch_dir_finish(HistBufs& h, int cur, Scalars* sc, BatchBufs& b, hipStream_t s) {
@@ -1378,6 +1473,7 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
             if (r == 0) {
                 put_desc(desc, part, dp, n, hi, lo, meta, tail);
                 for (int w2 = 0; w2 < HM_WORDS; w2++) pool.hmask[(int64_t)dp * HM_WORDS + w2] = spread_mask_word(n, w2);
+                if (FDBCS_DIR_PX) pool.pskip[dp] = -1;  // (k_page_px, after the batch)
             }
         }
         __syncthreads();
@@ -1555,6 +1651,7 @@ void launch_compact(BatchBufs& b, HistBufs& h, int cur, Scalars* sc, int64_t old
                        b.win_keep, b.win_cnt, h.free_stack, da, h.tail_arena, h.tail_cap, gc);
     hipLaunchKernelGGL(k_win_dir, dim3(std::min(WIN_DIR_BLOCKS, cdiv(h.cap_dir, 1024))), dim3(1024), 0, s, src, dst,
                        sc, da, h.free_stack, h.mirror, (const int64_t*)h.pool.ver);
+    launch_dir_px(h, cur ^ 1, sc, s);
 }
 
 // --------------------------------------------------------- nth after ----
@@ -1829,10 +1926,11 @@ void launch_sh_edges_cat_fixed(const int32_t* recv, const int64_t* slots, int G,
 }
 // ------------------------------------------------------------------ reset ----
 __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int cap_pages, Scalars* sc,
-                                              uint64_t* hmask) {
+                                              uint64_t* hmask, int32_t* pskip) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < HM_WORDS) hmask[i] = 0;  // page 0: empty
     if (i < cap_pages - 1) free_stack[i] = cap_pages - 1 - i;  // pops yield page 1, 2, ...
+    if (i < cap_pages) pskip[i] = 0;
     if (i == 0) {
         d.page[0] = 0; d.cnt[0] = 0; d.nr[0] = 0; d.maxv[0] = INT64_MIN; d.start[0] = 0; d.start[1] = 0;
         d.fhi[0] = 0; d.flo[0] = 0; d.fmeta[0] = 0; d.ftail[0] = nullptr; d.bmax[0] = INT64_MIN;
@@ -1850,7 +1948,7 @@ __global__ __launch_bounds__(256) void k_reset(Dir d, int32_t* free_stack, int c
 
 void launch_reset_history(HistBufs& h, int cur, Scalars* sc, hipStream_t s) {
     hipLaunchKernelGGL(k_reset, dim3(cdiv(h.cap_pages, 256)), dim3(256), 0, s, h.dir[cur], h.free_stack,
-                       h.cap_pages, sc, h.pool.hmask);
+                       h.cap_pages, sc, h.pool.hmask, h.pool.pskip);
 }
 
 }  // namespace fdbcs_dev

@@ -337,6 +337,13 @@ int  fdbcs_batch_stats(fdbcs* cs, int64_t* out, int cap);
  * batch.  Returns the number of entries written (0 in normal builds). */
 int  fdbcs_debug_phases(fdbcs* cs, int64_t* out, int cap);
 
+/* Test hook: the searches' long-prefix skips of the current history
+ * (DESIGN.md §4 "Long shared prefixes"): [0] directory windows (16 entries,
+ * level 0) with a skip, [1] live pages with a skip (Pool::pskip > 0), [2]
+ * live pages waiting for k_page_px (< 0).  Synchronizes.  Returns the count
+ * written. */
+int  fdbcs_debug_prefix_skips(fdbcs* cs, int64_t* out, int cap);
+
 /* The HIP stream the conflict set enqueues on (as void*), for callers that
  * want to time or order around it. */
 void* fdbcs_stream(fdbcs* cs);
