@@ -371,7 +371,8 @@ struct Scalars {
     // protocol B's edge exchange at a fixed capacity (k_sh_edges_cat_fixed):
     // the largest shard count when some shard's did not fit (0: they did)
     int32_t sh_need;
-    int32_t n_pxd;          // rewritten pages listed for k_page_px (pskip < 0)
+    int32_t px_on;          // some key longer than 17 bytes was ingested or loaded (sticky): k_dir_px runs
+    int32_t n_pxd[2];       // rewritten pages listed for k_page_px (pskip < 0), by launch parity
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds
 };
 constexpr int32_t LV_RUNNING = 0, LV_FINAL = 1, LV_CANCEL = 2, LV_TIMEOUT = 3;

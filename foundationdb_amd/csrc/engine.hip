@@ -1356,6 +1356,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         hipHostGetDevicePointer((void**)&cs->h.mirror, cs->sc_mapped, 0) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
     memset(cs->sc_mapped, 0, sizeof(Scalars));
+    cs->h.mirror_host = cs->sc_mapped;
     // Every initialisation goes on the engine's own stream: it is
     // non-blocking, so the legacy null stream (hipMemset, hipMemcpy) does not
     // order against the kernels that follow on it.
@@ -1733,6 +1734,8 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     tmp.D = (int32_t)np;
     tmp.free_top = 0;
     tmp.tail_used = toff;
+    tmp.px_on = toff > 0 || cs->sc_host->px_on;  // (long keys loaded: the prefix skips)
+    if (tmp.px_on) h.px_host = true;
     HIPOK(hipMemcpyAsync(cs->sc, &tmp, sizeof(Scalars), hipMemcpyHostToDevice, s));
     launch_push_free(h, 0, (int32_t)np, (int32_t)(h.cap_pages - np), s);
     HIPOK(hipStreamSynchronize(s));

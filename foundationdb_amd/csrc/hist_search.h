@@ -156,6 +156,7 @@ __device__ inline uint64_t q_bytes_at(const Group<G>& g, uint64_t qtw, const Key
 #define FDBCS_PX_SPEC 1
 #endif
 __device__ inline const uint64_t* dir_px(const Dir& d, int l) { return l == 0 ? d.fpx : d.spx + sidx_off(d.cap, l); }
+template <bool PX>
 __device__ inline int dir_count(const Group<SIDX_B>& g, const Dir& d, int l, int n, int w, uint64_t v, const Key& k,
                                 uint64_t qtw, bool& spec, int s0, uint64_t x0) {
     const int i = w + g.lane;
@@ -164,7 +165,7 @@ __device__ inline int dir_count(const Group<SIDX_B>& g, const Dir& d, int l, int
     bool le = in && (i == 0 || v < k.hi);
     const bool any = g.ballot(tie) != 0;
     if (any) {
-        const int s = !FDBCS_DIR_PX ? 0 : spec ? s0 : d.wsk[wsk_off(d.cap, l) + (w >> SIDX_LOG)];
+        const int s = !PX ? 0 : spec ? s0 : d.wsk[wsk_off(d.cap, l) + (w >> SIDX_LOG)];
         if (s) {
             const uint64_t x = !tie ? 0 : spec ? x0 : dir_px(d, l)[i];
             const uint64_t qx = q_bytes_at(g, qtw, k, s);
@@ -173,7 +174,7 @@ __device__ inline int dir_count(const Group<SIDX_B>& g, const Dir& d, int l, int
             le = kcmp(dir_first(d, (int)((int64_t)i << (SIDX_LOG * l))), k) <= 0;
         }
     }
-    spec = FDBCS_DIR_PX && FDBCS_PX_SPEC && any;
+    spec = PX && FDBCS_PX_SPEC && any;
     return __popc(g.ballot(le));
 }
 // (the speculative loads of a level: its window skip and the lane's word)
@@ -188,10 +189,13 @@ __device__ inline void dir_spec(const Group<SIDX_B>& g, const Dir& d, int l, int
 }
 
 // dir_search(d, D, k, 1) for two keys by a group of 16 lanes
+// PX: the history holds long keys (Scalars::px_on) -- the prefix skips;
+// without, the plain searches (no tie bookkeeping on the hot path)
+template <bool PX = false>
 __device__ inline void grp_dir_find2(const Group<SIDX_B>& g, const Dir& d, int D, const Key& k1, const Key& k2,
                                      DirHit& h1, DirHit& h2) {
     int w1 = 0, w2 = 0;  // window starts (entry index at the current level)
-    const uint64_t q1 = q_tail_word(g, k1), q2 = q_tail_word(g, k2);  // (long keys only)
+    const uint64_t q1 = PX ? q_tail_word(g, k1) : 0, q2 = PX ? q_tail_word(g, k2) : 0;  // (long keys only)
     bool sp1 = false, sp2 = false;
     int s1, s2;
     uint64_t x1, x2;
@@ -203,8 +207,8 @@ __device__ inline void grp_dir_find2(const Group<SIDX_B>& g, const Dir& d, int D
         const uint64_t v2 = w2 == w1 ? v1 : (i2 < n ? arr[i2] : 0);
         dir_spec(g, d, l, n, w1, sp1, s1, x1);
         dir_spec(g, d, l, n, w2, sp2, s2, x2);
-        const int c1 = dir_count(g, d, l, n, w1, v1, k1, q1, sp1, s1, x1);  // >= 1: slot w is <= k
-        const int c2 = dir_count(g, d, l, n, w2, v2, k2, q2, sp2, s2, x2);
+        const int c1 = dir_count<PX>(g, d, l, n, w1, v1, k1, q1, sp1, s1, x1);  // >= 1: slot w is <= k
+        const int c2 = dir_count<PX>(g, d, l, n, w2, v2, k2, q2, sp2, s2, x2);
         w1 = (w1 + c1 - 1) << SIDX_LOG;
         w2 = (w2 + c2 - 1) << SIDX_LOG;
     }
@@ -226,8 +230,8 @@ __device__ inline void grp_dir_find2(const Group<SIDX_B>& g, const Dir& d, int D
     }
     dir_spec(g, d, 0, D, w1, sp1, s1, x1);
     dir_spec(g, d, 0, D, w2, sp2, s2, x2);
-    const int c1 = dir_count(g, d, 0, D, w1, v1, k1, q1, sp1, s1, x1);
-    const int c2 = dir_count(g, d, 0, D, w2, v2, k2, q2, sp2, s2, x2);
+    const int c1 = dir_count<PX>(g, d, 0, D, w1, v1, k1, q1, sp1, s1, x1);
+    const int c2 = dir_count<PX>(g, d, 0, D, w2, v2, k2, q2, sp2, s2, x2);
     h1.x = w1 + c1 - 1;
     h2.x = w2 + c2 - 1;
     h1.page = __shfl(pg1, g.shift + c1 - 1);
@@ -303,6 +307,7 @@ struct PageWin {
 // page's skip and 8 bytes of each key from there (common.h Pool::pskip) when
 // the page's directory window vouches for the skip (Dir::wsk of entry x):
 // *ps and *qx return the skip (0: none) and k's 8 bytes for step 2.
+template <bool PX>
 __device__ inline void pwin_step1(const Group<PIDX_STRIDE>& g, const Pool& p, const Dir& d, int x, int page,
                                   int64_t base, int cnt, const Key& k, uint64_t v, uint64_t qtw, PageWin& W, int& ps,
                                   uint64_t& qx) {
@@ -312,7 +317,7 @@ __device__ inline void pwin_step1(const Group<PIDX_STRIDE>& g, const Pool& p, co
     ps = 0;
     qx = 0;
     if (g.ballot(tie)) {
-        if (FDBCS_DIR_PX) {
+        if (PX) {
             const int s = p.pskip[page];
             if (s > 0 && s <= d.wsk[x >> SIDX_LOG]) ps = s;
         }
@@ -355,18 +360,19 @@ __device__ inline void pwin_step2(const Group<PIDX_STRIDE>& g, const Pool& p, in
 }
 
 // x1, x2: the pages' directory entries (their window's skip, Dir::wsk)
+template <bool PX = false>
 __device__ inline void grp_page_find2(const Group<PIDX_STRIDE>& g, const Pool& p, const Dir& d, int x1, int page1,
                                       int cnt1, const Key& k1, int x2, int page2, int cnt2, const Key& k2, int& i1,
                                       bool& eq1, int& i2, bool& eq2) {
     const int64_t b1 = (int64_t)page1 * PAGE, b2 = (int64_t)page2 * PAGE;
     const uint64_t u1 = p.pidx[(int64_t)page1 * (PAGE / PIDX_STRIDE) + g.lane];
     const uint64_t u2 = page2 == page1 ? u1 : p.pidx[(int64_t)page2 * (PAGE / PIDX_STRIDE) + g.lane];
-    const uint64_t q1 = q_tail_word(g, k1), q2 = q_tail_word(g, k2);  // (long keys only)
+    const uint64_t q1 = PX ? q_tail_word(g, k1) : 0, q2 = PX ? q_tail_word(g, k2) : 0;  // (long keys only)
     PageWin W1, W2;
     int ps1, ps2;
     uint64_t qx1, qx2;
-    pwin_step1(g, p, d, x1, page1, b1, cnt1, k1, u1, q1, W1, ps1, qx1);
-    pwin_step1(g, p, d, x2, page2, b2, cnt2, k2, u2, q2, W2, ps2, qx2);
+    pwin_step1<PX>(g, p, d, x1, page1, b1, cnt1, k1, u1, q1, W1, ps1, qx1);
+    pwin_step1<PX>(g, p, d, x2, page2, b2, cnt2, k2, u2, q2, W2, ps2, qx2);
     const bool s1 = !W1.done, s2 = !W2.done;
     const uint64_t* a1 = ps1 ? p.px : p.hi;
     const uint64_t* a2 = ps2 ? p.px : p.hi;

@@ -257,6 +257,7 @@ struct HistBufs {
     int32_t cap_pages;
     int32_t* free_stack;
     int32_t* px_list;  // [cap_pages] directory entries of rewritten pages (k_dir_px -> k_page_px)
+    int px_par = 0;    // which Scalars::n_pxd counts the next list
     Dir dir[2];
     int32_t cap_dir;
     uint8_t* tail_arena;
@@ -269,6 +270,10 @@ struct HistBufs {
     // host-mapped copy of the scalars, written by the kernel that ends a batch
     // (the host reads it after a stream sync instead of issuing a copy)
     Scalars* mirror;
+    const volatile Scalars* mirror_host;  // (the same memory, host address)
+    // the host has seen Scalars::px_on (sticky): from then on every directory
+    // gets its prefix skips rebuilt (k_dir_px); before, none was ever built
+    bool px_host = false;
 };
 
 // ---- scans (scan.hip) ----

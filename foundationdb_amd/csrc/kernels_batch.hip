@@ -221,13 +221,17 @@ __device__ inline void read_check_group(const ReadCheckArgs& A, const Group<RC_G
         const int xe = dir_entry_after(g, dir, D, xb, e);
         hb = DirHit{xb, dir.page[xb], dir.cnt[xb]};
         he = DirHit{xe, dir.page[xe], dir.cnt[xe]};
-    } else {
-        grp_dir_find2(g, dir, D, b, e, hb, he);
+    }
+    const bool px = FDBCS_DIR_PX && A.sc->px_on;  // (long keys: the searches' prefix skips)
+    if (!A.qx) {
+        if (px) grp_dir_find2<true>(g, dir, D, b, e, hb, he);
+        else grp_dir_find2<false>(g, dir, D, b, e, hb, he);
     }
     const int pb = hb.x, pe = he.x, cb = hb.cnt;
     int ib, ie;
     bool eqb, eqe;
-    grp_page_find2(g, pool, dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    if (px) grp_page_find2<true>(g, pool, dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    else grp_page_find2<false>(g, pool, dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
     const int64_t baseb = (int64_t)hb.page * PAGE, basee = (int64_t)he.page * PAGE;
     const int i0 = eqb ? ib : ib - 1;  // the slot whose version covers b
     bool c = i0 < 0 && v0 > s;
@@ -2114,12 +2118,16 @@ __device__ inline void write_search_group(const WriteSearchArgs& A, const Group<
         const int xb = A.qx[A.R + 2 * w], xe = A.qx[A.R + 2 * w + 1];
         hb = DirHit{xb, A.dir.page[xb], A.dir.cnt[xb]};
         he = DirHit{xe, A.dir.page[xe], A.dir.cnt[xe]};
-    } else {
-        grp_dir_find2(g, A.dir, D, b, e, hb, he);
+    }
+    const bool px = FDBCS_DIR_PX && A.sc->px_on;  // (long keys: the searches' prefix skips)
+    if (!A.qx) {
+        if (px) grp_dir_find2<true>(g, A.dir, D, b, e, hb, he);
+        else grp_dir_find2<false>(g, A.dir, D, b, e, hb, he);
     }
     int ib, ie;
     bool eqb, eqe;
-    grp_page_find2(g, A.pool, A.dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    if (px) grp_page_find2<true>(g, A.pool, A.dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
+    else grp_page_find2<false>(g, A.pool, A.dir, hb.x, hb.page, hb.cnt, b, he.x, he.page, he.cnt, e, ib, eqb, ie, eqe);
     if (g.lane != 0) return;
     uint64_t hmb[HM_WORDS], hme[HM_WORDS];  // real positions for the merge plan's counts (holes, common.h)
     load_hmask(A.pool, hb.page, hmb);

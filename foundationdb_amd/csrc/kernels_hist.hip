@@ -502,16 +502,18 @@ struct MergeArgs {
     uint8_t* arena;
     uint64_t arena_cap;
     int64_t now;
+    int px;  // HistBufs::px_host: pages may hold prefix skips (else none was ever set)
 };
 
 __device__ inline void put_entry(const Pool& pool, int64_t d, uint64_t hi, uint64_t lo, uint32_t meta, int64_t ver,
-                                 const uint8_t* tail, uint64_t px = 0) {
+                                 const uint8_t* tail) {
     pool.hi[d] = hi; pool.lo[d] = lo; pool.meta[d] = meta; pool.ver[d] = ver; pool.tail[d] = tail;
     if ((d & (PIDX_STRIDE - 1)) == 0) pool.pidx[d / PIDX_STRIDE] = hi;
-    if (FDBCS_DIR_PX) {
-        pool.px[d] = px;
-        if ((d & (PIDX_STRIDE - 1)) == 0) pool.pxidx[d / PIDX_STRIDE] = px;
-    }
+}
+// a slot's 8 bytes past its page's prefix skip (common.h Pool::px)
+__device__ inline void put_px(const Pool& pool, int64_t d, uint64_t px) {
+    pool.px[d] = px;
+    if ((d & (PIDX_STRIDE - 1)) == 0) pool.pxidx[d / PIDX_STRIDE] = px;
 }
 
 __device__ inline void put_desc(const DescArrays& D, int x, int page, int n, uint64_t hi, uint64_t lo,
@@ -691,25 +693,34 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
     }
     wave_lds_sync();
     // ---- read the boundaries that move, then write them
-    uint64_t ohi[4], olo[4], opx[4];
+    uint64_t ohi[4], olo[4];
     uint32_t ometa[4];
     int64_t over[4];
     const uint8_t* otail[4];
-    const int pskip = FDBCS_DIR_PX ? A.pool.pskip[pg] : 0;  // (< 0: rewritten this batch -- not here)
+    const int pskip = FDBCS_DIR_PX && A.px ? A.pool.pskip[pg] : 0;  // (<= 0: no prefix words to keep)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if (!((movem >> q) & 1)) continue;
         const int64_t sl = pbase + i0 + q;
         ohi[q] = A.pool.hi[sl]; olo[q] = A.pool.lo[sl]; ometa[q] = A.pool.meta[sl];
         over[q] = A.pool.ver[sl]; otail[q] = A.pool.tail[sl];
-        opx[q] = pskip > 0 ? A.pool.px[sl] : 0;
     }
     wave_loads_done();
+    if (pskip > 0) {  // the moving slots' prefix words, in a pass of their own (fewer live registers)
+        uint64_t opx[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if ((movem >> q) & 1) opx[q] = A.pool.px[pbase + i0 + q];
+        wave_loads_done();
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if ((movem >> q) & 1) put_px(A.pool, pbase + i0 + q + cb[q] + av[q], opx[q]);
+    }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int i = i0 + q;
         if ((movem >> q) & 1)
-            put_entry(A.pool, pbase + i + cb[q] + av[q], ohi[q], olo[q], ometa[q], over[q], otail[q], opx[q]);
+            put_entry(A.pool, pbase + i + cb[q] + av[q], ohi[q], olo[q], ometa[q], over[q], otail[q]);
         if ((usem >> q) & 1) atomicAnd(&S.hm[i >> 6], ~(1ull << (i & 63)));
     }
     // ---- the new entries, by the plan lanes: b_j (version now), then e_j
@@ -734,7 +745,8 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
             const int out = at + S.er[at] + (k - S.ins[at]);
             const uint8_t* tl;
             copy_tail(kk, A.arena, A.arena_cap, A.sc, &tl);
-            put_entry(A.pool, pbase + out, kk.hi, kk.lo, kk.meta, ver, tl, pskip > 0 ? key_bytes_at(kk, pskip) : 0);
+            put_entry(A.pool, pbase + out, kk.hi, kk.lo, kk.meta, ver, tl);
+            if (pskip > 0) put_px(A.pool, pbase + out, key_bytes_at(kk, pskip));
             vmax = max(vmax, ver);
             maxout = max(maxout, out);
             if (out == 0) part_first(S, A.dst, A, a, doff, 0, 1, 1, pg, kk.hi, kk.lo, kk.meta, tl);
@@ -1185,23 +1197,35 @@ __device__ inline int window_skip(const Dir& d, int D, int l, int w) {
     return skip < PX_MIN_SKIP ? 0 : min(skip, PX_MAX_SKIP);  // (a shorter skip is as valid)
 }
 
-__global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool pool, int32_t* list, Scalars* sc) {
+__global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool pool, int32_t* list, int32_t* n_list,
+                                              int32_t* n_next, const int32_t* px_on) {
+    __shared__ int s_skip[256 / SIDX_B];
     const int D = *Dp;
     const int64_t cap = d.cap;
-    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_next = 0;  // (the other parity's list: the next directory's)
+    if (!*px_on) return;  // (no key past 17 bytes yet: every skip is still 0)
     for (int l = 0; l <= SIDX_LEVELS; l++) {
         const int n = sidx_n(D, l);  // entries of level l
         if (l > 0 && n <= 1) break;
-        for (int i = tid; i < n; i += nth) {
+        // (block-uniform trip count: the barrier below)
+        for (int i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
+            const int i = i0 + threadIdx.x;
             const int w = i >> SIDX_LOG;
-            const int skip = window_skip(d, D, l, w);
-            if ((i & (SIDX_B - 1)) == 0) d.wsk[wsk_off(cap, l) + w] = skip;
+            if ((i & (SIDX_B - 1)) == 0) {
+                const int sk = i < n ? window_skip(d, D, l, w) : 0;
+                s_skip[threadIdx.x / SIDX_B] = sk;
+                if (i < n) d.wsk[wsk_off(cap, l) + w] = sk;
+            }
+            __syncthreads();
+            const int skip = s_skip[threadIdx.x / SIDX_B];
+            __syncthreads();
+            if (i >= n || !skip) continue;
             const int x = (int)((int64_t)i << (SIDX_LOG * l));
-            if (skip) (l == 0 ? d.fpx : d.spx + sidx_off(cap, l))[i] = key_bytes_at(dir_first(d, x), skip);
+            (l == 0 ? d.fpx : d.spx + sidx_off(cap, l))[i] = key_bytes_at(dir_first(d, x), skip);
             // (a page's skip counts only under a window skip: pages elsewhere
             // stay listed as rewritten until their window has one)
-            if (l == 0 && skip && pool.pskip[d.page[x]] < 0) {
-                const int k = atomicAdd(&sc->n_pxd, 1);
+            if (l == 0 && pool.pskip[d.page[x]] < 0) {
+                const int k = atomicAdd(n_list, 1);
                 if (k < d.cap) list[k] = x;
             }
         }
@@ -1212,8 +1236,8 @@ __global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool p
 // the skip is the common prefix of the page's first and last keys (so of
 // all of them), used by the searches only where the page's directory window
 // vouches for it (common.h Pool).
-__global__ __launch_bounds__(256) void k_page_px(Dir d, Pool pool, const int32_t* list, Scalars* sc) {
-    const int n = min(sc->n_pxd, d.cap);
+__global__ __launch_bounds__(256) void k_page_px(Dir d, Pool pool, const int32_t* list, const int32_t* n_list) {
+    const int n = min(*n_list, d.cap);
     const int lane = threadIdx.x & 63;
     for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
         const int x = list[k];
@@ -1241,12 +1265,22 @@ __global__ __launch_bounds__(256) void k_page_px(Dir d, Pool pool, const int32_t
     }
 }
 
+// (the list's count alternates between two scalars: each k_dir_px zeroes the
+// one the next k_dir_px counts into, so no memset node sits in the chain)
+// Launched only once the host has seen a long key come through (the
+// batch-ending kernel's mirror, one batch late at most): until then no skip
+// was ever built, so the zero skips stay right and the two launches (~9 us
+// of the update chain) are saved.
 void launch_dir_px(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
     if (!FDBCS_DIR_PX) return;
-    (void)hipMemsetAsync(&sc->n_pxd, 0, sizeof(int32_t), s);
-    hipLaunchKernelGGL(k_dir_px, dim3(std::max(1, std::min(2048, cdiv(h.cap_dir, 256)))), dim3(256), 0, s,
-                       h.dir[which], &sc->D, h.pool, h.px_list, sc);
-    hipLaunchKernelGGL(k_page_px, dim3(256), dim3(256), 0, s, h.dir[which], h.pool, (const int32_t*)h.px_list, sc);
+    if (!h.px_host && h.mirror_host && h.mirror_host->px_on) h.px_host = true;
+    if (!h.px_host) return;
+    const int par = h.px_par;
+    h.px_par ^= 1;
+    hipLaunchKernelGGL(k_dir_px, dim3(std::max(1, std::min(256, cdiv(h.cap_dir, 256)))), dim3(256), 0, s,
+                       h.dir[which], &sc->D, h.pool, h.px_list, &sc->n_pxd[par], &sc->n_pxd[par ^ 1], &sc->px_on);
+    hipLaunchKernelGGL(k_page_px, dim3(64), dim3(256), 0, s, h.dir[which], h.pool, (const int32_t*)h.px_list,
+                       (const int32_t*)&sc->n_pxd[par]);
 }
 
 void launch_sidx_build(HistBufs& h, int which, Scalars* sc, hipStream_t s) {
@@ -1307,7 +1341,8 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
         if (end_of_batch) {  // the next batch's encoder allocates from these
             sc->last_err = sc->err;
             sc->err = 0;
-            sc->btail_used = 0;
+            if (sc->btail_used) sc->px_on = 1;  // (a long key came through: the prefix skips, from now on)
+        sc->btail_used = 0;
             lm_end_of_batch(sc);
         }
     }
@@ -1369,6 +1404,7 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         A.pb = b.pb; A.ib = b.ib; A.pe = b.pe; A.ie = b.ie; A.need_e = b.need_e; A.vb = b.vb;
         A.rb = b.rkb; A.re = b.rke; A.ne = b.ne; A.ne_ins = b.ne_ins;
         A.arena = h.tail_arena; A.arena_cap = h.tail_cap; A.now = now;
+        A.px = h.px_host ? 1 : 0;
         A.full_list = b.full_list;
         const int grid = std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)));
         hipLaunchKernelGGL(k_page_merge, dim3(grid), dim3(256), 0, s, A);
@@ -1570,6 +1606,7 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         }
         sc->last_err = sc->err;  // end of batch: the next batch's encoder allocates from these
         sc->err = 0;
+        if (sc->btail_used) sc->px_on = 1;
         sc->btail_used = 0;
         lm_end_of_batch(sc);
     }
