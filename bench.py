@@ -930,9 +930,10 @@ def run_multi(args, rank, world):
     dist.barrier()
     if rank == 0:
         how = ("protocol B: each GPU takes only the ranges on its keys (the proxy's keep-all split, before the clock); "
-               "RCCL MAX all-reduce of abort flags + slots carrying every shard's edge count, one all-gather of the "
-               "overlap edges when any shard has some, all-gather for the compaction window; carry-ins, compaction "
-               "plan and removalKey owner on the device" if proto == "b" else
+               "RCCL MAX all-reduce of abort flags + slots carrying every shard's edge count, one fixed-capacity "
+               "all-gather of the overlap edges (no host read mid-batch; a short one reruns in-stream), all-gather "
+               "for the compaction window; carry-ins, compaction plan and removalKey owner on the device"
+               if proto == "b" else
                "protocol A: every GPU takes the whole batch; RCCL MAX all-reduce of abort flags + all-gather for the "
                "compaction window")
         per_gpu = f"{T} txns split over the GPUs" if strong else f"{args.txns}/GPU"

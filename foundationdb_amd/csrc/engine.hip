@@ -2282,8 +2282,22 @@ int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, ui
     int32_t* send = sh->ebuf;
     int32_t* recv = send + 2 * M;
     int32_t* cat = recv + 2 * M * G;
-    launch_sh_edges_pack(b, cs->sc, M, send, s);
-    if ((r = sh_allgather(sh, send, recv, (size_t)(2 * M) * 4))) return r;
+    // Host collectives (rehearsals, tests) hold the gathered counts on the
+    // host already (sh_allreduce_max synchronizes): with no edge anywhere the
+    // lists' all-gather -- another synchronous host round -- is skipped and
+    // the received lists are zeros, as a gather of empty lists would leave them.
+    bool any = true;
+    if (sh->host_ops) {
+        const int64_t* hs = reinterpret_cast<const int64_t*>(sh->hx);
+        any = false;
+        for (int64_t g = 0; g < G; g++) any |= hs[g * SH_WORDS + 2] != 0 || hs[g * SH_WORDS + 3] != 0;
+    }
+    if (any) {
+        launch_sh_edges_pack(b, cs->sc, M, send, s);
+        if ((r = sh_allgather(sh, send, recv, (size_t)(2 * M) * 4))) return r;
+    } else {
+        HIPOK(hipMemsetAsync(recv, 0, (size_t)(2 * M * G) * sizeof(int32_t), s));
+    }
     launch_sh_edges_cat_fixed(recv, sl, (int)G, M, cat, cat + M * G, cs->sc, s);
     launch_set_edges(b, cs->sc, (int)T, cat, cat + M * G, -(M * G), s);
     return FDBCS_OK;
