@@ -282,9 +282,15 @@ __device__ inline int key_lcp(const Key& a, const Key& b) {
     const uint64_t* ta = reinterpret_cast<const uint64_t*>(a.tail);
     const uint64_t* tb = reinterpret_cast<const uint64_t*>(b.tail);
     const int words = (m - 17 + 7) >> 3;
-    for (int w = 0; w < words; w++) {
-        const uint64_t d = ta[w] ^ tb[w];  // (little-endian words: the first byte is the lowest)
-        if (d) return min(m, 17 + 8 * w + (__ffsll((unsigned long long)d) - 1) / 8);
+    // (four independent loads a step: a shared 64-byte prefix is six words,
+    // one round trip each when the loop exits word by word)
+    for (int w = 0; w < words; w += 4) {
+        uint64_t d[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = w + k < words ? ta[w + k] ^ tb[w + k] : 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)  // (little-endian words: the first byte is the lowest)
+            if (d[k]) return min(m, 17 + 8 * (w + k) + (__ffsll((unsigned long long)d[k]) - 1) / 8);
     }
     return m;
 }

@@ -1197,6 +1197,38 @@ __device__ inline int window_skip(const Dir& d, int D, int l, int w) {
     return skip < PX_MIN_SKIP ? 0 : min(skip, PX_MAX_SKIP);  // (a shorter skip is as valid)
 }
 
+// The levels lie side by side in one index space, each from a multiple of
+// 16 (so a window never straddles a block): every level's windows at once,
+// not one dependent pass per level.  Position f -> level l, its index i, and
+// n = the level's entries (0 past the last level).
+__device__ inline void px_level_of(int D, int f, int& l, int& i, int& n) {
+    int base = 0;
+    l = 0;
+    n = D;
+    for (;;) {
+        const int span = (n + SIDX_B - 1) & ~(SIDX_B - 1);
+        if (f < base + span) break;
+        const int nn = l < SIDX_LEVELS ? sidx_n(D, l + 1) : 0;
+        base += span;
+        l++;
+        if (nn <= 1) {  // (past the last level k_dir_px builds)
+            n = 0;
+            break;
+        }
+        n = nn;
+    }
+    i = f - base;
+}
+__device__ inline int px_positions(int D) {  // (the first position past the last level)
+    int f = 0;
+    for (int k = 0; k <= SIDX_LEVELS; k++) {
+        const int nk = sidx_n(D, k);
+        if (k > 0 && nk <= 1) break;
+        f += (nk + SIDX_B - 1) & ~(SIDX_B - 1);
+    }
+    return f;
+}
+
 __global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool pool, int32_t* list, int32_t* n_list,
                                               int32_t* n_next, const int32_t* px_on) {
     __shared__ int s_skip[256 / SIDX_B];
@@ -1204,30 +1236,28 @@ __global__ __launch_bounds__(256) void k_dir_px(Dir d, const int32_t* Dp, Pool p
     const int64_t cap = d.cap;
     if (blockIdx.x == 0 && threadIdx.x == 0) *n_next = 0;  // (the other parity's list: the next directory's)
     if (!*px_on) return;  // (no key past 17 bytes yet: every skip is still 0)
-    for (int l = 0; l <= SIDX_LEVELS; l++) {
-        const int n = sidx_n(D, l);  // entries of level l
-        if (l > 0 && n <= 1) break;
-        // (block-uniform trip count: the barrier below)
-        for (int i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {
-            const int i = i0 + threadIdx.x;
-            const int w = i >> SIDX_LOG;
-            if ((i & (SIDX_B - 1)) == 0) {
-                const int sk = i < n ? window_skip(d, D, l, w) : 0;
-                s_skip[threadIdx.x / SIDX_B] = sk;
-                if (i < n) d.wsk[wsk_off(cap, l) + w] = sk;
-            }
-            __syncthreads();
-            const int skip = s_skip[threadIdx.x / SIDX_B];
-            __syncthreads();
-            if (i >= n || !skip) continue;
-            const int x = (int)((int64_t)i << (SIDX_LOG * l));
-            (l == 0 ? d.fpx : d.spx + sidx_off(cap, l))[i] = key_bytes_at(dir_first(d, x), skip);
-            // (a page's skip counts only under a window skip: pages elsewhere
-            // stay listed as rewritten until their window has one)
-            if (l == 0 && pool.pskip[d.page[x]] < 0) {
-                const int k = atomicAdd(n_list, 1);
-                if (k < d.cap) list[k] = x;
-            }
+    const int nf = px_positions(D);
+    // (block-uniform trip count: the barrier below)
+    for (int f0 = blockIdx.x * blockDim.x; f0 < nf; f0 += gridDim.x * blockDim.x) {
+        int l, i, n;
+        px_level_of(D, f0 + (int)threadIdx.x, l, i, n);
+        const int w = i >> SIDX_LOG;
+        if ((i & (SIDX_B - 1)) == 0) {  // (levels start on a multiple of 16: i's window starts with f's)
+            const int sk = i < n ? window_skip(d, D, l, w) : 0;
+            s_skip[threadIdx.x / SIDX_B] = sk;
+            if (i < n) d.wsk[wsk_off(cap, l) + w] = sk;
+        }
+        __syncthreads();
+        const int skip = s_skip[threadIdx.x / SIDX_B];
+        __syncthreads();
+        if (i >= n || !skip) continue;
+        const int x = (int)((int64_t)i << (SIDX_LOG * l));
+        (l == 0 ? d.fpx : d.spx + sidx_off(cap, l))[i] = key_bytes_at(dir_first(d, x), skip);
+        // (a page's skip counts only under a window skip: pages elsewhere
+        // stay listed as rewritten until their window has one)
+        if (l == 0 && pool.pskip[d.page[x]] < 0) {
+            const int k = atomicAdd(n_list, 1);
+            if (k < d.cap) list[k] = x;
         }
     }
 }
@@ -1255,12 +1285,24 @@ __global__ __launch_bounds__(256) void k_page_px(Dir d, Pool pool, const int32_t
                 if (skip < PX_MIN_SKIP) skip = 0;
             }
         }
-        if (skip)
-            for (int i = lane; i < c; i += 64) {
-                const uint64_t v = key_bytes_at(pool_key(pool, b + i), skip);
-                pool.px[b + i] = v;
-                if ((i & (PIDX_STRIDE - 1)) == 0) pool.pxidx[(b + i) / PIDX_STRIDE] = v;
+        if (skip) {
+            // (every slot's words loaded before any store: a store between
+            // them would keep the next slot's loads behind it, two round
+            // trips a slot)
+            uint64_t v[PAGE / 64];
+#pragma unroll
+            for (int q = 0; q < PAGE / 64; q++) {
+                const int i = lane + 64 * q;
+                v[q] = i < c ? key_bytes_at(pool_key(pool, b + i), skip) : 0;
             }
+#pragma unroll
+            for (int q = 0; q < PAGE / 64; q++) {
+                const int i = lane + 64 * q;
+                if (i >= c) continue;
+                pool.px[b + i] = v[q];
+                if ((i & (PIDX_STRIDE - 1)) == 0) pool.pxidx[(b + i) / PIDX_STRIDE] = v[q];
+            }
+        }
         if (lane == 0) pool.pskip[pg] = skip;
     }
 }
