@@ -560,10 +560,49 @@ __device__ inline void splitter_fill(const SortJobs& J, int job, uint64_t* sp) {
     for (int k = threadIdx.x; k < nb - 1; k += blockDim.x) sp[k] = J.quant[job * SS_Q + (k + 1) * step].hi;
 }
 
+// rec_lt_quant for an x longer than 17 bytes whose tail is xt: the splitter,
+// its kept tail and x's first tail words are loaded together -- one round
+// trip a search step where rec_lt_quant takes two (the splitter, then both
+// tails); config 4's keys tie on their first 64 bytes, so every step of
+// their splitter search compares tails.  (x's words past the compared ones
+// are loaded and ignored: every compare stops within SS_QT tail bytes.)
+__device__ inline bool rec_lt_quant_long(const SRec& x, const uint8_t* xt, const SRec* qp, const uint8_t* qt,
+                                         const uint8_t* const* tails) {
+    constexpr int NW = SS_QT / 8;
+    const uint32_t lx = key_len(x.meta);
+    const int xwords = (int)min<uint32_t>((lx - 17 + 7) >> 3, (uint32_t)NW);
+    const uint64_t* a = reinterpret_cast<const uint64_t*>(xt);
+    const uint64_t* b = reinterpret_cast<const uint64_t*>(qt);
+    uint64_t xa[NW], yb[NW];
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        xa[k] = k < xwords ? a[k] : 0;
+        yb[k] = k < xwords ? b[k] : 0;
+    }
+    const SRec q = *qp;
+    const bool tail_case = (x.hi == q.hi) & (x.lo == q.lo) & ((x.meta >> 24) == (q.meta >> 24)) &
+                           (key_len(q.meta) > 17);
+    if (!tail_case) return rec_lt(x, q, tails);  // (decided without tails)
+    // as rec_lt_quant_tail: a cut splitter stands for its kept prefix
+    const uint32_t lq = key_len(q.meta);
+    const bool cut = lq - 17 > (uint32_t)SS_QT;
+    const uint32_t lb = cut ? 17 + SS_QT : lq;
+    const int words = (int)(((lx < lb ? lx : lb) - 17 + 7) >> 3);  // (<= xwords)
+    int c = 0;
+#pragma unroll
+    for (int k = NW - 1; k >= 0; k--)  // (the first differing word decides)
+        if (k < words && xa[k] != yb[k]) c = __builtin_bswap64(xa[k]) < __builtin_bswap64(yb[k]) ? -1 : 1;
+    if (c == 0) c = lx < lb ? -1 : (lx > lb ? 1 : 0);
+    if (cut || c) return c < 0;
+    const uint32_t px = x.idx & 1, pq = q.idx & 1;
+    return px != pq ? px > pq : x.idx < q.idx;
+}
+
 // bucket of record x = number of splitters <= x (splitters nondecreasing)
 __device__ inline int bucket_of(const SortJobs& J, int job, const uint64_t* sp, const SRec& x,
                                 const uint8_t* const* tails) {
     const int nb = J.nb[job], step = SS_Q / nb;
+    const uint8_t* xt = key_len(x.meta) > 17 ? tails[x.idx] : nullptr;  // (once, not per step)
     int lo = 0, len = nb - 1;
     while (len > 0) {
         const int half = len >> 1, k = lo + half;
@@ -573,7 +612,8 @@ __device__ inline int bucket_of(const SortJobs& J, int job, const uint64_t* sp, 
             le = h < x.hi;
         } else {
             const int q = job * SS_Q + (k + 1) * step;
-            le = !rec_lt_quant(x, J.quant[q], J.qtail + (int64_t)q * SS_QT, tails);
+            const uint8_t* qt = J.qtail + (int64_t)q * SS_QT;
+            le = xt ? !rec_lt_quant_long(x, xt, J.quant + q, qt, tails) : !rec_lt_quant(x, J.quant[q], qt, tails);
         }
         if (le) {
             lo += half + 1;
