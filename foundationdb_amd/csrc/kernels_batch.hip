@@ -290,15 +290,30 @@ static constexpr int SS_WAVE = 128;      // bucket size sorted in registers
 static constexpr int SS_ROW = 512;       // staging row per bucket (LDS path)
 static constexpr int SS_CNT = 3 * SS_MAXB;  // counter words per parity: counts of both jobs, job 1's cover deltas
 
+// A sort record's tail: the pointer its scatter kept in `pad` (the batch's
+// tail bytes, one load fewer per tail compare of a sorted record), else the
+// key arrays' (records rebuilt from LDS or loaded by slot carry pad 0;
+// quantiles, which outlive the batch, are stored with pad 0).
+__device__ inline uint64_t rec_pad(const Key& k) { return (uint64_t)(uintptr_t)k.tail; }
+__device__ inline const uint8_t* rec_tail(const SRec& a, const uint8_t* const* tails) {
+    return a.pad ? reinterpret_cast<const uint8_t*>(a.pad) : tails[a.idx];
+}
+
 // Total order on sort records: key, then END (odd slot) before BEGIN, then
 // slot.  Branch-free on the fixed-width part; the tails are consulted only
 // when both keys are > 17 bytes and equal on 17 bytes.  (hi, lo, meta) as
 // integers is the key order otherwise: meta = byte16 << 24 | len.
-__device__ __noinline__ bool rec_lt_tail(const SRec& a, const SRec& b, const uint8_t* const* tails) {
-    const int c = tail_cmp(tails[a.idx], key_len(a.meta), tails[b.idx], key_len(b.meta));
+// (out of line with scalar arguments: a record passed by reference to an
+// out-of-line call is spilled to the stack)
+__device__ __noinline__ bool rec_lt_tail_at(const uint8_t* ta, uint32_t ma, uint32_t ia, const uint8_t* tb,
+                                            uint32_t mb, uint32_t ib) {
+    const int c = tail_cmp(ta, key_len(ma), tb, key_len(mb));
     if (c) return c < 0;
-    const uint32_t pa = a.idx & 1, pb = b.idx & 1;
-    return pa != pb ? pa > pb : a.idx < b.idx;
+    const uint32_t pa = ia & 1, pb = ib & 1;
+    return pa != pb ? pa > pb : ia < ib;
+}
+__device__ inline bool rec_lt_tail(const SRec& a, const SRec& b, const uint8_t* const* tails) {
+    return rec_lt_tail_at(rec_tail(a, tails), a.meta, a.idx, rec_tail(b, tails), b.meta, b.idx);
 }
 
 __device__ inline bool rec_lt(const SRec& a, const SRec& b, const uint8_t* const* tails) {
@@ -314,8 +329,11 @@ __device__ inline bool rec_lt(const SRec& a, const SRec& b, const uint8_t* const
 }
 
 // key-only three-way compare of a record against a key
-__device__ __noinline__ int rec_vs_key_tail(const SRec& a, const Key& k, const uint8_t* const* tails) {
-    return tail_cmp(tails[a.idx], key_len(a.meta), k.tail, key_len(k.meta));
+__device__ __noinline__ int tail_cmp_at(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
+    return tail_cmp(ta, la, tb, lb);
+}
+__device__ inline int rec_vs_key_tail(const SRec& a, const Key& k, const uint8_t* const* tails) {
+    return tail_cmp_at(rec_tail(a, tails), key_len(a.meta), k.tail, key_len(k.meta));
 }
 
 __device__ inline int rec_vs_key(const SRec& a, const Key& k, const uint8_t* const* tails) {
@@ -352,28 +370,34 @@ struct SortJobs {
 // splitter whose tail was cut stands for the prefix it kept (the smallest key
 // with that prefix), which is still a consistent split point.
 __device__ inline void put_quantile(const SortJobs& J, int job, int q, const SRec& x, const uint8_t* const* tails) {
-    J.quant[job * SS_Q + q] = x;
+    SRec y = x;
+    y.pad = 0;  // (the batch's tail pointer: quantiles outlive the batch, qtail keeps their bytes)
+    J.quant[job * SS_Q + q] = y;
     const uint32_t L = key_len(x.meta);
     if (L > 17) {
         const int words = (int)min<uint32_t>((L - 17 + 7) / 8, SS_QT / 8);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(tails[x.idx]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(rec_tail(x, tails));
         uint64_t* dst = reinterpret_cast<uint64_t*>(J.qtail + (int64_t)(job * SS_Q + q) * SS_QT);
         for (int w = 0; w < words; w++) dst[w] = src[w];
     }
 }
 
-__device__ __noinline__ bool rec_lt_quant_tail(const SRec& x, const SRec& q, const uint8_t* qt,
-                                               const uint8_t* const* tails) {
-    const uint32_t lx = key_len(x.meta), lq = key_len(q.meta);
+__device__ __noinline__ bool rec_lt_quant_tail_at(const uint8_t* xt, uint32_t xm, uint32_t xi, uint32_t qm, uint32_t qi,
+                                                  const uint8_t* qt) {
+    const uint32_t lx = key_len(xm), lq = key_len(qm);
     if (lq - 17 > (uint32_t)SS_QT) {  // q was cut: compare with its kept prefix
         const uint32_t lp = 17 + SS_QT;
-        const int c = tail_cmp(tails[x.idx], lx, qt, lp);
+        const int c = tail_cmp(xt, lx, qt, lp);
         return c < 0;  // (a key that starts with the prefix is not below it)
     }
-    const int c = tail_cmp(tails[x.idx], lx, qt, lq);
+    const int c = tail_cmp(xt, lx, qt, lq);
     if (c) return c < 0;
-    const uint32_t px = x.idx & 1, pq = q.idx & 1;
-    return px != pq ? px > pq : x.idx < q.idx;
+    const uint32_t px = xi & 1, pq = qi & 1;
+    return px != pq ? px > pq : xi < qi;
+}
+__device__ inline bool rec_lt_quant_tail(const SRec& x, const SRec& q, const uint8_t* qt,
+                                         const uint8_t* const* tails) {
+    return rec_lt_quant_tail_at(rec_tail(x, tails), x.meta, x.idx, q.meta, q.idx, qt);
 }
 
 __device__ inline bool rec_lt_quant(const SRec& x, const SRec& q, const uint8_t* qt, const uint8_t* const* tails) {
@@ -602,7 +626,7 @@ __device__ inline bool rec_lt_quant_long(const SRec& x, const uint8_t* xt, const
 __device__ inline int bucket_of(const SortJobs& J, int job, const uint64_t* sp, const SRec& x,
                                 const uint8_t* const* tails) {
     const int nb = J.nb[job], step = SS_Q / nb;
-    const uint8_t* xt = key_len(x.meta) > 17 ? tails[x.idx] : nullptr;  // (once, not per step)
+    const uint8_t* xt = key_len(x.meta) > 17 ? rec_tail(x, tails) : nullptr;  // (once, not per step)
     int lo = 0, len = nb - 1;
     while (len > 0) {
         const int half = len >> 1, k = lo + half;
@@ -714,11 +738,11 @@ __global__ __launch_bounds__(FDBCS_INGEST_BLOCK) void k_ingest(IngestArgs A, Sor
     if constexpr (SCATTER) {
         const uint8_t* const* tails = A.keys.tail;
         if (i < A.R) {
-            if (J.nb[0]) scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[0]);
+            if (J.nb[0]) scatter_rec(J, 0, (int)i, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), rec_pad(b)}, tails, sp[0]);
         } else {
             const int w = (int)(i - A.R);
-            scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), 0}, tails, sp[1]);
-            scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(2 * i + 1), 0}, tails, sp[1]);
+            scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)(2 * i), rec_pad(b)}, tails, sp[1]);
+            scatter_rec(J, 1, 2 * w + 1, SRec{e.hi, e.lo, e.meta, (uint32_t)(2 * i + 1), rec_pad(e)}, tails, sp[1]);
         }
     }
 }
@@ -937,10 +961,10 @@ __device__ inline void staged_group(const IngestArgs& A, const SortJobs& J, cons
         A.keys.put(i + 1, en);
         if constexpr (SCATTER) {
             if (w < 0) {
-                if (J.nb[0]) scatter_rec(J, 0, r, SRec{b.hi, b.lo, b.meta, (uint32_t)i, 0}, tails, sp0);
+                if (J.nb[0]) scatter_rec(J, 0, r, SRec{b.hi, b.lo, b.meta, (uint32_t)i, rec_pad(b)}, tails, sp0);
             } else {
-                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)i, 0}, tails, sp1);
-                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(i + 1), 0}, tails, sp1);
+                scatter_rec(J, 1, 2 * w, SRec{b.hi, b.lo, b.meta, (uint32_t)i, rec_pad(b)}, tails, sp1);
+                scatter_rec(J, 1, 2 * w + 1, SRec{en.hi, en.lo, en.meta, (uint32_t)(i + 1), rec_pad(en)}, tails, sp1);
             }
         }
     }
@@ -1271,7 +1295,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 if (lane + 64 * q >= c) continue;
-                const uint64_t* t = reinterpret_cast<const uint64_t*>(tails[x[q].idx]);
+                const uint64_t* t = reinterpret_cast<const uint64_t*>(rec_tail(x[q], tails));
                 const uint32_t nm = min(tail_words(x[q].meta), n0);
                 uint32_t w = 0;
                 while (w < nm) {  // (four independent loads a step)
@@ -1300,7 +1324,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
             for (int q = 0; q < 2; q++) {
                 const int e = lane + 64 * q;
                 if (e >= c) continue;
-                const uint64_t* t = reinterpret_cast<const uint64_t*>(tails[x[q].idx]);
+                const uint64_t* t = reinterpret_cast<const uint64_t*>(rec_tail(x[q], tails));
                 const uint32_t n = tail_words(x[q].meta);
                 xt[q][0] = W < n ? __builtin_bswap64(t[W]) : 0;
                 xt[q][1] = W + 1 < n ? __builtin_bswap64(t[W + 1]) : 0;
@@ -2274,7 +2298,7 @@ __device__ inline void bsearch2(const SRec* a, const Key& k1, bool strict1, int 
 
 __device__ inline bool rec_key_eq(const SRec& a, const SRec& b, const uint8_t* const* tails) {
     if (a.hi != b.hi || a.lo != b.lo || a.meta != b.meta) return false;
-    return key_len(a.meta) <= 17 || tail_cmp(tails[a.idx], key_len(a.meta), tails[b.idx], key_len(b.meta)) == 0;
+    return key_len(a.meta) <= 17 || tail_cmp(rec_tail(a, tails), key_len(a.meta), rec_tail(b, tails), key_len(b.meta)) == 0;
 }
 
 // rounds mode, two kinds of lanes:
@@ -2712,7 +2736,7 @@ __global__ __launch_bounds__(256) void k_read_check_list(ReadCheckArgs RA, const
 // between its two search results.  Workgroups take MS_CHUNK merged positions
 // (merge-path cuts, the two pieces staged in LDS), lanes MS_ITEMS each.
 __device__ inline bool rd_before_wr(const SRec& r, const SRec& w, const uint8_t* const* tails) {
-    return rec_vs_key(r, Key{w.hi, w.lo, w.meta, tails[w.idx]}, tails) <= 0;  // key(r) <= key(w)
+    return rec_vs_key(r, Key{w.hi, w.lo, w.meta, rec_tail(w, tails)}, tails) <= 0;  // key(r) <= key(w)
 }
 
 __global__ __launch_bounds__(MS_THREADS) void k_edges_merge(EdgesArgs A) {
