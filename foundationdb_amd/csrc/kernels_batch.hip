@@ -1263,7 +1263,7 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
                 x[q] = row[e];
                 s_r4[2 * e] = make_uint4((uint32_t)x[q].hi, (uint32_t)(x[q].hi >> 32), (uint32_t)x[q].lo,
                                          (uint32_t)(x[q].lo >> 32));
-                s_r4[2 * e + 1] = make_uint4(x[q].meta, x[q].idx, 0, 0);
+                s_r4[2 * e + 1] = make_uint4(x[q].meta, x[q].idx, (uint32_t)x[q].pad, (uint32_t)(x[q].pad >> 32));
             }
         }
         // Long-key buckets (config 4: a 64-byte tenant prefix): when every
@@ -1283,13 +1283,19 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
                 same &= (x[q].hi == h0) & (x[q].lo == l0) & ((x[q].meta >> 24) == (m0 >> 24)) &
                         (key_len(x[q].meta) > 17);
         const bool longb = c > 1 && key_len(m0) > 17 && __ballot(!same) == 0;  // (wave-uniform)
+        // (LW ranked words: 32 bytes past the shared ones, so that a point
+        // write's k and k\x00 -- equal words, zero-padded -- are told apart by
+        // their lengths for keys up to 32 bytes past W, not by a full compare)
+        constexpr int LW = 4;
         uint64_t* s_t = s_buf + 4 * (SS_WAVE + 8);  // (after the records' 2 uint4 each, read 8 past c)
-        static_assert(4 * (SS_WAVE + 8) + 2 * (SS_WAVE + 8) <= 3 * SS_ROW, "long-key staging");
-        uint64_t xt[2][2] = {{0, 0}, {0, 0}};
-        uint32_t lim = 0;  // keys up to this long end inside the ranked 16 bytes
+        static_assert(4 * (SS_WAVE + 8) + LW * (SS_WAVE + 8) <= 3 * SS_ROW, "long-key staging");
+        uint64_t xt[2][LW] = {};
+        uint32_t lim = 0;  // keys up to this long end inside the ranked words
         if (longb) {
             auto tail_words = [](uint32_t meta) { return (key_len(meta) - 17 + 7) >> 3; };
-            const uint64_t* t0 = reinterpret_cast<const uint64_t*>(tails[i0]);
+            const uint64_t pd0 = __shfl(x[0].pad, 0);  // (record 0's tail: its scatter's pointer, or the key arrays')
+            const uint64_t* t0 = reinterpret_cast<const uint64_t*>(pd0 ? reinterpret_cast<const uint8_t*>(pd0)
+                                                                         : tails[i0]);
             const uint32_t n0 = tail_words(m0);
             uint32_t wmin = 0xFFFFFFFFu;
 #pragma unroll
@@ -1319,17 +1325,18 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
                 wmin = min(wmin, min(w, nm));
             }
             const uint32_t W = wave_reduce_min(wmin);
-            lim = 17 + 8 * (W + 2);
+            lim = 17 + 8 * (W + LW);
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 const int e = lane + 64 * q;
                 if (e >= c) continue;
                 const uint64_t* t = reinterpret_cast<const uint64_t*>(rec_tail(x[q], tails));
                 const uint32_t n = tail_words(x[q].meta);
-                xt[q][0] = W < n ? __builtin_bswap64(t[W]) : 0;
-                xt[q][1] = W + 1 < n ? __builtin_bswap64(t[W + 1]) : 0;
-                s_t[2 * e] = xt[q][0];
-                s_t[2 * e + 1] = xt[q][1];
+#pragma unroll
+                for (int k = 0; k < LW; k++) {
+                    xt[q][k] = W + k < n ? __builtin_bswap64(t[W + k]) : 0;
+                    s_t[LW * e + k] = xt[q][k];
+                }
             }
         }
         const int64_t c2 = PCLK();
@@ -1339,9 +1346,10 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
         // they tie and a key runs past them -- resolved after the loop, every
         // lane's ties at once, instead of a wave-wide stall on each record a
         // lane ties with: a point write's begin k and end k\x00 always do)
-        auto long_cmp = [&](uint64_t a0, uint64_t a1, const SRec& a, uint64_t b0, uint64_t b1, const SRec& bb) {
-            if (a0 != b0) return a0 < b0 ? -1 : 1;
-            if (a1 != b1) return a1 < b1 ? -1 : 1;
+        auto long_cmp = [&](const uint64_t* aw, const SRec& a, const uint64_t* bw, const SRec& bb) {
+#pragma unroll
+            for (int k = 0; k < LW; k++)
+                if (aw[k] != bw[k]) return aw[k] < bw[k] ? -1 : 1;
             const uint32_t la = key_len(a.meta), lb = key_len(bb.meta);
             if (la > lim || lb > lim) return 0;
             if (la != lb) return la < lb ? -1 : 1;
@@ -1351,7 +1359,8 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
         int rank[2] = {0, 0}, dsum[2] = {0, 0};
         auto rec_at = [&](int j) {
             const uint4 a = s_r4[2 * j], m = s_r4[2 * j + 1];
-            return SRec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), m.x, m.y, 0};
+            return SRec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), m.x, m.y,
+                        (uint64_t)m.z | ((uint64_t)m.w << 32)};  // (with the tail pointer: rec_tail)
         };
         if (!longb) {
             for (int j0 = 0; j0 < c; j0 += 8) {  // eight records per round: their LDS reads overlap
@@ -1371,23 +1380,24 @@ __device__ void ss_bucket_wave(const SortJobs& J, const KeyArrays& keys, int bid
         } else {
             constexpr int NPEND = 4;
             int pend[2][NPEND], np[2] = {0, 0};
-            for (int j0 = 0; j0 < c; j0 += 8) {
-                SRec y[8];
-                uint64_t yt[8][2];
+            constexpr int YU = 16 / LW;  // records per round (8 of 4 words each: 193 VGPRs)
+            for (int j0 = 0; j0 < c; j0 += YU) {
+                SRec y[YU];
+                uint64_t yt[YU][LW];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < YU; u++) {
                     y[u] = rec_at(j0 + u);
-                    yt[u][0] = s_t[2 * (j0 + u)];
-                    yt[u][1] = s_t[2 * (j0 + u) + 1];
+#pragma unroll
+                    for (int k = 0; k < LW; k++) yt[u][k] = s_t[LW * (j0 + u) + k];
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++)
+                for (int u = 0; u < YU; u++)
                     if (j0 + u < c)
 #pragma unroll
                         for (int q = 0; q < 2; q++) {
                             bool lt = false;
                             if (lane + 64 * q < c) {
-                                const int r = long_cmp(yt[u][0], yt[u][1], y[u], xt[q][0], xt[q][1], x[q]);
+                                const int r = long_cmp(yt[u], y[u], xt[q], x[q]);
                                 if (r == 0 && np[q] < NPEND) pend[q][np[q]++] = j0 + u;
                                 else lt = r == 0 ? rec_lt(y[u], x[q], tails) : r < 0;
                             }
