@@ -378,7 +378,14 @@ __device__ inline void put_quantile(const SortJobs& J, int job, int q, const SRe
         const int words = (int)min<uint32_t>((L - 17 + 7) / 8, SS_QT / 8);
         const uint64_t* src = reinterpret_cast<const uint64_t*>(rec_tail(x, tails));
         uint64_t* dst = reinterpret_cast<uint64_t*>(J.qtail + (int64_t)(job * SS_Q + q) * SS_QT);
-        for (int w = 0; w < words; w++) dst[w] = src[w];
+        // (every word loaded before any store: a store between them would
+        // keep the next load behind it, a round trip a word)
+        uint64_t v[SS_QT / 8];
+#pragma unroll
+        for (int w = 0; w < SS_QT / 8; w++) v[w] = w < words ? src[w] : 0;
+#pragma unroll
+        for (int w = 0; w < SS_QT / 8; w++)
+            if (w < words) dst[w] = v[w];
     }
 }
 
