@@ -643,6 +643,7 @@ constexpr int SAT_NONE = -(1 << 28);
 
 // 2a.  Returns false (nothing written) if the new entries do not fit to the
 // right of their insertion points; S.er / S.ins then still hold step 1's marks.
+template <bool PX>
 __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S, int a, int p, int pg, int C, const HoleMask& hm,
                                int jlo, int jhi, const RangePlan& r0, bool has0, int doff, int nn) {
     const int lane = threadIdx.x & 63;
@@ -697,7 +698,9 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
     uint32_t ometa[4];
     int64_t over[4];
     const uint8_t* otail[4];
-    const int pskip = FDBCS_DIR_PX && A.px ? A.pool.pskip[pg] : 0;  // (<= 0: no prefix words to keep)
+    // (<= 0: no prefix words to keep; PX false -- no long key yet -- compiles the
+    // prefix-word moves out, so the plain path carries none of their registers)
+    const int pskip = FDBCS_DIR_PX && PX ? A.pool.pskip[pg] : 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if (!((movem >> q) & 1)) continue;
@@ -786,7 +789,7 @@ __device__ __forceinline__ bool merge_in_place(const MergeArgs& A, WaveMerge& S,
 #ifndef FDBCS_PM_REWRITE_AT  // (A/B: pages receiving this many new boundaries are rewritten, not shifted in place)
 #define FDBCS_PM_REWRITE_AT (PAGE + 1)
 #endif
-template <bool INPLACE, bool UNIFIED = false>
+template <bool INPLACE, bool UNIFIED = false, bool PX = true>
 __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top0) {
     Scalars* sc = A.sc;
     const int lane = threadIdx.x & 63;
@@ -837,7 +840,7 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
     wave_lds_sync();
     if (INPLACE) {
         if (parts == 1 && !__ballot(erases) && nn < FDBCS_PM_REWRITE_AT &&
-            merge_in_place(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
+            merge_in_place<PX>(A, S, a, p, pg, cntp, hm, jlo, jhi, r0, has0, doff, nn))
             return;
         if (!UNIFIED) {
             if (lane == 0) A.full_list[atomicAdd(&sc->n_full, 1)] = a;
@@ -984,6 +987,10 @@ __device__ void merge_page_wave(const MergeArgs& A, WaveMerge& S, int a, int top
 #ifndef FDBCS_PM_UNIFIED
 #define FDBCS_PM_UNIFIED 1
 #endif
+// PX: HistBufs::px_host (pages may hold prefix skips).  Two instantiations so
+// that short-key histories (configs 2, 3, 5) never pay the long-key path's
+// registers (its spill showed up as page-merge writes).
+template <bool PX>
 __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A) {
     __shared__ WaveMerge S[MW_WAVES];
     Scalars* sc = A.sc;
@@ -992,7 +999,7 @@ __global__ __launch_bounds__(256, FDBCS_PM_WAVES) void k_page_merge(MergeArgs A)
     const int top0 = sc->free_top;
     const int w = threadIdx.x >> 6;
     for (int a = blockIdx.x * MW_WAVES + w; a < naff; a += gridDim.x * MW_WAVES)
-        merge_page_wave<true, FDBCS_PM_UNIFIED != 0>(A, S[w], a, top0);
+        merge_page_wave<true, FDBCS_PM_UNIFIED != 0, PX>(A, S[w], a, top0);
 }
 
 __global__ __launch_bounds__(256, 2) void k_page_merge_full(MergeArgs A) {
@@ -1449,7 +1456,10 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
         A.px = h.px_host ? 1 : 0;
         A.full_list = b.full_list;
         const int grid = std::max(1, std::min(GRID_PAGES, cdiv(max_aff, MW_WAVES)));
-        hipLaunchKernelGGL(k_page_merge, dim3(grid), dim3(256), 0, s, A);
+        if (A.px)
+            hipLaunchKernelGGL(k_page_merge<true>, dim3(grid), dim3(256), 0, s, A);
+        else
+            hipLaunchKernelGGL(k_page_merge<false>, dim3(grid), dim3(256), 0, s, A);
         if (!FDBCS_PM_UNIFIED) hipLaunchKernelGGL(k_page_merge_full, dim3(std::min(grid, 1024)), dim3(256), 0, s, A);
     }
     launch_bmax_commit(h, cur ^ 1, sc, s, end_of_batch, b.freed_list);
