@@ -137,6 +137,7 @@ FDBCS_FUNCS = [
     ("fdbcs_sharded_batch_detect", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_sharded_detect_device", C.c_int, [C.c_void_p, C.POINTER(BatchView), C.c_int64, C.c_int64, C.c_void_p]),
     ("fdbcs_sharded_set_protocol", C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    ("fdbcs_sharded_exchange_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_sharded_local", C.c_void_p, [C.c_void_p]),
     ("fdbcs_sharded_removal_key_owner", C.c_int32, [C.c_void_p]),
     ("fdbcs_sharded_header_version", C.c_int64, [C.c_void_p]),

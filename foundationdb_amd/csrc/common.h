@@ -377,6 +377,8 @@ struct Scalars {
     // protocol B's edge exchange at a fixed capacity (k_sh_edges_cat_fixed):
     // the largest shard count when some shard's did not fit (0: they did)
     int32_t sh_need;
+    int32_t sh_max;         // every batch: the largest shard count (the host's capacity decay)
+    int32_t sh_pad;
     int32_t px_on;          // some key longer than 17 bytes was ingested or loaded (sticky): k_dir_px runs
     int32_t n_pxd[2];       // rewritten pages listed for k_page_px (pskip < 0), by launch parity
     int64_t ph[32];         // phase timestamps (wall_clock64 ticks) in FDBCS_PHASES builds

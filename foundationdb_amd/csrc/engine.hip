@@ -244,7 +244,9 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
         (r = dalloc(h.pool.px, slots)) || (r = dalloc(h.pool.pxidx, slots / PIDX_STRIDE)) ||
         (r = dalloc(h.pool.pskip, pages)) || (r = dalloc(h.px_list, (int64_t)pages + 1)))
         return r;
-    HIPOK(hipMemset(h.pool.pskip, 0, (size_t)pages * sizeof(int32_t)));
+    // (on the engine's non-blocking stream: a null-stream memset is not
+    // ordered against grow_pool's copies and k_dir_px / k_page_px behind it)
+    HIPOK(hipMemsetAsync(h.pool.pskip, 0, (size_t)pages * sizeof(int32_t), cs->stream));
     h.cap_dir = pages + 1;
     for (int d = 0; d < 2; d++) {
         Dir& x = h.dir[d];
@@ -257,7 +259,7 @@ int alloc_pool(fdbcs* cs, int32_t pages) {
             (r = dalloc(x.spx, sidx_off(h.cap_dir, SIDX_LEVELS + 1))) ||
             (r = dalloc(x.wsk, wsk_off(h.cap_dir, SIDX_LEVELS + 1))))
             return r;
-        HIPOK(hipMemset(x.wsk, 0, wsk_off(h.cap_dir, SIDX_LEVELS + 1) * sizeof(int32_t)));
+        HIPOK(hipMemsetAsync(x.wsk, 0, wsk_off(h.cap_dir, SIDX_LEVELS + 1) * sizeof(int32_t), cs->stream));
         x.cap = h.cap_dir;
     }
     return FDBCS_OK;
@@ -897,7 +899,7 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
 // update behind them) and check the scalar snapshot taken with them: err =
 // this batch's stages so far, last_err = the previous batch's history update
 // (so a failed update is reported by the next detectConflicts).
-int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nullptr) {
+int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nullptr, int64_t* sh_max = nullptr) {
     int r;
     if (cs->early_mapped) {
         // poll the flag the decision kernel sets after its verdicts (no copy,
@@ -916,6 +918,7 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nul
         if (err[0]) return err[0];
         if (err[1]) return err[1];
         if (lm_count) *lm_count = (int64_t)reinterpret_cast<const uint32_t*>(cs->vmap)[3];
+        if (sh_max) *sh_max = (int64_t)reinterpret_cast<const uint32_t*>(cs->vmap)[4];
         if (T) memcpy(verdict, cs->vmap + 64, (size_t)T);
         return FDBCS_OK;
     }
@@ -924,6 +927,7 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nul
     if (snap->err) return snap->err;
     if (snap->last_err) return snap->last_err;
     if (lm_count) *lm_count = snap->lm_count;
+    if (sh_max) *sh_max = snap->sh_max;
     if (T) memcpy(verdict, cs->vpin, (size_t)T);
     return FDBCS_OK;
 }
@@ -2142,7 +2146,18 @@ struct fdbcs_sharded {
     int32_t* ebuf = nullptr;               // device: [send 2M | recv G x 2M | readers E | writers E]
     int64_t ebuf_cap = 0;                  // (int32 elements)
     int64_t ecap = 4096;                   // edge pairs per shard in the exchange (grows on a short batch)
+    int64_t ecap0 = 4096;                  // the floor it decays back to (FDBCS_TEST_SH_ECAP in tests)
     int64_t retries = 0;                   // batches whose exchange was short and ran again (stats)
+    // (one burst used to raise every later batch's all-gather for
+    // good) the largest shard count of each of the last ECAP_WINDOW batches,
+    // which every rank reads from its own verdicts -- the same values on
+    // every rank, so every rank resizes at the same batch
+    static constexpr int ECAP_WINDOW_MAX = 64;
+    int ecap_window = 32;
+    int64_t need_ring[ECAP_WINDOW_MAX] = {};
+    int64_t need_seen = 0;                 // batches recorded since the last resize
+    int64_t last_max = 0;                  // the last batch's largest shard count (stats)
+    int64_t shrinks = 0;                   // (stats)
     std::atomic<bool> aborted{false};      // fdbcs_sharded_abort (any thread)
     // The communicator is touched by the rank's own thread (init, enqueues,
     // progress polls) and by fdbcs_sharded_abort from another one: every use
@@ -2303,6 +2318,30 @@ int sh_exchange_b(fdbcs_sharded* sh, const fdbcs_batch_view& v, size_t slots, ui
     return FDBCS_OK;
 }
 
+// Protocol B's exchange capacity follows the recent batches down again: once
+// a whole window of batches (sh->ecap_window, each recorded after its
+// verdicts) needed at most half of it, it drops to that need plus a quarter
+// and min(1024, ecap0) (never below ecap0), and the exchange
+// buffer is released so that it is sized again for the new capacity.
+void sh_ecap_decay(fdbcs_sharded* sh) {
+    sh->need_ring[sh->need_seen % sh->ecap_window] = sh->last_max;
+    if (++sh->need_seen < sh->ecap_window || sh->ecap <= sh->ecap0) return;
+    int64_t mx = 0;
+    for (int i = 0; i < sh->ecap_window; i++) mx = std::max(mx, sh->need_ring[i]);
+    const int64_t target = std::max(sh->ecap0, mx + mx / 4 + std::min<int64_t>(1024, sh->ecap0));
+    if (2 * target > sh->ecap) return;
+    GROWLOG("sharded edge exchange capacity %lld -> %lld\n", (long long)sh->ecap, (long long)target);
+    sh->ecap = target;
+    sh->shrinks++;
+    sh->need_seen = 0;
+    if (sh->ebuf) {  // (the last batch's exchange may still read it)
+        (void)hipStreamSynchronize(sh->cs->stream);
+        hipFree(sh->ebuf);
+        sh->ebuf = nullptr;
+        sh->ebuf_cap = 0;
+    }
+}
+
 // one batch of the sharded resolver on the device-resident view v
 int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
     sh->cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
@@ -2405,7 +2444,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     launch_sh_slot_out(sc, reinterpret_cast<int64_t*>(sh->x1), sh->rank, sh->world, s);
     // the one wait: the verdicts
     if (!T) return FDBCS_OK;
-    r = verdict_wait(cs, T, verdict);
+    r = verdict_wait(cs, T, verdict, nullptr, &sh->last_max);
     if (r != E_SH_RETRY) {
         if (r) return r;
         break;
@@ -2416,22 +2455,27 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     // is copied to the other buffer, k_sh_plan opens no window).  Grow the
     // capacity, search the edges again (the gathered list overwrote this
     // shard's own), and run the batch from exchange 1 on once more.
+    // (an error exit restores oldestVersion: the device skipped this
+    // attempt's compaction.  Every rank sees the same gathered counts, so the
+    // attempt limit is reached on all of them alike.)
+    cs->oldest = oldest0;
     if (attempt >= 4) return FDBCS_E_CAPACITY;
     if ((r = sync_state(cs))) return r;
     const int64_t need = cs->sc_host->sh_need;
     sh->retries++;
     GROWLOG("sharded edge exchange short: need %lld, capacity %lld\n", (long long)need, (long long)sh->ecap);
     sh->ecap = std::max<int64_t>(2 * sh->ecap, need + need / 4 + 1024);
-    cs->oldest = oldest0;
     HIPOK(hipMemsetAsync(&sc->err, 0, sizeof(int32_t), s));
     HIPOK(hipMemsetAsync(&sc->last_err, 0, sizeof(int32_t), s));
     HIPOK(hipMemsetAsync(&sc->sh_need, 0, sizeof(int32_t), s));
+    sh->need_seen = 0;  // (the decay window restarts at a growth)
     const int64_t cap = std::max<int64_t>(need + need / 4 + 1024, sh->ecap * sh->world);
     if (cap > b.edge_cap && (r = grow_edges(b, cap))) return r;
     if (T) HIPOK(hipMemsetAsync(b.deg, 0, (size_t)T * sizeof(int32_t), s));
     HIPOK(hipMemsetAsync(&sc->edges_total, 0, sizeof(int32_t), s));
     launch_edges_read_check(v, b, cs->h, cs->cur, sc, sh->v0, s);
     }
+    if (sh->proto == FDBCS_PROTOCOL_B) sh_ecap_decay(sh);
     cs->last_dv = v;
     cs->have_last_dv = true;
     return FDBCS_OK;
@@ -2463,7 +2507,9 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
     sh->rank = rank;
     sh->world = world;
     sh->v0 = v0;
-    if (const char* e = getenv("FDBCS_TEST_SH_ECAP")) sh->ecap = std::max(1, atoi(e));  // (tests: short exchanges)
+    if (const char* e = getenv("FDBCS_TEST_SH_ECAP")) sh->ecap = sh->ecap0 = std::max(1, atoi(e));  // (tests: short exchanges)
+    if (const char* e = getenv("FDBCS_SH_ECAP_WINDOW"))
+        sh->ecap_window = std::min(fdbcs_sharded::ECAP_WINDOW_MAX, std::max(1, atoi(e)));
     auto fail = [&](int code) {
         fdbcs_sharded_destroy(sh);
         return code;
@@ -2588,6 +2634,14 @@ int fdbcs_sharded_batch_begin(fdbcs_sharded* sh) {
     return FDBCS_OK;
 }
 
+int fdbcs_sharded_exchange_stats(const fdbcs_sharded* sh, int64_t* out, int cap) {
+    if (!sh || !out || cap < 0) return FDBCS_E_ARG;
+    const int64_t v[5] = {sh->ecap, sh->retries, sh->last_max, sh->shrinks, sh->ebuf_cap};
+    const int n = std::min(cap, 5);
+    for (int i = 0; i < n; i++) out[i] = v[i];
+    return n;
+}
+
 int fdbcs_sharded_set_protocol(fdbcs_sharded* sh, int protocol, int flags) {
     if (!sh || sh->in_batch || (protocol != FDBCS_PROTOCOL_A && protocol != FDBCS_PROTOCOL_B) ||
         (flags & ~FDBCS_SHARD_PRESPLIT))
@@ -2632,7 +2686,6 @@ int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbc
         return (!sh->has_lo || keycmp(x.end, x.end_len, lo, ll) > 0) &&
                (!sh->has_hi || keycmp(x.begin, x.begin_len, hi, hl) < 0);
     };
-    if (sh->lm_host) sh_roll_host(sh, reads, nreads, writes, nwrites);
     std::vector<fdbcs_range>& k = sh->keep;
     k.clear();
     for (int32_t i = 0; i < nreads; i++)
@@ -2643,7 +2696,11 @@ int fdbcs_sharded_batch_add(fdbcs_sharded* sh, int64_t read_snapshot, const fdbc
             k.push_back(writes[i]);
     // (a read dropped here still makes the transaction tooOld-capable: the
     // shard holding it reports the flag, and the MAX picks it)
-    return fdbcs_batch_add(sh->cs, read_snapshot, k.data(), kr, k.data() + kr, (int32_t)k.size() - kr);
+    const int r = fdbcs_batch_add(sh->cs, read_snapshot, k.data(), kr, k.data() + kr, (int32_t)k.size() - kr);
+    // the whole transaction to the attached sample, only once it was taken
+    // (as under A: a refused one uses no sample positions)
+    if (r == FDBCS_OK && sh->lm_host) sh_roll_host(sh, reads, nreads, writes, nwrites);
+    return r;
 }
 
 int fdbcs_sharded_batch_skip(fdbcs_sharded* sh, int32_t n) {

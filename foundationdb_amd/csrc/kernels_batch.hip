@@ -3083,11 +3083,12 @@ __global__ __launch_bounds__(DC_THREADS) void k_decide_rounds(RoundArgs A) {
     PHASE(sc, 0);
     // (the flag's error words, final before this launch: loaded now, off the
     // way from the verdicts to the flag)
-    uint32_t eo_err = 0, eo_last = 0, eo_lm = 0;
+    uint32_t eo_err = 0, eo_last = 0, eo_lm = 0, eo_shmax = 0;
     if (A.eo.flag && tid == 0) {
         eo_err = (uint32_t)sc->err;
         eo_last = (uint32_t)sc->last_err;
         eo_lm = (uint32_t)sc->lm_count;  // (the ingest's load-metrics entries, if a sample is attached)
+        eo_shmax = (uint32_t)sc->sh_max;  // (protocol B: the largest shard edge count, identical on every rank)
     }
 
     // ---- U: 4 transactions per lane from one 4-byte load of each flag array ----
@@ -3300,6 +3301,7 @@ decided:
             A.eo.flag[1] = eo_err;
             A.eo.flag[2] = eo_last;
             A.eo.flag[3] = eo_lm;
+            A.eo.flag[4] = eo_shmax;
         }
         __threadfence_system();
         __syncthreads();

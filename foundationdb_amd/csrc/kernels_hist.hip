@@ -1995,6 +1995,7 @@ __global__ __launch_bounds__(1024) void k_sh_edges_cat_fixed(const int32_t* __re
     }
     if (threadIdx.x == 0) {
         sc->edges_total = (int32_t)off;
+        sc->sh_max = (int32_t)min<int64_t>(mx, INT32_MAX);
         if (mx > M || ovf) {
             sc->sh_need = (int32_t)min<int64_t>(mx, INT32_MAX);
             atomicCAS(&sc->err, 0, E_SH_RETRY);

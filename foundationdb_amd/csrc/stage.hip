@@ -366,6 +366,14 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
     bool go_live = false;
+    // (the detect sizes nothing anew for a live batch: run_batch refuses one
+    // whose stream or key bytes outgrew what live_begin sized its buffers
+    // for.  live_check keeps every add within the capacities and the bound
+    // counts every publish's padding, so this cannot trip; should it, the
+    // batch falls back to the whole-stream ingest here instead -- ADVICE r05)
+    if (live_ && !live_broken_ &&
+        std::max<uint64_t>(used_ + 144, key_total()) > std::max<uint64_t>(lcaps_.key_bytes, live_stream_bound(lcaps_)))
+        live_cancel();
     if (live_ && !live_broken_ && staged && pad_published()) {
         // the final word: the kernel finishes the last groups and leaves
         prog_[3] = (uint64_t)T_;

@@ -701,6 +701,15 @@ class ShardedResolver:
     def clear(self, v):
         check(self._lib.fdbcs_sharded_clear(self._h, v), "clearConflictSet")
 
+    EXCHANGE_STATS = ("ecap", "retries", "last_max", "shrinks", "ebuf_elems")
+
+    def exchange_stats(self):
+        """Protocol B's edge exchange (fdbcs_sharded_exchange_stats)."""
+        import ctypes as C
+        out = (C.c_int64 * len(self.EXCHANGE_STATS))()
+        n = check(self._lib.fdbcs_sharded_exchange_stats(self._h, out, len(out)), "fdbcs_sharded_exchange_stats")
+        return dict(zip(self.EXCHANGE_STATS[:n], out[:n]))
+
     def removal_key_owner(self):
         r = self._lib.fdbcs_sharded_removal_key_owner(self._h)
         if r < -1:

@@ -68,13 +68,24 @@ struct ConflictSet {
 
 namespace {
 
-// ASSERT -> internal_error in the reference (flow/Error.h:86); the resolver
-// role dies on it.  The shim throws so that the caller's error path runs.
+// ASSERT -> internal_error() in the reference (flow/Error.h:86-90, code
+// 4100 in flow/error_definitions.h:201); the resolver role dies on it and its
+// trace names that code.  Inside fdbserver, ConflictSet.h's includes
+// (fdbclient/CommitTransaction.h -> flow) define the internal_error() macro,
+// so the shim throws the reference's own Error; a non-Error exception would
+// reach the actor wrappers as unknown_error.  The stand-alone test build
+// (tests/shim/stub, no flow) throws std::runtime_error instead.
+[[noreturn]] void fail_internal(const std::string& msg) {
+    fprintf(stderr, "fdbcs: %s\n", msg.c_str());
+#ifdef internal_error
+    throw internal_error();
+#else
+    throw std::runtime_error(msg);
+#endif
+}
+
 void ok_or_throw(int status, const char* what) {
-    if (status != FDBCS_OK) {
-        fprintf(stderr, "fdbcs: %s failed: %s\n", what, fdbcs_strerror(status));
-        throw std::runtime_error(fdbcs_strerror(status));
-    }
+    if (status != FDBCS_OK) fail_internal(std::string(what) + " failed: " + fdbcs_strerror(status));
 }
 
 fdbcs_range to_range(const KeyRangeRef& r) {
@@ -112,7 +123,7 @@ struct ChunkLog {
     // k contiguous free entries (k <= CH), moving to the next chunk if needed
     X* reserve(size_t k) {
         if (n % CH + k > CH) n = (n / CH + 1) * CH;
-        if (n / CH >= MAXCH) throw std::runtime_error("fdbcs: batch too large for the shim's log");
+        if (n / CH >= MAXCH) fail_internal("fdbcs: batch too large for the shim's log");
         std::unique_ptr<X[]>& c = ch[n / CH];
         if (!c) c.reset(new X[CH]);
         X* p = &c[n % CH];
@@ -335,9 +346,9 @@ std::vector<uint8_t> from_hex(const std::string& h) {
         if (c >= '0' && c <= '9') return c - '0';
         if (c >= 'a' && c <= 'f') return c - 'a' + 10;
         if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-        throw std::runtime_error("FDBCS_SHARD_BOUNDS: '" + h + "' is not hex");
+        fail_internal("FDBCS_SHARD_BOUNDS: '" + h + "' is not hex");
     };
-    if (h.size() % 2) throw std::runtime_error("FDBCS_SHARD_BOUNDS: '" + h + "' has an odd number of hex digits");
+    if (h.size() % 2) fail_internal("FDBCS_SHARD_BOUNDS: '" + h + "' has an odd number of hex digits");
     std::vector<uint8_t> out;
     for (size_t i = 0; i < h.size(); i += 2) out.push_back((uint8_t)(nib(h[i]) << 4 | nib(h[i + 1])));
     return out;
@@ -385,7 +396,7 @@ MultiGpu* make_multi(int G) {
     if (const char* p = getenv("FDBCS_SHARD_PROTOCOL")) {
         if (!strcmp(p, "a")) mg->proto = FDBCS_PROTOCOL_A;
         else if (!strcmp(p, "b")) mg->proto = FDBCS_PROTOCOL_B;
-        else throw std::runtime_error("FDBCS_SHARD_PROTOCOL: a or b");
+        else fail_internal("FDBCS_SHARD_PROTOCOL: a or b");
     }
     // split keys: G-1, strictly increasing (the header's requirement)
     std::vector<std::vector<uint8_t>> bounds;
@@ -397,10 +408,10 @@ MultiGpu* make_multi(int G) {
             bounds.push_back({(uint8_t)(v >> 8), (uint8_t)v});
         }
     }
-    if ((int)bounds.size() != G - 1) throw std::runtime_error("FDBCS_SHARD_BOUNDS: need G-1 keys");
+    if ((int)bounds.size() != G - 1) fail_internal("FDBCS_SHARD_BOUNDS: need G-1 keys");
     for (int g = 1; g + 1 < G; g++)
         if (keycmp(bounds[g - 1].data(), (uint32_t)bounds[g - 1].size(), bounds[g].data(), (uint32_t)bounds[g].size()) >= 0)
-            throw std::runtime_error("FDBCS_SHARD_BOUNDS: split keys must increase strictly");
+            fail_internal("FDBCS_SHARD_BOUNDS: split keys must increase strictly");
     std::vector<uint8_t> bb;
     std::vector<uint64_t> bo;
     std::vector<uint32_t> bl;
@@ -452,7 +463,7 @@ int shard_count() {
 }
 
 MultiGpu* usable(MultiGpu* mg) {
-    if (mg->broken) throw std::runtime_error("fdbcs: a shard failed earlier; the conflict set is unusable");
+    if (mg->broken) fail_internal("fdbcs: a shard failed earlier; the conflict set is unusable");
     return mg;
 }
 
@@ -577,7 +588,7 @@ void ConflictBatch::detectConflicts(Version now, Version newOldestVersion, vecto
     cs->verdict.assign((size_t)transactionCount, 0);
     if (MultiGpu* mg = cs->multi) {
         usable(mg);
-        if (!mg->open) throw std::runtime_error("fdbcs: detectConflicts without an open ConflictBatch");
+        if (!mg->open) fail_internal("fdbcs: detectConflicts without an open ConflictBatch");
         mg->now = now;
         mg->new_oldest = newOldestVersion;
         mg->closed.store(true, std::memory_order_release);  // (now / new_oldest published with it)

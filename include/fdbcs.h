@@ -504,9 +504,11 @@ int  fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_
  * shard-local instead of growing with the whole batch.  Transactions keep
  * their global batch indices (a rank with none of a transaction's ranges
  * still counts it).  Exchange 1 also carries each rank's overlap-edge count;
- * the host reads the counts (mapped memory) to size one all-gather of the
- * edge lists, skipped when no rank has any, and every rank runs the
- * identical ordered decision over their union.  Flags: FDBCS_SHARD_PRESPLIT
+ * one all-gather of a fixed capacity of edge pairs per rank follows with no
+ * host read in between (a batch whose lists do not fit runs from exchange 1
+ * again with a larger capacity; the capacity decays back once a window of
+ * batches needed at most half of it), and every rank runs the identical
+ * ordered decision over their union.  Flags: FDBCS_SHARD_PRESPLIT
  * = the caller's adds already carry only this rank's ranges (the proxy's
  * per-resolver split, fdbcs_split_batch_keep_all); without it
  * fdbcs_sharded_batch_add drops the others itself (after checking every
@@ -520,6 +522,12 @@ int  fdbcs_sharded_detect_device(fdbcs_sharded* sh, const fdbcs_batch_view* dev_
 #define FDBCS_PROTOCOL_B     1
 #define FDBCS_SHARD_PRESPLIT 1
 int  fdbcs_sharded_set_protocol(fdbcs_sharded* sh, int protocol, int flags);
+/* Protocol B's edge exchange (no reference counterpart: instrumentation of
+ * the sharded mode): [0] edge pairs per rank the all-gather carries now
+ * [1] batches whose exchange was short and ran again [2] the last batch's
+ * largest rank edge count [3] times the capacity decayed [4] the exchange
+ * buffer's int32 elements.  Returns the count written. */
+int  fdbcs_sharded_exchange_stats(const fdbcs_sharded* sh, int64_t* out, int cap);
 /* This rank's engine: its part of the history (fdbcs_dump_history,
  * fdbcs_history_size); the owner's fdbcs_removal_key is removalKey. */
 fdbcs* fdbcs_sharded_local(fdbcs_sharded* sh);

@@ -182,6 +182,88 @@ def test_sharded_abi_protocol_b_short_exchange(gpu, world, kind):
     test_sharded_abi_equals_one_conflict_set(gpu, world, kind, "b", sh_ecap=2)
 
 
+def _burst_stream(seed):
+    """One batch dense with overlapping ranges (hundreds of overlap edges per
+    shard), then sparse point batches over a wide key space (almost none)."""
+    from gen import PackedBatch
+    rng = random.Random(seed)
+    now = 1000
+    for i in range(24):
+        now += 100
+        txns = []
+        n, space, wide = (600, 400, 0.5) if i == 1 else (60, 200000, 0.0)
+        for _t in range(n):
+            def rr():
+                a = rng.randrange(space)
+                b = min(space, a + rng.randint(1, space // 4)) if rng.random() < wide else a + 1
+                return (b"k%07d" % a, b"k%07d" % b)
+            txns.append((now - rng.randint(1, 90), [rr() for _ in range(3)], [rr() for _ in range(2)]))
+        yield PackedBatch.from_txns(txns), now, now - 500
+
+
+def _burst_rank(rank, world, port, bounds, q):
+    os.environ["FDBCS_TEST_SH_ECAP"] = "64"
+    os.environ["FDBCS_SH_ECAP_WINDOW"] = "4"
+    import torch
+    import torch.distributed as dist
+
+    from foundationdb_amd.sharded import ShardedResolver
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        sh = ShardedResolver(bounds, rank, world, device=0, protocol="b")
+        out = []
+        for i, (batch, now, nold) in enumerate(_burst_stream(5)):
+            v = sh.detect_txns(batch.txns(), now, nold) if i % 2 else sh.detect_packed(batch, now, nold)
+            out.append((v.tolist(), sh.history(), sh.exchange_stats()))
+        sh.close()
+        q.put((rank, out))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_abi_protocol_b_exchange_decays_after_burst(gpu):
+    """protocol B's edge exchange capacity grows on a
+    burst batch and returns to its floor once a window of batches (4 here)
+    needed at most half of it, on every rank at the same batch -- so one
+    burst no longer raises every later batch's all-gather.  Verdicts and
+    histories as one conflict set's after every batch."""
+    world = 2
+    bounds = [b"k0000200"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + random.Random(os.getpid() * 19 + 3).randint(0, 3000)
+    procs = [ctx.Process(target=_burst_rank, args=(r, world, port, bounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(got[r], str), f"rank {r}: {got[r]}"
+    c = CpuSpec()
+    for i, (batch, now, nold) in enumerate(_burst_stream(5)):
+        vc = c.detect_packed(batch, now, nold).tolist()
+        hist = []
+        for r in range(world):
+            v, h, _st = got[r][i]
+            assert v == vc, (i, r)
+            hist += h
+        assert hist == c.history(), i
+        assert got[0][i][2]["ecap"] == got[1][i][2]["ecap"], (i, got[0][i][2], got[1][i][2])
+    c.close()
+    st = [got[0][i][2] for i in range(len(got[0]))]
+    caps = [x["ecap"] for x in st]
+    assert st[1]["retries"] >= 1 and max(caps) > 64, st[:3]  # the burst ran short and grew the exchange
+    assert caps[-1] <= 128 and st[-1]["shrinks"] >= 1, caps  # and it came back down
+    assert max(x["last_max"] for x in st[8:]) < 64, st[8:]
+
+
 @pytest.mark.gpu
 def test_sharded_abi_rccl_one_rank(gpu):
     """The RCCL path (exchanges on the engine's stream) with one rank: the same
