@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="key-range shards of the N-core CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--borrow", choices=["off", "large", "always"], default="large",
+                   help="fdbcs_config.flags: how the adds hold the caller's keys (include/fdbcs.h FDBCS_BORROW_*); "
+                        "'large' borrows only batches of >= 65,536 transactions (config 5), so configs 1-4 copy")
     p.add_argument("--no-shim", action="store_true", help="skip the shim's skipListTest rate")
     p.add_argument("--impl", choices=["abi", "py"], default="abi",
                    help="exact protocol A: fdbcs_sharded (C ABI, RCCL inside libfdbcs) or the Python orchestration")
@@ -362,6 +365,9 @@ def shim_skiplisttest():
                     "D.MergeWrite from a stage-timed second run"}
 
 
+BORROW_FLAGS = {"off": 0, "large": 2, "always": 1}  # include/fdbcs.h FDBCS_BORROW_*
+
+
 def run_single(args):
     """N = 1: steady-state prefill, then the Resolver's per-transaction window."""
     import torch
@@ -375,7 +381,7 @@ def run_single(args):
 
     cfg = args.config
     wl = Workload(cfg, txns=args.txns)
-    cs = ConflictSet(device=0, max_history=max_history(cfg))
+    cs = ConflictSet(device=0, max_history=max_history(cfg), flags=BORROW_FLAGS[args.borrow])
     # ---- steady state (untimed, regardless of --warmup) -------------------------
     t_w = time.time()
     if cfg == 5:  # preload: 50 blind-write batches of 10^6 point writes, no compaction
@@ -678,7 +684,10 @@ def run_single(args):
         "config": {"workload": workload, "txns_per_batch": T, "prefill_batches": args.prefill,
                    "history_pre": H_pre, "history_post": H_post, "parallelism": "single", "host_affinity": affinity,
                    "window": "Resolver.actor.cpp:139-154: fdbcs_batch_begin + T x fdbcs_batch_add (pinned append, "
-                             "chunked H2D) + fdbcs_batch_detect (device pipeline, verdict D2H), native loop"},
+                             "chunked H2D) + fdbcs_batch_detect (device pipeline, verdict D2H), native loop",
+                   "keys": "borrowed (pointers recorded by the adds; checked and packed at detect on host threads)"
+                           if args.borrow == "always" or (args.borrow == "large" and T >= 65536)
+                           else "copied by each add into the pinned stream"},
         "hbm_resident": hbm,
         "packed_path": packed,
         "shim_skiplisttest": shim,

@@ -41,7 +41,7 @@ class BatchView(C.Structure):
 class Config(C.Structure):
     _fields_ = [
         ("device", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("flags", C.c_int32),  # FDBCS_BORROW_*
         ("max_history", C.c_int64),
         ("max_batch_keys", C.c_int64),
         ("tail_arena_bytes", C.c_int64),
@@ -86,6 +86,7 @@ FDBCS_FUNCS = [
     ("fdbcs_stage_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
     ("fdbcs_stream", C.c_void_p, [C.c_void_p]),
     ("fdbcs_batch_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
+    ("fdbcs_batch_refused_txn", C.c_int64, [C.c_void_p]),
     ("fdbcs_debug_phases", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_debug_prefix_skips", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int]),
     ("fdbcs_split_batch", C.c_int,

@@ -24,9 +24,9 @@ from .batch import PackedBatch, unpack_history
 
 
 class ConflictSet:
-    def __init__(self, v0=0, device=-1, max_history=0, tail_arena_bytes=0):
+    def __init__(self, v0=0, device=-1, max_history=0, tail_arena_bytes=0, flags=0):
         self._lib = _abi.lib()
-        cfg = _abi.Config(device=device, max_history=max_history, tail_arena_bytes=tail_arena_bytes)
+        cfg = _abi.Config(device=device, flags=flags, max_history=max_history, tail_arena_bytes=tail_arena_bytes)
         h = C.c_void_p()
         check(self._lib.fdbcs_create(C.byref(h), v0, C.byref(cfg)), "newConflictSet")
         self._h = h
@@ -207,8 +207,9 @@ class ConflictBatch:
             return arr
 
         rs, ws = list(read_ranges), list(write_ranges)
-        check(self._lib.fdbcs_batch_add(self.cs.handle, read_snapshot, ranges(rs), len(rs), ranges(ws), len(ws)),
-              "addTransaction")
+        ra, wa = ranges(rs), ranges(ws)
+        keep.append((ra, wa))  # (the range arrays too: a borrowed batch, FDBCS_BORROW_*, reads them at detect)
+        check(self._lib.fdbcs_batch_add(self.cs.handle, read_snapshot, ra, len(rs), wa, len(ws)), "addTransaction")
         self._keep.append(keep)
         self._count += 1
 

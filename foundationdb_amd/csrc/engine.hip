@@ -148,6 +148,7 @@ struct fdbcs {
     size_t vpin_cap = 0;
     // stage timing
     bool timing = false;
+    int32_t borrow_flags = 0;  // fdbcs_config.flags (FDBCS_BORROW_*)
     hipEvent_t ev[8] = {};
     // early verdicts: D2H of the verdicts and a scalar snapshot right after
     // the decision; the history update keeps running behind them
@@ -985,6 +986,7 @@ bool live_enabled() {
 void live_begin(fdbcs* cs) {
     cs->lv_lm = false;
     if (!live_enabled() || cs->timing || !cs->have_quantiles || cs->lv_prev_T <= 0 || cs->sparse_edges ||
+        cs->st.borrowing() ||
         (cs->h.shard.has_lo | cs->h.shard.has_hi))
         return;
     auto up = [](int64_t x) { return x + x / 4 + 256; };
@@ -1343,6 +1345,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     }
     cs->device = dev;
+    cs->borrow_flags = cfg ? cfg->flags & (FDBCS_BORROW_ALWAYS | FDBCS_BORROW_LARGE) : 0;
     int r = FDBCS_OK;
     auto fail = [&](int code) {
         fdbcs_destroy(cs);
@@ -1458,7 +1461,11 @@ int fdbcs_batch_begin(fdbcs* cs) {
     if (cs->sub_head != cs->sub_tail) return FDBCS_E_STATE;  // (pipelined batches still in flight)
     live_quiesce(cs);  // (a live batch begun and never detected)
     int r;
-    if ((r = cs->st.begin())) return r;
+    // (borrowed batches: stage.h TxnStage::begin; FDBCS_BORROW_LARGE follows
+    // the previous batch's size, as the live capacities do)
+    const bool borrow = (cs->borrow_flags & FDBCS_BORROW_ALWAYS) ||
+                        ((cs->borrow_flags & FDBCS_BORROW_LARGE) && cs->lv_prev_T >= FDBCS_BORROW_MIN_TXNS);
+    if ((r = cs->st.begin(borrow))) return r;
     cs->have_last_dv = false;  // (the staged bytes of the last batch are overwritten from here on)
     cs->last_wbase = 0;
     cs->in_batch = true;
@@ -1475,6 +1482,8 @@ int fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot, const fdbcs_range* reads, 
 }
 
 int32_t fdbcs_batch_txn_count(const fdbcs* cs) { return cs ? (int32_t)cs->st.txns() : 0; }
+
+int64_t fdbcs_batch_refused_txn(const fdbcs* cs) { return cs ? cs->st.refused_at() : -1; }
 
 int fdbcs_batch_skip(fdbcs* cs, int32_t n) {
     if (!cs) return FDBCS_E_ARG;
@@ -2515,7 +2524,12 @@ int fdbcs_sharded_create(fdbcs_sharded** out, int32_t rank, int32_t world, const
         return code;
     };
     int r;
-    if ((r = fdbcs_create(&sh->cs, v0, cfg))) return fail(r);
+    // (no borrowed batches here: a protocol-B rank's adds hand the engine a
+    // filtered copy of the ranges that lives only for the call)
+    fdbcs_config local{};
+    if (cfg) local = *cfg;
+    local.flags &= ~(FDBCS_BORROW_ALWAYS | FDBCS_BORROW_LARGE);
+    if ((r = fdbcs_create(&sh->cs, v0, &local))) return fail(r);
     fdbcs* cs = sh->cs;
     // this rank's keys: [bound[rank-1], bound[rank])
     const uint8_t* lo = rank > 0 ? bound_bytes + bound_off[rank - 1] : nullptr;

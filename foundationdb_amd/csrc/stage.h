@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "kernels.h"
 
@@ -44,7 +45,16 @@ class TxnStage {
     // free the buffers and forget the stream (before the owner destroys it)
     void release();
 
-    int begin();
+    // borrow: the adds record the caller's range arrays only, as the
+    // reference's addTransaction keeps StringRefs into the caller's arena until
+    // detectConflicts returns (SkipList.cpp:993-1004); finish() then checks and
+    // packs the whole batch on host threads (pack_borrowed).  Large batches
+    // (config 5: 10^6 transactions) no longer pack on the caller's one core.
+    int begin(bool borrow = false);
+    bool borrowing() const { return borrow_; }
+    // a borrowed batch refused at finish(): the first transaction whose
+    // ranges the add would have refused (-1: none)
+    int64_t refused_at() const { return bad_txn_; }
     // Live ingest: after begin(), make this batch live --
     // the stream, offsets and view sized for `caps`, the progress words reset
     // -- before the engine launches k_live_ingest over them.  The adds then
@@ -99,6 +109,17 @@ class TxnStage {
 
     void sync();
     static bool pull_rest();
+    int pack_borrowed();
+    struct BorrowRec {
+        int64_t snap;
+        const fdbcs_range* rd;
+        const fdbcs_range* wr;
+        int32_t nr, nw;
+    };
+    bool borrow_ = false;
+    std::vector<BorrowRec> brec_;
+    int64_t bad_txn_ = -1;
+    bool toff_in_stream_ = false;  // pack_borrowed wrote the record offsets after the records
 
     hipStream_t stream_ = nullptr;
     hipStream_t copy_ = nullptr;

@@ -5,8 +5,11 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 namespace fdbcs_dev {
 
@@ -91,8 +94,12 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
     return FDBCS_OK;
 }
 
-int TxnStage::begin() {
+int TxnStage::begin(bool borrow) {
     live_cancel();  // (a batch begun and never detected)
+    borrow_ = borrow;
+    brec_.clear();
+    bad_txn_ = -1;
+    toff_in_stream_ = false;
     T_ = R_ = W_ = 0;
     K_ = 0;
     used_ = sent_ = 0;
@@ -185,6 +192,13 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     if (!open_) return FDBCS_E_STATE;
     if (nr < 0 || nw < 0 || (nr && !reads) || (nw && !writes)) return FDBCS_E_ARG;
     if (T_ >= MAX_T || R_ + nr > INT32_MAX / 2 || W_ + nw > INT32_MAX / 2) return FDBCS_E_CAPACITY;
+    if (borrow_) {  // (checked and packed at finish: pack_borrowed)
+        brec_.push_back(BorrowRec{snap, reads, writes, nr, nw});
+        T_++;
+        R_ += nr;
+        W_ += nw;
+        return FDBCS_OK;
+    }
     const int n = nr + nw;
     if (n == 0) {  // no record: the offset entry says so (kernels.h STAGE_EMPTY)
         if (T_ + 1 > toff_cap_ || used_ + 8 * (uint64_t)(T_ + 1) + 16 > cap_) {
@@ -251,6 +265,147 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     return FDBCS_OK;
 }
 
+// ---- borrowed batches ----------------------------------------------------------
+// finish() of a borrowed batch: the records the adds would have written, made
+// on host threads from the caller's range arrays (still valid: the caller
+// keeps them until detectConflicts returns, as the reference's arena).
+//   1. every piece of the batch is checked (FDBCS_E_KEY / FDBCS_E_RANGE as
+//      the add would refuse it) and measured: record bytes, reads, writes, key
+//      bytes;
+//   2. a prefix over the pieces places them; each worker writes its pieces'
+//      records and offset entries, the offsets straight after the records.
+// The pieces are round-major (round c = pieces c*N .. c*N + N - 1, one
+// contiguous part of the stream), and the caller's thread sends each round
+// on the copy stream as soon as its last piece is written, so the copies of
+// the first rounds overlap the packing of the later ones.  A refused batch
+// changes nothing (FDBCS_E_KEY / FDBCS_E_RANGE from detectConflicts; the
+// reference would ASSERT in detectConflicts, SkipList.cpp:1117, 1127).
+// Point ranges share their end's bytes whatever the key length (SHARE_ABOVE
+// 0): no jump of the caller's loop to mispredict here, and fewer PCIe bytes.
+namespace {
+int host_threads() {
+    static const int n = [] {
+        const char* e = getenv("FDBCS_HOST_THREADS");
+        const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+        return std::max(1, e ? atoi(e) : std::min(16, hw));
+    }();
+    return n;
+}
+}  // namespace
+
+int TxnStage::pack_borrowed() {
+    const int64_t T = T_;
+    const int N = T < 8192 ? 1 : (int)std::min<int64_t>(host_threads(), T / 4096);
+    const int C = T >= (1 << 17) ? 4 : 1;
+    const int P = C * N;
+    struct Piece {
+        int64_t t0, t1;
+        uint64_t bytes = 0, keys = 0;
+        int64_t reads = 0, writes = 0;
+        int64_t bad = -1;
+        int code = FDBCS_OK;
+        uint64_t off = 0;
+        int64_t ro = 0, wo = 0;
+    };
+    std::vector<Piece> pc((size_t)P);
+    for (int p = 0; p < P; p++) {
+        pc[p].t0 = T * p / P;
+        pc[p].t1 = T * (p + 1) / P;
+    }
+    const BorrowRec* br = brec_.data();
+    auto measure = [&](Piece& q) {
+        for (int64_t t = q.t0; t < q.t1; t++) {
+            const BorrowRec& x = br[t];
+            q.reads += x.nr;
+            q.writes += x.nw;
+            if (x.nr + x.nw == 0) continue;
+            int st;
+            const uint64_t kb = fdbcs_pack::ranges_bytes<0>(x.rd, x.nr, x.wr, x.nw, st);
+            if (st != FDBCS_OK) {
+                q.bad = t;
+                q.code = st;
+                return;
+            }
+            for (int i = 0; i < x.nr; i++) q.keys += (uint64_t)x.rd[i].begin_len + x.rd[i].end_len;
+            for (int i = 0; i < x.nw; i++) q.keys += (uint64_t)x.wr[i].begin_len + x.wr[i].end_len;
+            q.bytes += (sizeof(StageHdr) + 8 * (uint64_t)(x.nr + x.nw) + kb + 7) & ~uint64_t(7);
+        }
+    };
+    auto run = [&](auto f) {  // f(worker) on N threads, the caller's one of them
+        std::vector<std::thread> th;
+        th.reserve(N - 1);
+        for (int w = 1; w < N; w++) th.emplace_back(f, w);
+        f(0);
+        for (auto& x : th) x.join();
+    };
+    run([&](int w) {
+        for (int c = 0; c < C; c++) measure(pc[(size_t)c * N + w]);
+    });
+    uint64_t off = 0, keys = 0;
+    int64_t ro = 0, wo = 0;
+    for (Piece& q : pc) {
+        if (q.bad >= 0) {  // (the first refused transaction, in batch order)
+            bad_txn_ = q.bad;
+            return q.code;
+        }
+        q.off = off;
+        q.ro = ro;
+        q.wo = wo;
+        off += q.bytes;
+        keys += q.keys;
+        ro += q.reads;
+        wo += q.writes;
+    }
+    // (the record offsets after the records: finish() sends them with the rest)
+    const uint64_t need = off + 8 * (uint64_t)(T + 1) + 16;
+    int r;
+    if ((r = grow(T + 1, need))) return r;
+    uint64_t* toff = reinterpret_cast<uint64_t*>(pin_ + off);
+    std::vector<std::atomic<int>> done((size_t)C);
+    for (auto& d : done) d.store(0);
+    std::atomic<int> err{FDBCS_OK};
+    auto pack = [&](const Piece& q) {
+        uint64_t o = q.off;
+        int64_t R = q.ro, W = q.wo;
+        for (int64_t t = q.t0; t < q.t1; t++) {
+            const BorrowRec& x = br[t];
+            if (x.nr + x.nw == 0) {
+                toff[t] = STAGE_EMPTY | ((uint64_t)W << 32) | (uint64_t)R;
+                continue;
+            }
+            uint8_t* p = pin_ + o;
+            StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
+            uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)(x.nr + x.nw);
+            fdbcs_pack::put_ranges<StageRange, STAGE_SHARED, 0>(x.rd, x.nr, ent, p, kp);
+            fdbcs_pack::put_ranges<StageRange, STAGE_SHARED, 0>(x.wr, x.nw, ent + x.nr, p, kp);
+            const StageHdr h{x.snap, (int32_t)R, (int32_t)W, x.nr, x.nw};
+            memcpy(p, &h, sizeof h);
+            toff[t] = o;
+            o += ((uint64_t)(kp - p) + 7) & ~uint64_t(7);
+            R += x.nr;
+            W += x.nw;
+        }
+    };
+    run([&](int w) {
+        for (int c = 0; c < C; c++) {
+            pack(pc[(size_t)c * N + w]);
+            done[c].fetch_add(1, std::memory_order_acq_rel);
+            if (w != 0) continue;
+            // the caller's thread: this round to the device once every piece of it is written
+            while (done[c].load(std::memory_order_acquire) < N) _mm_pause();
+            const uint64_t a = pc[(size_t)c * N].off, b = c + 1 < C ? pc[(size_t)(c + 1) * N].off : off;
+            if (b > a && hipMemcpyAsync(dev_ + a, pin_ + a, b - a, hipMemcpyHostToDevice, copy_) != hipSuccess)
+                err.store(FDBCS_E_HIP);
+        }
+    });
+    if (err.load()) return err.load();
+    used_ = off;
+    sent_ = off;  // (finish() sends the offsets and makes the engine's stream wait for the copies)
+    K_ = keys;
+    toff_in_stream_ = true;
+    return FDBCS_OK;
+}
+
 // FDBCS_PULL_REST=1: finish() has the engine's queue read the stream's rest
 // from the mapped pinned buffer (launch_pull) instead of a last SDMA copy and
 // a cross-queue event behind it (A/B knob: ~5 us per batch, within the
@@ -264,6 +419,11 @@ int TxnStage::skip(int32_t n) {
     if (!open_) return FDBCS_E_STATE;
     if (n < 0) return FDBCS_E_ARG;
     if (T_ + n > MAX_T) return FDBCS_E_CAPACITY;
+    if (borrow_) {
+        brec_.insert(brec_.end(), (size_t)n, BorrowRec{0, nullptr, nullptr, 0, 0});
+        T_ += n;
+        return FDBCS_OK;
+    }
     const uint64_t need = used_ + 8 * (uint64_t)(T_ + n) + 16;
     if (T_ + n > toff_cap_ || need > cap_) {
         int r = grow(T_ + n, need);
@@ -365,6 +525,11 @@ int TxnStage::begin_live(const LiveCaps& caps) {
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
+    if (borrow_) {
+        const int r = pack_borrowed();
+        brec_.clear();
+        if (r) return r;
+    }
     bool go_live = false;
     // (the detect sizes nothing anew for a live batch: run_batch refuses one
     // whose stream or key bytes outgrew what live_begin sized its buffers
@@ -433,7 +598,7 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     const uint64_t o_toff = used_;
     dtoff = reinterpret_cast<const uint64_t*>(dev_ + o_toff);
     early_at_ = early_ && used_ > early_ ? used_ - early_ : ~0ull;  // (the next batch's extra chunk)
-    if (T_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
+    if (T_ && !toff_in_stream_) memcpy(pin_ + o_toff, toff_, (size_t)T_ * 8);
     const uint64_t end = o_toff + 8 * (uint64_t)T_;
     if (pull_rest()) {
         // the chunks already sent: their last copy's event (recorded at the

@@ -125,7 +125,7 @@ __attribute__((always_inline)) inline void copy_small(uint8_t* d, const uint8_t*
 //   longer keys: a point range [k, k\x00) is written as k\x00 once (flag
 //     SHARED in the entry's end length; kernels.h STAGE_SHARED), which saves
 //     a long key's copy and its PCIe bytes.
-template <class Ent, uint16_t SHARED>
+template <class Ent, uint16_t SHARED, uint32_t SHARE_ABOVE = FDBCS_PACK_SHARE_ABOVE>
 __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int n, Ent* ent, const uint8_t* rec,
                                                       uint8_t*& kp_io) {
     // (a local cursor: kp_io itself may alias the bytes stored through it, so
@@ -137,7 +137,7 @@ __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int
         const uint32_t bl = rg[i].begin_len, el = rg[i].end_len;
         const int c = key_cmp(b, bl, e, el);
         bad |= c >= 0;
-        if (bl <= FDBCS_PACK_SHARE_ABOVE) {
+        if (bl <= SHARE_ABOVE) {
             if (bl == 16) memcpy(kp, b, 16);  // (the configs' 16-byte keys: one store)
             else copy_small(kp, b, bl);
             copy_small(kp + bl, e, el);
@@ -158,6 +158,32 @@ __attribute__((always_inline)) inline bool put_ranges(const fdbcs_range* rg, int
     }
     kp_io = kp;
     return bad;
+}
+
+// The key bytes put_ranges<_, _, SHARE_ABOVE> writes for a transaction's
+// ranges (reads, then writes: n of them in all) and its status as the add
+// would refuse it -- FDBCS_E_KEY (a key over FDBCS_MAX_KEY, any range) before
+// FDBCS_E_RANGE (begin >= end) -- for the borrowed batches' first pass at
+// detect (stage.hip TxnStage::pack_borrowed).
+template <uint32_t SHARE_ABOVE>
+inline uint64_t ranges_bytes(const fdbcs_range* rd, int nr, const fdbcs_range* wr, int nw, int& status) {
+    uint64_t k = 0;
+    bool range_bad = false;
+    status = FDBCS_OK;
+    for (int i = 0; i < nr + nw; i++) {
+        const fdbcs_range& g = i < nr ? rd[i] : wr[i - nr];
+        const uint8_t *b = g.begin, *e = g.end;
+        const uint32_t bl = g.begin_len, el = g.end_len;
+        if (bl > FDBCS_MAX_KEY || el > FDBCS_MAX_KEY) {
+            status = FDBCS_E_KEY;
+            return 0;
+        }
+        const int c = key_cmp(b, bl, e, el);
+        range_bad |= c >= 0;
+        k += bl <= SHARE_ABOVE || !(c == -2 && el == bl + 1 && e[bl] == 0) ? bl + el : bl + 1;
+    }
+    if (range_bad) status = FDBCS_E_RANGE;
+    return k;
 }
 
 }  // namespace fdbcs_pack

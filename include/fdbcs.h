@@ -93,11 +93,29 @@ typedef struct fdbcs_batch_view {
 /* Optional construction parameters (NULL = defaults). */
 typedef struct fdbcs_config {
     int32_t  device;            /* HIP device ordinal, -1 = current            */
-    int32_t  reserved0;
+    int32_t  flags;             /* FDBCS_BORROW_* below (0 = copy every key)   */
     int64_t  max_history;       /* boundaries to pre-size for (0 = default)    */
     int64_t  max_batch_keys;    /* key slots per batch to pre-size (0 = grow)  */
     int64_t  tail_arena_bytes;  /* device bytes for keys > 17 B (0 = default)  */
 } fdbcs_config;
+
+/* fdbcs_config.flags: how fdbcs_batch_add holds the caller's keys.
+ *   FDBCS_BORROW_ALWAYS: every per-transaction batch borrows the caller's
+ *     range arrays and key bytes until fdbcs_batch_detect returns, as the
+ *     reference's addTransaction keeps StringRefs into the request's arena
+ *     (SkipList.cpp:993-1004); the add records the pointers only, and
+ *     detectConflicts checks and packs the batch on host threads.
+ *   FDBCS_BORROW_LARGE: borrow when the previous per-transaction batch had at
+ *     least FDBCS_BORROW_MIN_TXNS transactions (config 5's 10^6-transaction
+ *     batches), copy otherwise.
+ * A borrowed batch refuses nothing at add time: a transaction the add would
+ * refuse (FDBCS_E_KEY / FDBCS_E_RANGE) makes fdbcs_batch_detect return that
+ * status with the history unchanged (the reference ASSERTs inside
+ * detectConflicts, SkipList.cpp:1117, 1127), and fdbcs_batch_refused_txn
+ * names the first such transaction. */
+#define FDBCS_BORROW_ALWAYS 1
+#define FDBCS_BORROW_LARGE  2
+#define FDBCS_BORROW_MIN_TXNS 65536
 
 /* ---- ConflictSet lifecycle ------------------------------------------------ */
 
@@ -128,7 +146,9 @@ int  fdbcs_batch_begin(fdbcs* cs);
  * arena may be released at once (stricter than the reference, which borrows
  * them until detectConflicts returns).  A range with begin >= end
  * (FDBCS_E_RANGE) or a key over FDBCS_MAX_KEY (FDBCS_E_KEY) refuses the
- * transaction: it is not added, and the batch goes on. */
+ * transaction: it is not added, and the batch goes on.  A borrowed batch
+ * (fdbcs_config.flags, FDBCS_BORROW_*) records the pointers only: the range
+ * arrays and key bytes must stay valid until fdbcs_batch_detect returns. */
 int  fdbcs_batch_add(fdbcs* cs, int64_t read_snapshot,
                      const fdbcs_range* reads, int32_t nreads,
                      const fdbcs_range* writes, int32_t nwrites);
@@ -149,6 +169,11 @@ int  fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* ver
 
 /* Number of transactions added to the current batch. */
 int32_t fdbcs_batch_txn_count(const fdbcs* cs);
+
+/* A borrowed batch that fdbcs_batch_detect refused: the index of its first
+ * transaction with a range the add would have refused; -1 otherwise (no
+ * reference counterpart: see FDBCS_BORROW_ALWAYS). */
+int64_t fdbcs_batch_refused_txn(const fdbcs* cs);
 
 /* Whole-batch variants of addTransaction x T + detectConflicts.
  *   _packed: host-resident batch view; copied H2D through pinned staging.

@@ -24,13 +24,14 @@ static int ref_cmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl)
     return al < bl ? -1 : (al > bl ? 1 : 0);
 }
 
-static bool ref_put(const fdbcs_range* rg, int n, Ent* ent, const uint8_t* rec, uint8_t*& kp) {
+static bool ref_put(const fdbcs_range* rg, int n, Ent* ent, const uint8_t* rec, uint8_t*& kp,
+                    uint32_t share_above = FDBCS_PACK_SHARE_ABOVE) {
     bool bad = false;
     for (int i = 0; i < n; i++) {
         const fdbcs_range& r = rg[i];
         if (ref_cmp(r.begin, r.begin_len, r.end, r.end_len) >= 0) bad = true;
         // (keys up to FDBCS_PACK_SHARE_ABOVE bytes are copied whole: no shared end)
-        const bool point = r.begin_len > FDBCS_PACK_SHARE_ABOVE && r.end_len == r.begin_len + 1 &&
+        const bool point = r.begin_len > share_above && r.end_len == r.begin_len + 1 &&
                            memcmp(r.begin, r.end, r.begin_len) == 0 && r.end[r.begin_len] == 0;
         ent[i].kofs = (uint32_t)(kp - rec);
         ent[i].blen = (uint16_t)r.begin_len;
@@ -114,6 +115,24 @@ int main(int argc, char** argv) {
             const int d2 = ref_cmp(x.end, x.end_len, x.begin, x.begin_len);
             ok = (c1 == -2 ? -1 : c1) == c2 && (d1 == -2 ? -1 : d1) == d2;
             if (ok && c1 == -2) ok = x.begin_len < x.end_len && (x.begin_len == 0 || !memcmp(x.begin, x.end, x.begin_len));
+        }
+        // the borrowed batches' pack (every point range shares its end) and
+        // its size pass (stage.hip pack_borrowed): same records as the
+        // restatement at threshold 0, and the size pass's bytes and status
+        {
+            std::vector<uint8_t> r3(4096, 0xAB), r4(4096, 0xAB);
+            std::vector<Ent> e3(n), e4(n);
+            uint8_t *k3 = r3.data(), *k4 = r4.data();
+            const int nr = (int)(rnd() % (n + 1));
+            const bool b3 = fdbcs_pack::put_ranges<Ent, SHARED, 0>(rg.data(), nr, e3.data(), r3.data(), k3) |
+                            fdbcs_pack::put_ranges<Ent, SHARED, 0>(rg.data() + nr, n - nr, e3.data() + nr, r3.data(), k3);
+            const bool b4 = ref_put(rg.data(), n, e4.data(), r4.data(), k4, 0);
+            int st = 0;
+            const uint64_t sz = fdbcs_pack::ranges_bytes<0>(rg.data(), nr, rg.data() + nr, n - nr, st);
+            ok = ok && b3 == b4 && (k3 - r3.data()) == (k4 - r4.data()) && r3 == r4 &&
+                 st == (b4 ? FDBCS_E_RANGE : FDBCS_OK) && (b4 || sz == (uint64_t)(k4 - r4.data()));
+            for (int i = 0; ok && i < n; i++)
+                ok = e3[i].kofs == e4[i].kofs && e3[i].blen == e4[i].blen && e3[i].elen == e4[i].elen;
         }
         if (!ok) {
             printf("mismatch at round %d (bad %d/%d, bytes %ld/%ld)\n", it, b1, b2, (long)(k1 - r1.data()),

@@ -148,3 +148,144 @@ def test_detect_without_batch_is_state_error(gpu):
     g = ConflictSet()
     assert g._lib.fdbcs_batch_detect(g.handle, 20, 0, None) == _abi.E_STATE  # no ConflictBatch open
     g.close()
+
+
+# ---- borrowed batches (fdbcs_config.flags FDBCS_BORROW_*: the adds record the
+# caller's range arrays only; detectConflicts checks and packs them on host
+# threads -- SkipList.cpp:993-1004 borrows the keys the same way) ----
+
+BORROW_ALWAYS, BORROW_LARGE = 1, 2
+
+
+@pytest.mark.parametrize("maxlen", [3, 40])
+def test_borrowed_tiny_and_mixed_streams(gpu, maxlen):
+    """Borrowed batches (every one, FDBCS_BORROW_ALWAYS) through the Python
+    ConflictBatch mirror: "" and short keys, prefixes, \\x00, long keys, empty
+    transactions, then larger mixed batches -- verdicts and the whole history as
+    the oracle's after every batch."""
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    for batch, now, nold in tiny_stream(300 + maxlen, n_batches=12, max_txns=60, maxlen=maxlen, max_reads=3,
+                                        max_writes=3):
+        v = ConflictBatch_run(g, batch.txns(), now, nold)
+        assert np.array_equal(v, c.detect_packed(batch, now, nold))
+        same_history(g, c)
+    for batch, now, nold in mixed_stream(11, n_batches=6, max_txns=9000, keyspace=40000):
+        now += 2000
+        v = ConflictBatch_run(g, batch.txns(), now, nold)
+        assert np.array_equal(v, c.detect_packed(batch, now, nold))
+    same_history(g, c)
+    g.close()
+
+
+def _ranges(lib_keys, spec):
+    """ctypes Range array over the bytes of lib_keys (a bytearray the test keeps
+    and later overwrites): spec = [(begin offset, begin len, end offset, end len)]."""
+    import ctypes as C
+    arr = (_abi.Range * max(1, len(spec)))()
+    base = C.addressof((C.c_char * len(lib_keys)).from_buffer(lib_keys))
+    for i, (bo, bl, eo, el) in enumerate(spec):
+        arr[i].begin, arr[i].begin_len, arr[i].end, arr[i].end_len = base + bo, bl, base + eo, el
+    return arr
+
+
+def test_borrowed_keys_overwritten_after_detect(gpu):
+    """a borrowed batch whose keys (and range arrays) the
+    caller overwrites right after detectConflicts returns -- nothing of the
+    library may still read them.  Each batch's buffers are scribbled over
+    before the next batch; the history must equal the oracle's."""
+    import random
+    from foundationdb_amd.batch import PackedBatch
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    lib = g._lib
+    rng = random.Random(5)
+    now = 100
+    for _ in range(6):
+        now += 50
+        txns = []
+        for _t in range(3000):
+            def rr():
+                a = rng.randrange(5000)
+                k = b"key%06d" % a
+                return (k, k + b"\x00") if rng.random() < 0.7 else (k, b"key%06d" % (a + rng.randint(1, 30)))
+            txns.append((now - rng.randint(1, 40), [rr() for _ in range(rng.randint(0, 3))],
+                         [rr() for _ in range(rng.randint(0, 2))]))
+        buf = bytearray()
+        specs = []
+        for snap, reads, writes in txns:
+            sp = []
+            for b, e in list(reads) + list(writes):
+                bo = len(buf); buf += b
+                eo = len(buf); buf += e
+                sp.append((bo, len(b), eo, len(e)))
+            specs.append((snap, sp, len(reads)))
+        arrays = []
+        assert lib.fdbcs_batch_begin(g.handle) == 0
+        for snap, sp, nr in specs:
+            ra, wa = _ranges(buf, sp[:nr]), _ranges(buf, sp[nr:])
+            arrays.append((ra, wa))
+            assert lib.fdbcs_batch_add(g.handle, snap, ra, nr, wa, len(sp) - nr) == 0
+        out = np.zeros(len(txns), np.uint8)
+        assert lib.fdbcs_batch_detect(g.handle, now, now - 200, out.ctypes.data) == 0
+        # the caller's arena is reused at once: keys and range arrays scribbled over
+        buf[:] = bytes([0xA5]) * len(buf)
+        for ra, wa in arrays:
+            for a in (ra, wa):
+                for x in a:
+                    x.begin_len, x.end_len = 7, 3
+        pb = PackedBatch.from_txns(txns)
+        assert np.array_equal(out, c.detect_packed(pb, now, now - 200))
+        same_history(g, c)
+    g.close()
+
+
+def test_borrowed_refusal(gpu):
+    """A borrowed batch refuses nothing at add time: a range the add would
+    refuse makes detectConflicts fail with that status (the reference ASSERTs
+    inside detectConflicts, SkipList.cpp:1117/1127), names the transaction
+    (fdbcs_batch_refused_txn), and leaves the history as it was; the next
+    batch goes on."""
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    lib = g._lib
+    good = [(1, [(b"a", b"b")], [(b"a", b"c")]), (1, [], [(b"c", b"d")])]
+    for bad, code in (((1, [(b"b", b"b")], []), _abi.E_RANGE),
+                      ((1, [(b"a", b"b" * (_abi.MAX_KEY + 1))], []), _abi.E_KEY)):
+        before = g.dump_arrays()
+        b = ConflictBatch(g)
+        for snap, reads, writes in good[:1] + [bad] + good[1:]:
+            b.add_transaction(reads, writes, snap)  # (no refusal here)
+        with pytest.raises(FdbcsError) as e:
+            b.detect_conflicts(10, 0)
+        assert e.value.status == code
+        assert lib.fdbcs_batch_refused_txn(g.handle) == 1
+        after = g.dump_arrays()
+        assert all(np.array_equal(x, y) for x, y in zip(before, after))
+    from foundationdb_amd.batch import PackedBatch
+    v = ConflictBatch_run(g, good, 10, 0)
+    assert lib.fdbcs_batch_refused_txn(g.handle) == -1
+    assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(good), 10, 0))
+    same_history(g, c)
+    g.close()
+
+
+def test_borrowed_large_batches_match_oracle(gpu):
+    """Config 5's shape through the bench's native Resolver loop with
+    FDBCS_BORROW_LARGE: the first 10^6-transaction batch copies its keys
+    (no earlier batch), the next ones borrow and pack on host threads in
+    rounds whose copies overlap the packing -- verdicts and history as the
+    oracle's."""
+    g = ConflictSet(flags=BORROW_LARGE)
+    c = CpuSpec()
+    wl = Workload(5, txns=1_000_000)
+    nb = 3
+    run = wl.prepare_run(0, nb)
+    us, add_us, verdicts = run.run(g)
+    for i in range(nb):
+        b, now, nold = wl.batch(i)
+        vc = c.detect_packed(b, now, nold)
+        assert np.array_equal(verdicts[i], vc), (i, np.nonzero(verdicts[i] != vc)[0][:10])
+    same_history(g, c)
+    assert add_us[1] < 0.6 * add_us[0], add_us  # (borrowed adds record pointers only)
+    g.close()
