@@ -32,6 +32,8 @@
 
 namespace fdbcs_dev {
 
+class HostPool;  // (stage.hip: the borrowed batches' packing threads)
+
 class TxnStage {
    public:
     TxnStage() = default;
@@ -110,6 +112,8 @@ class TxnStage {
     void sync();
     static bool pull_rest();
     int pack_borrowed();
+    void drop_pool();
+    HostPool* pool_ = nullptr;  // created at the first borrowed batch large enough to share
     struct BorrowRec {
         int64_t snap;
         const fdbcs_range* rd;
@@ -117,7 +121,11 @@ class TxnStage {
         int32_t nr, nw;
     };
     bool borrow_ = false;
-    std::vector<BorrowRec> brec_;
+    // the adds' records: written with non-temporal stores (a 10^6-transaction
+    // batch's 32 MB would otherwise be read for ownership first: 3x slower)
+    BorrowRec* brec_ = nullptr;
+    int64_t brec_cap_ = 0;
+    int grow_brec(int64_t need);
     int64_t bad_txn_ = -1;
     bool toff_in_stream_ = false;  // pack_borrowed wrote the record offsets after the records
 

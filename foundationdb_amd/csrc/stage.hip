@@ -6,8 +6,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -41,6 +44,10 @@ void TxnStage::sync() {
 void TxnStage::release() {
     live_cancel();  // (a live kernel waiting for this batch leaves: the syncs below return)
     sync();
+    drop_pool();
+    free(brec_);
+    brec_ = nullptr;
+    brec_cap_ = 0;
     auto free_host_or_dev = [this](void* p) {
         if (!p) return;
         if (bar_) hipFree(p);
@@ -97,7 +104,6 @@ int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
 int TxnStage::begin(bool borrow) {
     live_cancel();  // (a batch begun and never detected)
     borrow_ = borrow;
-    brec_.clear();
     bad_txn_ = -1;
     toff_in_stream_ = false;
     T_ = R_ = W_ = 0;
@@ -193,7 +199,14 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
     if (nr < 0 || nw < 0 || (nr && !reads) || (nw && !writes)) return FDBCS_E_ARG;
     if (T_ >= MAX_T || R_ + nr > INT32_MAX / 2 || W_ + nw > INT32_MAX / 2) return FDBCS_E_CAPACITY;
     if (borrow_) {  // (checked and packed at finish: pack_borrowed)
-        brec_.push_back(BorrowRec{snap, reads, writes, nr, nw});
+        if (T_ >= brec_cap_) {
+            const int r = grow_brec(T_ + 1);
+            if (r) return r;
+        }
+        __m128i* d = reinterpret_cast<__m128i*>(brec_ + T_);
+        _mm_stream_si128(d, _mm_set_epi64x((long long)(uintptr_t)reads, (long long)snap));
+        _mm_stream_si128(d + 1, _mm_set_epi64x((long long)(((uint64_t)(uint32_t)nw << 32) | (uint32_t)nr),
+                                               (long long)(uintptr_t)writes));
         T_++;
         R_ += nr;
         W_ += nw;
@@ -268,20 +281,81 @@ int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbc
 // ---- borrowed batches ----------------------------------------------------------
 // finish() of a borrowed batch: the records the adds would have written, made
 // on host threads from the caller's range arrays (still valid: the caller
-// keeps them until detectConflicts returns, as the reference's arena).
+// keeps them until detectConflicts returns, as the reference's arena).  One
+// parallel region over N workers (the caller's thread is worker 0):
 //   1. every piece of the batch is checked (FDBCS_E_KEY / FDBCS_E_RANGE as
 //      the add would refuse it) and measured: record bytes, reads, writes, key
 //      bytes;
-//   2. a prefix over the pieces places them; each worker writes its pieces'
-//      records and offset entries, the offsets straight after the records.
+//   2. worker 0 places the pieces (a prefix over them) and sizes the stream;
+//   3. each worker writes its pieces' records and offset entries, the offsets
+//      straight after the records.
 // The pieces are round-major (round c = pieces c*N .. c*N + N - 1, one
-// contiguous part of the stream), and the caller's thread sends each round
-// on the copy stream as soon as its last piece is written, so the copies of
-// the first rounds overlap the packing of the later ones.  A refused batch
-// changes nothing (FDBCS_E_KEY / FDBCS_E_RANGE from detectConflicts; the
-// reference would ASSERT in detectConflicts, SkipList.cpp:1117, 1127).
-// Point ranges share their end's bytes whatever the key length (SHARE_ABOVE
-// 0): no jump of the caller's loop to mispredict here, and fewer PCIe bytes.
+// contiguous part of the stream), and worker 0 sends each round on the copy
+// stream as soon as its last piece is written, so the copies of the first
+// rounds overlap the packing of the later ones.  A refused batch changes
+// nothing (FDBCS_E_KEY / FDBCS_E_RANGE from detectConflicts; the reference
+// would ASSERT in detectConflicts, SkipList.cpp:1117, 1127).  Point ranges
+// share their end's bytes whatever the key length (SHARE_ABOVE 0): no jump of
+// the caller's add loop to mispredict here, and fewer PCIe bytes.
+//
+// The workers are a pool kept by the stage and blocked on a condition
+// variable between batches: spinning helper threads made the caller's own add
+// loop 3x slower ("Measured and dropped" (ii)), and creating
+// threads per batch costs more than a config-2 batch's whole pack.
+class HostPool {
+   public:
+    explicit HostPool(int n) : n_(n) {
+        for (int w = 1; w < n_; w++) th_.emplace_back([this, w] { loop(w); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return n_; }
+    // f(worker) on every worker, the caller's thread as worker 0
+    void run(const std::function<void(int)>& f) {
+        left_.store(n_ - 1, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            f_ = &f;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        while (left_.load(std::memory_order_acquire) > 0) _mm_pause();
+    }
+
+   private:
+    void loop(int w) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (quit_) return;
+                f = f_;
+            }
+            (*f)(w);
+            left_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+    const std::function<void(int)>* f_ = nullptr;
+    std::atomic<int> left_{0};
+};
+
 namespace {
 int host_threads() {
     static const int n = [] {
@@ -291,12 +365,39 @@ int host_threads() {
     }();
     return n;
 }
+// transactions per worker below which fewer workers pack (FDBCS_BORROW_GRAIN)
+int64_t borrow_grain() {
+    static const int64_t g = getenv("FDBCS_BORROW_GRAIN") ? std::max(1LL, atoll(getenv("FDBCS_BORROW_GRAIN"))) : 512;
+    return g;
+}
 }  // namespace
+
+int TxnStage::grow_brec(int64_t need) {
+    static_assert(sizeof(BorrowRec) == 32 && offsetof(BorrowRec, rd) == 8 && offsetof(BorrowRec, wr) == 16 &&
+                      offsetof(BorrowRec, nr) == 24 && offsetof(BorrowRec, nw) == 28,
+                  "the adds store a record as two 16-byte halves");
+    const int64_t nc = (std::max<int64_t>(need, std::max<int64_t>(4096, 2 * brec_cap_)) + 1) & ~int64_t(1);  // (64-byte multiple)
+    BorrowRec* n = static_cast<BorrowRec*>(aligned_alloc(64, (size_t)nc * sizeof(BorrowRec)));
+    if (!n) return FDBCS_E_NOMEM;
+    _mm_sfence();
+    if (T_) memcpy(n, brec_, (size_t)T_ * sizeof(BorrowRec));
+    free(brec_);
+    brec_ = n;
+    brec_cap_ = nc;
+    return FDBCS_OK;
+}
+
+void TxnStage::drop_pool() {
+    delete pool_;
+    pool_ = nullptr;
+}
 
 int TxnStage::pack_borrowed() {
     const int64_t T = T_;
-    const int N = T < 8192 ? 1 : (int)std::min<int64_t>(host_threads(), T / 4096);
-    const int C = T >= (1 << 17) ? 4 : 1;
+    if (!pool_ && T >= 2 * borrow_grain() && host_threads() > 1) pool_ = new HostPool(host_threads());
+    const int N = pool_ ? (int)std::max<int64_t>(1, std::min<int64_t>(pool_->size(), T / borrow_grain())) : 1;
+    // rounds: one H2D copy each, the first ones overlapping the later packing
+    const int C = T >= (1 << 17) ? 8 : (T >= 4096 ? 2 : 1);
     const int P = C * N;
     struct Piece {
         int64_t t0, t1;
@@ -312,7 +413,7 @@ int TxnStage::pack_borrowed() {
         pc[p].t0 = T * p / P;
         pc[p].t1 = T * (p + 1) / P;
     }
-    const BorrowRec* br = brec_.data();
+    const BorrowRec* br = brec_;
     auto measure = [&](Piece& q) {
         for (int64_t t = q.t0; t < q.t1; t++) {
             const BorrowRec& x = br[t];
@@ -331,40 +432,7 @@ int TxnStage::pack_borrowed() {
             q.bytes += (sizeof(StageHdr) + 8 * (uint64_t)(x.nr + x.nw) + kb + 7) & ~uint64_t(7);
         }
     };
-    auto run = [&](auto f) {  // f(worker) on N threads, the caller's one of them
-        std::vector<std::thread> th;
-        th.reserve(N - 1);
-        for (int w = 1; w < N; w++) th.emplace_back(f, w);
-        f(0);
-        for (auto& x : th) x.join();
-    };
-    run([&](int w) {
-        for (int c = 0; c < C; c++) measure(pc[(size_t)c * N + w]);
-    });
-    uint64_t off = 0, keys = 0;
-    int64_t ro = 0, wo = 0;
-    for (Piece& q : pc) {
-        if (q.bad >= 0) {  // (the first refused transaction, in batch order)
-            bad_txn_ = q.bad;
-            return q.code;
-        }
-        q.off = off;
-        q.ro = ro;
-        q.wo = wo;
-        off += q.bytes;
-        keys += q.keys;
-        ro += q.reads;
-        wo += q.writes;
-    }
-    // (the record offsets after the records: finish() sends them with the rest)
-    const uint64_t need = off + 8 * (uint64_t)(T + 1) + 16;
-    int r;
-    if ((r = grow(T + 1, need))) return r;
-    uint64_t* toff = reinterpret_cast<uint64_t*>(pin_ + off);
-    std::vector<std::atomic<int>> done((size_t)C);
-    for (auto& d : done) d.store(0);
-    std::atomic<int> err{FDBCS_OK};
-    auto pack = [&](const Piece& q) {
+    auto pack = [&](const Piece& q, uint64_t* toff) {
         uint64_t o = q.off;
         int64_t R = q.ro, W = q.wo;
         for (int64_t t = q.t0; t < q.t1; t++) {
@@ -386,21 +454,65 @@ int TxnStage::pack_borrowed() {
             W += x.nw;
         }
     };
-    run([&](int w) {
+    // (phase flags: worker 0 publishes the placement, or an abort, once every
+    // worker has measured; the workers spin only inside this one region)
+    std::atomic<int> measured{0}, phase{0};  // phase: 1 placed, 2 abort
+    std::vector<std::atomic<int>> done((size_t)C);
+    for (auto& d : done) d.store(0, std::memory_order_relaxed);
+    int status = FDBCS_OK;
+    uint64_t total = 0, keys = 0;
+    auto body = [&](int w) {
+        if (w < N)
+            for (int c = 0; c < C; c++) measure(pc[(size_t)c * N + w]);
+        measured.fetch_add(1, std::memory_order_acq_rel);
+        if (w != 0) {
+            int ph;
+            while ((ph = phase.load(std::memory_order_acquire)) == 0) _mm_pause();
+            if (ph != 1 || w >= N) return;
+        } else {
+            const int all = pool_ ? pool_->size() : 1;
+            while (measured.load(std::memory_order_acquire) < all) _mm_pause();
+            uint64_t off = 0;
+            int64_t ro = 0, wo = 0;
+            for (Piece& q : pc) {
+                if (q.bad >= 0) {  // (the first refused transaction, in batch order)
+                    bad_txn_ = q.bad;
+                    status = q.code;
+                    break;
+                }
+                q.off = off;
+                q.ro = ro;
+                q.wo = wo;
+                off += q.bytes;
+                keys += q.keys;
+                ro += q.reads;
+                wo += q.writes;
+            }
+            // (the record offsets after the records: finish() sends them with the rest)
+            if (status == FDBCS_OK) status = grow(T + 1, off + 8 * (uint64_t)(T + 1) + 16);
+            if (status != FDBCS_OK) {
+                phase.store(2, std::memory_order_release);
+                return;
+            }
+            total = off;
+            phase.store(1, std::memory_order_release);
+        }
         for (int c = 0; c < C; c++) {
-            pack(pc[(size_t)c * N + w]);
+            pack(pc[(size_t)c * N + w], reinterpret_cast<uint64_t*>(pin_ + total));  // (offsets after the records)
             done[c].fetch_add(1, std::memory_order_acq_rel);
             if (w != 0) continue;
-            // the caller's thread: this round to the device once every piece of it is written
+            // worker 0: this round to the device once every piece of it is written
             while (done[c].load(std::memory_order_acquire) < N) _mm_pause();
-            const uint64_t a = pc[(size_t)c * N].off, b = c + 1 < C ? pc[(size_t)(c + 1) * N].off : off;
+            const uint64_t a = pc[(size_t)c * N].off, b = c + 1 < C ? pc[(size_t)(c + 1) * N].off : total;
             if (b > a && hipMemcpyAsync(dev_ + a, pin_ + a, b - a, hipMemcpyHostToDevice, copy_) != hipSuccess)
-                err.store(FDBCS_E_HIP);
+                status = FDBCS_E_HIP;
         }
-    });
-    if (err.load()) return err.load();
-    used_ = off;
-    sent_ = off;  // (finish() sends the offsets and makes the engine's stream wait for the copies)
+    };
+    if (pool_) pool_->run(body);
+    else body(0);
+    if (status != FDBCS_OK) return status;
+    used_ = total;
+    sent_ = total;  // (finish() sends the offsets and makes the engine's stream wait for the copies)
     K_ = keys;
     toff_in_stream_ = true;
     return FDBCS_OK;
@@ -420,7 +532,11 @@ int TxnStage::skip(int32_t n) {
     if (n < 0) return FDBCS_E_ARG;
     if (T_ + n > MAX_T) return FDBCS_E_CAPACITY;
     if (borrow_) {
-        brec_.insert(brec_.end(), (size_t)n, BorrowRec{0, nullptr, nullptr, 0, 0});
+        if (T_ + n > brec_cap_) {
+            const int r = grow_brec(T_ + n);
+            if (r) return r;
+        }
+        std::fill(brec_ + T_, brec_ + T_ + n, BorrowRec{0, nullptr, nullptr, 0, 0});
         T_ += n;
         return FDBCS_OK;
     }
@@ -526,8 +642,8 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
     if (borrow_) {
+        _mm_sfence();  // (the adds' non-temporal stores, before the workers read them)
         const int r = pack_borrowed();
-        brec_.clear();
         if (r) return r;
     }
     bool go_live = false;
