@@ -985,8 +985,11 @@ bool live_enabled() {
 // from an earlier batch, an unsharded set, small batches, no stage timing.
 void live_begin(fdbcs* cs) {
     cs->lv_lm = false;
+    // (a borrowed batch goes live with helper threads packing it, unless
+    // FDBCS_BORROW_LIVE=0: then it is packed at detect, pack_borrowed)
+    static const bool borrow_live = !(getenv("FDBCS_BORROW_LIVE") && !atoi(getenv("FDBCS_BORROW_LIVE")));
     if (!live_enabled() || cs->timing || !cs->have_quantiles || cs->lv_prev_T <= 0 || cs->sparse_edges ||
-        cs->st.borrowing() ||
+        (cs->st.borrowing() && !borrow_live) ||
         (cs->h.shard.has_lo | cs->h.shard.has_hi))
         return;
     auto up = [](int64_t x) { return x + x / 4 + 256; };
@@ -1504,7 +1507,16 @@ int fdbcs_batch_detect(fdbcs* cs, int64_t now, int64_t new_oldest, uint8_t* verd
     cs->last_wbase = 0;
     int r;
     fdbcs_batch_view dv;
-    if ((r = cs->st.finish(dv, &cs->b.staged))) return r;
+    if ((r = cs->st.finish(dv, &cs->b.staged))) {
+        // (a borrowed batch refused at detect: whatever a live kernel did for it is undone, as a cancel's)
+        if (cs->st.began_live()) {
+            cs->b.lv_wbase = 0;
+            cs->b.lv_nb1 = 0;
+            cs->b.staged = StagedBatch{};
+            launch_live_reset(cs->b, cs->sc, (int)(cs->sorts & 1), cs->stream);
+        }
+        return r;
+    }
     cs->stage_key_total = cs->st.key_total();
     cs->lv_prev_T = dv.txn_count;  // (the next batch's live capacities)
     cs->lv_prev_R = dv.read_count;

@@ -57,6 +57,11 @@ class TxnStage {
     // a borrowed batch refused at finish(): the first transaction whose
     // ranges the add would have refused (-1: none)
     int64_t refused_at() const { return bad_txn_; }
+    // this batch began live (begin_live): a refused one must have the live
+    // kernel's partial work undone (the engine's k_live_reset)
+    bool began_live() const { return began_live_; }
+    // a live batch that borrows: helper threads pack it while the adds go on
+    bool live_borrowed() const { return lb_; }
     // Live ingest: after begin(), make this batch live --
     // the stream, offsets and view sized for `caps`, the progress words reset
     // -- before the engine launches k_live_ingest over them.  The adds then
@@ -113,6 +118,18 @@ class TxnStage {
     static bool pull_rest();
     int pack_borrowed();
     void drop_pool();
+    // Live borrowed batches (begin_live after begin(true)): the caller's adds
+    // record pointers; helper threads of the pool take chunks of LB_CHUNK
+    // transactions as they are added, check and pack them into the stream in
+    // chunk order and publish them to the live kernel -- the copy and the
+    // checks leave the caller's thread, and the device still encodes the
+    // batch during the adds.
+    struct LbShared;
+    LbShared* lbs_ = nullptr;
+    bool lb_ = false;
+    bool began_live_ = false;
+    void lb_work();
+    void lb_abandon();  // stop the helpers; the batch goes on as a plain borrowed one
     HostPool* pool_ = nullptr;  // created at the first borrowed batch large enough to share
     struct BorrowRec {
         int64_t snap;

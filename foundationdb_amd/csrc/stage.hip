@@ -36,248 +36,6 @@ using fdbcs_pack::put_ranges;
 
 }  // namespace
 
-void TxnStage::sync() {
-    if (copy_) hipStreamSynchronize(copy_);
-    if (stream_) hipStreamSynchronize(stream_);
-}
-
-void TxnStage::release() {
-    live_cancel();  // (a live kernel waiting for this batch leaves: the syncs below return)
-    sync();
-    drop_pool();
-    free(brec_);
-    brec_ = nullptr;
-    brec_cap_ = 0;
-    auto free_host_or_dev = [this](void* p) {
-        if (!p) return;
-        if (bar_) hipFree(p);
-        else hipHostFree(p);
-    };
-    free_host_or_dev(pin_);
-    if (dev_ && dev_ != pin_) hipFree(dev_);
-    if (view_) hipFree(view_);
-    if (copied_) hipEventDestroy(copied_);
-    free_host_or_dev(toff_);
-    free_host_or_dev(prog_);
-    pin_ = dev_ = view_ = nullptr;
-    toff_ = toff_dev_ = nullptr;
-    prog_ = prog_dev_ = nullptr;
-    live_ = false;
-    copied_ = nullptr;
-    cap_ = view_cap_ = 0;
-    toff_cap_ = 0;
-    stream_ = copy_ = nullptr;
-    open_ = false;
-}
-
-int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
-    stream_ = stream;
-    copy_ = copy;
-    chunk_ = std::max<uint64_t>(4096, chunk);
-    if (const char* e = getenv("FDBCS_STAGE_EARLY")) early_ = strtoull(e, nullptr, 0);
-    if (const char* e = getenv("FDBCS_LIVE_PUB")) pub_every_ = std::max<int64_t>(8, strtoll(e, nullptr, 0));  // (default 16)
-    if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
-    if (!prog_) {
-        // FDBCS_STAGE_BAR=1 (A/B): the stream in device memory the host writes
-        // through the large BAR (fine-grained, uncached on the device): the
-        // kernels read it from HBM, no copies.  Measured at config 2: detect
-        // ~6 us shorter, but the adds' small write-combined stores over PCIe
-        // took 245-270 us per batch against 192 into pinned host memory, so
-        // the default stays pinned host memory (chunk copies / live reads).
-        const bool bar = getenv("FDBCS_STAGE_BAR") && atoi(getenv("FDBCS_STAGE_BAR"));
-        bar_ = bar && hipExtMallocWithFlags((void**)&prog_, 64, hipDeviceMallocUncached) == hipSuccess;
-        if (bar_) {
-            volatile uint64_t* w = prog_;
-            for (int i = 0; i < 8; i++) w[i] = 0;  // (the host's store through the BAR: it works or faults here)
-            _mm_sfence();
-            prog_dev_ = prog_;
-        } else {
-            if (hipHostMalloc((void**)&prog_, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-                return FDBCS_E_NOMEM;
-            memset(prog_, 0, 64);
-            if (hipHostGetDevicePointer((void**)&prog_dev_, prog_, 0) != hipSuccess) return FDBCS_E_HIP;
-        }
-    }
-    return FDBCS_OK;
-}
-
-int TxnStage::begin(bool borrow) {
-    live_cancel();  // (a batch begun and never detected)
-    borrow_ = borrow;
-    bad_txn_ = -1;
-    toff_in_stream_ = false;
-    T_ = R_ = W_ = 0;
-    K_ = 0;
-    used_ = sent_ = 0;
-    chunk_sent_ = false;
-    live_ = live_broken_ = false;
-    if (!pin_) {
-        int r = grow(8192, 4 << 20);
-        if (r) return r;
-    }
-    open_ = true;
-    return FDBCS_OK;
-}
-
-// Grow the offsets and / or the stream.  Chunks already sent went to the old
-// device buffer: the whole stream is sent again (sent_ = 0).
-int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
-    if (need_txns > toff_cap_ || need_bytes > cap_) {
-        live_cancel();  // (the live kernel reads the old buffers: it leaves first)
-        sync();         // copies in flight read the old buffers
-    }
-    if (bar_) return grow_bar(need_txns, need_bytes);
-    if (need_txns > toff_cap_) {
-        const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
-        uint64_t* nt = nullptr;
-        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, stream_flags((uint64_t)nc * 8)) != hipSuccess)
-            return FDBCS_E_NOMEM;
-        toff_live_ = (uint64_t)nc * 8 <= LIVE_STREAM_MAX;
-        if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
-        if (toff_) hipHostFree(toff_);
-        toff_ = nt;
-        toff_cap_ = nc;
-        if (hipHostGetDevicePointer((void**)&toff_dev_, toff_, 0) != hipSuccess) return FDBCS_E_HIP;
-    }
-    if (need_bytes > cap_) {
-        const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
-        uint8_t* np = nullptr;
-        // (coherent: the live kernel reads the records over PCIe as they are
-        // written, which a device-cached line of a half-written record would break)
-        if (hipHostMalloc((void**)&np, nc, stream_flags(nc)) != hipSuccess)
-            return FDBCS_E_NOMEM;
-        pin_live_ = nc <= LIVE_STREAM_MAX;
-        if (used_) memcpy(np, pin_, used_);
-        if (pin_) hipHostFree(pin_);
-        pin_ = np;
-        if (hipHostGetDevicePointer((void**)&pin_dev_, pin_, 0) != hipSuccess) return FDBCS_E_HIP;
-        if (dev_) hipFree(dev_);
-        dev_ = nullptr;
-        cap_ = 0;
-        if (hipMalloc((void**)&dev_, nc) != hipSuccess) return FDBCS_E_NOMEM;
-        cap_ = nc;
-        sent_ = 0;
-    }
-    return FDBCS_OK;
-}
-
-// The BAR stream: device memory, grown by a device-to-device copy (the host
-// never reads it back: reads through the BAR are uncached PCIe round trips).
-int TxnStage::grow_bar(int64_t need_txns, uint64_t need_bytes) {
-    if (need_txns > toff_cap_) {
-        const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
-        uint64_t* nt = nullptr;
-        if (hipExtMallocWithFlags((void**)&nt, (size_t)nc * 8, hipDeviceMallocUncached) != hipSuccess)
-            return FDBCS_E_NOMEM;
-        if (T_) {
-            _mm_sfence();
-            if (hipMemcpy(nt, toff_, (size_t)T_ * 8, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
-        }
-        if (toff_) hipFree(toff_);
-        toff_ = toff_dev_ = nt;
-        toff_cap_ = nc;
-        toff_live_ = true;
-    }
-    if (need_bytes > cap_) {
-        const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
-        uint8_t* np = nullptr;
-        if (hipExtMallocWithFlags((void**)&np, nc, hipDeviceMallocUncached) != hipSuccess) return FDBCS_E_NOMEM;
-        if (used_) {
-            _mm_sfence();
-            if (hipMemcpy(np, pin_, used_, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
-        }
-        if (pin_) hipFree(pin_);
-        pin_ = pin_dev_ = dev_ = np;
-        cap_ = nc;
-        pin_live_ = true;
-    }
-    return FDBCS_OK;
-}
-
-int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw) {
-    if (!open_) return FDBCS_E_STATE;
-    if (nr < 0 || nw < 0 || (nr && !reads) || (nw && !writes)) return FDBCS_E_ARG;
-    if (T_ >= MAX_T || R_ + nr > INT32_MAX / 2 || W_ + nw > INT32_MAX / 2) return FDBCS_E_CAPACITY;
-    if (borrow_) {  // (checked and packed at finish: pack_borrowed)
-        if (T_ >= brec_cap_) {
-            const int r = grow_brec(T_ + 1);
-            if (r) return r;
-        }
-        __m128i* d = reinterpret_cast<__m128i*>(brec_ + T_);
-        _mm_stream_si128(d, _mm_set_epi64x((long long)(uintptr_t)reads, (long long)snap));
-        _mm_stream_si128(d + 1, _mm_set_epi64x((long long)(((uint64_t)(uint32_t)nw << 32) | (uint32_t)nr),
-                                               (long long)(uintptr_t)writes));
-        T_++;
-        R_ += nr;
-        W_ += nw;
-        return FDBCS_OK;
-    }
-    const int n = nr + nw;
-    if (n == 0) {  // no record: the offset entry says so (kernels.h STAGE_EMPTY)
-        if (T_ + 1 > toff_cap_ || used_ + 8 * (uint64_t)(T_ + 1) + 16 > cap_) {
-            int r = grow(T_ + 1, used_ + 8 * (uint64_t)(T_ + 1) + 16);
-            if (r) return r;
-        }
-        toff_[T_++] = STAGE_EMPTY | ((uint64_t)W_ << 32) | (uint64_t)R_;
-        return FDBCS_OK;
-    }
-    uint64_t kbytes = 0;
-    uint32_t longest = 0;
-    // (the keys are requested here, all at once, and read in the copy pass)
-    for (int i = 0; i < nr; i++) {
-        kbytes += (uint64_t)reads[i].begin_len + reads[i].end_len;
-        longest = std::max({longest, reads[i].begin_len, reads[i].end_len});
-        __builtin_prefetch(reads[i].begin);
-        __builtin_prefetch(reads[i].end);
-    }
-    for (int i = 0; i < nw; i++) {
-        kbytes += (uint64_t)writes[i].begin_len + writes[i].end_len;
-        longest = std::max({longest, writes[i].begin_len, writes[i].end_len});
-        __builtin_prefetch(writes[i].begin);
-        __builtin_prefetch(writes[i].end);
-    }
-    if (longest > FDBCS_MAX_KEY) return FDBCS_E_KEY;
-    const uint64_t rec = (sizeof(StageHdr) + 8 * (uint64_t)n + kbytes + 7) & ~uint64_t(7);
-    // (room for the record offsets appended at finish)
-    const uint64_t need = used_ + rec + 8 * (uint64_t)(T_ + 1) + 16;
-    if (T_ + 1 > toff_cap_ || need > cap_) {
-        int r = grow(T_ + 1, need);
-        if (r) return r;
-    }
-    // one pass: check begin < end and copy, reads then writes
-    uint8_t* p = pin_ + used_;
-    StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
-    uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)n;
-    bool bad = put_ranges<StageRange, STAGE_SHARED>(reads, nr, ent, p, kp);
-    bad |= put_ranges<StageRange, STAGE_SHARED>(writes, nw, ent + nr, p, kp);
-    if (bad) return FDBCS_E_RANGE;  // (the record is not committed: used_ stays)
-    const uint64_t rec_used = ((uint64_t)(kp - p) + 7) & ~uint64_t(7);  // (<= rec: point ranges share bytes)
-    const StageHdr h{snap, (int32_t)R_, (int32_t)W_, nr, nw};
-    memcpy(p, &h, sizeof h);
-    toff_[T_] = used_;
-    used_ += rec_used;
-    T_++;
-    K_ += kbytes;
-    R_ += nr;
-    W_ += nw;
-    if (live_) {
-        live_check();
-        if (!live_broken_) return FDBCS_OK;  // (no chunk copies: the live kernel reads the stream itself)
-    }
-    if (bar_) return FDBCS_OK;  // (the stream is in device memory already)
-    // a chunk every chunk_ bytes, and one more `early_` bytes before where the
-    // previous batch ended (batches are alike): detectConflicts then sends
-    // only that much and the record offsets
-    if (used_ - sent_ >= chunk_ || (used_ >= early_at_ && sent_ < early_at_)) {
-        if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
-            return FDBCS_E_HIP;
-        sent_ = used_;
-        chunk_sent_ = true;
-        if (pull_rest() && hipEventRecord(copied_, copy_) != hipSuccess) return FDBCS_E_HIP;
-    }
-    return FDBCS_OK;
-}
-
 // ---- borrowed batches ----------------------------------------------------------
 // finish() of a borrowed batch: the records the adds would have written, made
 // on host threads from the caller's range arrays (still valid: the caller
@@ -319,14 +77,22 @@ class HostPool {
     int size() const { return n_; }
     // f(worker) on every worker, the caller's thread as worker 0
     void run(const std::function<void(int)>& f) {
-        left_.store(n_ - 1, std::memory_order_relaxed);
+        start(&f, n_);
+        f(0);
+        wait();
+    }
+    // f(w) on workers 1 .. n-1, returning at once (*f must outlive wait())
+    void start(const std::function<void(int)>* f, int n) {
+        left_.store(n - 1, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> g(mu_);
-            f_ = &f;
+            f_ = f;
+            active_ = n;
             gen_++;
         }
         cv_.notify_all();
-        f(0);
+    }
+    void wait() {
         while (left_.load(std::memory_order_acquire) > 0) _mm_pause();
     }
 
@@ -335,13 +101,16 @@ class HostPool {
         uint64_t seen = 0;
         for (;;) {
             const std::function<void(int)>* f;
+            int active;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return gen_ != seen; });
                 seen = gen_;
                 if (quit_) return;
                 f = f_;
+                active = active_;
             }
+            if (w >= active) continue;
             (*f)(w);
             left_.fetch_sub(1, std::memory_order_acq_rel);
         }
@@ -352,6 +121,7 @@ class HostPool {
     std::condition_variable cv_;
     uint64_t gen_ = 0;
     bool quit_ = false;
+    int active_ = 0;
     const std::function<void(int)>* f_ = nullptr;
     std::atomic<int> left_{0};
 };
@@ -372,6 +142,158 @@ int64_t borrow_grain() {
 }
 }  // namespace
 
+// ---- live borrowed batches -------------------------------------------------------
+namespace {
+constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes at once
+int lb_helpers() {  // FDBCS_LB_HELPERS (default 4)
+    static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 4;
+    return n;
+}
+}  // namespace
+
+struct TxnStage::LbShared {
+    alignas(64) std::atomic<int64_t> added{0};  // transactions added (the caller publishes whole chunks)
+    alignas(64) std::atomic<int> fin{0};        // the caller is in finish(): `added` is final
+    alignas(64) std::atomic<int64_t> next{0};   // the next chunk a helper takes
+    alignas(64) std::atomic<int64_t> ticket{0}; // the chunk whose stream bytes are reserved next
+    uint64_t cursor = 0;                        // stream bytes reserved (the ticket's holder only)
+    alignas(64) std::atomic<int> stop{0};       // refused, over a capacity, or abandoned: helpers leave
+    std::atomic<int> broken{0};                 // over the stream or key-byte capacity (finish repacks)
+    std::atomic<int64_t> bad{INT64_MAX};        // the first refused transaction
+    std::atomic<int> code{FDBCS_OK};
+    std::atomic<uint64_t> keys{0};
+    std::mutex pub_mu;
+    int64_t pub = 0;                            // chunks published (pub_mu)
+    int64_t nchunks = 0;
+    std::unique_ptr<std::atomic<uint8_t>[]> done;
+    std::vector<uint64_t> end;                  // per chunk: its reserved bytes' end (a fresh line after)
+    std::vector<int64_t> tend;                  // per chunk: its last transaction + 1
+    std::vector<int64_t> ro, wo;                // per chunk: reads / writes before it (the caller writes these)
+    std::function<void(int)> fn;
+    void reset(int64_t n) {
+        added.store(0);
+        fin.store(0);
+        next.store(0);
+        ticket.store(0);
+        cursor = 0;
+        stop.store(0);
+        broken.store(0);
+        bad.store(INT64_MAX);
+        code.store(FDBCS_OK);
+        keys.store(0);
+        pub = 0;
+        if (n > nchunks) {
+            done.reset(new std::atomic<uint8_t>[(size_t)n]);
+            end.resize((size_t)n);
+            tend.resize((size_t)n);
+            ro.resize((size_t)n);
+            wo.resize((size_t)n);
+            nchunks = n;
+        }
+        for (int64_t k = 0; k < nchunks; k++) done[k].store(0, std::memory_order_relaxed);
+    }
+};
+
+// One helper: chunks in the order taken; each measured (and checked), its
+// stream bytes reserved in chunk order (so the published bytes stay a
+// prefix, each chunk starting on a fresh 128-byte line: pad_published's rule),
+// packed, then the prefix of finished chunks published.
+void TxnStage::lb_work() {
+    LbShared& S = *lbs_;
+    const BorrowRec* br = brec_;
+    for (;;) {
+        const int64_t k = S.next.fetch_add(1, std::memory_order_relaxed);
+        const int64_t t0 = k * LB_CHUNK;
+        int64_t t1;
+        for (;;) {  // until the chunk is whole (or the batch ends inside it)
+            if (S.stop.load(std::memory_order_acquire)) return;
+            const int64_t a = S.added.load(std::memory_order_acquire);
+            if (a >= t0 + LB_CHUNK) {
+                t1 = t0 + LB_CHUNK;
+                break;
+            }
+            if (S.fin.load(std::memory_order_acquire)) {
+                t1 = std::min(t0 + LB_CHUNK, S.added.load(std::memory_order_acquire));
+                break;
+            }
+            _mm_pause();
+        }
+        if (t1 <= t0 || k >= S.nchunks) return;  // (past the batch's end)
+        uint64_t bytes = 0, keys = 0;
+        for (int64_t t = t0; t < t1; t++) {
+            const BorrowRec& x = br[t];
+            if (x.nr + x.nw == 0) continue;
+            int st;
+            const uint64_t kb = fdbcs_pack::ranges_bytes<0>(x.rd, x.nr, x.wr, x.nw, st);
+            if (st != FDBCS_OK) {
+                int64_t b = S.bad.load();
+                while (t < b && !S.bad.compare_exchange_weak(b, t)) {
+                }
+                if (S.bad.load() == t) S.code.store(st);
+                S.stop.store(1, std::memory_order_release);
+                return;
+            }
+            for (int i = 0; i < x.nr; i++) keys += (uint64_t)x.rd[i].begin_len + x.rd[i].end_len;
+            for (int i = 0; i < x.nw; i++) keys += (uint64_t)x.wr[i].begin_len + x.wr[i].end_len;
+            bytes += (sizeof(StageHdr) + 8 * (uint64_t)(x.nr + x.nw) + kb + 7) & ~uint64_t(7);
+        }
+        while (S.ticket.load(std::memory_order_acquire) != k) {
+            if (S.stop.load(std::memory_order_acquire)) return;
+            _mm_pause();
+        }
+        const uint64_t off = S.cursor;
+        const uint64_t nxt = (off + bytes + 16 + 127) & ~uint64_t(127);
+        const bool over = nxt + 8 * ((uint64_t)lcaps_.T + 1) + 16 > cap_ ||
+                          S.keys.fetch_add(keys, std::memory_order_relaxed) + keys > lcaps_.key_bytes;
+        if (over) {
+            S.broken.store(1);
+            S.stop.store(1, std::memory_order_release);
+            return;
+        }
+        S.cursor = nxt;
+        S.end[k] = nxt;
+        S.tend[k] = t1;
+        S.ticket.store(k + 1, std::memory_order_release);
+        uint64_t o = off;
+        int64_t R = S.ro[k], W = S.wo[k];
+        for (int64_t t = t0; t < t1; t++) {
+            const BorrowRec& x = br[t];
+            if (x.nr + x.nw == 0) {
+                toff_[t] = STAGE_EMPTY | ((uint64_t)W << 32) | (uint64_t)R;
+                continue;
+            }
+            uint8_t* p = pin_ + o;
+            StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
+            uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)(x.nr + x.nw);
+            fdbcs_pack::put_ranges<StageRange, STAGE_SHARED, 0>(x.rd, x.nr, ent, p, kp);
+            fdbcs_pack::put_ranges<StageRange, STAGE_SHARED, 0>(x.wr, x.nw, ent + x.nr, p, kp);
+            const StageHdr h{x.snap, (int32_t)R, (int32_t)W, x.nr, x.nw};
+            memcpy(p, &h, sizeof h);
+            toff_[t] = o;
+            o += ((uint64_t)(kp - p) + 7) & ~uint64_t(7);
+            R += x.nr;
+            W += x.nw;
+        }
+        S.done[k].store(1, std::memory_order_release);
+        std::lock_guard<std::mutex> g(S.pub_mu);  // the finished prefix to the live kernel (publish()'s word)
+        int64_t p = S.pub;
+        while (p < S.nchunks && S.done[p].load(std::memory_order_acquire)) p++;
+        if (p > S.pub) {
+            S.pub = p;
+            if (bar_) _mm_sfence();
+            __atomic_store_n(&prog_[0], S.end[p - 1] << 20 | (uint64_t)S.tend[p - 1], __ATOMIC_RELEASE);
+        }
+    }
+}
+
+void TxnStage::lb_abandon() {
+    if (!lb_) return;
+    lbs_->stop.store(1, std::memory_order_release);
+    pool_->wait();
+    lb_ = false;
+    live_cancel();
+}
+
 int TxnStage::grow_brec(int64_t need) {
     static_assert(sizeof(BorrowRec) == 32 && offsetof(BorrowRec, rd) == 8 && offsetof(BorrowRec, wr) == 16 &&
                       offsetof(BorrowRec, nr) == 24 && offsetof(BorrowRec, nw) == 28,
@@ -388,8 +310,11 @@ int TxnStage::grow_brec(int64_t need) {
 }
 
 void TxnStage::drop_pool() {
+    if (lb_) lb_abandon();
     delete pool_;
     pool_ = nullptr;
+    delete lbs_;
+    lbs_ = nullptr;
 }
 
 int TxnStage::pack_borrowed() {
@@ -518,6 +443,263 @@ int TxnStage::pack_borrowed() {
     return FDBCS_OK;
 }
 
+void TxnStage::sync() {
+    if (copy_) hipStreamSynchronize(copy_);
+    if (stream_) hipStreamSynchronize(stream_);
+}
+
+void TxnStage::release() {
+    live_cancel();  // (a live kernel waiting for this batch leaves: the syncs below return)
+    sync();
+    drop_pool();
+    free(brec_);
+    brec_ = nullptr;
+    brec_cap_ = 0;
+    auto free_host_or_dev = [this](void* p) {
+        if (!p) return;
+        if (bar_) hipFree(p);
+        else hipHostFree(p);
+    };
+    free_host_or_dev(pin_);
+    if (dev_ && dev_ != pin_) hipFree(dev_);
+    if (view_) hipFree(view_);
+    if (copied_) hipEventDestroy(copied_);
+    free_host_or_dev(toff_);
+    free_host_or_dev(prog_);
+    pin_ = dev_ = view_ = nullptr;
+    toff_ = toff_dev_ = nullptr;
+    prog_ = prog_dev_ = nullptr;
+    live_ = false;
+    copied_ = nullptr;
+    cap_ = view_cap_ = 0;
+    toff_cap_ = 0;
+    stream_ = copy_ = nullptr;
+    open_ = false;
+}
+
+int TxnStage::configure(hipStream_t stream, hipStream_t copy, uint64_t chunk) {
+    stream_ = stream;
+    copy_ = copy;
+    chunk_ = std::max<uint64_t>(4096, chunk);
+    if (const char* e = getenv("FDBCS_STAGE_EARLY")) early_ = strtoull(e, nullptr, 0);
+    if (const char* e = getenv("FDBCS_LIVE_PUB")) pub_every_ = std::max<int64_t>(8, strtoll(e, nullptr, 0));  // (default 16)
+    if (!copied_ && hipEventCreateWithFlags(&copied_, hipEventDisableTiming) != hipSuccess) return FDBCS_E_HIP;
+    if (!prog_) {
+        // FDBCS_STAGE_BAR=1 (A/B): the stream in device memory the host writes
+        // through the large BAR (fine-grained, uncached on the device): the
+        // kernels read it from HBM, no copies.  Measured at config 2: detect
+        // ~6 us shorter, but the adds' small write-combined stores over PCIe
+        // took 245-270 us per batch against 192 into pinned host memory, so
+        // the default stays pinned host memory (chunk copies / live reads).
+        const bool bar = getenv("FDBCS_STAGE_BAR") && atoi(getenv("FDBCS_STAGE_BAR"));
+        bar_ = bar && hipExtMallocWithFlags((void**)&prog_, 64, hipDeviceMallocUncached) == hipSuccess;
+        if (bar_) {
+            volatile uint64_t* w = prog_;
+            for (int i = 0; i < 8; i++) w[i] = 0;  // (the host's store through the BAR: it works or faults here)
+            _mm_sfence();
+            prog_dev_ = prog_;
+        } else {
+            if (hipHostMalloc((void**)&prog_, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                return FDBCS_E_NOMEM;
+            memset(prog_, 0, 64);
+            if (hipHostGetDevicePointer((void**)&prog_dev_, prog_, 0) != hipSuccess) return FDBCS_E_HIP;
+        }
+    }
+    return FDBCS_OK;
+}
+
+int TxnStage::begin(bool borrow) {
+    live_cancel();  // (a batch begun and never detected)
+    if (lb_) lb_abandon();  // (a live borrowed batch begun and never detected)
+    borrow_ = borrow;
+    bad_txn_ = -1;
+    began_live_ = false;
+    toff_in_stream_ = false;
+    T_ = R_ = W_ = 0;
+    K_ = 0;
+    used_ = sent_ = 0;
+    chunk_sent_ = false;
+    live_ = live_broken_ = false;
+    if (!pin_) {
+        int r = grow(8192, 4 << 20);
+        if (r) return r;
+    }
+    open_ = true;
+    return FDBCS_OK;
+}
+
+// Grow the offsets and / or the stream.  Chunks already sent went to the old
+// device buffer: the whole stream is sent again (sent_ = 0).
+int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
+    if (need_txns > toff_cap_ || need_bytes > cap_) {
+        live_cancel();  // (the live kernel reads the old buffers: it leaves first)
+        sync();         // copies in flight read the old buffers
+    }
+    if (bar_) return grow_bar(need_txns, need_bytes);
+    if (need_txns > toff_cap_) {
+        const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
+        uint64_t* nt = nullptr;
+        if (hipHostMalloc((void**)&nt, (size_t)nc * 8, stream_flags((uint64_t)nc * 8)) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        toff_live_ = (uint64_t)nc * 8 <= LIVE_STREAM_MAX;
+        if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
+        if (toff_) hipHostFree(toff_);
+        toff_ = nt;
+        toff_cap_ = nc;
+        if (hipHostGetDevicePointer((void**)&toff_dev_, toff_, 0) != hipSuccess) return FDBCS_E_HIP;
+    }
+    if (need_bytes > cap_) {
+        const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
+        uint8_t* np = nullptr;
+        // (coherent: the live kernel reads the records over PCIe as they are
+        // written, which a device-cached line of a half-written record would break)
+        if (hipHostMalloc((void**)&np, nc, stream_flags(nc)) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        pin_live_ = nc <= LIVE_STREAM_MAX;
+        if (used_) memcpy(np, pin_, used_);
+        if (pin_) hipHostFree(pin_);
+        pin_ = np;
+        if (hipHostGetDevicePointer((void**)&pin_dev_, pin_, 0) != hipSuccess) return FDBCS_E_HIP;
+        if (dev_) hipFree(dev_);
+        dev_ = nullptr;
+        cap_ = 0;
+        if (hipMalloc((void**)&dev_, nc) != hipSuccess) return FDBCS_E_NOMEM;
+        cap_ = nc;
+        sent_ = 0;
+    }
+    return FDBCS_OK;
+}
+
+// The BAR stream: device memory, grown by a device-to-device copy (the host
+// never reads it back: reads through the BAR are uncached PCIe round trips).
+int TxnStage::grow_bar(int64_t need_txns, uint64_t need_bytes) {
+    if (need_txns > toff_cap_) {
+        const int64_t nc = std::max<int64_t>(need_txns, 2 * toff_cap_);
+        uint64_t* nt = nullptr;
+        if (hipExtMallocWithFlags((void**)&nt, (size_t)nc * 8, hipDeviceMallocUncached) != hipSuccess)
+            return FDBCS_E_NOMEM;
+        if (T_) {
+            _mm_sfence();
+            if (hipMemcpy(nt, toff_, (size_t)T_ * 8, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
+        }
+        if (toff_) hipFree(toff_);
+        toff_ = toff_dev_ = nt;
+        toff_cap_ = nc;
+        toff_live_ = true;
+    }
+    if (need_bytes > cap_) {
+        const uint64_t nc = std::max<uint64_t>(need_bytes, 2 * cap_);
+        uint8_t* np = nullptr;
+        if (hipExtMallocWithFlags((void**)&np, nc, hipDeviceMallocUncached) != hipSuccess) return FDBCS_E_NOMEM;
+        if (used_) {
+            _mm_sfence();
+            if (hipMemcpy(np, pin_, used_, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
+        }
+        if (pin_) hipFree(pin_);
+        pin_ = pin_dev_ = dev_ = np;
+        cap_ = nc;
+        pin_live_ = true;
+    }
+    return FDBCS_OK;
+}
+
+int TxnStage::add(int64_t snap, const fdbcs_range* reads, int32_t nr, const fdbcs_range* writes, int32_t nw) {
+    if (!open_) return FDBCS_E_STATE;
+    if (nr < 0 || nw < 0 || (nr && !reads) || (nw && !writes)) return FDBCS_E_ARG;
+    if (T_ >= MAX_T || R_ + nr > INT32_MAX / 2 || W_ + nw > INT32_MAX / 2) return FDBCS_E_CAPACITY;
+    if (lb_ && (T_ + 1 > lcaps_.T || R_ + nr > lcaps_.R || W_ + nw > lcaps_.W)) lb_abandon();  // (live caps)
+    if (lb_) {  // live borrowed: the helpers take whole chunks (lb_work)
+        if ((T_ & (LB_CHUNK - 1)) == 0) {
+            lbs_->ro[T_ / LB_CHUNK] = R_;
+            lbs_->wo[T_ / LB_CHUNK] = W_;
+        }
+        brec_[T_] = BorrowRec{snap, reads, writes, nr, nw};
+        T_++;
+        R_ += nr;
+        W_ += nw;
+        if ((T_ & (LB_CHUNK - 1)) == 0) lbs_->added.store(T_, std::memory_order_release);
+        return FDBCS_OK;
+    }
+    if (borrow_) {  // (checked and packed at finish: pack_borrowed)
+        if (T_ >= brec_cap_) {
+            const int r = grow_brec(T_ + 1);
+            if (r) return r;
+        }
+        __m128i* d = reinterpret_cast<__m128i*>(brec_ + T_);
+        _mm_stream_si128(d, _mm_set_epi64x((long long)(uintptr_t)reads, (long long)snap));
+        _mm_stream_si128(d + 1, _mm_set_epi64x((long long)(((uint64_t)(uint32_t)nw << 32) | (uint32_t)nr),
+                                               (long long)(uintptr_t)writes));
+        T_++;
+        R_ += nr;
+        W_ += nw;
+        return FDBCS_OK;
+    }
+    const int n = nr + nw;
+    if (n == 0) {  // no record: the offset entry says so (kernels.h STAGE_EMPTY)
+        if (T_ + 1 > toff_cap_ || used_ + 8 * (uint64_t)(T_ + 1) + 16 > cap_) {
+            int r = grow(T_ + 1, used_ + 8 * (uint64_t)(T_ + 1) + 16);
+            if (r) return r;
+        }
+        toff_[T_++] = STAGE_EMPTY | ((uint64_t)W_ << 32) | (uint64_t)R_;
+        return FDBCS_OK;
+    }
+    uint64_t kbytes = 0;
+    uint32_t longest = 0;
+    // (the keys are requested here, all at once, and read in the copy pass)
+    for (int i = 0; i < nr; i++) {
+        kbytes += (uint64_t)reads[i].begin_len + reads[i].end_len;
+        longest = std::max({longest, reads[i].begin_len, reads[i].end_len});
+        __builtin_prefetch(reads[i].begin);
+        __builtin_prefetch(reads[i].end);
+    }
+    for (int i = 0; i < nw; i++) {
+        kbytes += (uint64_t)writes[i].begin_len + writes[i].end_len;
+        longest = std::max({longest, writes[i].begin_len, writes[i].end_len});
+        __builtin_prefetch(writes[i].begin);
+        __builtin_prefetch(writes[i].end);
+    }
+    if (longest > FDBCS_MAX_KEY) return FDBCS_E_KEY;
+    const uint64_t rec = (sizeof(StageHdr) + 8 * (uint64_t)n + kbytes + 7) & ~uint64_t(7);
+    // (room for the record offsets appended at finish)
+    const uint64_t need = used_ + rec + 8 * (uint64_t)(T_ + 1) + 16;
+    if (T_ + 1 > toff_cap_ || need > cap_) {
+        int r = grow(T_ + 1, need);
+        if (r) return r;
+    }
+    // one pass: check begin < end and copy, reads then writes
+    uint8_t* p = pin_ + used_;
+    StageRange* ent = reinterpret_cast<StageRange*>(p + sizeof(StageHdr));
+    uint8_t* kp = p + sizeof(StageHdr) + sizeof(StageRange) * (size_t)n;
+    bool bad = put_ranges<StageRange, STAGE_SHARED>(reads, nr, ent, p, kp);
+    bad |= put_ranges<StageRange, STAGE_SHARED>(writes, nw, ent + nr, p, kp);
+    if (bad) return FDBCS_E_RANGE;  // (the record is not committed: used_ stays)
+    const uint64_t rec_used = ((uint64_t)(kp - p) + 7) & ~uint64_t(7);  // (<= rec: point ranges share bytes)
+    const StageHdr h{snap, (int32_t)R_, (int32_t)W_, nr, nw};
+    memcpy(p, &h, sizeof h);
+    toff_[T_] = used_;
+    used_ += rec_used;
+    T_++;
+    K_ += kbytes;
+    R_ += nr;
+    W_ += nw;
+    if (live_) {
+        live_check();
+        if (!live_broken_) return FDBCS_OK;  // (no chunk copies: the live kernel reads the stream itself)
+    }
+    if (bar_) return FDBCS_OK;  // (the stream is in device memory already)
+    // a chunk every chunk_ bytes, and one more `early_` bytes before where the
+    // previous batch ended (batches are alike): detectConflicts then sends
+    // only that much and the record offsets
+    if (used_ - sent_ >= chunk_ || (used_ >= early_at_ && sent_ < early_at_)) {
+        if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, used_ - sent_, hipMemcpyHostToDevice, copy_) != hipSuccess)
+            return FDBCS_E_HIP;
+        sent_ = used_;
+        chunk_sent_ = true;
+        if (pull_rest() && hipEventRecord(copied_, copy_) != hipSuccess) return FDBCS_E_HIP;
+    }
+    return FDBCS_OK;
+}
+
 // FDBCS_PULL_REST=1: finish() has the engine's queue read the stream's rest
 // from the mapped pinned buffer (launch_pull) instead of a last SDMA copy and
 // a cross-queue event behind it (A/B knob: ~5 us per batch, within the
@@ -531,6 +713,7 @@ int TxnStage::skip(int32_t n) {
     if (!open_) return FDBCS_E_STATE;
     if (n < 0) return FDBCS_E_ARG;
     if (T_ + n > MAX_T) return FDBCS_E_CAPACITY;
+    lb_abandon();  // (runs of empty transactions: a plain borrowed batch from here)
     if (borrow_) {
         if (T_ + n > brec_cap_) {
             const int r = grow_brec(T_ + n);
@@ -633,14 +816,44 @@ int TxnStage::begin_live(const LiveCaps& caps) {
     if (bar_) _mm_sfence();
     lcaps_ = caps;
     next_pub_ = pub_every_;
+    if (borrow_) {  // live borrowed: the helpers, spinning until the first chunk is added
+        if (!pool_ && host_threads() > 1) pool_ = new HostPool(host_threads());
+        if (!pool_) return FDBCS_E_STATE;
+        if ((r = grow_brec((int64_t)caps.T + LB_CHUNK))) return r;
+        if (!lbs_) lbs_ = new LbShared();
+        lbs_->reset((int64_t)caps.T / LB_CHUNK + 2);
+        lbs_->fn = [this](int) { lb_work(); };
+        pool_->start(&lbs_->fn, 1 + std::min(lb_helpers(), pool_->size() - 1));
+        lb_ = true;
+    }
     live_ = true;
     live_broken_ = false;
+    began_live_ = true;
     return FDBCS_OK;
 }
 
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
     if (!open_) return FDBCS_E_STATE;
     open_ = false;
+    if (lb_) {  // live borrowed: the last chunks, then the batch is live, refused, or repacked whole
+        LbShared& S = *lbs_;
+        S.added.store(T_, std::memory_order_release);
+        S.fin.store(1, std::memory_order_release);
+        pool_->wait();
+        lb_ = false;
+        if (S.bad.load() != INT64_MAX) {
+            bad_txn_ = S.bad.load();
+            live_cancel();
+            return S.code.load();
+        }
+        if (S.stop.load()) {  // (over a capacity: repacked below, and ingested whole)
+            live_cancel();
+        } else {
+            used_ = S.cursor;
+            K_ = S.keys.load();
+            borrow_ = false;  // (the stream and the offsets are complete: finish as a copied batch)
+        }
+    }
     if (borrow_) {
         _mm_sfence();  // (the adds' non-temporal stores, before the workers read them)
         const int r = pack_borrowed();

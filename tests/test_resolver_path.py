@@ -289,3 +289,77 @@ def test_borrowed_large_batches_match_oracle(gpu):
     same_history(g, c)
     assert add_us[1] < 0.6 * add_us[0], add_us  # (borrowed adds record pointers only)
     g.close()
+
+
+@pytest.mark.parametrize("cfg,T,nb", [(2, 5000, 30), (3, 3000, 12), (4, 800, 8)])
+def test_borrowed_live_resolver_loop(gpu, cfg, T, nb):
+    """Borrowed batches in the steady state go live: the adds record pointers,
+    helper threads check and pack chunks of 64 transactions into the stream
+    while the adds go on, and the live kernel encodes them (stage.hip
+    lb_work).  The bench's native Resolver loop against the oracle; most
+    batches must have gone live."""
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    wl = Workload(cfg, txns=T)
+    run = wl.prepare_run(0, nb)
+    s0 = g.batch_stats()
+    us, add_us, verdicts = run.run(g)
+    s1 = g.batch_stats()
+    for i in range(nb):
+        b, now, nold = wl.batch(i)
+        vc = c.detect_packed(b, now, nold)
+        assert np.array_equal(verdicts[i], vc), (i, np.nonzero(verdicts[i] != vc)[0][:10])
+    same_history(g, c)
+    assert s1["live_batches"] - s0["live_batches"] >= nb - 3, (s0, s1)
+    g.close()
+
+
+def test_borrowed_live_fallbacks(gpu):
+    """Live borrowed batches that leave the live capacities -- twice the
+    transactions, then the same count with 150-byte keys (key bytes past the
+    cap), then a refused transaction in the middle of a live batch -- fall
+    back to the whole-batch ingest (or refuse the batch) and stay exact."""
+    from foundationdb_amd.batch import PackedBatch
+    import random
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    rng = random.Random(9)
+    now = 1000
+
+    def batch(n, klen):
+        txns = []
+        for _ in range(n):
+            def rr():
+                a = rng.randrange(20000)
+                k = (b"%08d" % a) * (klen // 8 + 1)
+                k = k[:klen]
+                return (k, k + b"\x00")
+            txns.append((now - rng.randint(1, 50), [rr() for _ in range(2)], [rr()]))
+        return txns
+
+    shapes = [(1000, 16)] * 4 + [(2000, 16), (2000, 16), (2000, 150), (2000, 16), (2000, 16)]
+    for n, klen in shapes:
+        now += 100
+        txns = batch(n, klen)
+        v = ConflictBatch_run(g, txns, now, now - 400)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, now - 400))
+        same_history(g, c)
+    # a refused transaction deep in a live batch: the batch fails, nothing changes, the next one is exact
+    before = g.dump_arrays()
+    now += 100
+    txns = batch(2000, 16)
+    b = ConflictBatch(g)
+    for i, (snap, reads, writes) in enumerate(txns):
+        b.add_transaction(reads if i != 1500 else [(b"zz", b"aa")], writes, snap)
+    with pytest.raises(FdbcsError) as e:
+        b.detect_conflicts(now, now - 400)
+    assert e.value.status == _abi.E_RANGE
+    assert g._lib.fdbcs_batch_refused_txn(g.handle) == 1500
+    assert all(np.array_equal(x, y) for x, y in zip(before, g.dump_arrays()))
+    for _ in range(3):
+        now += 100
+        txns = batch(2000, 16)
+        v = ConflictBatch_run(g, txns, now, now - 400)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, now - 400))
+    same_history(g, c)
+    g.close()
