@@ -145,9 +145,21 @@ int64_t borrow_grain() {
 // ---- live borrowed batches -------------------------------------------------------
 namespace {
 constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes at once
-int lb_helpers() {  // FDBCS_LB_HELPERS (default 4)
-    static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 4;
+int lb_helpers() {  // FDBCS_LB_HELPERS (default 8)
+    static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 8;
     return n;
+}
+// The caller's batch arrays are cold (a Resolver request arrives from the
+// network): the range entries of transaction t + 8 and the keys of t + 4 are
+// requested ahead, as the copying add does for its own keys.
+inline void lb_prefetch_ranges(const fdbcs_range* r, int n) {
+    for (int i = 0; i < n; i += 2) __builtin_prefetch(r + i);
+}
+inline void lb_prefetch_keys(const fdbcs_range* r, int n) {
+    for (int i = 0; i < n; i++) {
+        __builtin_prefetch(r[i].begin);
+        __builtin_prefetch(r[i].end);
+    }
 }
 }  // namespace
 
@@ -220,7 +232,19 @@ void TxnStage::lb_work() {
         }
         if (t1 <= t0 || k >= S.nchunks) return;  // (past the batch's end)
         uint64_t bytes = 0, keys = 0;
+        for (int64_t t = t0; t < std::min(t1, t0 + 8); t++) {
+            lb_prefetch_ranges(br[t].rd, br[t].nr);
+            lb_prefetch_ranges(br[t].wr, br[t].nw);
+        }
         for (int64_t t = t0; t < t1; t++) {
+            if (t + 8 < t1) {
+                lb_prefetch_ranges(br[t + 8].rd, br[t + 8].nr);
+                lb_prefetch_ranges(br[t + 8].wr, br[t + 8].nw);
+            }
+            if (t + 4 < t1) {
+                lb_prefetch_keys(br[t + 4].rd, br[t + 4].nr);
+                lb_prefetch_keys(br[t + 4].wr, br[t + 4].nw);
+            }
             const BorrowRec& x = br[t];
             if (x.nr + x.nw == 0) continue;
             int st;
