@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -69,7 +70,7 @@ class HostPool {
         {
             std::lock_guard<std::mutex> g(mu_);
             quit_ = true;
-            gen_++;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -88,7 +89,7 @@ class HostPool {
             std::lock_guard<std::mutex> g(mu_);
             f_ = f;
             active_ = n;
-            gen_++;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
     }
@@ -97,20 +98,39 @@ class HostPool {
     }
 
    private:
+    // A worker that just finished polls for the next job for a while before
+    // it sleeps: a Resolver's batches follow each other closely, and a
+    // sleeping thread's wake-up took longer than the adds it should overlap
+    // (config 2: ~25 us of adds; FDBCS_POOL_SPIN_US, default 2000).
+    static int64_t spin_ns() {
+        static const int64_t ns = 1000 * (getenv("FDBCS_POOL_SPIN_US") ? atoll(getenv("FDBCS_POOL_SPIN_US")) : 2000);
+        return ns;
+    }
     void loop(int w) {
         uint64_t seen = 0;
+        bool worked = false;  // (only the workers of the last job poll: the others sleep at once)
         for (;;) {
             const std::function<void(int)>* f;
             int active;
+            if (worked) {
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int it = 1; gen_.load(std::memory_order_acquire) == seen; it++) {
+                    _mm_pause();
+                    if ((it & 1023) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                std::chrono::steady_clock::now() - t0).count() > spin_ns())
+                        break;
+                }
+            }
             {
                 std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return gen_ != seen; });
-                seen = gen_;
+                cv_.wait(g, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+                seen = gen_.load(std::memory_order_relaxed);
                 if (quit_) return;
                 f = f_;
                 active = active_;
             }
-            if (w >= active) continue;
+            worked = w < active;
+            if (!worked) continue;
             (*f)(w);
             left_.fetch_sub(1, std::memory_order_acq_rel);
         }
@@ -119,7 +139,7 @@ class HostPool {
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_;
-    uint64_t gen_ = 0;
+    std::atomic<uint64_t> gen_{0};
     bool quit_ = false;
     int active_ = 0;
     const std::function<void(int)>* f_ = nullptr;
@@ -145,8 +165,8 @@ int64_t borrow_grain() {
 // ---- live borrowed batches -------------------------------------------------------
 namespace {
 constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes at once
-int lb_helpers() {  // FDBCS_LB_HELPERS (default 8)
-    static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 8;
+int lb_helpers() {  // FDBCS_LB_HELPERS (default 4: 4, 8 and 12 gave the same config-2 window)
+    static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 4;
     return n;
 }
 // The caller's batch arrays are cold (a Resolver request arrives from the
