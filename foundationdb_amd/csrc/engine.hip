@@ -985,19 +985,27 @@ bool live_enabled() {
 // from an earlier batch, an unsharded set, small batches, no stage timing.
 void live_begin(fdbcs* cs) {
     cs->lv_lm = false;
-    // (a borrowed batch goes live with helper threads packing it, unless
-    // FDBCS_BORROW_LIVE=0: then it is packed at detect, pack_borrowed)
-    static const bool borrow_live = !(getenv("FDBCS_BORROW_LIVE") && !atoi(getenv("FDBCS_BORROW_LIVE")));
-    if (!live_enabled() || cs->timing || !cs->have_quantiles || cs->lv_prev_T <= 0 || cs->sparse_edges ||
-        (cs->st.borrowing() && !borrow_live) ||
-        (cs->h.shard.has_lo | cs->h.shard.has_hi))
-        return;
     auto up = [](int64_t x) { return x + x / 4 + 256; };
     LiveCaps c{};
     c.T = (int32_t)std::min<int64_t>(up(cs->lv_prev_T), LARGE_T);
     c.R = (int32_t)up(cs->lv_prev_R);
     c.W = (int32_t)up(cs->lv_prev_W);
     c.key_bytes = cs->lv_prev_K + cs->lv_prev_K / 4 + 65536;
+    // A borrowed batch: helper threads pack it during the adds and copy it to
+    // the device as it grows (TxnStage::begin_helpers), and detectConflicts
+    // ingests it whole from device memory -- the live kernel's PCIe reads,
+    // no longer paced by the adds, were the slower way in.
+    // FDBCS_BORROW_LIVE=1: the helpers publish to the live kernel instead.
+    // (Large batches pack at detect on every host thread: pack_borrowed.)
+    const char* bl = getenv("FDBCS_BORROW_LIVE");  // (read per batch: tests switch it)
+    const bool borrow_live = bl && atoi(bl);
+    if (cs->st.borrowing() && !borrow_live) {
+        if (cs->lv_prev_T > 0 && !large_batch_mode(c.T) && !large_batch_mode(cs->lv_prev_T)) cs->st.begin_helpers(c);
+        return;
+    }
+    if (!live_enabled() || cs->timing || !cs->have_quantiles || cs->lv_prev_T <= 0 || cs->sparse_edges ||
+        (cs->h.shard.has_lo | cs->h.shard.has_hi))
+        return;
     if (large_batch_mode(c.T) || large_batch_mode(cs->lv_prev_T)) return;
     // the batch buffers at their final size before the kernel writes them (the
     // detect's ensure_batch must not move them): keys and the stream's bytes

@@ -62,6 +62,11 @@ class TxnStage {
     bool began_live() const { return began_live_; }
     // a live batch that borrows: helper threads pack it while the adds go on
     bool live_borrowed() const { return lb_; }
+    // A borrowed batch that does not go live: helper threads pack it during
+    // the adds and send it to the device as it grows (caps: as the live
+    // capacities, for the helpers' buffers; a batch past them is packed at
+    // finish instead)
+    int begin_helpers(const LiveCaps& caps);
     // Live ingest: after begin(), make this batch live --
     // the stream, offsets and view sized for `caps`, the progress words reset
     // -- before the engine launches k_live_ingest over them.  The adds then
@@ -127,7 +132,9 @@ class TxnStage {
     struct LbShared;
     LbShared* lbs_ = nullptr;
     bool lb_ = false;
+    bool lb_live_ = false;  // the helpers publish to the live kernel (else they copy)
     bool began_live_ = false;
+    int start_helpers(bool live);
     void lb_work();
     void lb_abandon();  // stop the helpers; the batch goes on as a plain borrowed one
     HostPool* pool_ = nullptr;  // created at the first borrowed batch large enough to share

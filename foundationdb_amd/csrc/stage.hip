@@ -165,6 +165,7 @@ int64_t borrow_grain() {
 // ---- live borrowed batches -------------------------------------------------------
 namespace {
 constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes at once
+constexpr uint64_t LB_COPY_MIN = 128 << 10;  // (copy mode) bytes per H2D copy of the finished prefix
 int lb_helpers() {  // FDBCS_LB_HELPERS (default 4: 4, 8 and 12 gave the same config-2 window)
     static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 4;
     return n;
@@ -324,8 +325,18 @@ void TxnStage::lb_work() {
         while (p < S.nchunks && S.done[p].load(std::memory_order_acquire)) p++;
         if (p > S.pub) {
             S.pub = p;
-            if (bar_) _mm_sfence();
-            __atomic_store_n(&prog_[0], S.end[p - 1] << 20 | (uint64_t)S.tend[p - 1], __ATOMIC_RELEASE);
+            if (lb_live_) {  // to the live kernel
+                if (bar_) _mm_sfence();
+                __atomic_store_n(&prog_[0], S.end[p - 1] << 20 | (uint64_t)S.tend[p - 1], __ATOMIC_RELEASE);
+            } else if (S.end[p - 1] - sent_ >= LB_COPY_MIN) {  // to the device, on the copy stream
+                if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, S.end[p - 1] - sent_, hipMemcpyHostToDevice, copy_) !=
+                    hipSuccess) {
+                    S.broken.store(1);
+                    S.stop.store(1, std::memory_order_release);
+                    return;
+                }
+                sent_ = S.end[p - 1];
+            }
         }
     }
 }
@@ -860,20 +871,40 @@ int TxnStage::begin_live(const LiveCaps& caps) {
     if (bar_) _mm_sfence();
     lcaps_ = caps;
     next_pub_ = pub_every_;
-    if (borrow_) {  // live borrowed: the helpers, spinning until the first chunk is added
-        if (!pool_ && host_threads() > 1) pool_ = new HostPool(host_threads());
-        if (!pool_) return FDBCS_E_STATE;
-        if ((r = grow_brec((int64_t)caps.T + LB_CHUNK))) return r;
-        if (!lbs_) lbs_ = new LbShared();
-        lbs_->reset((int64_t)caps.T / LB_CHUNK + 2);
-        lbs_->fn = [this](int) { lb_work(); };
-        pool_->start(&lbs_->fn, 1 + std::min(lb_helpers(), pool_->size() - 1));
-        lb_ = true;
-    }
+    if (borrow_ && (r = start_helpers(true))) return r;  // (the caps above size the helpers' buffers)  // live borrowed: the helpers publish to the kernel
     live_ = true;
     live_broken_ = false;
     began_live_ = true;
     return FDBCS_OK;
+}
+
+// The helpers of a borrowed batch (lb_work), spinning until the first chunk
+// is added.  live: they publish to the live kernel; else they send the
+// finished prefix to the device on the copy stream, every LB_COPY_MIN bytes,
+// and detectConflicts ingests the batch whole from device memory (the live
+// kernel's reads of the records over PCIe were slower than these copies
+// once the adds no longer paced it).
+int TxnStage::start_helpers(bool live) {
+    if (!pool_ && host_threads() > 1) pool_ = new HostPool(host_threads());
+    if (!pool_) return FDBCS_E_STATE;
+    int r;
+    if ((r = grow_brec((int64_t)lcaps_.T + LB_CHUNK))) return r;
+    if (!lbs_) lbs_ = new LbShared();
+    lbs_->reset((int64_t)lcaps_.T / LB_CHUNK + 2);
+    lbs_->fn = [this](int) { lb_work(); };
+    lb_live_ = live;
+    sent_ = 0;
+    pool_->start(&lbs_->fn, 1 + std::min(lb_helpers(), pool_->size() - 1));
+    lb_ = true;
+    return FDBCS_OK;
+}
+
+int TxnStage::begin_helpers(const LiveCaps& caps) {
+    if (!open_ || T_ || live_ || !borrow_) return FDBCS_E_STATE;
+    int r;
+    if ((r = grow(caps.T + 1, live_stream_bound(caps) + 8 * ((uint64_t)caps.T + 1)))) return r;
+    lcaps_ = caps;
+    return start_helpers(false);
 }
 
 int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
@@ -892,6 +923,9 @@ int TxnStage::finish(fdbcs_batch_view& dv, StagedBatch* staged) {
         }
         if (S.stop.load()) {  // (over a capacity: repacked below, and ingested whole)
             live_cancel();
+            _mm_sfence();
+            if (hipStreamSynchronize(copy_) != hipSuccess) return FDBCS_E_HIP;  // (helpers' copies read the stream)
+            sent_ = 0;
         } else {
             used_ = S.cursor;
             K_ = S.keys.load();

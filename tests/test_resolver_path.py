@@ -291,13 +291,16 @@ def test_borrowed_large_batches_match_oracle(gpu):
     g.close()
 
 
+@pytest.mark.parametrize("live", [False, True])
 @pytest.mark.parametrize("cfg,T,nb", [(2, 5000, 30), (3, 3000, 12), (4, 800, 8)])
-def test_borrowed_live_resolver_loop(gpu, cfg, T, nb):
-    """Borrowed batches in the steady state go live: the adds record pointers,
+def test_borrowed_helpers_resolver_loop(gpu, cfg, T, nb, live, monkeypatch):
+    """Borrowed batches in the steady state: the adds record pointers and
     helper threads check and pack chunks of 64 transactions into the stream
-    while the adds go on, and the live kernel encodes them (stage.hip
-    lb_work).  The bench's native Resolver loop against the oracle; most
-    batches must have gone live."""
+    while the adds go on (stage.hip lb_work), copying the finished prefix to
+    the device (default) or publishing it to the live kernel
+    (FDBCS_BORROW_LIVE=1).  The bench's native Resolver loop against the
+    oracle; with live=True most batches must have gone live."""
+    monkeypatch.setenv("FDBCS_BORROW_LIVE", "1" if live else "0")
     g = ConflictSet(flags=BORROW_ALWAYS)
     c = CpuSpec()
     wl = Workload(cfg, txns=T)
@@ -310,17 +313,22 @@ def test_borrowed_live_resolver_loop(gpu, cfg, T, nb):
         vc = c.detect_packed(b, now, nold)
         assert np.array_equal(verdicts[i], vc), (i, np.nonzero(verdicts[i] != vc)[0][:10])
     same_history(g, c)
-    assert s1["live_batches"] - s0["live_batches"] >= nb - 3, (s0, s1)
+    if live:
+        assert s1["live_batches"] - s0["live_batches"] >= nb - 3, (s0, s1)
+    else:
+        assert s1["live_batches"] == s0["live_batches"], (s0, s1)
     g.close()
 
 
-def test_borrowed_live_fallbacks(gpu):
-    """Live borrowed batches that leave the live capacities -- twice the
+@pytest.mark.parametrize("live", [False, True])
+def test_borrowed_helpers_fallbacks(gpu, live, monkeypatch):
+    """Borrowed batches whose helpers run past their capacities -- twice the
     transactions, then the same count with 150-byte keys (key bytes past the
     cap), then a refused transaction in the middle of a live batch -- fall
     back to the whole-batch ingest (or refuse the batch) and stay exact."""
     from foundationdb_amd.batch import PackedBatch
     import random
+    monkeypatch.setenv("FDBCS_BORROW_LIVE", "1" if live else "0")
     g = ConflictSet(flags=BORROW_ALWAYS)
     c = CpuSpec()
     rng = random.Random(9)
