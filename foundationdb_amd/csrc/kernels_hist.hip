@@ -1086,6 +1086,35 @@ __device__ inline int wave_start_search(const int64_t* start, int D, int64_t g) 
     return lo - 1 + __popcll(__ballot(q < hi && start[q] <= g));
 }
 
+// The compaction window's end from its start (win_setup_wave): the last q
+// with start[q] <= g and the last with start[q] <= g + 1, counted over 256
+// entries a step from `from` (start[] never decreases, and start[from] <= g).
+// A window of 3|C| + 10 boundaries spans ~160 directory entries at config 2:
+// one round trip, where the 64-ary search over the whole directory took
+// three or four dependent ones.
+__device__ inline void wave_start_walk(const int64_t* start, int D, int64_t g, int from, int& le_g, int& le_g1) {
+    const int lane = threadIdx.x & 63;
+    for (int base = from;; base += 256) {
+        int64_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // (every load issued before the compares)
+            const int q = base + 64 * k + lane;
+            v[k] = q < D ? start[q] : INT64_MAX;
+        }
+        int c0 = 0, c1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            c0 += __popcll(__ballot(v[k] <= g));
+            c1 += __popcll(__ballot(v[k] <= g + 1));
+        }
+        if (c1 < 256 || base + 256 >= D) {
+            le_g = base + c0 - 1;
+            le_g1 = base + c1 - 1;
+            return;
+        }
+    }
+}
+
 // pool slot of real boundary r of directory entry q (by one wavefront)
 __device__ inline int64_t real_slot(const Pool& pool, const Dir& dir, int q, int64_t r) {
     const int pg = dir.page[q];
@@ -1129,9 +1158,9 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
             const int64_t budget = 3 * (int64_t)sc->n_comb + 10;
             g1 = min(H, g0 + budget);
             pA = i0 < dir.cnt[p0] ? p0 : p0 + 1;
-            pB = wave_start_search(dir.start, D, g1 - 1);
+            int q1;  // the entry holding g1 (when g1 < H)
+            wave_start_walk(dir.start, D, g1 - 1, p0, pB, q1);
             if (g1 < H) {
-                const int q1 = pB + 1 < D && dir.start[pB + 1] <= g1 ? pB + 1 : pB;  // entry holding g1
                 nk = pool_key(pool, real_slot(pool, dir, q1, g1 - dir.start[q1]));
                 has_key = true;
             }
