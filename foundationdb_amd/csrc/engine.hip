@@ -473,7 +473,7 @@ void free_keys(KeyArrays& k) { dfree(k.hi); dfree(k.lo); dfree(k.meta); dfree(k.
 
 void free_plan(BatchBufs& b) {
     dfree(b.acc.er); dfree(b.acc.nn); dfree(b.acc.jlo); dfree(b.acc.jhi); dfree(b.acc.diff);
-    dfree(b.blk_agg); dfree(b.blk_diff); dfree(b.plan_gran);
+    dfree(b.blk_agg); dfree(b.blk_diff);
     dfree(b.aff_list); dfree(b.aff_jlo); dfree(b.aff_jhi); dfree(b.aff_nn); dfree(b.aff_parts);
     dfree(b.aff_nn_off); dfree(b.aff_parts_off); dfree(b.aff_extra_off); dfree(b.aff_free_off); dfree(b.aff_start);
     dfree(b.freed_list); dfree(b.full_list); dfree(b.aff_page); dfree(b.aff_cnt);
@@ -654,15 +654,12 @@ int ensure_batch(fdbcs* cs, int64_t T, int64_t R, int64_t W, uint64_t key_bytes)
         const int64_t nblk = plan_blocks((int)cd) + 1;
         if ((r = dalloc(b.acc.er, n)) || (r = dalloc(b.acc.nn, n)) || (r = dalloc(b.acc.jlo, n)) ||
             (r = dalloc(b.acc.jhi, n)) || (r = dalloc(b.acc.diff, n)) || (r = dalloc(b.blk_agg, 6 * nblk)) ||
-            (r = dalloc(b.blk_diff, nblk)) || (r = dalloc(b.plan_gran, 13 * nblk)) ||
-            (r = dalloc(b.aff_list, n)) || (r = dalloc(b.aff_jlo, n)) ||
+            (r = dalloc(b.blk_diff, nblk)) || (r = dalloc(b.aff_list, n)) || (r = dalloc(b.aff_jlo, n)) ||
             (r = dalloc(b.aff_jhi, n)) || (r = dalloc(b.aff_nn, n)) || (r = dalloc(b.aff_parts, n)) ||
             (r = dalloc(b.aff_nn_off, n)) || (r = dalloc(b.aff_parts_off, n)) || (r = dalloc(b.aff_extra_off, n)) ||
             (r = dalloc(b.aff_free_off, n)) || (r = dalloc(b.aff_start, n)) || (r = dalloc(b.freed_list, n)) ||
             (r = dalloc(b.aff_page, n)) || (r = dalloc(b.aff_cnt, n)) || (r = dalloc(b.full_list, n)))
             return r;
-        HIPOK(hipMemsetAsync(b.plan_gran, 0, 13 * nblk * 8, s));  // (tag 0: never a launch's)
-        b.plan_gen = 0;
         HIPOK(hipMemsetAsync(b.acc.er, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.nn, 0, n * 4, s));
         HIPOK(hipMemsetAsync(b.acc.diff, 0, n * 4, s));

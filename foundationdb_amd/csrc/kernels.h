@@ -215,8 +215,6 @@ struct BatchBufs {
     PageAcc acc;
     int64_t* blk_agg;    // [plan blocks * 6] per-block plan aggregates (2 start states x 3 packed words)
     int32_t* blk_diff;   // [plan blocks]
-    uint64_t* plan_gran = nullptr;  // [plan blocks * 13] k_plan_scan1's {aggregate half, tag} granules
-    uint32_t plan_gen = 0;          // the tag of the last k_plan_scan1 launch
     // affected pages, compacted [cap_dir + 2]
     int32_t* aff_list;   // directory entry
     int32_t* aff_jlo; int32_t* aff_jhi;  // combined ranges touching it

@@ -426,175 +426,6 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
     }
 }
 
-// K2 in one launch (k_plan_scan1: k_plan_aggr + k_plan_scan, ~6 us of the
-// update chain and one kernel boundary saved): every block reduces its two
-// start-state aggregates, publishes them as 8-byte {data, tag} granules (one
-// relaxed agent-scope store each: `sc1`, past the XCD L2s, untorn), and wave 0
-// then polls its predecessors' granules (relaxed agent-scope loads) instead
-// of reading k_plan_aggr's output after a kernel boundary.  A block waits only
-// on lower-numbered blocks, which are dispatched before it
-// (MI355X_MICROARCH.md, inter-workgroup visibility: granule hand-off).  The
-// tag is the launch's generation (BatchBufs::plan_gen), so nothing is reset
-// between launches.
-constexpr int PG_WORDS = 13;  // granules per block: 6 packed aggregate words as 12 halves, the diff total
-__device__ inline void pg_put(uint64_t* g, uint32_t tag, uint32_t v) {
-    __hip_atomic_store(g, (uint64_t)tag << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline uint32_t pg_get(const uint64_t* g, uint32_t tag) {
-    uint64_t x;
-    while (((x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != tag)
-        __builtin_amdgcn_s_sleep(1);
-    return (uint32_t)x;
-}
-
-__global__ __launch_bounds__(PS_THREADS) void k_plan_scan1(PlanArgs A, uint64_t* __restrict__ gran, uint32_t tag) {
-    __shared__ int32_t red32[PS_THREADS / 64 + 1];
-    __shared__ int64_t red64[PS_THREADS / 64 + 1];
-    __shared__ int64_t red[PS_THREADS / 64][7];
-    __shared__ int64_t s_pre[4];  // block prefix: 3 packed words + start state
-    Scalars* sc = A.sc;
-    const int D = sc->D;
-    const int base = blockIdx.x * PS_BLOCK;
-    if (base >= D) return;
-    const int lane = threadIdx.x & 63;
-    const int x0 = base + threadIdx.x * PS_ITEMS;
-    int dl[PS_ITEMS], dsum = 0, cnt[PS_ITEMS];
-#pragma unroll
-    for (int k = 0; k < PS_ITEMS; k++) {
-        dl[k] = x0 + k < D ? A.acc.diff[x0 + k] : 0;
-        cnt[k] = x0 + k < D ? A.src.nr[x0 + k] : 0;
-        dsum += dl[k];
-    }
-    int dtot;
-    const int cov0 = block_excl_scan(dsum, red32, dtot);  // local prefix, excluding this thread's items
-    // ---- both start states' items and this block's aggregates
-    PlanItem it[2][PS_ITEMS];
-    int64_t w[2][PS_ITEMS][3];
-    int64_t v[7] = {0, 0, 0, 0, 0, 0, 0};
-    {
-        int cov = cov0;
-#pragma unroll
-        for (int k = 0; k < PS_ITEMS; k++) {
-            cov += dl[k];
-            const int x = x0 + k;
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                it[s][k] = PlanItem{false, 0, 0, 0, 0, -1};
-                w[s][k][0] = w[s][k][1] = w[s][k][2] = 0;
-                if (x < D) {
-                    it[s][k] = plan_item(A.acc, cnt[k], x, s + cov > 0);
-                    pack_item(it[s][k], cnt[k], w[s][k]);
-                }
-                v[3 * s + 0] += w[s][k][0];
-                v[3 * s + 1] += w[s][k][1];
-                v[3 * s + 2] += w[s][k][2];
-            }
-        }
-    }
-    block_reduce_n<7>(v, red);
-    uint64_t* my = gran + (int64_t)blockIdx.x * PG_WORDS;
-    if (threadIdx.x < 12) {  // (12 lanes, one granule each)
-        const int k = threadIdx.x >> 1;
-        pg_put(my + threadIdx.x, tag, (uint32_t)((uint64_t)v[k] >> (32 * (threadIdx.x & 1))));
-    } else if (threadIdx.x == 12) {
-        pg_put(my + 12, tag, (uint32_t)dtot);
-    }
-    // ---- this block's prefix from its predecessors' granules (wave 0) ----
-    if (threadIdx.x < 64) {
-        int64_t p0 = 0, p1 = 0, p2 = 0;
-        int carry = 0;
-        for (int k0 = 0; k0 < (int)blockIdx.x; k0 += 64) {
-            const int k = k0 + lane;
-            const bool ok = k < (int)blockIdx.x;
-            const uint64_t* g = gran + (int64_t)k * PG_WORDS;
-            const int d = ok ? (int)pg_get(g + 12, tag) : 0;
-            const int st = carry + wave_incl_scan(d) - d;  // state at block k's start
-            if (ok) {
-                const int s3 = 6 * (st > 0);
-                p0 += (int64_t)((uint64_t)pg_get(g + s3 + 1, tag) << 32 | pg_get(g + s3 + 0, tag));
-                p1 += (int64_t)((uint64_t)pg_get(g + s3 + 3, tag) << 32 | pg_get(g + s3 + 2, tag));
-                p2 += (int64_t)((uint64_t)pg_get(g + s3 + 5, tag) << 32 | pg_get(g + s3 + 4, tag));
-            }
-            carry += wave_reduce_sum(d);
-        }
-        p0 = wave_reduce_sum(p0);
-        p1 = wave_reduce_sum(p1);
-        p2 = wave_reduce_sum(p2);
-        if (lane == 0) {
-            s_pre[0] = p0;
-            s_pre[1] = p1;
-            s_pre[2] = p2;
-            s_pre[3] = carry;
-        }
-    }
-    __syncthreads();
-    const int s0 = s_pre[3] > 0 ? 1 : 0;  // (the state at this block's start: 0 or 1, ranges are disjoint)
-    int64_t tsum[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < PS_ITEMS; k++) {
-        tsum[0] += w[s0][k][0];
-        tsum[1] += w[s0][k][1];
-        tsum[2] += w[s0][k][2];
-    }
-    int64_t tot[3], ex[3];
-#pragma unroll
-    for (int f = 0; f < 3; f++) ex[f] = s_pre[f] + block_excl_scan(tsum[f], red64, tot[f]);
-    const int64_t top0 = sc->free_top;
-#pragma unroll
-    for (int k = 0; k < PS_ITEMS; k++) {
-        const int x = x0 + k;
-        if (x < D) {
-            const PlanItem& ik = it[s0][k];
-            const int pos = (int)(ex[0] >> 32);
-            const int64_t st = A.src.start[x] + (int64_t)(int32_t)(uint32_t)((uint64_t)ex[2] >> 32);
-            if (ik.affected) {
-                const int a = (int)(uint32_t)ex[0];
-                A.aff_list[a] = x;
-                A.aff_page[a] = A.src.page[x];
-                A.aff_cnt[a] = A.src.cnt[x];  // slots in use
-                A.aff_jlo[a] = ik.jlo;
-                A.aff_jhi[a] = ik.jhi;
-                A.aff_nn[a] = ik.nn;
-                A.aff_parts[a] = ik.parts;
-                A.aff_nn_off[a] = (int)(uint32_t)ex[2];
-                A.aff_parts_off[a] = pos;
-                A.aff_extra_off[a] = (int)(uint32_t)ex[1];
-                A.aff_free_off[a] = (int)(ex[1] >> 32);
-                A.aff_start[a] = st;
-            } else {
-                A.dst.page[pos] = A.src.page[x];
-                A.dst.cnt[pos] = A.src.cnt[x];
-                A.dst.nr[pos] = cnt[k];
-                A.dst.maxv[pos] = A.src.maxv[x];
-                A.dst.fhi[pos] = A.src.fhi[x];
-                A.dst.flo[pos] = A.src.flo[x];
-                A.dst.fmeta[pos] = A.src.fmeta[x];
-                A.dst.ftail[pos] = A.src.ftail[x];
-                A.dst.start[pos] = st;
-            }
-            A.acc.er[x] = 0;
-            A.acc.nn[x] = 0;
-            A.acc.jlo[x] = INT32_MAX;
-            A.acc.jhi[x] = -1;
-            A.acc.diff[x] = 0;
-#pragma unroll
-            for (int f = 0; f < 3; f++) ex[f] += w[s0][k][f];
-        }
-    }
-    if (blockIdx.x == (D - 1) / PS_BLOCK && threadIdx.x == 0) {
-        const int64_t t0 = s_pre[0] + tot[0], t1 = s_pre[1] + tot[1], t2 = s_pre[2] + tot[2];
-        const int Dn = (int)(t0 >> 32);
-        const int extra = (int)(uint32_t)t1, freed = (int)(t1 >> 32);
-        sc->n_aff = (int)(uint32_t)t0;
-        sc->n_full = 0;
-        sc->D_next = Dn;
-        sc->extra_total = extra;
-        sc->free_next = (int)(top0 - extra + freed);
-        sc->free_base = (int)(top0 - extra);
-        A.dst.start[Dn] = A.src.start[D] + (int64_t)(int32_t)(uint32_t)((uint64_t)t2 >> 32);
-    }
-}
-
 __device__ inline void copy_tail(const Key& k, uint8_t* arena, uint64_t cap, Scalars* sc, const uint8_t** out) {
     const uint32_t L = key_len(k.meta);
     if (L <= 17) {
@@ -1631,22 +1462,15 @@ void launch_merge(const fdbcs_batch_view& v, BatchBufs& b, HistBufs& h, int cur,
                            write_base(b, v), v0, h.shard, sc, b.pb, b.ib, b.pe, b.ie, b.need_e, b.vb, b.acc, b.rkb, b.rke);
     }
     const int nblk = plan_blocks(h.cap_dir);
-    static const bool two_pass = getenv("FDBCS_PLAN_TWO_PASS") != nullptr;  // (A/B: k_plan_aggr + k_plan_scan)
-    if (two_pass)
-        hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
-                           b.blk_diff);
+    hipLaunchKernelGGL(k_plan_aggr, dim3(nblk), dim3(PS_THREADS), 0, s, src, (const Scalars*)sc, b.acc, b.blk_agg,
+                       b.blk_diff);
     PlanArgs P;
     P.src = src; P.dst = dst; P.sc = sc; P.acc = b.acc; P.blk_agg = b.blk_agg; P.blk_diff = b.blk_diff;
     P.aff_list = b.aff_list; P.aff_jlo = b.aff_jlo; P.aff_jhi = b.aff_jhi; P.aff_nn = b.aff_nn;
     P.aff_parts = b.aff_parts; P.aff_nn_off = b.aff_nn_off; P.aff_parts_off = b.aff_parts_off;
     P.aff_extra_off = b.aff_extra_off; P.aff_free_off = b.aff_free_off; P.aff_start = b.aff_start;
     P.aff_page = b.aff_page; P.aff_cnt = b.aff_cnt;
-    if (two_pass) {
-        hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
-    } else {
-        if (++b.plan_gen == 0) b.plan_gen = 1;  // (tag 0: the granules' initial value)
-        hipLaunchKernelGGL(k_plan_scan1, dim3(nblk), dim3(PS_THREADS), 0, s, P, b.plan_gran, b.plan_gen);
-    }
+    hipLaunchKernelGGL(k_plan_scan, dim3(nblk), dim3(PS_THREADS), 0, s, P);
     if (W > 0) {
         const int max_aff = std::min<int64_t>(h.cap_dir, 4 * (int64_t)W + 4);
         MergeArgs A;
