@@ -67,9 +67,10 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="key-range shards of the N-core CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--borrow", choices=["off", "large", "always"], default="large",
+    p.add_argument("--borrow", choices=["off", "large", "always"], default="always",
                    help="fdbcs_config.flags: how the adds hold the caller's keys (include/fdbcs.h FDBCS_BORROW_*); "
-                        "'large' borrows only batches of >= 65,536 transactions (config 5), so configs 1-4 copy")
+                        "default always: the Resolver keeps a request's transactions until detectConflicts returns, as the "
+                        "reference's addTransaction borrows them (SkipList.cpp:993-1004); 'off' copies every key at its add")
     p.add_argument("--no-shim", action="store_true", help="skip the shim's skipListTest rate")
     p.add_argument("--impl", choices=["abi", "py"], default="abi",
                    help="exact protocol A: fdbcs_sharded (C ABI, RCCL inside libfdbcs) or the Python orchestration")
