@@ -1021,7 +1021,7 @@ def run_multi_resolvers(args, rank, world):
                                      sparse=sparse)
         cs = eng.shard.cs
     else:
-        cs = ConflictSet(device=local, max_history=max_history(cfg))
+        cs = ConflictSet(device=local, max_history=max_history(cfg), flags=BORROW_FLAGS[args.borrow])  # (key-range resolvers)
 
     def global_h():
         if mode != "exact":
