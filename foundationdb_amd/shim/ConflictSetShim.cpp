@@ -64,6 +64,12 @@ struct ConflictSet {
     fdbcs* h = nullptr;        // one GPU
     MultiGpu* multi = nullptr;  // or G GPUs as one resolver (FDBCS_SHARDS)
     std::vector<uint8_t> verdict;  // last batch (GetTooOldTransactions)
+    // One GPU, borrowed batches (FDBCS_BORROW_ALWAYS; FDBCS_SHIM_BORROW=0
+    // copies instead): the batch's ranges as fdbcs_range, kept until
+    // detectConflicts returns (a ChunkLog never moves an entry)
+    bool borrow = false;
+    void* ranges = nullptr;  // ChunkLog<fdbcs_range>
+    std::vector<std::unique_ptr<fdbcs_range[]>> big;
 };
 
 namespace {
@@ -131,6 +137,9 @@ struct ChunkLog {
         return p;
     }
 };
+
+// the one-GPU set's range log (ConflictSet::ranges)
+ChunkLog<fdbcs_range>& range_log(ConflictSet* cs) { return *static_cast<ChunkLog<fdbcs_range>*>(cs->ranges); }
 
 // ---- G GPUs as one resolver ------------------------------------------------
 // Rank g lives on worker thread g (its device context, its RCCL rank).  Jobs
@@ -489,6 +498,16 @@ ConflictSet* newConflictSet() {
     }
     fdbcs_config cfg{};
     cfg.device = device_ordinal();
+    // The Resolver keeps a request's transactions until detectConflicts
+    // returns (the reference's addTransaction borrows their KeyRefs,
+    // SkipList.cpp:993-1004): the engine records pointers at each add and its
+    // helper threads pack the batch (include/fdbcs.h FDBCS_BORROW_ALWAYS).
+    const char* b = getenv("FDBCS_SHIM_BORROW");
+    cs->borrow = !(b && !atoi(b));
+    if (cs->borrow) {
+        cfg.flags = FDBCS_BORROW_ALWAYS;
+        cs->ranges = new ChunkLog<fdbcs_range>();
+    }
     ok_or_throw(fdbcs_create(&cs->h, 0, &cfg), "newConflictSet");
     return cs.release();
 }
@@ -507,6 +526,7 @@ void clearConflictSet(ConflictSet* cs, Version v) {
 void destroyConflictSet(ConflictSet* cs) {
     if (cs->multi) free_multi(cs->multi);
     else fdbcs_destroy(cs->h);
+    delete static_cast<ChunkLog<fdbcs_range>*>(cs->ranges);
     delete cs;
 }
 
@@ -528,6 +548,10 @@ ConflictBatch::ConflictBatch(ConflictSet* cs)
         mg->open = true;
         mg->start([mg](int g) { return mg->batch_job(g); });  // the ranks add as transactions arrive
         return;
+    }
+    if (cs->borrow) {
+        range_log(cs).n = 0;
+        cs->big.clear();
     }
     ok_or_throw(fdbcs_batch_begin(cs->h), "ConflictBatch");
 }
@@ -566,6 +590,22 @@ void ConflictBatch::addTransaction(const CommitTransactionRef& tr) {
         const int64_t t = mg->published.load(std::memory_order_relaxed);
         *mg->txns.reserve(1) = TxnRec{tr.read_snapshot, nr, nw, rg};
         mg->published.store(t + 1, std::memory_order_release);
+        transactionCount++;
+        return;
+    }
+    if (cs->borrow) {  // the ranges into the batch's log, checked here (a bad one throws, as when copied)
+        fdbcs_range* rg;
+        if ((size_t)(nr + nw) <= ChunkLog<fdbcs_range>::CH) {
+            rg = range_log(cs).reserve((size_t)std::max(nr + nw, 1));
+        } else {
+            cs->big.emplace_back(new fdbcs_range[(size_t)(nr + nw)]);
+            rg = cs->big.back().get();
+        }
+        int k = 0;
+        for (const auto& r : tr.read_conflict_ranges) rg[k++] = to_range(r);
+        for (const auto& w : tr.write_conflict_ranges) rg[k++] = to_range(w);
+        ok_or_throw(check_ranges(rg, nr + nw), "addTransaction");
+        ok_or_throw(fdbcs_batch_add(cs->h, tr.read_snapshot, rg, nr, rg + nr, nw), "addTransaction");
         transactionCount++;
         return;
     }
