@@ -597,7 +597,9 @@ int TxnStage::grow(int64_t need_txns, uint64_t need_bytes) {
         if (hipHostMalloc((void**)&nt, (size_t)nc * 8, stream_flags((uint64_t)nc * 8)) != hipSuccess)
             return FDBCS_E_NOMEM;
         toff_live_ = (uint64_t)nc * 8 <= LIVE_STREAM_MAX;
-        if (T_) memcpy(nt, toff_, (size_t)T_ * 8);
+        // (the entries written so far: a borrowed batch's adds write none --
+        // its T_ counts transactions whose entries pack_borrowed writes later)
+        if (T_ && !borrow_) memcpy(nt, toff_, (size_t)T_ * 8);
         if (toff_) hipHostFree(toff_);
         toff_ = nt;
         toff_cap_ = nc;
@@ -633,7 +635,7 @@ int TxnStage::grow_bar(int64_t need_txns, uint64_t need_bytes) {
         uint64_t* nt = nullptr;
         if (hipExtMallocWithFlags((void**)&nt, (size_t)nc * 8, hipDeviceMallocUncached) != hipSuccess)
             return FDBCS_E_NOMEM;
-        if (T_) {
+        if (T_ && !borrow_) {  // (see grow: a borrowed batch's adds wrote no entries)
             _mm_sfence();
             if (hipMemcpy(nt, toff_, (size_t)T_ * 8, hipMemcpyDeviceToDevice) != hipSuccess) return FDBCS_E_HIP;
         }

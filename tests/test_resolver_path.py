@@ -270,6 +270,24 @@ def test_borrowed_refusal(gpu):
     g.close()
 
 
+def test_borrowed_first_batch_past_the_initial_offsets(gpu):
+    """A conflict set whose very first per-transaction batch is borrowed and
+    larger than the stage's initial offset table (8,192 entries): the table
+    grows at detect without copying entries the adds never wrote (a 10^6-txn
+    first batch read past the old table: bench.py --config 5 --borrow always
+    crashed)."""
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    wl = Workload(2, txns=200_000)
+    run = wl.prepare_run(0, 2)
+    us, add_us, verdicts = run.run(g)
+    for i in range(2):
+        b, now, nold = wl.batch(i)
+        assert np.array_equal(verdicts[i], c.detect_packed(b, now, nold)), i
+    same_history(g, c)
+    g.close()
+
+
 def test_borrowed_large_batches_match_oracle(gpu):
     """Config 5's shape through the bench's native Resolver loop with
     FDBCS_BORROW_LARGE: the first 10^6-transaction batch copies its keys
