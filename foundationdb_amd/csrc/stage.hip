@@ -468,8 +468,13 @@ int TxnStage::pack_borrowed() {
                 ro += q.reads;
                 wo += q.writes;
             }
-            // (the record offsets after the records: finish() sends them with the rest)
-            if (status == FDBCS_OK) status = grow(T + 1, off + 8 * (uint64_t)(T + 1) + 16);
+            // (the record offsets after the records: finish() sends them with
+            // the rest.  An eighth more than this batch needs, so that the next
+            // batch of about this size does not re-pin the stream: pinning
+            // ~300 MB again put 40 ms batches into config 5's timed region)
+            const uint64_t need = off + 8 * (uint64_t)(T + 1) + 16;
+            if (status == FDBCS_OK && (need > cap_ || T + 1 > toff_cap_))
+                status = grow(T + 1 + T / 8, need + need / 8);
             if (status != FDBCS_OK) {
                 phase.store(2, std::memory_order_release);
                 return;
