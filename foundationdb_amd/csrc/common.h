@@ -134,6 +134,13 @@ struct KeyArrays {           // one key per slot
     uint32_t* meta;
     const uint8_t** tail;
     __device__ Key get(int64_t i) const { return Key{hi[i], lo[i], meta[i], tail[i]}; }
+    // the tail pointer only for a key past 17 bytes (the only one that has
+    // a tail): a random 8-byte load saved per short key, at the cost of a
+    // dependent load for long ones
+    __device__ Key get_short(int64_t i) const {
+        const uint32_t m = meta[i];
+        return Key{hi[i], lo[i], m, key_len(m) > 17 ? tail[i] : nullptr};
+    }
     __device__ void put(int64_t i, const Key& k) const {
         hi[i] = k.hi; lo[i] = k.lo; meta[i] = k.meta; tail[i] = k.tail;
     }

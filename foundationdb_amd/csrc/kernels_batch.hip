@@ -2689,7 +2689,7 @@ __global__ __launch_bounds__(256) void k_page_join(PageJoinArgs A) {
         const int64_t s = A.read_snap[r];
         if (s == INT64_MAX) return;
         const Key b{rec.hi, rec.lo, rec.meta, key_len(rec.meta) > 17 ? A.keys.tail[2 * (int64_t)r] : nullptr};
-        const Key e = A.keys.get(2 * (int64_t)r + 1);
+        const Key e = A.keys.get_short(2 * (int64_t)r + 1);  // (config 5: 64 of ~610 bytes a read fetched)
         bool past = false;  // e > the next page's first key: e lies past this page
         if (x + 1 < A.sc->D) {
             const uint64_t fh = d.fhi[x + 1];
