@@ -165,7 +165,12 @@ int64_t borrow_grain() {
 // ---- live borrowed batches -------------------------------------------------------
 namespace {
 constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes at once
-constexpr uint64_t LB_COPY_MIN = 128 << 10;  // (copy mode) bytes per H2D copy of the finished prefix
+// (copy mode) bytes per H2D copy of the finished prefix (FDBCS_LB_COPY, default 128 KiB)
+uint64_t lb_copy_min() {
+    static const uint64_t n = getenv("FDBCS_LB_COPY") ? std::max(4096ULL, strtoull(getenv("FDBCS_LB_COPY"), nullptr, 0))
+                                                       : (128ull << 10);
+    return n;
+}
 int lb_helpers() {  // FDBCS_LB_HELPERS (default 4: 4, 8 and 12 gave the same config-2 window)
     static const int n = getenv("FDBCS_LB_HELPERS") ? std::max(1, atoi(getenv("FDBCS_LB_HELPERS"))) : 4;
     return n;
@@ -328,7 +333,7 @@ void TxnStage::lb_work() {
             if (lb_live_) {  // to the live kernel
                 if (bar_) _mm_sfence();
                 __atomic_store_n(&prog_[0], S.end[p - 1] << 20 | (uint64_t)S.tend[p - 1], __ATOMIC_RELEASE);
-            } else if (S.end[p - 1] - sent_ >= LB_COPY_MIN) {  // to the device, on the copy stream
+            } else if (S.end[p - 1] - sent_ >= lb_copy_min()) {  // to the device, on the copy stream
                 if (hipMemcpyAsync(dev_ + sent_, pin_ + sent_, S.end[p - 1] - sent_, hipMemcpyHostToDevice, copy_) !=
                     hipSuccess) {
                     S.broken.store(1);
