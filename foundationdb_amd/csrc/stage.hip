@@ -168,7 +168,7 @@ constexpr int64_t LB_CHUNK = 64;  // transactions a helper packs and publishes a
 // (copy mode) bytes per H2D copy of the finished prefix (FDBCS_LB_COPY, default 128 KiB)
 uint64_t lb_copy_min() {
     static const uint64_t n = getenv("FDBCS_LB_COPY") ? std::max(4096ULL, strtoull(getenv("FDBCS_LB_COPY"), nullptr, 0))
-                                                       : (128ull << 10);
+                                                       : (512ull << 10);  // (A/B: profiles/r06_ab_lb_copy.txt)
     return n;
 }
 int lb_helpers() {  // FDBCS_LB_HELPERS (default 4: 4, 8 and 12 gave the same config-2 window)

@@ -178,6 +178,47 @@ def test_borrowed_tiny_and_mixed_streams(gpu, maxlen):
     g.close()
 
 
+def _long_key_stream(seed, n_batches, T):
+    """Batches of short and long (> 17 bytes, tails) keys over a small key
+    space, so reads hit the previous batches' writes."""
+    import random
+    rng = random.Random(seed)
+    now = 1000
+
+    def key(i):
+        return (b"tenant/%03d/" % (i % 7)) * 3 + b"%05d" % i if i % 3 == 0 else b"k%05d" % i
+
+    for _ in range(n_batches):
+        now += rng.randint(20, 60)
+        txns = []
+        for _t in range(T):
+            def rr():
+                a = rng.randrange(6000)
+                k = key(a)
+                return (k, k + b"\x00") if rng.random() < 0.6 else tuple(sorted((k, key(a + rng.randint(1, 40)))))
+            rs = [r for r in (rr() for _ in range(rng.randint(0, 3))) if r[0] < r[1]]
+            ws = [r for r in (rr() for _ in range(rng.randint(0, 2))) if r[0] < r[1]]
+            txns.append((now - rng.randint(1, 120), rs, ws))
+        yield txns, now, now - rng.randint(150, 400)
+
+
+def test_borrowed_back_to_back_long_keys(gpu):
+    """Back-to-back borrowed batches with short and long keys (tails: the
+    merge of one batch still reads its batch's tails while the host packs the
+    next), verdicts as the oracle's every batch, the history at a midpoint
+    (a dump queues work on the stream between batches) and at the end."""
+    from foundationdb_amd.batch import PackedBatch
+    g = ConflictSet(flags=BORROW_ALWAYS)
+    c = CpuSpec()
+    for i, (txns, now, nold) in enumerate(_long_key_stream(17, 14, 2500)):
+        v = ConflictBatch_run(g, txns, now, nold)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, nold)), i
+        if i == 8:
+            same_history(g, c)
+    same_history(g, c)
+    g.close()
+
+
 def _ranges(lib_keys, spec):
     """ctypes Range array over the bytes of lib_keys (a bytearray the test keeps
     and later overwrites): spec = [(begin offset, begin len, end offset, end len)]."""
