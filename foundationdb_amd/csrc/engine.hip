@@ -153,6 +153,7 @@ struct fdbcs {
     // early verdicts: D2H of the verdicts and a scalar snapshot right after
     // the decision; the history update keeps running behind them
     hipEvent_t ev_verdict = nullptr;
+    bool vev_rec = true;  // ev_verdict was recorded for the batch in flight (else its fallback is ev_end)
     // host-mapped verdict area the decision kernel writes (kernels.h EarlyOut):
     // [0] flag, [4] err, [8] last_err, verdicts from byte 64
     uint8_t* vmap = nullptr;
@@ -869,7 +870,12 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
             if (T) HIPOK(hipMemcpyAsync(cs->vpin, dev_verdict ? dev_verdict : b.verdict, (size_t)T, hipMemcpyDeviceToHost, s));
             HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
         }
-        HIPOK(hipEventRecord(cs->ev_verdict, s));
+        // (mapped verdicts: the host polls their flag, and its fallback waits
+        // for ev_end -- a marker here held the next launch ~10 us: A/B knob
+        // FDBCS_VERDICT_EVENT=1)
+        static const bool vev = getenv("FDBCS_VERDICT_EVENT") && atoi(getenv("FDBCS_VERDICT_EVENT"));
+        cs->vev_rec = !cs->early_mapped || vev;
+        if (cs->vev_rec) HIPOK(hipEventRecord(cs->ev_verdict, s));
         launch_write_search(v, b, cs->h, cs->cur, sc, cs->v0, s);  // (grid decision: for the merge, after the verdicts)
         if (split) launch_combine(v, b, sc, s);  // (the combined write ranges: after the verdicts)
     }
@@ -904,13 +910,13 @@ int verdict_wait(fdbcs* cs, int64_t T, uint8_t* verdict, int64_t* lm_count = nul
     int r;
     if (cs->early_mapped) {
         // poll the flag the decision kernel sets after its verdicts (no copy,
-        // no interrupt); past ~2 ms block on the event behind it instead
+        // no interrupt); past ~2 ms block on the batch's end instead
         const uint32_t* flag = reinterpret_cast<const uint32_t*>(cs->vmap);
         const auto t0 = std::chrono::steady_clock::now();
         for (int it = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != cs->vseq; it++) {
             _mm_pause();
             if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-                if ((r = wait_event(cs->ev_verdict))) return r;
+                if ((r = wait_event(cs->vev_rec ? cs->ev_verdict : cs->ev_end))) return r;
                 if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != cs->vseq) return FDBCS_E_HIP;
                 break;
             }
@@ -2454,6 +2460,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
         HIPOK(hipMemcpyAsync(cs->vpin + vpin_scalars_off(T), sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
     }
     HIPOK(hipEventRecord(cs->ev_verdict, s));
+    cs->vev_rec = true;
     launch_combine(v, b, sc, s);
     // 5: this shard's part of the merge (carry-in: sc->carry_apply)
     const bool compact = new_oldest > cs->oldest;
