@@ -1123,6 +1123,10 @@ __device__ inline int64_t real_slot(const Pool& pool, const Dir& dir, int q, int
     return (int64_t)pg * PAGE + wave_select_real(hm, dir.cnt[q], (int)r);
 }
 
+#ifndef FDBCS_WIN_SETUP_FUSED
+#define FDBCS_WIN_SETUP_FUSED 1  // (A/B: scripts/build_variants.sh "old:-DFDBCS_WIN_SETUP_FUSED=0")
+#endif
+
 struct RemovalKey {
     uint64_t* hi;
     uint64_t* lo;
@@ -1149,6 +1153,72 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
     Key nk{0, 0, 0, nullptr};
     if (!sc->err) {
         const Key rk{rk_hi[0], rk_lo[0], rk_meta[0], rk_tail};
+#if FDBCS_WIN_SETUP_FUSED
+        // After the search: the start / page / count of the 256 entries from
+        // p0 in one round (the walk's, p0's own and usually q1's), p0's keys
+        // and hole mask in the next, then q1's hole mask and the key at g1 --
+        // two dependent round trips fewer than the separate steps below
+        // (k_bmax_commit 13.6 -> 12.6 us, config 2,
+        // profiles/r06_ab_win_setup.txt; a 1024-probe directory search in one
+        // wavefront made it 30.9 us: 64 scattered loads a lane).
+        const int p0 = wave_dir_search(dir, D, rk);
+        int64_t st[4];
+        int pgv[4], cnv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int q = p0 + 64 * k + lane;
+            st[k] = q < D ? dir.start[q] : INT64_MAX;
+            pgv[k] = q < D ? dir.page[q] : 0;
+            cnv[k] = q < D ? dir.cnt[q] : 0;
+        }
+        const int pg0 = __shfl(pgv[0], 0), c0 = __shfl(cnv[0], 0);
+        const int64_t s0 = __shfl(st[0], 0);
+        uint64_t hm[HM_WORDS];
+        load_hmask(pool, pg0, hm);
+        const int i0 = wave_page_lb(pool, pg0, c0, rk);
+        g0 = s0 + real_before(hm, i0);
+        if (g0 < H) {
+            const int64_t budget = 3 * (int64_t)sc->n_comb + 10;
+            g1 = min(H, g0 + budget);
+            pA = i0 < c0 ? p0 : p0 + 1;
+            // the window's end (wave_start_walk's counts, over the entries loaded above first)
+            int n0 = 0, n1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                n0 += __popcll(__ballot(st[k] <= g1 - 1));
+                n1 += __popcll(__ballot(st[k] <= g1));
+            }
+            int q1 = p0 + n1 - 1;
+            pB = p0 + n0 - 1;
+            if (n1 == 256 && p0 + 256 < D) {  // (a window past 256 entries: the walk goes on from there)
+                int a, b;
+                wave_start_walk(dir.start, D, g1 - 1, p0 + 256, a, b);
+                if (n0 == 256) pB = a;
+                q1 = b;
+            }
+            if (g1 < H) {
+                const int d = q1 - p0;  // (>= 0: start[p0] <= g0 < g1)
+                int pq, cq;
+                int64_t sq;
+                if (d < 256) {
+                    const int k = d >> 6, ln = d & 63;
+                    pq = __shfl(k == 0 ? pgv[0] : k == 1 ? pgv[1] : k == 2 ? pgv[2] : pgv[3], ln);
+                    cq = __shfl(k == 0 ? cnv[0] : k == 1 ? cnv[1] : k == 2 ? cnv[2] : cnv[3], ln);
+                    sq = __shfl(k == 0 ? st[0] : k == 1 ? st[1] : k == 2 ? st[2] : st[3], ln);
+                } else {
+                    pq = dir.page[q1];
+                    cq = dir.cnt[q1];
+                    sq = dir.start[q1];
+                }
+                uint64_t hq[HM_WORDS];
+                load_hmask(pool, pq, hq);
+                nk = pool_key(pool, (int64_t)pq * PAGE + wave_select_real(hq, cq, (int)(g1 - sq)));
+                has_key = true;
+            }
+        } else {
+            g0 = g1 = H;
+        }
+#else
         const int p0 = wave_dir_search(dir, D, rk);
         const int i0 = wave_page_lb(pool, dir.page[p0], dir.cnt[p0], rk);
         uint64_t hm[HM_WORDS];
@@ -1167,6 +1237,7 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
         } else {
             g0 = g1 = H;
         }
+#endif
     }
     if (lane == 0 && update_rk && !sc->err && g0 < g1) {  // tail arena GC: where this sweep stands
         int tf = sc->tail_flags;
