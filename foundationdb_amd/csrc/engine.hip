@@ -122,7 +122,10 @@ struct fdbcs {
     BatchBufs b{};
     Scalars* sc = nullptr;       // device
     Scalars* sc_host = nullptr;  // pinned mirror
-    Scalars* sc_mapped = nullptr;  // host-mapped copy the batch-ending kernel writes (HistBufs::mirror)
+    Scalars* sc_mapped = nullptr;  // host-mapped copies the batch-ending kernels write (HistBufs::mirror): two
+                                   // slots, by run_batch parity (mirror_batch), so the one an earlier batch
+                                   // published stays readable while the next batch's update runs
+    Scalars* mirror_dev = nullptr;  // (their device address)
     int cur = 0;
     int64_t v0 = 0;
     int64_t oldest = 0;
@@ -195,8 +198,15 @@ struct fdbcs {
     hipStream_t copy_stream = nullptr;
     // end of the last run_batch's history update (its scalars are then in the
     // host-mapped mirror: ensure_history refreshes its budget without a sync)
-    hipEvent_t ev_end = nullptr;
+    hipEvent_t ev_end = nullptr;  // (= ev_slot[] of the last run_batch's mirror slot)
     bool end_mirror = false;
+    // the two mirror slots: the run_batch that published into each (batches;
+    // ~0: none) and the end event recorded behind it; last_need_*: the
+    // budget the latest run_batch reserved
+    hipEvent_t ev_slot[2] = {nullptr, nullptr};
+    uint64_t mirror_batch[2] = {~0ull, ~0ull};
+    int64_t last_need_pages = 0;
+    uint64_t last_need_tail = 0;
     int64_t sub_head = 0, sub_tail = 0;  // batches submitted / waited for
     // The Resolver's load-metrics roll (iopsSample, Resolver.actor.cpp:146-151)
     // of an attached sample (fdbcs_sample_attach), done by the per-transaction
@@ -332,15 +342,37 @@ int sync_state(fdbcs* cs) {
     return FDBCS_OK;
 }
 
+// (a path other than run_batch changed the state behind the mirror slots:
+// reset, load, pool or tail growth, the sharded steps)
+void mirrors_stale(fdbcs* cs) {
+    cs->end_mirror = false;
+    cs->mirror_batch[0] = cs->mirror_batch[1] = ~0ull;
+}
+
 // The scalars after everything issued: from the host-mapped mirror when the
-// last run_batch (which publishes them at its end) has finished -- usually
-// so by the next detectConflicts, whose adds overlap that batch's history
-// update -- else by a stream sync.
+// last run_batch (which publishes them at its end) has finished; else from
+// the one before it, whose slot the last batch's update does not touch (the
+// budget then keeps what the last batch reserved, last_need_*).  When the
+// device is the bottleneck the last batch's update is still running at the
+// next batch's ensure_history: the stream sync this used to take there (one
+// batch in four to eight at config 2) held the next launches back.  Else a
+// stream sync.
 int refresh_state(fdbcs* cs) {
-    if (cs->end_mirror && hipEventQuery(cs->ev_end) == hipSuccess) {
-        memcpy(cs->sc_host, (const void*)cs->sc_mapped, sizeof(Scalars));
-        adopt_scalars(cs);
-        return FDBCS_OK;
+    if (cs->end_mirror && cs->batches) {
+        const uint64_t n = cs->batches - 1;  // (inside run_batch: batch n + 1 is being set up)
+        static const bool prev = !getenv("FDBCS_MIRROR_PREV") || atoi(getenv("FDBCS_MIRROR_PREV"));  // (A/B)
+        const int backs = prev ? (int)std::min<uint64_t>(n, 1) : 0;
+        for (int back = 0; back <= backs; back++) {
+            const int slot = (int)((n - back) & 1);
+            if (cs->mirror_batch[slot] != n - back || hipEventQuery(cs->ev_slot[slot]) != hipSuccess) continue;
+            memcpy(cs->sc_host, (const void*)(cs->sc_mapped + slot), sizeof(Scalars));
+            adopt_scalars(cs);
+            if (back) {
+                cs->pending_pages = cs->last_need_pages;
+                cs->pending_tail = cs->last_need_tail;
+            }
+            return FDBCS_OK;
+        }
     }
     return sync_state(cs);
 }
@@ -386,7 +418,7 @@ int wait_event(hipEvent_t ev) {
 int sync_batch(fdbcs* cs) {
     int r;
     if ((r = wait_stream(cs))) return r;
-    memcpy(cs->sc_host, (const void*)cs->sc_mapped, sizeof(Scalars));
+    memcpy(cs->sc_host, (const void*)cs->h.mirror_host, sizeof(Scalars));  // (the slot of the last publish)
     adopt_scalars(cs);
     return FDBCS_OK;
 }
@@ -395,6 +427,7 @@ int sync_batch(fdbcs* cs) {
 int grow_pool(fdbcs* cs, int64_t pages) {
     int r;
     if ((r = sync_state(cs))) return r;
+    mirrors_stale(cs);  // (the slots' free counts are the old pool's)
     HistBufs old = cs->h;
     int64_t np = std::max<int64_t>(pages, (int64_t)old.cap_pages * 2);
     GROWLOG("pool %d -> %lld pages (asked %lld)\n", old.cap_pages, (long long)np, (long long)pages);
@@ -448,6 +481,7 @@ int grow_pool(fdbcs* cs, int64_t pages) {
 int grow_tail(fdbcs* cs, uint64_t need_half) {
     int r;
     if ((r = sync_state(cs))) return r;
+    mirrors_stale(cs);  // (the slots' tail figures are the old arena's)
     HistBufs& h = cs->h;
     const uint64_t ncap = std::max<uint64_t>(2 * need_half + 16, h.tail_cap * 2);
     GROWLOG("tail arena %llu -> %llu bytes\n", (unsigned long long)h.tail_cap, (unsigned long long)ncap);
@@ -720,6 +754,8 @@ int ensure_history(fdbcs* cs, int64_t W, uint64_t write_tail_bytes) {
     }
     cs->pending_pages += need;
     cs->pending_tail += tneed;
+    cs->last_need_pages = need;
+    cs->last_need_tail = tneed;
     return FDBCS_OK;
 }
 
@@ -881,6 +917,9 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     }
     record(cs, 4);
     const bool compact = new_oldest > cs->oldest;
+    const int mslot = (int)(cs->batches & 1);  // (this batch's mirror slot: refresh_state)
+    h.mirror = cs->mirror_dev + mslot;
+    h.mirror_host = cs->sc_mapped + mslot;
     launch_merge(v, b, h, cs->cur, sc, now, cs->v0, !compact, s);
     cs->cur ^= 1;
     if ((r = debug_check_dir(cs, "merge"))) return r;
@@ -892,7 +931,9 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
     }
     record(cs, 6);
     if (compact) cs->oldest = new_oldest;
+    cs->ev_end = cs->ev_slot[mslot];
     HIPOK(hipEventRecord(cs->ev_end, s));
+    cs->mirror_batch[mslot] = cs->batches;
     cs->end_mirror = true;
     if (sync) {
         if ((r = sync_batch(cs))) return r;
@@ -1098,6 +1139,7 @@ int reset_history(fdbcs* cs, int64_t v) {
     cs->v0 = v;
     cs->cur = 0;
     launch_reset_history(cs->h, cs->cur, cs->sc, cs->stream);
+    mirrors_stale(cs);
     launch_dir_finish(cs->h, cs->cur, cs->sc, cs->b, cs->stream);
     int r = sync_state(cs);
     return r ? r : debug_check_dir(cs, "reset");
@@ -1375,12 +1417,15 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if (hipHostMalloc((void**)&cs->sc_host, sizeof(Scalars), hipHostMallocDefault) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
     memset(cs->sc_host, 0, sizeof(Scalars));
-    if (hipHostMalloc((void**)&cs->sc_mapped, sizeof(Scalars), hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (hipHostMalloc((void**)&cs->sc_mapped, 2 * sizeof(Scalars), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
-        hipHostGetDevicePointer((void**)&cs->h.mirror, cs->sc_mapped, 0) != hipSuccess)
+        hipHostGetDevicePointer((void**)&cs->mirror_dev, cs->sc_mapped, 0) != hipSuccess)
         return fail(FDBCS_E_NOMEM);
-    memset(cs->sc_mapped, 0, sizeof(Scalars));
+    memset(cs->sc_mapped, 0, 2 * sizeof(Scalars));
+    cs->h.mirror = cs->mirror_dev;
     cs->h.mirror_host = cs->sc_mapped;
+    for (int i = 0; i < 2; i++)
+        if (hipEventCreateWithFlags(&cs->ev_slot[i], hipEventDisableTiming) != hipSuccess) return fail(FDBCS_E_HIP);
     // Every initialisation goes on the engine's own stream: it is
     // non-blocking, so the legacy null stream (hipMemset, hipMemcpy) does not
     // order against the kernels that follow on it.
@@ -1411,9 +1456,7 @@ int fdbcs_create(fdbcs** out, int64_t v0, const fdbcs_config* cfg) {
     if ((r = ensure_batch(cs, 1024, 1024, 1024, 1 << 16))) return fail(r);
     if ((r = reset_history(cs, v0))) return fail(r);
     cs->oldest = 0;
-    if (hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&cs->ev_end, hipEventDisableTiming) != hipSuccess)
-        return fail(FDBCS_E_HIP);
+    if (hipStreamCreateWithFlags(&cs->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FDBCS_E_HIP);
     {
         const char* c = getenv("FDBCS_STAGE_CHUNK");  // bytes per streamed H2D chunk of the per-transaction path
         if ((r = cs->st.configure(cs->stream, cs->copy_stream, c ? strtoull(c, nullptr, 0) : 512 << 10))) return fail(r);
@@ -1468,7 +1511,8 @@ void fdbcs_destroy(fdbcs* cs) {
     if (cs->vmap) hipHostFree(cs->vmap);
     cs->st.release();  // (its destructor would otherwise synchronize a destroyed stream)
     if (cs->copy_stream) hipStreamDestroy(cs->copy_stream);
-    if (cs->ev_end) hipEventDestroy(cs->ev_end);
+    for (auto e : cs->ev_slot)
+        if (e) hipEventDestroy(e);
     if (cs->stream) hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -1605,7 +1649,7 @@ int fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict) {
         if (cs->sc_host->last_err) return cs->sc_host->last_err;
     } else {
         HIPOK(hipEventSynchronize(S.done));
-        const int32_t e = ((const volatile Scalars*)cs->sc_mapped)->last_err;
+        const int32_t e = cs->h.mirror_host->last_err;
         if (e) return e;
     }
     if (S.T && verdict) memcpy(verdict, S.vpin, (size_t)S.T);
@@ -1780,6 +1824,7 @@ int fdbcs_load_history(fdbcs* cs, int64_t n, const int64_t* versions, const uint
     HIPOK(hipStreamSynchronize(s));
     tmp.free_top = (int32_t)(h.cap_pages - np);
     HIPOK(hipMemcpyAsync(cs->sc, &tmp, sizeof(Scalars), hipMemcpyHostToDevice, s));
+    mirrors_stale(cs);
     launch_dir_finish(h, cs->cur, cs->sc, cs->b, s);
     if ((r = set_removal_key(cs, removal_key, removal_key_len))) return r;
     cs->v0 = v0;
@@ -1961,7 +2006,7 @@ int fdbcs_set_shard(fdbcs* cs, const uint8_t* lo, uint32_t lo_len, int has_lo, c
 int fdbcs_shard_check(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_t new_oldest, int64_t carry_in,
                       uint8_t* dev_hist) {
     if (cs) live_quiesce(cs);
-    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
+    if (cs) mirrors_stale(cs);  // (refresh_state: the mirror follows run_batch only)
     (void)now;
     (void)new_oldest;
     if (!cs || !db) return FDBCS_E_ARG;
@@ -2016,7 +2061,7 @@ int fdbcs_shard_apply(fdbcs* cs, const fdbcs_batch_view* db, int64_t now, int64_
                       const uint8_t* removal_key, int32_t removal_key_len, const uint8_t* dev_hist,
                       uint8_t* dev_verdict, int64_t* info) {
     if (cs) live_quiesce(cs);
-    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
+    if (cs) mirrors_stale(cs);  // (refresh_state: the mirror follows run_batch only)
     if (!cs || !db || !info || removal_key_len > FDBCS_MAX_KEY) return FDBCS_E_ARG;
     cs->edges_known = false;
     const fdbcs_batch_view& v = *db;
@@ -2098,7 +2143,7 @@ int fdbcs_shard_set_edges(fdbcs* cs, const int32_t* dev_et, const int32_t* dev_e
 int fdbcs_shard_compact(fdbcs* cs, int64_t a, int64_t b, int keep_first, int64_t prev_version, int64_t new_oldest,
                         int64_t key_index, uint8_t* key_buf, int32_t key_cap, int64_t* info) {
     if (cs) live_quiesce(cs);
-    if (cs) cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
+    if (cs) mirrors_stale(cs);  // (refresh_state: the mirror follows run_batch only)
     // (the window lies in the history the last apply left: known_H, synchronized there)
     if (!cs || !info || a < 0 || b < a || b > cs->known_H || key_index >= cs->known_H) return FDBCS_E_ARG;
     hipStream_t s = cs->stream;
@@ -2379,7 +2424,7 @@ void sh_ecap_decay(fdbcs_sharded* sh) {
 
 // one batch of the sharded resolver on the device-resident view v
 int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
-    sh->cs->end_mirror = false;  // (refresh_state: the mirror follows run_batch only)
+    mirrors_stale(sh->cs);  // (refresh_state: the mirror follows run_batch only)
     fdbcs* cs = sh->cs;
     cs->batches++;
     int r;
