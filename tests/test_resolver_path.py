@@ -219,6 +219,22 @@ def test_borrowed_back_to_back_long_keys(gpu):
     g.close()
 
 
+def test_borrowed_budget_refresh_under_pressure(gpu):
+    """The budget refresh (engine.hip refresh_state) adopts the mirror slot of
+    the batch before the last one while the last one's update still runs.
+    With a small tail arena and an empty initial pool, refreshes, pool growth
+    and tail-arena growth come every few batches: verdicts as the oracle's
+    every batch and the history at the end."""
+    from foundationdb_amd.batch import PackedBatch
+    g = ConflictSet(flags=BORROW_ALWAYS, tail_arena_bytes=1 << 16)
+    c = CpuSpec()
+    for i, (txns, now, nold) in enumerate(_long_key_stream(23, 24, 1500)):
+        v = ConflictBatch_run(g, txns, now, nold)
+        assert np.array_equal(v, c.detect_packed(PackedBatch.from_txns(txns), now, nold)), i
+    same_history(g, c)
+    g.close()
+
+
 def _ranges(lib_keys, spec):
     """ctypes Range array over the bytes of lib_keys (a bytearray the test keeps
     and later overwrites): spec = [(begin offset, begin len, end offset, end len)]."""
