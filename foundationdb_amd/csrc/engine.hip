@@ -194,6 +194,7 @@ struct fdbcs {
         int64_t dverd_cap = 0;
         hipEvent_t copied = nullptr, done = nullptr;
         int64_t T = 0;
+        const volatile Scalars* mirror = nullptr;  // the mirror slot its run_batch published into
     } slot[2];
     hipStream_t copy_stream = nullptr;
     // end of the last run_batch's history update (its scalars are then in the
@@ -1634,6 +1635,7 @@ int fdbcs_batch_submit_packed(fdbcs* cs, const fdbcs_batch_view* hb, int64_t now
     if (T) HIPOK(hipMemcpyAsync(S.vpin, S.dverd, (size_t)T, hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipEventRecord(S.done, cs->stream));
     S.T = T;
+    S.mirror = cs->h.mirror_host;
     cs->sub_head++;
     return FDBCS_OK;
 }
@@ -1649,7 +1651,7 @@ int fdbcs_batch_wait(fdbcs* cs, uint8_t* verdict) {
         if (cs->sc_host->last_err) return cs->sc_host->last_err;
     } else {
         HIPOK(hipEventSynchronize(S.done));
-        const int32_t e = cs->h.mirror_host->last_err;
+        const int32_t e = (S.mirror ? S.mirror : cs->h.mirror_host)->last_err;  // (this batch's slot)
         if (e) return e;
     }
     if (S.T && verdict) memcpy(verdict, S.vpin, (size_t)S.T);
