@@ -2426,7 +2426,8 @@ void sh_ecap_decay(fdbcs_sharded* sh) {
 
 // one batch of the sharded resolver on the device-resident view v
 int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t new_oldest, uint8_t* verdict) {
-    mirrors_stale(sh->cs);  // (refresh_state: the mirror follows run_batch only)
+    static const bool sh_mirror = !getenv("FDBCS_SH_MIRROR") || atoi(getenv("FDBCS_SH_MIRROR"));  // (A/B; 0: sync)
+    if (!sh_mirror) mirrors_stale(sh->cs);
     fdbcs* cs = sh->cs;
     cs->batches++;
     int r;
@@ -2471,6 +2472,11 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     hipStream_t s = cs->stream;
     Scalars* sc = cs->sc;
     uint8_t* flags = sh->x1 + slots;
+    // this batch's mirror slot (refresh_state, as run_batch's): the batch-ending
+    // kernel of the last attempt publishes there, the event follows the attempt
+    const int mslot = (int)(cs->batches & 1);
+    h.mirror = cs->mirror_dev + mslot;
+    h.mirror_host = cs->sc_mapped + mslot;
     // 1-2: the check, clipped to this shard (carry-in: sc->carry_check)
     const bool scatter = cs->have_quantiles && !b.large;
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
@@ -2525,6 +2531,12 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
         cs->oldest = new_oldest;
     }
     launch_sh_slot_out(sc, reinterpret_cast<int64_t*>(sh->x1), sh->rank, sh->world, s);
+    if (sh_mirror) {
+        cs->ev_end = cs->ev_slot[mslot];
+        HIPOK(hipEventRecord(cs->ev_end, s));
+        cs->mirror_batch[mslot] = cs->batches;
+        cs->end_mirror = true;
+    }
     // the one wait: the verdicts
     if (!T) return FDBCS_OK;
     r = verdict_wait(cs, T, verdict, nullptr, &sh->last_max);
@@ -2544,6 +2556,7 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     cs->oldest = oldest0;
     if (attempt >= 4) return FDBCS_E_CAPACITY;
     if ((r = sync_state(cs))) return r;
+    mirrors_stale(cs);  // (the attempt published; the next one publishes again)
     const int64_t need = cs->sc_host->sh_need;
     sh->retries++;
     GROWLOG("sharded edge exchange short: need %lld, capacity %lld\n", (long long)need, (long long)sh->ecap);
