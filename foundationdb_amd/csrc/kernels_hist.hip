@@ -314,18 +314,30 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
     if (threadIdx.x < 64) {
         int64_t p0 = 0, p1 = 0, p2 = 0;
         int carry = 0;
-        for (int k0 = 0; k0 < (int)blockIdx.x; k0 += 64) {
-            const int k = k0 + lane;
-            const bool ok = k < (int)blockIdx.x;
-            const int d = ok ? A.blk_diff[k] : 0;
-            const int st = carry + wave_incl_scan(d) - d;  // state at block k's start
-            if (ok) {
-                const int64_t* g = A.blk_agg + (int64_t)k * 6 + 3 * (st > 0);
-                p0 += g[0];
-                p1 += g[1];
-                p2 += g[2];
+        // 256 predecessors a round: their differences and both halves of
+        // their aggregates (either start state) loaded together, the state
+        // chosen after the scan -- one round trip where loading each
+        // aggregate behind its state took two per 64 predecessors
+        const int nb = (int)blockIdx.x;
+        for (int k0 = 0; k0 < nb; k0 += 256) {
+            int d[4];
+            int64_t a[4][6];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + 64 * u + lane;
+                const bool ok = k < nb;
+                d[u] = ok ? A.blk_diff[k] : 0;
+#pragma unroll
+                for (int j = 0; j < 6; j++) a[u][j] = ok ? A.blk_agg[(int64_t)k * 6 + j] : 0;
             }
-            carry += wave_reduce_sum(d);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int st = carry + wave_incl_scan(d[u]) - d[u];  // state at block k's start
+                p0 += st > 0 ? a[u][3] : a[u][0];
+                p1 += st > 0 ? a[u][4] : a[u][1];
+                p2 += st > 0 ? a[u][5] : a[u][2];
+                carry += wave_reduce_sum(d[u]);
+            }
         }
         p0 = wave_reduce_sum(p0);
         p1 = wave_reduce_sum(p1);
@@ -1616,6 +1628,28 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
     const int np = sc->win_np;
     const int pA = sc->win_pA;
     const int top0 = sc->free_top;
+    // this block's first page (usually its only one): its entry, keep flags
+    // and slots loaded before the survivor sums below, so those loads do not
+    // wait behind the sums' barriers (two dependent round trips)
+    const int i = threadIdx.x;
+    int pg0 = 0, c0 = 0, kp0 = 0;
+    uint64_t hi0 = 0, lo0 = 0;
+    uint32_t meta0 = 0;
+    int64_t ver0 = 0;
+    const uint8_t* tail0 = nullptr;
+    if ((int)blockIdx.x < np) {
+        pg0 = dir.page[pA + blockIdx.x];
+        c0 = dir.cnt[pA + blockIdx.x];
+        if (i < c0) {
+            kp0 = keep[(int64_t)blockIdx.x * PAGE + i];
+            const int64_t sidx = (int64_t)pg0 * PAGE + i;
+            hi0 = pool.hi[sidx];
+            lo0 = pool.lo[sidx];
+            meta0 = pool.meta[sidx];
+            ver0 = pool.ver[sidx];
+            tail0 = pool.tail[sidx];
+        }
+    }
     // survivors in all window pages (S) and before this block's first page:
     // the window is a few hundred pages, so every block sums the counts
     int all = 0;
@@ -1635,11 +1669,11 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
         before += block_reduce_sum(part_sum, tmp);
         wprev = w;
         const int offw = before;
+        const bool first = w == (int)blockIdx.x;
         const int q = pA + w;
-        const int pg = dir.page[q], c = dir.cnt[q];
-        const int i = threadIdx.x;
+        const int pg = first ? pg0 : dir.page[q], c = first ? c0 : dir.cnt[q];
         if (i < 4) lmax[i] = INT64_MIN;
-        const int kp = i < c ? keep[(int64_t)w * PAGE + i] : 0;
+        const int kp = first ? kp0 : (i < c ? keep[(int64_t)w * PAGE + i] : 0);
         int tot;
         const int ex = block_excl_scan(kp, tmp, tot);
         const int part0 = offw / per;
@@ -1649,10 +1683,10 @@ __global__ __launch_bounds__(256) void k_win_repack(Pool pool, Dir dir, Scalars*
             const int n = min(per, S - part * per), g = spread_gap(n);  // spread with fresh holes
             const int dp = free_stack[top0 - 1 - part];
             const int64_t sidx = (int64_t)pg * PAGE + i;
-            const uint64_t hi = pool.hi[sidx], lo = pool.lo[sidx];
-            const uint32_t meta = pool.meta[sidx];
-            const int64_t ver = pool.ver[sidx];
-            const uint8_t* tail = pool.tail[sidx];
+            const uint64_t hi = first ? hi0 : pool.hi[sidx], lo = first ? lo0 : pool.lo[sidx];
+            const uint32_t meta = first ? meta0 : pool.meta[sidx];
+            const int64_t ver = first ? ver0 : pool.ver[sidx];
+            const uint8_t* tail = first ? tail0 : pool.tail[sidx];
             if (gc) tail = move_tail(tail, meta, arena, arena_cap, sc);
             const int64_t d = (int64_t)dp * PAGE + spread_slot(r, g);
             put_entry(pool, d, hi, lo, meta, ver, tail);
