@@ -194,19 +194,28 @@ struct PlanItem {
     int32_t nout, parts, nn, jlo, jhi;
 };
 
-// cnt: the entry's real boundaries (Dir::nr)
-__device__ inline PlanItem plan_item(const PageAcc& acc, int cnt, int x, bool covered) {
+// An entry's accumulators and real boundary count (Dir::nr), loaded
+// together before the plan kernels' scans (not behind their barriers).
+struct PlanIn {
+    int cnt, jlo, jhi, nn, er;
+};
+__device__ inline PlanIn plan_load(const PageAcc& acc, const int32_t* nr, int x) {
+    return PlanIn{nr[x], acc.jlo[x], acc.jhi[x], acc.nn[x], acc.er[x]};
+}
+
+__device__ inline PlanItem plan_item(const PlanIn& in, int x, bool covered) {
     PlanItem it;
-    it.jlo = acc.jlo[x];
-    it.jhi = acc.jhi[x];
+    const int cnt = in.cnt;
+    it.jlo = in.jlo;
+    it.jhi = in.jhi;
     it.nn = 0;
     if (covered) {
         it.affected = true;
         it.nout = 0;
     } else if (it.jhi >= 0) {
         it.affected = true;
-        it.nn = acc.nn[x];
-        it.nout = cnt - acc.er[x] + it.nn;
+        it.nn = in.nn;
+        it.nout = cnt - in.er + it.nn;
     } else {
         it.affected = false;
         it.nout = cnt;
@@ -257,9 +266,11 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_aggr(Dir dir, const Scalars
     if (base >= D) return;
     const int x0 = base + threadIdx.x * PS_ITEMS;
     int dl[PS_ITEMS], dsum = 0;
+    PlanIn in[PS_ITEMS];
 #pragma unroll
     for (int k = 0; k < PS_ITEMS; k++) {
         dl[k] = x0 + k < D ? acc.diff[x0 + k] : 0;
+        in[k] = x0 + k < D ? plan_load(acc, dir.nr, x0 + k) : PlanIn{0, 0, -1, 0, 0};
         dsum += dl[k];
     }
     int dtot;
@@ -270,10 +281,10 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_aggr(Dir dir, const Scalars
         cov += dl[k];
         const int x = x0 + k;
         if (x < D) {
-            const int cnt = dir.nr[x];
+            const int cnt = in[k].cnt;
 #pragma unroll
             for (int s = 0; s < 2; s++) {  // s = state at the block start
-                const PlanItem it = plan_item(acc, cnt, x, s + cov > 0);
+                const PlanItem it = plan_item(in[k], x, s + cov > 0);
                 int64_t w[3];
                 pack_item(it, cnt, w);
                 v[3 * s + 0] += w[0];
@@ -310,6 +321,31 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
     const int base = blockIdx.x * PS_BLOCK;
     if (base >= D) return;
     const int lane = threadIdx.x & 63;
+    // this thread's entries: accumulators and directory fields, loaded before
+    // the prefix and the scans (their barriers would hold these loads back)
+    const int x0 = base + threadIdx.x * PS_ITEMS;
+    int dl[PS_ITEMS];
+    PlanIn in[PS_ITEMS];
+    int64_t e_start[PS_ITEMS], e_maxv[PS_ITEMS];
+    int e_page[PS_ITEMS], e_cnt[PS_ITEMS];
+    uint64_t e_fhi[PS_ITEMS], e_flo[PS_ITEMS];
+    uint32_t e_fmeta[PS_ITEMS];
+    const uint8_t* e_ftail[PS_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PS_ITEMS; k++) {
+        const int x = x0 + k;
+        const bool ok = x < D;
+        dl[k] = ok ? A.acc.diff[x] : 0;
+        in[k] = ok ? plan_load(A.acc, A.src.nr, x) : PlanIn{0, 0, -1, 0, 0};
+        e_start[k] = ok ? A.src.start[x] : 0;
+        e_page[k] = ok ? A.src.page[x] : 0;
+        e_cnt[k] = ok ? A.src.cnt[x] : 0;
+        e_maxv[k] = ok ? A.src.maxv[x] : 0;
+        e_fhi[k] = ok ? A.src.fhi[x] : 0;
+        e_flo[k] = ok ? A.src.flo[x] : 0;
+        e_fmeta[k] = ok ? A.src.fmeta[x] : 0;
+        e_ftail[k] = ok ? A.src.ftail[x] : nullptr;
+    }
     // ---- this block's prefix from its predecessors (wave 0) ----
     if (threadIdx.x < 64) {
         int64_t p0 = 0, p1 = 0, p2 = 0;
@@ -350,13 +386,9 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         }
     }
     __syncthreads();
-    const int x0 = base + threadIdx.x * PS_ITEMS;
-    int dl[PS_ITEMS], dsum = 0;
+    int dsum = 0;
 #pragma unroll
-    for (int k = 0; k < PS_ITEMS; k++) {
-        dl[k] = x0 + k < D ? A.acc.diff[x0 + k] : 0;
-        dsum += dl[k];
-    }
+    for (int k = 0; k < PS_ITEMS; k++) dsum += dl[k];
     int dtot;
     int cov = (int)s_pre[3] + block_excl_scan(dsum, red32, dtot);
     PlanItem it[PS_ITEMS];
@@ -370,8 +402,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         it[k] = PlanItem{false, 0, 0, 0, 0, -1};
         w[k][0] = w[k][1] = w[k][2] = 0;
         if (x < D) {
-            cnt[k] = A.src.nr[x];
-            it[k] = plan_item(A.acc, cnt[k], x, cov > 0);
+            cnt[k] = in[k].cnt;
+            it[k] = plan_item(in[k], x, cov > 0);
             pack_item(it[k], cnt[k], w[k]);
         }
         tsum[0] += w[k][0];
@@ -387,12 +419,12 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
         const int x = x0 + k;
         if (x < D) {
             const int pos = (int)(ex[0] >> 32);
-            const int64_t st = A.src.start[x] + (int64_t)(int32_t)(uint32_t)((uint64_t)ex[2] >> 32);
+            const int64_t st = e_start[k] + (int64_t)(int32_t)(uint32_t)((uint64_t)ex[2] >> 32);
             if (it[k].affected) {
                 const int a = (int)(uint32_t)ex[0];
                 A.aff_list[a] = x;
-                A.aff_page[a] = A.src.page[x];
-                A.aff_cnt[a] = A.src.cnt[x];  // slots in use
+                A.aff_page[a] = e_page[k];
+                A.aff_cnt[a] = e_cnt[k];  // slots in use
                 A.aff_jlo[a] = it[k].jlo;
                 A.aff_jhi[a] = it[k].jhi;
                 A.aff_nn[a] = it[k].nn;
@@ -403,14 +435,14 @@ __global__ __launch_bounds__(PS_THREADS) void k_plan_scan(PlanArgs A) {
                 A.aff_free_off[a] = (int)(ex[1] >> 32);
                 A.aff_start[a] = st;
             } else {
-                A.dst.page[pos] = A.src.page[x];
-                A.dst.cnt[pos] = A.src.cnt[x];
+                A.dst.page[pos] = e_page[k];
+                A.dst.cnt[pos] = e_cnt[k];
                 A.dst.nr[pos] = cnt[k];
-                A.dst.maxv[pos] = A.src.maxv[x];
-                A.dst.fhi[pos] = A.src.fhi[x];
-                A.dst.flo[pos] = A.src.flo[x];
-                A.dst.fmeta[pos] = A.src.fmeta[x];
-                A.dst.ftail[pos] = A.src.ftail[x];
+                A.dst.maxv[pos] = e_maxv[k];
+                A.dst.fhi[pos] = e_fhi[k];
+                A.dst.flo[pos] = e_flo[k];
+                A.dst.fmeta[pos] = e_fmeta[k];
+                A.dst.ftail[pos] = e_ftail[k];
                 A.dst.start[pos] = st;
             }
             // reset the accumulators for the next batch
@@ -1281,6 +1313,15 @@ __device__ void win_setup_wave(const Pool& pool, const Dir& dir, int D, Scalars*
 
 // level-1 entry i of the search index, and the entries of higher levels it
 // starts (i a multiple of 16^(l-1))
+__device__ inline void sidx_put(const Dir& d, int i, uint64_t v) {
+    d.sidx[i] = v;
+    int ii = i;
+    for (int l = 2; l <= SIDX_LEVELS && (ii & (SIDX_B - 1)) == 0; l++) {
+        ii >>= SIDX_LOG;
+        d.sidx[sidx_off(d.cap, l) + ii] = v;
+    }
+}
+
 __device__ inline void sidx_build(const Dir& d, int i) {
     const uint64_t v = d.fhi[(int64_t)i * SIDX_B];
     d.sidx[i] = v;
@@ -1729,22 +1770,32 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         const int y = y0 + threadIdx.x;
         int64_t mv = INT64_MIN;
         if (y < Dn) {
+            // (the entry's fields in registers: its maximum and first key feed
+            // the group maxima and the search index without reading back
+            // what was just stored -- a round trip each)
+            int pg, cn, nrr;
+            int64_t st;
+            uint64_t fh, fl;
+            uint32_t fm;
+            const uint8_t* ft;
             if (keep) {  // (Dn == 1)
-                dst.page[0] = src.page[0]; dst.cnt[0] = 0; dst.maxv[0] = INT64_MIN;
-                dst.fhi[0] = 0; dst.flo[0] = 0; dst.fmeta[0] = 0; dst.ftail[0] = nullptr;
-                dst.start[0] = 0;
-            } else if (np == 0 || y < pA) {
-                dir_copy(src, y, dst, y);
-                dst.start[y] = src.start[y];
-            } else if (y < pA + k) {
-                desc_copy(desc, y - pA, dst, y);
-                dst.start[y] = src.start[pA] + (int64_t)(y - pA) * per;
+                pg = src.page[0]; cn = 0; nrr = 0; mv = INT64_MIN;
+                fh = 0; fl = 0; fm = 0; ft = nullptr; st = 0;
+            } else if (np == 0 || y < pA || y >= pA + k) {
+                const int x = np == 0 || y < pA ? y : y - k + np;
+                pg = src.page[x]; cn = src.cnt[x]; nrr = src.nr[x]; mv = src.maxv[x];
+                fh = src.fhi[x]; fl = src.flo[x]; fm = src.fmeta[x]; ft = src.ftail[x];
+                st = np == 0 || y < pA ? src.start[x] : src.start[x] - removed;
             } else {
-                dir_copy(src, y - k + np, dst, y);
-                dst.start[y] = src.start[y - k + np] - removed;
+                const int x = y - pA;
+                pg = desc.page[x]; cn = desc.cnt[x]; nrr = desc.nr[x]; mv = desc.maxv[x];
+                fh = desc.fhi[x]; fl = desc.flo[x]; fm = desc.fmeta[x]; ft = desc.ftail[x];
+                st = src.start[pA] + (int64_t)x * per;
             }
-            mv = dst.maxv[y];
-            if ((y & (SIDX_B - 1)) == 0) sidx_build(dst, y / SIDX_B);
+            dst.page[y] = pg; dst.cnt[y] = cn; dst.nr[y] = nrr; dst.maxv[y] = mv;
+            dst.fhi[y] = fh; dst.flo[y] = fl; dst.fmeta[y] = fm; dst.ftail[y] = ft;
+            dst.start[y] = st;
+            if ((y & (SIDX_B - 1)) == 0) sidx_put(dst, y / SIDX_B, fh);
         }
         if (y < np - keep) free_stack[top - k + y] = src.page[pA + keep + y];
         mv = wave_reduce_max(mv);  // one wavefront = one 64-entry group
