@@ -378,6 +378,28 @@ int refresh_state(fdbcs* cs) {
     return sync_state(cs);
 }
 
+// The sort's overflow guard (k_ss_guard, ≈ 4.6 us a batch even when it finds
+// nothing): launched unless the last finished batch's buckets stayed well
+// inside their staging rows (Scalars::ss_maxc below SORT_GUARD_MAXC, not
+// bucketed twice), read from its mirror slot (refresh_state's).  A bucket
+// that overflows without it is ranked by the bucket kernel's global path --
+// the same result, slower for that batch -- and the next batch's splitters
+// come from this one's sorted output.  FDBCS_SORT_GUARD=1 / 0: always / never.
+bool sort_guard(fdbcs* cs) {
+    const char* e = getenv("FDBCS_SORT_GUARD");  // (read per batch: tests switch it)
+    const int env = e ? atoi(e) : -1;
+    if (env >= 0) return env != 0;
+    if (!cs->end_mirror || cs->batches < 2) return true;
+    const uint64_t n = cs->batches - 1;  // (inside run_batch: the latest published batch)
+    for (int back = 0; back <= 1; back++) {
+        const int slot = (int)((n - back) & 1);
+        if (cs->mirror_batch[slot] != n - back || hipEventQuery(cs->ev_slot[slot]) != hipSuccess) continue;
+        const Scalars* m = cs->sc_mapped + slot;
+        return m->ss_resample != 0 || m->ss_maxc >= SORT_GUARD_MAXC;
+    }
+    return true;
+}
+
 // Wait for the stream.  FDBCS_SYNC_SPIN=1: poll instead of the runtime's
 // blocking wait (the resolver thread stays on its core).
 int wait_stream(fdbcs* cs) {
@@ -882,7 +904,8 @@ int run_batch(fdbcs* cs, const fdbcs_batch_view& v, int64_t now, int64_t new_old
                       (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0, lm);
     }
     record(cs, 1);
-    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, cs->v0)) {
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, cs->v0,
+                           sort_guard(cs))) {
         cs->sorts++;
         cs->have_quantiles = true;
     }

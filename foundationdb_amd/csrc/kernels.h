@@ -310,8 +310,17 @@ void launch_ingest(const fdbcs_batch_view& v, int64_t oldest, BatchBufs& b, Scal
 // h (optional): the history the batch's read check searches -- the check of
 // every read then runs in the sort's bucket launch (b.rc_fused), and the next
 // launch_edges_read_check leaves it out; v0: as launch_edges_read_check's
+// guard false: no k_ss_guard launch after a scattering ingest (run_batch's
+// adaptive policy, SORT_GUARD_MAXC); an overflowed bucket is then ranked by
+// the bucket kernel's global path, and the next batch's splitters come from
+// this batch's sorted output
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        bool scattered, hipStream_t s, HistBufs* h = nullptr, int cur = 0, int64_t v0 = 0);
+                        bool scattered, hipStream_t s, HistBufs* h = nullptr, int cur = 0, int64_t v0 = 0,
+                        bool guard = true);
+// run_batch launches the sort's overflow guard only when the last finished
+// batch's largest bucket (Scalars::ss_maxc) reached this, or it was bucketed
+// twice (half of a bucket's 512-record staging row)
+constexpr int SORT_GUARD_MAXC = 256;
 int64_t sort_staging_records(int R, int W, bool large);
 // Large-batch mode (T > LARGE_T, or forced by FDBCS_TEST_LARGE_BATCH for tests):
 // the endpoint sort is a merge sort (no per-batch splitter balance limits)

@@ -2099,7 +2099,7 @@ void launch_live_reset(BatchBufs& b, Scalars* sc, int parity, hipStream_t s) {
 }
 
 bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bool sample, int parity,
-                        bool scattered, hipStream_t s, HistBufs* h, int cur, int64_t v0) {
+                        bool scattered, hipStream_t s, HistBufs* h, int cur, int64_t v0, bool guard) {
     const SortJobs J = make_sort_jobs(v, b, sc, parity);
     b.sr = b.rec_r0;
     b.sw = b.rec_w0;
@@ -2114,7 +2114,8 @@ bool launch_sort_ranges(const fdbcs_batch_view& v, BatchBufs& b, Scalars* sc, bo
         if (sample) hipLaunchKernelGGL(k_ss_sample, dim3(2), dim3(1024), 0, s, J, b.keys, 0);
         hipLaunchKernelGGL(k_ss_scatter, dim3(J.blocks0 + cdiv(J.n[1], 256)), dim3(256), 0, s, J, b.keys);
     }
-    hipLaunchKernelGGL(k_ss_guard, dim3(2), dim3(1024), 0, s, J, b.keys, b.ss_gsamp);  // overflow guard
+    if (guard || !scattered)
+        hipLaunchKernelGGL(k_ss_guard, dim3(2), dim3(1024), 0, s, J, b.keys, b.ss_gsamp);  // overflow guard
     const int nbk = J.nb[0] + J.nb[1];
     static const bool separate = getenv("FDBCS_SEPARATE_READ_CHECK") != nullptr;  // (A/B measurements)
     const int R = v.read_count;

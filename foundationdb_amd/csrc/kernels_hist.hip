@@ -1544,7 +1544,8 @@ __global__ __launch_bounds__(256) void k_bmax_commit(Dir d, Scalars* sc, const i
             sc->last_err = sc->err;
             sc->err = 0;
             if (sc->btail_used) sc->px_on = 1;  // (a long key came through: the prefix skips, from now on)
-        sc->btail_used = 0;
+            sc->btail_used = 0;
+            sc->ss_over[0] = sc->ss_over[1] = 0;  // (a sort overflow no guard ran for: not the next batch's)
             lm_end_of_batch(sc);
         }
     }
@@ -1845,6 +1846,7 @@ __global__ __launch_bounds__(1024) void k_win_dir(Dir src, Dir dst, Scalars* sc,
         sc->err = 0;
         if (sc->btail_used) sc->px_on = 1;
         sc->btail_used = 0;
+        sc->ss_over[0] = sc->ss_over[1] = 0;  // (a sort overflow no guard ran for: not the next batch's)
         lm_end_of_batch(sc);
     }
     __syncthreads();

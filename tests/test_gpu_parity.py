@@ -381,13 +381,22 @@ def test_load_dump_roundtrip(cs):
     assert cs.header_version == 11 and cs.oldest_version == 2
 
 
-def test_sort_distribution_shift(cs):
+@pytest.mark.parametrize("guard", ["1", None])
+def test_sort_distribution_shift(cs, guard, monkeypatch):
     """The sort buckets by the previous batch's quantiles; a batch whose keys
-    all lie outside them (a moved key distribution) overflows one bucket, and
-    the guard re-buckets it by splitters from its own sample in the same batch
-    (stats: sort_rebucketed).  Verdicts and history must not change."""
+    all lie outside them (a moved key distribution) overflows one bucket.
+    With the guard (FDBCS_SORT_GUARD=1) it is re-bucketed by splitters from
+    its own sample in the same batch (stats: sort_rebucketed).  By default the
+    guard runs only after a batch whose largest bucket came near its staging
+    row (engine.hip sort_guard): the first overflowed batch is then ranked by
+    the bucket kernel's global path, and the next one, guarded, re-buckets.
+    Verdicts and history must not change either way."""
     import random
 
+    if guard:
+        monkeypatch.setenv("FDBCS_SORT_GUARD", guard)
+    else:
+        monkeypatch.delenv("FDBCS_SORT_GUARD", raising=False)
     cs.load_history([], [], v0=0, oldest=0, removal_key=b"")
     c = CpuSpec()
     rng = random.Random(7)
@@ -400,7 +409,7 @@ def test_sort_distribution_shift(cs):
         check_pair(cs, c, PackedBatch.from_txns(txns), 100 + 10 * i, 90 + 10 * i)
         st = cs.batch_stats()
         if i in (2, 3):
-            assert st["sort_rebucketed"] == 1, st
+            assert st["sort_rebucketed"] == (1 if guard or i == 3 else 0), st
         if i in (1, 4):
             assert st["sort_rebucketed"] == 0 and st["sort_max_bucket"] <= 512, st
 
