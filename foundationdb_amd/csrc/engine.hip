@@ -2504,7 +2504,8 @@ int sh_run(fdbcs_sharded* sh, const fdbcs_batch_view& v, int64_t now, int64_t ne
     const bool scatter = cs->have_quantiles && !b.large;
     launch_ingest(v, cs->oldest, b, sc, scatter, (int)(cs->sorts & 1), cs->h.dir[cs->cur], s,
                   (cs->h.shard.has_lo | cs->h.shard.has_hi) != 0);
-    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, sh->v0)) {
+    if (launch_sort_ranges(v, b, sc, !cs->have_quantiles, (int)(cs->sorts & 1), scatter, s, &cs->h, cs->cur, sh->v0,
+                           sort_guard(cs))) {
         cs->sorts++;
         cs->have_quantiles = true;
     }
